@@ -1,0 +1,359 @@
+"""Compile the rule SQL of a windowed GROUP BY into an ek_plan.
+
+Host-side mirror of the pieces of the reference front-end that feed the hot path:
+  * xsql parser for the window literal        internal/xsql/parser.go:926-975,1047-1153
+  * un-aliased aggregate field naming          internal/xsql/parser.go:479,504-509 (name = function name)
+  * planner window config (RawInterval, units) internal/topo/planner/planner.go:387-426,463-478
+  * rule options isEventTime / lateTolerance   internal/pkg/def/rule.go:27-66
+
+Supported subset (everything the BASELINE configs and the reference's window tests use):
+  SELECT <key | agg(col) | count(*) | window_start() | window_end()> [AS alias], ...
+  FROM <stream> [WHERE <expr>]
+  GROUP BY [<key>,] TUMBLINGWINDOW|HOPPINGWINDOW|SLIDINGWINDOW|SESSIONWINDOW|COUNTWINDOW(...)
+           [OVER (WHEN <expr>)]
+  [HAVING <expr>]
+Expressions: comparisons, AND/OR, + - * / %, numeric literals, column refs, aggregate calls (HAVING).
+The GROUP BY dimension must be a dictionary-encoded key column (type "key" in the schema).
+"""
+import re
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import abi as A
+
+_TOKEN = re.compile(r"\s*(?:(\d+\.\d*|\.\d+|\d+(?:[eE][-+]?\d+)?)|([A-Za-z_][A-Za-z0-9_.]*)|(<=|>=|!=|<>|[=<>(),*+\-/%])|(\"[^\"]*\"|'[^']*'))")
+
+WINDOW_TYPES = {
+    "tumblingwindow": A.EK_WINDOW_TUMBLING,
+    "hoppingwindow": A.EK_WINDOW_HOPPING,
+    "slidingwindow": A.EK_WINDOW_SLIDING,
+    "sessionwindow": A.EK_WINDOW_SESSION,
+    "countwindow": A.EK_WINDOW_COUNT,
+}
+_CMP = {"=": A.EK_OP_EQ, "!=": A.EK_OP_NEQ, "<>": A.EK_OP_NEQ, "<": A.EK_OP_LT, "<=": A.EK_OP_LTE,
+        ">": A.EK_OP_GT, ">=": A.EK_OP_GTE}
+_ADD = {"+": A.EK_OP_ADD, "-": A.EK_OP_SUB}
+_MUL = {"*": A.EK_OP_MUL, "/": A.EK_OP_DIV, "%": A.EK_OP_MOD}
+COLTYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32}
+
+
+class RuleError(ValueError):
+    pass
+
+
+@dataclass
+class OutputField:
+    name: str
+    kind: str            # "key" | "agg" | "window_start" | "window_end"
+    slot: int = -1
+
+
+@dataclass
+class CompiledRule:
+    plan: A.ek_plan
+    columns: List[str]
+    fields: List[OutputField]
+    sql: str
+    options: Dict = field(default_factory=dict)
+
+    def column_index(self, name: str) -> int:
+        return self.columns.index(name)
+
+
+def _tokenize(sql: str) -> List[str]:
+    pos, out = 0, []
+    sql = sql.strip().rstrip(";")
+    while pos < len(sql):
+        m = _TOKEN.match(sql, pos)
+        if not m or m.end() == pos:
+            if sql[pos:].strip() == "":
+                break
+            raise RuleError(f"unexpected character at {pos}: {sql[pos:pos + 10]!r}")
+        tok = next(g for g in m.groups() if g is not None)
+        out.append(tok)
+        pos = m.end()
+    return out
+
+
+class _Parser:
+    def __init__(self, sql: str, schema: Dict[str, str]):
+        self.toks = _tokenize(sql)
+        self.i = 0
+        self.schema = {k.lower(): (k, v) for k, v in schema.items()}
+        self.columns = list(schema.keys())
+        self.aggs: List[Tuple[int, int, float]] = []
+
+    # token helpers
+    def peek(self, k: int = 0) -> Optional[str]:
+        j = self.i + k
+        return self.toks[j] if j < len(self.toks) else None
+
+    def kw(self, word: str) -> bool:
+        t = self.peek()
+        if t is not None and t.lower() == word:
+            self.i += 1
+            return True
+        return False
+
+    def expect(self, tok: str):
+        t = self.peek()
+        if t is None or t.lower() != tok.lower():
+            raise RuleError(f"expected {tok!r} but found {t!r}")
+        self.i += 1
+
+    def col(self, name: str) -> int:
+        ent = self.schema.get(name.lower().split(".")[-1])
+        if ent is None:
+            raise RuleError(f"unknown field {name}")
+        return self.columns.index(ent[0])
+
+    def agg_slot(self, fn: int, col: int, p: float) -> int:
+        key = (fn, col, p)
+        if key not in self.aggs:
+            if len(self.aggs) >= A.EK_MAX_AGGS:
+                raise RuleError("too many aggregate calls")
+            self.aggs.append(key)
+        return self.aggs.index(key)
+
+    # aggregate call: name '(' args ')'
+    def parse_agg(self, name: str) -> int:
+        name = name.lower()
+        self.expect("(")
+        if name == "count" and self.peek() == "*":
+            self.i += 1
+            self.expect(")")
+            return self.agg_slot(A.EK_AGG_COUNT_STAR, -1, 0.0)
+        arg = self.peek()
+        self.i += 1
+        c = self.col(arg)
+        p = 0.0
+        if self.peek() == ",":
+            self.i += 1
+            p = float(self.peek())
+            self.i += 1
+        self.expect(")")
+        if name in ("percentile_cont", "percentile_disc") and p == 0.0 and name:
+            pass
+        return self.agg_slot(A.AGG_BY_NAME[name], c, p)
+
+    # expressions -> postfix program
+    def expr(self, allow_agg: bool) -> List[Tuple]:
+        return self.or_(allow_agg)
+
+    def or_(self, aa):
+        prog = self.and_(aa)
+        while self.kw("or"):
+            prog = prog + self.and_(aa) + [(A.EK_OP_OR,)]
+        return prog
+
+    def and_(self, aa):
+        prog = self.cmp(aa)
+        while self.kw("and"):
+            prog = prog + self.cmp(aa) + [(A.EK_OP_AND,)]
+        return prog
+
+    def cmp(self, aa):
+        prog = self.add(aa)
+        t = self.peek()
+        if t in _CMP:
+            self.i += 1
+            prog = prog + self.add(aa) + [(_CMP[t],)]
+        return prog
+
+    def add(self, aa):
+        prog = self.mul(aa)
+        while self.peek() in _ADD:
+            op = _ADD[self.peek()]
+            self.i += 1
+            prog = prog + self.mul(aa) + [(op,)]
+        return prog
+
+    def mul(self, aa):
+        prog = self.prim(aa)
+        while self.peek() in _MUL:
+            op = _MUL[self.peek()]
+            self.i += 1
+            prog = prog + self.prim(aa) + [(op,)]
+        return prog
+
+    def prim(self, aa):
+        t = self.peek()
+        if t is None:
+            raise RuleError("unexpected end of expression")
+        if t == "(":
+            self.i += 1
+            prog = self.expr(aa)
+            self.expect(")")
+            return prog
+        if t == "-" and self.peek(1) and re.match(r"[\d.]", self.peek(1)):
+            self.i += 1
+            v = self.peek()
+            self.i += 1
+            return [self._num("-" + v)]
+        if re.match(r"[\d.]", t):
+            self.i += 1
+            return [self._num(t)]
+        if t.lower() in ("true", "false"):
+            raise RuleError("boolean literals are not supported in the GPU plan")
+        self.i += 1
+        if self.peek() == "(":
+            if not aa or t.lower() not in A.AGG_BY_NAME:
+                raise RuleError(f"function {t} is not supported here")
+            return [(A.EK_OP_AGG, self.parse_agg(t))]
+        return [(A.EK_OP_COL, self.col(t))]
+
+    @staticmethod
+    def _num(s: str):
+        if re.fullmatch(r"-?\d+", s):
+            return (A.EK_OP_CONST_I64, int(s))
+        return (A.EK_OP_CONST_F64, float(s))
+
+
+def _fill_prog(dst, prog: List[Tuple]) -> int:
+    if len(prog) > A.EK_MAX_PROG:
+        raise RuleError("expression too long")
+    for k, ins in enumerate(prog):
+        dst[k].op = ins[0]
+        if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG):
+            dst[k].arg = ins[1]
+        elif ins[0] == A.EK_OP_CONST_I64:
+            dst[k].i64 = ins[1]
+            dst[k].f64 = float(ins[1])
+        elif ins[0] == A.EK_OP_CONST_F64:
+            dst[k].f64 = ins[1]
+    return len(prog)
+
+
+def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True, late_tolerance_ms: int = 0,
+                 timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
+                 debug_membership: bool = False) -> CompiledRule:
+    """schema: ordered {column: "bigint" | "float" | "key"}; the TIMESTAMP column must be bigint (epoch ms)."""
+    if len(schema) > A.EK_MAX_COLUMNS:
+        raise RuleError("too many columns")
+    p = _Parser(sql, schema)
+    plan = A.ek_plan()
+    plan.abi_version = A.EKGPU_ABI_VERSION
+    plan.n_columns = len(schema)
+    for k, (name, t) in enumerate(schema.items()):
+        if t not in COLTYPES:
+            raise RuleError(f"unsupported column type {t}")
+        plan.column_type[k] = COLTYPES[t]
+    plan.is_event_time = 1 if is_event_time else 0
+    plan.late_tolerance_ms = int(late_tolerance_ms)
+    plan.tz_offset_s = int(tz_offset_s)
+    plan.ts_column = p.col(timestamp) if (timestamp and is_event_time) else -1
+    plan.key_column = -1
+    plan.num_keys = int(num_keys)
+    plan.debug_membership = 1 if debug_membership else 0
+
+    p.expect("select")
+    fields: List[OutputField] = []
+    raw_select = []
+    while True:
+        start = p.i
+        t = p.peek()
+        if t is None:
+            raise RuleError("unexpected end of select list")
+        if p.peek(1) == "(" and t.lower() in ("window_start", "window_end"):
+            p.i += 3
+            name, kind, slot = t.lower(), t.lower(), -1
+        elif p.peek(1) == "(" and t.lower() in A.AGG_BY_NAME:
+            p.i += 1
+            slot = p.parse_agg(t)
+            name, kind = t.lower(), "agg"
+        else:
+            p.i += 1
+            name, kind, slot = t.split(".")[-1], "column", p.col(t)
+        if p.kw("as"):
+            name = p.peek()
+            p.i += 1
+        raw_select.append(OutputField(name, kind, slot))
+        if p.peek() == ",":
+            p.i += 1
+            continue
+        break
+    p.expect("from")
+    p.i += 1  # stream name
+    where = []
+    if p.kw("where"):
+        where = p.expr(False)
+    key_col = -1
+    trigger = []
+    wtype = A.EK_WINDOW_NONE
+    if p.kw("group"):
+        p.expect("by")
+        while True:
+            t = p.peek()
+            if t is not None and t.lower() in WINDOW_TYPES:
+                wtype = WINDOW_TYPES[t.lower()]
+                p.i += 1
+                p.expect("(")
+                nums = []
+                if wtype != A.EK_WINDOW_COUNT:
+                    unit = p.peek().lower()
+                    if unit not in A.UNIT_BY_NAME:
+                        raise RuleError(f"invalid time unit {unit}")
+                    plan.time_unit = A.UNIT_BY_NAME[unit]
+                    p.i += 1
+                while p.peek() == ",":
+                    p.i += 1
+                    nums.append(int(p.peek()))
+                    p.i += 1
+                if wtype == A.EK_WINDOW_COUNT and not nums:
+                    nums.append(int(p.peek()))
+                    p.i += 1
+                    while p.peek() == ",":
+                        p.i += 1
+                        nums.append(int(p.peek()))
+                        p.i += 1
+                p.expect(")")
+                plan.length = nums[0] if nums else 0
+                if wtype in (A.EK_WINDOW_HOPPING, A.EK_WINDOW_SESSION, A.EK_WINDOW_COUNT):
+                    plan.interval = nums[1] if len(nums) > 1 else 0
+                elif wtype == A.EK_WINDOW_SLIDING:
+                    plan.delay = nums[1] if len(nums) > 1 else 0
+                if p.kw("over"):
+                    p.expect("(")
+                    p.expect("when")
+                    trigger = p.expr(False)
+                    p.expect(")")
+            else:
+                c = p.col(t)
+                if schema[p.columns[c]] != "key":
+                    raise RuleError("GROUP BY dimension must be a dictionary-encoded key column")
+                if key_col >= 0:
+                    raise RuleError("only one GROUP BY dimension is supported")
+                key_col = c
+                p.i += 1
+            if p.peek() == ",":
+                p.i += 1
+                continue
+            break
+    having = []
+    if p.kw("having"):
+        having = p.expr(True)
+    if p.peek() is not None:
+        raise RuleError(f"unexpected token {p.peek()!r}")
+    if wtype == A.EK_WINDOW_NONE:
+        raise RuleError("the GPU window engine needs a window in GROUP BY")
+    plan.window_type = wtype
+    plan.key_column = key_col
+    for f in raw_select:
+        if f.kind == "column":
+            if f.slot != key_col:
+                raise RuleError(f"non-aggregate field {f.name} must be the GROUP BY key")
+            fields.append(OutputField(f.name, "key"))
+        else:
+            fields.append(f)
+    plan.n_aggs = len(p.aggs)
+    for k, (fn, c, prm) in enumerate(p.aggs):
+        plan.aggs[k].fn = fn
+        plan.aggs[k].column = c
+        plan.aggs[k].param = prm if fn in (A.EK_AGG_PERCENTILE_CONT, A.EK_AGG_PERCENTILE_DISC) else 0.0
+    plan.n_where = _fill_prog(plan.where_prog, where)
+    plan.n_having = _fill_prog(plan.having_prog, having)
+    plan.n_trigger = _fill_prog(plan.trigger_prog, trigger)
+    if key_col >= 0 and num_keys <= 0:
+        raise RuleError("num_keys (dictionary size of the GROUP BY key) is required")
+    return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
+                        options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms))

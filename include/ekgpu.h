@@ -1,0 +1,219 @@
+/*
+ * ekgpu.h — C ABI of the MI355X window & aggregate engine.
+ *
+ * This is the drop-in boundary for the hot path of an eKuiper rule:
+ *   [Watermark] -> WindowOperator -> [FilterOp] -> AggregateOp -> [HavingOp] -> ProjectOp(agg fields)
+ * i.e. the operator chain planned by internal/topo/planner/planner.go:387-446 (buildOps) and executed
+ * by internal/topo/node/{watermark_op.go,window_op.go,event_window_trigger.go} and
+ * internal/topo/operator/{filter,aggregate,having,project}_operator.go in the reference.
+ *
+ * One handle = one rule's window/aggregate node (reference: one WindowOperator goroutine,
+ * window_op.go:131-192, plus the UnaryOperator chain behind it, node/operations.go:42-130).
+ * A handle is single-consumer (not internally locked); distinct handles are independent.
+ * All entry points return 0 on success and a negative EK_ERR_* code on failure; the message
+ * is available from ek_last_error(h) and carries the reference's error prefixes
+ * ("run Where error: ...", "run Having error: ...", "run Window error: ...").
+ *
+ * Plain C types only: no HIP or torch types cross this boundary.  Device pointers are passed
+ * as void* together with EK_MEM_DEVICE.
+ */
+#ifndef EKGPU_H
+#define EKGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EKGPU_ABI_VERSION 1
+#define EK_MAX_COLUMNS 16
+#define EK_MAX_AGGS 16
+#define EK_MAX_PROG 48
+
+/* Window types: identical values to pkg/ast/statement.go:185-193 (ast.WindowType). */
+enum {
+    EK_WINDOW_NONE = 0,
+    EK_WINDOW_TUMBLING = 1,
+    EK_WINDOW_HOPPING = 2,
+    EK_WINDOW_SLIDING = 3,
+    EK_WINDOW_SESSION = 4,
+    EK_WINDOW_COUNT = 5
+};
+
+/* Time units of the window literal (pkg/ast/token.go:117-121: DD, HH, MI, SS, MS). */
+enum { EK_UNIT_DD = 1, EK_UNIT_HH = 2, EK_UNIT_MI = 3, EK_UNIT_SS = 4, EK_UNIT_MS = 5 };
+
+/* Column storage types. Stream schema BIGINT -> EK_COL_I64, FLOAT -> EK_COL_F64
+ * (converter/json/converter.go:429-460); group ids are dictionary-encoded EK_COL_U32. */
+enum { EK_COL_I64 = 1, EK_COL_F64 = 2, EK_COL_U32 = 3 };
+
+/* Aggregate functions (internal/binder/function/funcs_agg.go:28-370). */
+enum {
+    EK_AGG_COUNT_STAR = 1,      /* count(*)                         funcs_agg.go:87-95            */
+    EK_AGG_COUNT = 2,           /* count(col): non-nil values       common_array_funcs.go:101-109 */
+    EK_AGG_SUM = 3,             /* funcs_agg.go:114-143                                           */
+    EK_AGG_AVG = 4,             /* funcs_agg.go:56-86 (int: truncating int64 division)            */
+    EK_AGG_MIN = 5,             /* funcs_agg.go:105-113, common_array_funcs.go:59-99              */
+    EK_AGG_MAX = 6,             /* funcs_agg.go:96-104,  common_array_funcs.go:27-57              */
+    EK_AGG_STDDEV = 7,          /* stats.StandardDeviation          funcs_agg.go:206-228          */
+    EK_AGG_STDDEVS = 8,         /* stats.StandardDeviationSample    funcs_agg.go:229-251          */
+    EK_AGG_VAR = 9,             /* stats.Variance                   funcs_agg.go:252-274          */
+    EK_AGG_VARS = 10,           /* stats.SampleVariance             funcs_agg.go:275-297          */
+    EK_AGG_MEDIAN = 11,         /* funcs_agg.go:29-55,415-428                                     */
+    EK_AGG_PERCENTILE_CONT = 12,/* stats.Percentile(sorted, p*100)  funcs_agg.go:298-334          */
+    EK_AGG_PERCENTILE_DISC = 13 /* stats.PercentileNearestRank      funcs_agg.go:335-370          */
+};
+
+/* Expression programs (WHERE / HAVING / OVER(WHEN ...)) in postfix form.
+ * Evaluation follows xsql.ValuerEval.evalBinaryExpr / SimpleDataEval (internal/xsql/valuer.go:574-1000):
+ * nil in a relational or logical op yields false, nil in arithmetic yields nil, int64 op float64
+ * promotes to float64, divide/mod by zero is an error. */
+enum {
+    EK_OP_COL = 1,       /* push column[arg] of the current row (NULL when invalid)          */
+    EK_OP_AGG = 2,       /* push aggregate slot[arg] of the current group (HAVING only)       */
+    EK_OP_CONST_I64 = 3, /* push i64                                                          */
+    EK_OP_CONST_F64 = 4, /* push f64                                                          */
+    EK_OP_EQ = 5, EK_OP_NEQ = 6, EK_OP_LT = 7, EK_OP_LTE = 8, EK_OP_GT = 9, EK_OP_GTE = 10,
+    EK_OP_AND = 11, EK_OP_OR = 12,
+    EK_OP_ADD = 13, EK_OP_SUB = 14, EK_OP_MUL = 15, EK_OP_DIV = 16, EK_OP_MOD = 17
+};
+
+typedef struct {
+    int32_t op;
+    int32_t arg;
+    int64_t i64;
+    double f64;
+} ek_instr;
+
+typedef struct {
+    int32_t fn;      /* EK_AGG_*                                   */
+    int32_t column;  /* argument column (ignored for count(*))     */
+    double param;    /* percentile fraction p (percentile_* only)  */
+} ek_agg_spec;
+
+/* Compiled rule. POD with fixed arrays so a cgo / ctypes caller can fill it in place. */
+typedef struct {
+    int32_t abi_version;          /* must be EKGPU_ABI_VERSION                                  */
+    int32_t window_type;          /* EK_WINDOW_*                                                */
+    int32_t time_unit;            /* EK_UNIT_* (time windows)                                   */
+    int32_t length;               /* raw literal: TUMBLINGWINDOW(ss,10) -> 10; COUNTWINDOW(n) -> n */
+    int32_t interval;             /* HOPPINGWINDOW hop / SESSIONWINDOW timeout / COUNTWINDOW m   */
+    int32_t delay;                /* SLIDINGWINDOW delay                                         */
+    int32_t is_event_time;        /* def.RuleOption.IsEventTime                                  */
+    int32_t tz_offset_s;          /* local-time offset used by window alignment (time.Local)    */
+    int64_t late_tolerance_ms;    /* def.RuleOption.LateTol                                      */
+    int32_t n_columns;
+    int32_t column_type[EK_MAX_COLUMNS];
+    int32_t ts_column;            /* TIMESTAMP column (i64 epoch ms); -1 for processing time     */
+    int32_t key_column;           /* GROUP BY dimension as dense u32 id; -1 = no GROUP BY       */
+    uint32_t num_keys;            /* exclusive bound of key ids                                 */
+    int32_t debug_membership;     /* 1: report per-window member count + member-set hash        */
+    int32_t n_aggs;
+    ek_agg_spec aggs[EK_MAX_AGGS];
+    int32_t n_where;
+    ek_instr where_prog[EK_MAX_PROG];
+    int32_t n_having;
+    ek_instr having_prog[EK_MAX_PROG];
+    int32_t n_trigger;            /* SLIDINGWINDOW(...) OVER (WHEN <prog>)                       */
+    ek_instr trigger_prog[EK_MAX_PROG];
+} ek_plan;
+
+enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };
+
+/* One columnar micro-batch in arrival order. */
+typedef struct {
+    int64_t n_rows;
+    const void* columns[EK_MAX_COLUMNS];
+    const uint8_t* validity[EK_MAX_COLUMNS]; /* 1 byte per row, 1 = valid; NULL = all valid */
+    int32_t memory;                          /* EK_MEM_HOST or EK_MEM_DEVICE                */
+} ek_batch;
+
+/* Per-row value tags of aggregate outputs (Go dynamic type of the reference's result). */
+enum { EK_TAG_NULL = 0, EK_TAG_I64 = 1, EK_TAG_F64 = 2 };
+
+/* Window status (window-level error replaces the window's output, node/operations.go:108-113). */
+enum { EK_WIN_OK = 0, EK_WIN_WHERE_ERROR = 1, EK_WIN_HAVING_ERROR = 2, EK_WIN_AGG_ERROR = 3 };
+
+/* Results emitted since the previous poll, segmented by window in trigger order.
+ * Rows of window w are [win_row_offset[w], win_row_offset[w] + win_row_count[w]).
+ * Row order inside a window is unspecified (the reference emits groups in Go map order,
+ * aggregate_operator.go:67-72). Values are 8-byte slots interpreted through the tags. */
+typedef struct {
+    int64_t n_windows;
+    int64_t* win_start;            /* WindowRange.windowStart (window_op.go:688-716 quirks kept) */
+    int64_t* win_end;
+    int64_t* win_row_offset;
+    int64_t* win_row_count;
+    int32_t* win_status;
+    int64_t* win_member_count;     /* debug_membership: events in the window before WHERE        */
+    uint64_t* win_member_hash;     /* debug_membership: sum of ek_mix64(arrival index)           */
+    int64_t n_rows;
+    uint32_t* key;
+    int64_t* agg_value[EK_MAX_AGGS];  /* bit pattern of int64 or double per tag */
+    uint8_t* agg_tag[EK_MAX_AGGS];
+    int32_t n_aggs;
+    int32_t memory;                /* where the arrays live */
+    void* _owner;                  /* engine-private */
+} ek_result;
+
+typedef struct {
+    int64_t records_in;       /* events pushed                                  */
+    int64_t records_late;     /* dropped by the watermark (watermark_op.go:144-155) */
+    int64_t windows_out;      /* windows triggered                              */
+    int64_t rows_out;         /* result rows                                    */
+    double last_batch_device_ms; /* device time of the last push (HIP events)   */
+} ek_stats;
+
+/* Error codes. */
+enum {
+    EK_OK = 0,
+    EK_ERR_INVALID = -1,
+    EK_ERR_UNSUPPORTED = -2,
+    EK_ERR_DEVICE = -3,
+    EK_ERR_NOMEM = -4,
+    EK_ERR_STATE = -5
+};
+
+/* Library / device */
+int ek_abi_version(void);
+int ek_device_count(void);
+
+/* Create an engine instance for a compiled rule on HIP device `device`.
+ * Replaces node.NewWindowOp (window_op.go:93-122) + operator.{FilterOp,AggregateOp,HavingOp}
+ * as wired by planner.buildOps (planner.go:387-446). Plan errors mirror NewEventTimeTrigger
+ * (event_window_trigger.go:35-53), e.g. COUNTWINDOW with event time -> EK_ERR_UNSUPPORTED. */
+int ek_create(const ek_plan* plan, int device, void** out_handle);
+
+/* Ingest one micro-batch (arrival order). Replaces the per-tuple channel ingest of
+ * WatermarkOp (watermark_op.go:118-129) and WindowOperator (event_window_trigger.go:182-196,
+ * window_op.go:339-419). Windows whose end passes the new watermark are triggered and their
+ * GROUP BY results become available to ek_poll_results. */
+int ek_push_batch(void* h, const ek_batch* batch);
+
+/* Take the results produced so far. memory = EK_MEM_HOST copies them to host memory owned by
+ * the engine; EK_MEM_DEVICE hands out device pointers. Valid until ek_release_results. */
+int ek_poll_results(void* h, int32_t memory, ek_result* out);
+int ek_release_results(void* h, ek_result* res);
+
+/* Wait for all work queued on the handle's stream. */
+int ek_sync(void* h);
+/* Use the caller's HIP stream (hipStream_t passed as void*; NULL = handle-owned stream). */
+int ek_set_stream(void* h, void* hip_stream);
+int ek_get_stats(void* h, ek_stats* out);
+const char* ek_last_error(void* h);
+int ek_destroy(void* h);
+
+/* Membership hash used by debug_membership (splitmix64 finaliser). */
+static inline uint64_t ek_mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EKGPU_H */

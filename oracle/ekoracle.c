@@ -1,0 +1,800 @@
+/*
+ * ekoracle.c — CPU ORACLE for parity testing (test infrastructure only; see ekoracle.h).
+ *
+ * Restates, event by event, the reference's operator chain for a windowed GROUP BY rule:
+ *   WatermarkOp       internal/topo/node/watermark_op.go:144-225
+ *   WindowOperator    internal/topo/node/event_window_trigger.go:57-209, window_op.go:194-227,390-418,
+ *                     502-551,553-574,605-739
+ *   FilterOp          internal/topo/operator/filter_operator.go:36-90
+ *   AggregateOp       internal/topo/operator/aggregate_operator.go:34-82
+ *   HavingOp          internal/topo/operator/having_operator.go:32-104
+ *   aggregates        internal/binder/function/funcs_agg.go:28-428, common_array_funcs.go:27-247,
+ *                     function.go:155-171 (check guard), pkg/cast/cast.go:322-420,915-966,
+ *                     github.com/montanaflynn/stats v0.7.1 (Mean/Variance/Percentile/PercentileNearestRank,
+ *                     restated from the library's published source; not vendored in the reference)
+ *   expressions       internal/xsql/valuer.go:574-660 (evalBinaryExpr), 823-1000 (SimpleDataEval)
+ *
+ * Compiled with -ffp-contract=off so that every floating-point operation rounds like Go's.
+ */
+#include "ekoracle.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* Go's time.Time{} (year 1) in Unix ms, used for IsZero() comparisons. */
+#define ZERO_MS (-62135596800000LL)
+/* pkg/timex/time.go:28 Maxtime = 9999-12-31T23:59:59.999999999Z (ms, rounded up) */
+#define MAXT_MS (253402300800000LL)
+
+/* ------------------------------------------------------------------ vectors */
+typedef struct { int64_t* a; int64_t n, cap; } vec64;
+static void v_push(vec64* v, int64_t x) {
+    if (v->n == v->cap) { v->cap = v->cap ? v->cap * 2 : 64; v->a = (int64_t*)realloc(v->a, (size_t)v->cap * 8); }
+    v->a[v->n++] = x;
+}
+static void v_erase_front(vec64* v, int64_t k) {
+    if (k <= 0) return;
+    if (k >= v->n) { v->n = 0; return; }
+    memmove(v->a, v->a + k, (size_t)(v->n - k) * 8);
+    v->n -= k;
+}
+
+/* ------------------------------------------------------------------ time */
+static int64_t floordiv(int64_t a, int64_t b) { int64_t q = a / b; if ((a % b) != 0 && ((a < 0) != (b < 0))) q--; return q; }
+
+int64_t eko_aligned_window_end(int64_t ts_ms, int32_t interval, int32_t unit, int32_t tz_offset_s) {
+    /* window_op.go:194-227 */
+    int64_t off = (int64_t)tz_offset_s * 1000;
+    int64_t local = ts_ms + off;
+    int64_t day0 = floordiv(local, 86400000LL) * 86400000LL;
+    int64_t gap = interval;
+    switch (unit) {
+    case EK_UNIT_DD:
+        return day0 + (int64_t)interval * 86400000LL - off;
+    case EK_UNIT_HH: {
+        int64_t hour = (local - day0) / 3600000LL;
+        if (hour > interval) gap = (int64_t)interval * (hour / interval + 1);
+        return day0 + gap * 3600000LL - off;
+    }
+    case EK_UNIT_MI: {
+        int64_t h0 = floordiv(local, 3600000LL) * 3600000LL;
+        int64_t minute = (local - h0) / 60000LL;
+        if (minute > interval) gap = (int64_t)interval * (minute / interval + 1);
+        return h0 + gap * 60000LL - off;
+    }
+    case EK_UNIT_SS: {
+        int64_t m0 = floordiv(local, 60000LL) * 60000LL;
+        int64_t sec = (local - m0) / 1000LL;
+        if (sec > interval) gap = (int64_t)interval * (sec / interval + 1);
+        return m0 + gap * 1000LL - off;
+    }
+    case EK_UNIT_MS: {
+        int64_t s0 = floordiv(local, 1000LL) * 1000LL;
+        int64_t milli = local - s0;
+        if (milli > interval) gap = (int64_t)interval * (milli / interval + 1);
+        return s0 + gap - off;
+    }
+    default:
+        return ts_ms;
+    }
+}
+
+static int64_t unit_ms(int32_t unit) {
+    /* planner.go:463-478 convertFromDuration */
+    switch (unit) {
+    case EK_UNIT_DD: return 86400000LL;
+    case EK_UNIT_HH: return 3600000LL;
+    case EK_UNIT_MI: return 60000LL;
+    case EK_UNIT_SS: return 1000LL;
+    case EK_UNIT_MS: return 1LL;
+    }
+    return 1000LL;
+}
+
+/* ------------------------------------------------------------------ values */
+enum { V_NULL = 0, V_BOOL = 1, V_I64 = 2, V_F64 = 3, V_ERR = 4 };
+typedef struct { int tag; int64_t i; double f; } val_t;
+
+typedef struct {
+    const ek_plan* p;
+    int64_t n;
+    const void* const* cols;
+    const uint8_t* const* valid;
+} dataset;
+
+static val_t col_val(const dataset* d, int c, int64_t row) {
+    val_t v; v.tag = V_NULL; v.i = 0; v.f = 0;
+    if (c < 0 || c >= d->p->n_columns || !d->cols[c]) return v;
+    if (d->valid && d->valid[c] && !d->valid[c][row]) return v;
+    switch (d->p->column_type[c]) {
+    case EK_COL_I64: v.tag = V_I64; v.i = ((const int64_t*)d->cols[c])[row]; break;
+    case EK_COL_U32: v.tag = V_I64; v.i = ((const uint32_t*)d->cols[c])[row]; break;
+    case EK_COL_F64: v.tag = V_F64; v.f = ((const double*)d->cols[c])[row]; break;
+    }
+    return v;
+}
+
+static val_t mk_bool(int b) { val_t v; v.tag = V_BOOL; v.i = b ? 1 : 0; v.f = 0; return v; }
+static val_t mk_err(void) { val_t v; v.tag = V_ERR; v.i = 0; v.f = 0; return v; }
+static val_t mk_null(void) { val_t v; v.tag = V_NULL; v.i = 0; v.f = 0; return v; }
+
+/* valuer.go:823-1000 SimpleDataEval for the op subset of the plan ISA */
+static val_t simple_eval(val_t l, val_t r, int op) {
+    if (l.tag == V_NULL || r.tag == V_NULL) {
+        switch (op) {
+        case EK_OP_AND: case EK_OP_OR: case EK_OP_EQ: case EK_OP_NEQ: case EK_OP_GT: case EK_OP_GTE:
+        case EK_OP_LT: case EK_OP_LTE:
+            return mk_bool(0);
+        default:
+            return mk_null();
+        }
+    }
+    if (l.tag == V_BOOL) {
+        if (r.tag != V_BOOL) return mk_err();
+        switch (op) {
+        case EK_OP_AND: return mk_bool(l.i && r.i);
+        case EK_OP_OR: return mk_bool(l.i || r.i);
+        case EK_OP_EQ: return mk_bool(l.i == r.i);
+        case EK_OP_NEQ: return mk_bool(l.i != r.i);
+        default: return mk_err();
+        }
+    }
+    if (r.tag == V_BOOL) return mk_err();
+    if (l.tag == V_F64 || r.tag == V_F64) {
+        double a = l.tag == V_F64 ? l.f : (double)l.i;
+        double b = r.tag == V_F64 ? r.f : (double)r.i;
+        val_t v; v.tag = V_F64; v.i = 0;
+        switch (op) {
+        case EK_OP_EQ: return mk_bool(a == b);
+        case EK_OP_NEQ: return mk_bool(a != b);
+        case EK_OP_LT: return mk_bool(a < b);
+        case EK_OP_LTE: return mk_bool(a <= b);
+        case EK_OP_GT: return mk_bool(a > b);
+        case EK_OP_GTE: return mk_bool(a >= b);
+        case EK_OP_ADD: v.f = a + b; return v;
+        case EK_OP_SUB: v.f = a - b; return v;
+        case EK_OP_MUL: v.f = a * b; return v;
+        case EK_OP_DIV: if (b == 0) return mk_err(); v.f = a / b; return v;
+        case EK_OP_MOD: if (b == 0) return mk_err(); v.f = fmod(a, b); return v;
+        default: return mk_err();
+        }
+    }
+    {
+        int64_t a = l.i, b = r.i;
+        val_t v; v.tag = V_I64; v.f = 0;
+        switch (op) {
+        case EK_OP_EQ: return mk_bool(a == b);
+        case EK_OP_NEQ: return mk_bool(a != b);
+        case EK_OP_LT: return mk_bool(a < b);
+        case EK_OP_LTE: return mk_bool(a <= b);
+        case EK_OP_GT: return mk_bool(a > b);
+        case EK_OP_GTE: return mk_bool(a >= b);
+        case EK_OP_ADD: v.i = (int64_t)((uint64_t)a + (uint64_t)b); return v;
+        case EK_OP_SUB: v.i = (int64_t)((uint64_t)a - (uint64_t)b); return v;
+        case EK_OP_MUL: v.i = (int64_t)((uint64_t)a * (uint64_t)b); return v;
+        case EK_OP_DIV: if (b == 0) return mk_err(); v.i = (a == INT64_MIN && b == -1) ? a : a / b; return v;
+        case EK_OP_MOD: if (b == 0) return mk_err(); v.i = (b == -1) ? 0 : a % b; return v;
+        default: return mk_err();
+        }
+    }
+}
+
+/* Postfix evaluation equivalent to the tree walk of valuer.go:574-660 (AND/OR short-circuit on
+ * a decided lhs is reproduced: a false lhs of AND / true lhs of OR wins over an rhs error). */
+static val_t eval_prog(const ek_instr* prog, int n, const dataset* d, int64_t row, const val_t* aggs) {
+    val_t st[EK_MAX_PROG];
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        const ek_instr* in = &prog[k];
+        switch (in->op) {
+        case EK_OP_COL: st[sp++] = col_val(d, in->arg, row); break;
+        case EK_OP_AGG: st[sp++] = aggs ? aggs[in->arg] : mk_null(); break;
+        case EK_OP_CONST_I64: { val_t v; v.tag = V_I64; v.i = in->i64; v.f = 0; st[sp++] = v; } break;
+        case EK_OP_CONST_F64: { val_t v; v.tag = V_F64; v.i = 0; v.f = in->f64; st[sp++] = v; } break;
+        default: {
+            if (sp < 2) return mk_err();
+            val_t r = st[--sp], l = st[--sp], res;
+            if (l.tag == V_ERR) res = l;
+            else if (in->op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mk_bool(0);
+            else if (in->op == EK_OP_OR && l.tag == V_BOOL && l.i) res = mk_bool(1);
+            else if (r.tag == V_ERR) res = r;
+            else res = simple_eval(l, r, in->op);
+            st[sp++] = res;
+        }
+        }
+    }
+    return sp ? st[sp - 1] : mk_null();
+}
+
+/* ------------------------------------------------------------------ aggregates */
+static int cmp_f64(const void* a, const void* b) {
+    double x = *(const double*)a, y = *(const double*)b;
+    /* sort.Float64s order (NaN first); ties keep no particular order (value-equal) */
+    int xn = x != x, yn = y != y;
+    if (xn || yn) return yn - xn;
+    return (x < y) ? -1 : (x > y) ? 1 : 0;
+}
+static int cmp_i64(const void* a, const void* b) {
+    int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return (x < y) ? -1 : (x > y) ? 1 : 0;
+}
+
+typedef struct { int tag; int64_t i; double f; int err; char msg[160]; } agg_out;
+
+static void set_err(agg_out* o, const char* fmt, ...) {
+    va_list ap; va_start(ap, fmt); vsnprintf(o->msg, sizeof o->msg, fmt, ap); va_end(ap);
+    o->err = 1; o->tag = EK_TAG_NULL;
+}
+
+/* vals: typed values of the argument column over the group rows in window order, vnull[i] = 1 if nil */
+static void agg_eval(int fn, int is_float, int64_t n, const int64_t* iv, const double* fv, const uint8_t* vnull,
+                     double param, agg_out* o) {
+    memset(o, 0, sizeof *o);
+    o->tag = EK_TAG_NULL;
+    int64_t cnt = 0, first = -1;
+    for (int64_t k = 0; k < n; ++k) if (!vnull[k]) { if (first < 0) first = k; cnt++; }
+    switch (fn) {
+    case EK_AGG_COUNT_STAR: o->tag = EK_TAG_I64; o->i = n; return;
+    case EK_AGG_COUNT: o->tag = EK_TAG_I64; o->i = cnt; return;        /* getCount */
+    case EK_AGG_SUM:                                                   /* funcs_agg.go:114-143 */
+    case EK_AGG_AVG: {                                                 /* funcs_agg.go:56-86 */
+        if (n == 0 || first < 0) return;                              /* nil */
+        if (!is_float) {
+            int64_t t = 0;
+            for (int64_t k = 0; k < n; ++k) if (!vnull[k]) t = (int64_t)((uint64_t)t + (uint64_t)iv[k]);
+            o->tag = EK_TAG_I64;
+            o->i = (fn == EK_AGG_SUM) ? t : ((t == INT64_MIN && cnt == -1) ? t : t / cnt);
+        } else {
+            double t = 0;
+            for (int64_t k = 0; k < n; ++k) if (!vnull[k]) t += fv[k];
+            o->tag = EK_TAG_F64;
+            o->f = (fn == EK_AGG_SUM) ? t : t / (double)cnt;
+        }
+        return;
+    }
+    case EK_AGG_MIN:
+    case EK_AGG_MAX: {                                                 /* common_array_funcs.go:27-247 */
+        if (first < 0) return;
+        if (!is_float) {
+            int64_t m = iv[first];
+            for (int64_t k = 0; k < n; ++k) if (!vnull[k]) {
+                if (fn == EK_AGG_MAX ? (iv[k] > m) : (iv[k] < m)) m = iv[k];
+            }
+            o->tag = EK_TAG_I64; o->i = m;
+        } else {
+            double m = fv[first];
+            for (int64_t k = 0; k < n; ++k) if (!vnull[k]) {
+                if (fn == EK_AGG_MAX ? (m < fv[k]) : (m > fv[k])) m = fv[k];
+            }
+            o->tag = EK_TAG_F64; o->f = m;
+        }
+        return;
+    }
+    case EK_AGG_STDDEV: case EK_AGG_STDDEVS: case EK_AGG_VAR: case EK_AGG_VARS: {
+        /* cast.ToFloat64Slice(IGNORE_NIL) then stats v0.7.1 _variance: mean = Sum/len (sequential),
+         * Σ (x-m)*(x-m) sequential, / len or / (len-1); empty -> EmptyInputErr -> nil */
+        if (cnt == 0) return;
+        double s = 0;
+        for (int64_t k = 0; k < n; ++k) if (!vnull[k]) s += is_float ? fv[k] : (double)iv[k];
+        double m = s / (double)cnt, v = 0;
+        for (int64_t k = 0; k < n; ++k) if (!vnull[k]) {
+            double x = is_float ? fv[k] : (double)iv[k];
+            double dx = x - m;
+            v += dx * dx;
+        }
+        int sample = (fn == EK_AGG_STDDEVS || fn == EK_AGG_VARS);
+        v = v / (double)(cnt - sample);
+        if (fn == EK_AGG_STDDEV || fn == EK_AGG_STDDEVS) v = sqrt(v);
+        o->tag = EK_TAG_F64; o->f = v;
+        return;
+    }
+    case EK_AGG_MEDIAN: {                                              /* funcs_agg.go:29-55,415-428 */
+        if (n < 1) { o->tag = EK_TAG_I64; o->i = 0; return; }
+        if (vnull[0]) { set_err(o, "<nil> should be number"); return; }
+        if (is_float) {
+            double* a = (double*)malloc((size_t)cnt * 8); int64_t m = 0;
+            for (int64_t k = 0; k < n; ++k) if (!vnull[k]) a[m++] = fv[k];
+            qsort(a, (size_t)m, 8, cmp_f64);
+            if (m % 2 == 1) { o->tag = EK_TAG_F64; o->f = a[m / 2]; }
+            else { o->tag = EK_TAG_F64; o->f = (a[m / 2 - 1] + a[m / 2]) / 2; }
+            free(a);
+        } else {
+            if (cnt != n) { set_err(o, "cannot convert <nil> to int64"); return; } /* ToInt64Slice SAMEKIND */
+            int64_t* a = (int64_t*)malloc((size_t)n * 8);
+            memcpy(a, iv, (size_t)n * 8);
+            qsort(a, (size_t)n, 8, cmp_i64);
+            if (n % 2 == 1) { o->tag = EK_TAG_I64; o->i = a[n / 2]; }
+            else { o->tag = EK_TAG_F64; o->f = (double)(int64_t)((uint64_t)a[n / 2 - 1] + (uint64_t)a[n / 2]) / 2; }
+            free(a);
+        }
+        return;
+    }
+    case EK_AGG_PERCENTILE_CONT:
+    case EK_AGG_PERCENTILE_DISC: {
+        if (cnt == 0) return;                                          /* EmptyInputErr -> nil */
+        double percent = param * 100;
+        double* c = (double*)malloc((size_t)cnt * 8); int64_t m = 0;
+        for (int64_t k = 0; k < n; ++k) if (!vnull[k]) c[m++] = is_float ? fv[k] : (double)iv[k];
+        if (fn == EK_AGG_PERCENTILE_CONT) {
+            /* stats.Percentile v0.7.1 */
+            if (m == 1) { o->tag = EK_TAG_F64; o->f = c[0]; free(c); return; }
+            if (percent <= 0 || percent > 100) { set_err(o, "percentile exec with error: Input is outside of range."); free(c); return; }
+            qsort(c, (size_t)m, 8, cmp_f64);
+            double index = (percent / 100) * (double)m;
+            if (index == (double)(int64_t)index) {
+                int64_t i = (int64_t)index;
+                o->tag = EK_TAG_F64; o->f = c[i - 1];
+            } else if (index > 1) {
+                int64_t i = (int64_t)index;
+                double s = 0; s += c[i - 1]; s += c[i];
+                o->tag = EK_TAG_F64; o->f = s / 2;
+            } else {
+                set_err(o, "percentile exec with error: Input is outside of range.");
+            }
+        } else {
+            /* stats.PercentileNearestRank v0.7.1 */
+            if (percent < 0 || percent > 100) { set_err(o, "PopulationVariance exec with error: Input is outside of range."); free(c); return; }
+            qsort(c, (size_t)m, 8, cmp_f64);
+            if (percent == 100.0) { o->tag = EK_TAG_F64; o->f = c[m - 1]; free(c); return; }
+            int64_t r = (int64_t)ceil((double)m * percent / 100);
+            o->tag = EK_TAG_F64; o->f = (r == 0) ? c[0] : c[r - 1];
+        }
+        free(c);
+        return;
+    }
+    }
+    set_err(o, "unsupported aggregate %d", fn);
+}
+
+int eko_agg_exec(int32_t fn, int32_t col_type, int64_t n, const void* values, const uint8_t* valid,
+                 double param, int64_t* out_value, uint8_t* out_tag, char* err, int32_t err_len) {
+    int is_float = col_type == EK_COL_F64;
+    int64_t* iv = (int64_t*)calloc((size_t)(n ? n : 1), 8);
+    double* fv = (double*)calloc((size_t)(n ? n : 1), 8);
+    uint8_t* nul = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+    for (int64_t k = 0; k < n; ++k) {
+        nul[k] = valid ? !valid[k] : 0;
+        if (is_float) fv[k] = ((const double*)values)[k];
+        else if (col_type == EK_COL_U32) iv[k] = ((const uint32_t*)values)[k];
+        else iv[k] = ((const int64_t*)values)[k];
+    }
+    agg_out o;
+    agg_eval(fn, is_float, n, iv, fv, nul, param, &o);
+    free(iv); free(fv); free(nul);
+    if (o.err) { if (err && err_len > 0) snprintf(err, (size_t)err_len, "%s", o.msg); *out_tag = EK_TAG_NULL; return 1; }
+    *out_tag = (uint8_t)o.tag;
+    if (o.tag == EK_TAG_F64) memcpy(out_value, &o.f, 8); else *out_value = o.i;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ output building */
+typedef struct {
+    vec64 ws, we, roff, rcnt, st, mcnt, mhash, moff, mem;
+    vec64 key;
+    vec64 aval[EK_MAX_AGGS];
+    vec64 atag[EK_MAX_AGGS];
+    char* werr; int64_t werr_cap;
+} outbuf;
+
+/* Evaluate WHERE -> GROUP BY -> aggregates -> HAVING over one emitted window
+ * (filter_operator.go:36-90, aggregate_operator.go:34-82, having_operator.go:32-104,
+ *  project_operator.go:79-207 for the aggregate fields). */
+static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc) {
+    const ek_plan* p = d->p;
+    int64_t w = ob->ws.n;
+    v_push(&ob->ws, wstart);
+    v_push(&ob->we, wend);
+    v_push(&ob->roff, ob->key.n);
+    v_push(&ob->moff, ob->mem.n);
+    uint64_t h = 0;
+    for (int64_t k = 0; k < nc; ++k) { v_push(&ob->mem, content[k]); h += ek_mix64((uint64_t)content[k]); }
+    v_push(&ob->mcnt, nc);
+    v_push(&ob->mhash, (int64_t)h);
+    if (ob->werr_cap <= w) { ob->werr_cap = (w + 1) * 2; ob->werr = (char*)realloc(ob->werr, (size_t)ob->werr_cap * 128); }
+    ob->werr[w * 128] = 0;
+    int status = EK_WIN_OK;
+
+    /* WHERE (after the window in event time: windowPlan.go:82-99) */
+    int64_t* sel = (int64_t*)malloc((size_t)(nc ? nc : 1) * 8);
+    int64_t ns = 0;
+    for (int64_t k = 0; k < nc; ++k) {
+        if (p->n_where <= 0) { sel[ns++] = content[k]; continue; }
+        val_t r = eval_prog(p->where_prog, p->n_where, d, content[k], NULL);
+        if (r.tag == V_ERR) { status = EK_WIN_WHERE_ERROR; snprintf(ob->werr + w * 128, 128, "run Where error: evaluation error"); break; }
+        if (r.tag == V_BOOL) { if (r.i) sel[ns++] = content[k]; }
+        else if (r.tag != V_NULL) { status = EK_WIN_WHERE_ERROR; snprintf(ob->werr + w * 128, 128, "run Where error: invalid condition that returns non-bool value"); break; }
+    }
+    int64_t rows_before = ob->key.n;
+    if (status == EK_WIN_OK && ns > 0) {
+        /* GROUP BY key (first-appearance order; output order is unspecified in the reference) */
+        int64_t ng = 0;
+        int64_t* gstart = (int64_t*)malloc((size_t)ns * 8);  /* group id per selected row */
+        int64_t* gkey = (int64_t*)malloc((size_t)ns * 8);
+        int64_t* gcount = (int64_t*)calloc((size_t)ns, 8);
+        int64_t* rowg = (int64_t*)malloc((size_t)ns * 8);
+        if (p->key_column >= 0) {
+            /* open-addressing map key -> group */
+            int64_t cap = 16; while (cap < ns * 2) cap <<= 1;
+            int64_t* slot = (int64_t*)malloc((size_t)cap * 8);
+            for (int64_t k = 0; k < cap; ++k) slot[k] = -1;
+            for (int64_t k = 0; k < ns; ++k) {
+                val_t kv = col_val(d, p->key_column, sel[k]);
+                int64_t key = kv.tag == V_NULL ? -1 : kv.i;
+                uint64_t hh = ek_mix64((uint64_t)key) & (uint64_t)(cap - 1);
+                while (slot[hh] >= 0 && gkey[slot[hh]] != key) hh = (hh + 1) & (uint64_t)(cap - 1);
+                if (slot[hh] < 0) { slot[hh] = ng; gkey[ng] = key; ng++; }
+                rowg[k] = slot[hh];
+                gcount[slot[hh]]++;
+            }
+            free(slot);
+        } else {
+            ng = 1; gkey[0] = 0; gcount[0] = ns;
+            for (int64_t k = 0; k < ns; ++k) rowg[k] = 0;
+        }
+        /* bucket rows per group preserving order */
+        int64_t* goff = (int64_t*)calloc((size_t)ng + 1, 8);
+        for (int64_t g = 0; g < ng; ++g) goff[g + 1] = goff[g] + gcount[g];
+        int64_t* fill = (int64_t*)calloc((size_t)ng, 8);
+        int64_t* grows = (int64_t*)malloc((size_t)ns * 8);
+        for (int64_t k = 0; k < ns; ++k) { int64_t g = rowg[k]; grows[goff[g] + fill[g]++] = sel[k]; }
+        int64_t* iv = (int64_t*)malloc((size_t)ns * 8);
+        double* fv = (double*)malloc((size_t)ns * 8);
+        uint8_t* nul = (uint8_t*)malloc((size_t)ns);
+        val_t aggv[EK_MAX_AGGS];
+        agg_out ao[EK_MAX_AGGS];
+        for (int64_t g = 0; g < ng && status == EK_WIN_OK; ++g) {
+            int64_t gn = goff[g + 1] - goff[g];
+            const int64_t* rows = grows + goff[g];
+            for (int a = 0; a < p->n_aggs; ++a) {
+                const ek_agg_spec* as = &p->aggs[a];
+                int c = as->column;
+                int is_float = (c >= 0 && c < p->n_columns) ? (p->column_type[c] == EK_COL_F64) : 0;
+                for (int64_t k = 0; k < gn; ++k) {
+                    if (as->fn == EK_AGG_COUNT_STAR) { nul[k] = 0; iv[k] = 0; continue; }
+                    val_t v = col_val(d, c, rows[k]);
+                    nul[k] = v.tag == V_NULL;
+                    iv[k] = v.i; fv[k] = v.f;
+                }
+                agg_eval(as->fn, is_float, gn, iv, fv, nul, as->param, &ao[a]);
+                if (ao[a].err) {
+                    status = EK_WIN_AGG_ERROR;
+                    snprintf(ob->werr + w * 128, 128, "run Select error: %s", ao[a].msg);
+                    break;
+                }
+                aggv[a].tag = ao[a].tag == EK_TAG_NULL ? V_NULL : (ao[a].tag == EK_TAG_I64 ? V_I64 : V_F64);
+                aggv[a].i = ao[a].i; aggv[a].f = ao[a].f;
+            }
+            if (status != EK_WIN_OK) break;
+            if (p->n_having > 0) {
+                val_t r = eval_prog(p->having_prog, p->n_having, d, rows[0], aggv);
+                if (r.tag != V_BOOL) {
+                    status = EK_WIN_HAVING_ERROR;
+                    snprintf(ob->werr + w * 128, 128, r.tag == V_ERR ? "run Having error: evaluation error"
+                                                                      : "run Having error: invalid condition that returns non-bool value");
+                    break;
+                }
+                if (!r.i) continue;
+            }
+            v_push(&ob->key, gkey[g]);
+            for (int a = 0; a < p->n_aggs; ++a) {
+                int64_t bits = ao[a].i;
+                if (ao[a].tag == EK_TAG_F64) memcpy(&bits, &ao[a].f, 8);
+                v_push(&ob->aval[a], bits);
+                v_push(&ob->atag[a], ao[a].tag);
+            }
+        }
+        free(gstart); free(gkey); free(gcount); free(rowg); free(goff); free(fill); free(grows);
+        free(iv); free(fv); free(nul);
+    }
+    if (status != EK_WIN_OK) {
+        /* the window's output is replaced by the error */
+        ob->key.n = rows_before;
+        for (int a = 0; a < p->n_aggs; ++a) { ob->aval[a].n = rows_before; ob->atag[a].n = rows_before; }
+    }
+    free(sel);
+    v_push(&ob->rcnt, ob->key.n - rows_before);
+    v_push(&ob->st, status);
+}
+
+/* ------------------------------------------------------------------ window operator (event time) */
+typedef struct {
+    const dataset* d;
+    outbuf* ob;
+    int wtype;
+    int64_t L, I, D;           /* ms */
+    int32_t raw_interval, unit, tz;
+    vec64 inputs;              /* event indices, release order */
+    int has_trigger; int64_t trigger_time;
+    int64_t next_end, prev_end; /* prev_end ZERO_MS = IsZero */
+    vec64 trigger_ts, delay_ts;
+    int last_ticked;
+    int64_t* ts;
+    vec64 content;
+} winop;
+
+static int64_t ev_ts(const winop* o, int64_t e) { return o->ts[e]; }
+
+/* window_op.go:553-574 */
+static int is_time_related(const winop* o) {
+    switch (o->wtype) {
+    case EK_WINDOW_SLIDING: return o->D > 0;
+    case EK_WINDOW_TUMBLING: case EK_WINDOW_HOPPING: case EK_WINDOW_SESSION: return 1;
+    }
+    return 0;
+}
+static int is_overlap(const winop* o) { return o->wtype == EK_WINDOW_HOPPING || o->wtype == EK_WINDOW_SLIDING; }
+
+/* window_op.go:605-655 handleInputs; event time => calDelta == 0 once triggerTime is set (it is set by the
+ * first event, event_window_trigger.go:187-189), else MaxInt16 ns which is invisible at ms resolution. */
+static void handle_inputs(winop* o, int64_t right, int64_t* keep_from) {
+    int64_t length = o->L + o->D;
+    int64_t left = right - length;
+    int64_t nextleft = -1;
+    int all_discarded = 0;
+    int ov = is_overlap(o), tr = is_time_related(o);
+    o->content.n = 0;
+    for (int64_t i = 0; i < o->inputs.n; ++i) {
+        int64_t t = ev_ts(o, o->inputs.a[i]);
+        if (ov && !all_discarded) {
+            if (t < left) continue;
+        }
+        all_discarded = 1;
+        int meet = tr ? (t < right) : (t <= right);
+        if (meet) {
+            v_push(&o->content, o->inputs.a[i]);
+            if (nextleft < 0 && ov) nextleft = i;
+        } else {
+            if (nextleft < 0 && !ov) nextleft = i;
+        }
+    }
+    *keep_from = nextleft < 0 ? o->inputs.n : nextleft;
+}
+
+/* window_op.go:675-721 scan */
+static void scan(winop* o, int64_t t, int64_t length, int is_first_part) {
+    int64_t keep_from;
+    handle_inputs(o, t, &keep_from);
+    int64_t tt = o->has_trigger ? o->trigger_time : ZERO_MS;
+    int64_t ws = 0;
+    switch (o->wtype) {
+    case EK_WINDOW_TUMBLING: case EK_WINDOW_SESSION: ws = tt; break;
+    case EK_WINDOW_HOPPING: ws = tt - o->I; break;
+    case EK_WINDOW_SLIDING: ws = t - length; break;
+    }
+    if (ws <= 0) ws = t - length;
+    int64_t we = t;
+    if (!is_first_part) { ws = 0; we = 0; } /* WindowRange left unset (delayed sliding, no send-twice) */
+    emit_window(o->d, o->ob, ws, we, o->content.a, o->content.n);
+    v_erase_front(&o->inputs, keep_from);
+    o->trigger_time = t; o->has_trigger = 1;
+}
+
+/* event_window_trigger.go:211-219 */
+static int64_t earliest(const winop* o, int64_t start, int64_t end) {
+    int64_t m = MAXT_MS;
+    for (int64_t i = 0; i < o->inputs.n; ++i) {
+        int64_t t = ev_ts(o, o->inputs.a[i]);
+        if (t > start && t <= end && t < m) m = t;
+    }
+    return m;
+}
+
+/* event_window_trigger.go:57-75 */
+static int64_t next_window(const winop* o, int64_t current, int64_t wm) {
+    switch (o->wtype) {
+    case EK_WINDOW_TUMBLING: case EK_WINDOW_HOPPING: {
+        int64_t interval = o->wtype == EK_WINDOW_TUMBLING ? o->L : o->I;
+        if (current != ZERO_MS) return current + interval;
+        int64_t nt = earliest(o, ZERO_MS, wm);
+        if (nt == MAXT_MS) return nt;
+        return eko_aligned_window_end(nt, o->raw_interval, o->unit, o->tz);
+    }
+    case EK_WINDOW_SLIDING:
+        return earliest(o, current, wm);
+    }
+    return MAXT_MS;
+}
+
+/* event_window_trigger.go:77-110 */
+static int64_t next_session(const winop* o, int64_t now, int* ticked) {
+    *ticked = 0;
+    if (o->inputs.n > 0) {
+        int64_t timeout = o->I, duration = o->L;
+        int64_t et = ev_ts(o, o->inputs.a[0]);
+        int64_t tick = eko_aligned_window_end(et, o->raw_interval, o->unit, o->tz);
+        int64_t p = ZERO_MS;
+        for (int64_t i = 0; i < o->inputs.n; ++i) {
+            int64_t t = ev_ts(o, o->inputs.a[i]);
+            int64_t r = MAXT_MS;
+            if (p != ZERO_MS && t - p > timeout) r = p + timeout;
+            if (t > tick) {
+                if (tick - duration > et && tick < r) { r = tick; *ticked = 1; }
+                tick = tick + duration;
+            }
+            if (r < MAXT_MS) return r;
+            p = t;
+        }
+        if (p != ZERO_MS && now - p > timeout) return p + timeout;
+    }
+    *ticked = 0;
+    return MAXT_MS;
+}
+
+static int match_trigger(const winop* o, int64_t e) {
+    const ek_plan* p = o->d->p;
+    if (p->n_trigger <= 0 || o->wtype != EK_WINDOW_SLIDING) return 1;
+    val_t r = eval_prog(p->trigger_prog, p->n_trigger, o->d, e, NULL);
+    return r.tag == V_BOOL && r.i; /* window_op.go:741-768: nil/error/non-bool -> false */
+}
+
+/* event_window_trigger.go:182-196 (EventRow branch) */
+static void win_on_event(winop* o, int64_t e) {
+    if (!o->has_trigger) { o->has_trigger = 1; o->trigger_time = ev_ts(o, e); }
+    if (o->wtype == EK_WINDOW_SLIDING && match_trigger(o, e)) v_push(&o->trigger_ts, ev_ts(o, e));
+    v_push(&o->inputs, e);
+}
+
+/* event_window_trigger.go:124-180 (WatermarkTuple branch) */
+static void win_on_watermark(winop* o, int64_t wm) {
+    if (o->wtype == EK_WINDOW_SLIDING) {
+        while (o->delay_ts.n > 0 && wm >= o->delay_ts.a[0]) {
+            scan(o, o->delay_ts.a[0], o->D, 0);
+            v_erase_front(&o->delay_ts, 1);
+        }
+    }
+    int64_t we = o->next_end;
+    int ticked = 0;
+    if (we == MAXT_MS || o->wtype == EK_WINDOW_SESSION || o->wtype == EK_WINDOW_SLIDING) {
+        if (o->wtype == EK_WINDOW_SESSION) we = next_session(o, wm, &ticked);
+        else we = next_window(o, o->prev_end, wm);
+    }
+    while (we != ZERO_MS && we <= wm) {
+        if (o->wtype == EK_WINDOW_SESSION && !o->last_ticked && o->inputs.n > 0) {
+            o->trigger_time = ev_ts(o, o->inputs.a[0]); o->has_trigger = 1;
+        }
+        if (o->wtype == EK_WINDOW_SLIDING) {
+            while (o->trigger_ts.n > 0 && o->trigger_ts.a[0] <= wm) {
+                if (o->D > 0) v_push(&o->delay_ts, o->trigger_ts.a[0] + o->D);
+                else scan(o, o->trigger_ts.a[0], o->L + o->D, 1);
+                v_erase_front(&o->trigger_ts, 1);
+            }
+        } else {
+            scan(o, we, o->L + o->D, 1);
+        }
+        o->prev_end = we;
+        o->last_ticked = ticked;
+        if (o->wtype == EK_WINDOW_SESSION) we = next_session(o, wm, &ticked);
+        else we = next_window(o, o->prev_end, wm);
+    }
+    o->next_end = we;
+}
+
+/* ------------------------------------------------------------------ driver */
+static void set_status(eko_output* out, int st, const char* msg) {
+    out->status = st;
+    snprintf(out->error, sizeof out->error, "%s", msg);
+}
+
+static int64_t* take(vec64* v) { int64_t* a = v->a; v->a = NULL; v->n = v->cap = 0; return a ? a : (int64_t*)calloc(1, 8); }
+
+int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity, eko_output* out) {
+    memset(out, 0, sizeof *out);
+    if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
+    if (p->n_aggs < 0 || p->n_aggs > EK_MAX_AGGS) { set_status(out, EK_ERR_INVALID, "bad n_aggs"); return out->status; }
+    dataset d = { p, n, columns, validity };
+    outbuf ob; memset(&ob, 0, sizeof ob);
+
+    if (p->is_event_time) {
+        /* NewEventTimeTrigger (event_window_trigger.go:35-53) */
+        if (p->window_type == EK_WINDOW_COUNT || p->window_type > EK_WINDOW_COUNT || p->window_type < 0) {
+            set_status(out, EK_ERR_UNSUPPORTED, "unsupported window type"); return out->status;
+        }
+        if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "event time requires a timestamp column"); return out->status; }
+        int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
+        for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
+        winop o; memset(&o, 0, sizeof o);
+        o.d = &d; o.ob = &ob; o.wtype = p->window_type; o.ts = ts;
+        int64_t u = unit_ms(p->time_unit);
+        o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = (int64_t)p->delay * u;
+        o.raw_interval = (p->window_type == EK_WINDOW_HOPPING) ? p->interval : p->length; /* planner.go:394-400 */
+        o.unit = p->time_unit; o.tz = p->tz_offset_s;
+        o.next_end = MAXT_MS; o.prev_end = ZERO_MS;
+
+        /* WatermarkOp (single stream) watermark_op.go:54-67,144-225 */
+        int64_t lateTol = p->late_tolerance_ms;
+        int64_t stream_wm = ZERO_MS + lateTol;
+        int64_t last_wm = ZERO_MS;
+        vec64 buf; memset(&buf, 0, sizeof buf);
+        for (int64_t i = 0; i < n; ++i) {
+            int64_t t = ts[i];
+            if (t > stream_wm) stream_wm = t;
+            if (!(t >= last_wm)) { out->records_late++; continue; }
+            /* insert after all events with ts <= t (sort.Search(After)) */
+            int64_t lo = 0, hi = buf.n;
+            while (lo < hi) { int64_t mid = (lo + hi) / 2; if (ts[buf.a[mid]] > t) hi = mid; else lo = mid + 1; }
+            v_push(&buf, 0);
+            memmove(buf.a + lo + 1, buf.a + lo, (size_t)(buf.n - 1 - lo) * 8);
+            buf.a[lo] = i;
+            int64_t wm = stream_wm - lateTol;
+            if (wm > last_wm) {
+                if (wm >= ts[buf.a[0]]) {
+                    int64_t c = buf.n;
+                    for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
+                    for (int64_t k = 0; k < c; ++k) win_on_event(&o, buf.a[k]);
+                    v_erase_front(&buf, c);
+                }
+                win_on_watermark(&o, wm);
+                last_wm = wm;
+            }
+        }
+        free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
+        free(ts);
+    } else {
+        if (p->window_type != EK_WINDOW_COUNT) {
+            set_status(out, EK_ERR_UNSUPPORTED, "processing-time oracle supports COUNTWINDOW only"); return out->status;
+        }
+        /* window_op.go:390-418 + TupleList 502-551; CountInterval defaults to CountLength (window_op.go:100-103) */
+        int64_t len = p->length, itv = p->interval > 0 ? p->interval : p->length;
+        if (len <= 0) { set_status(out, EK_ERR_INVALID, "Window size should not be less than zero."); return out->status; }
+        vec64 inputs; memset(&inputs, 0, sizeof inputs);
+        int64_t msg = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            v_push(&inputs, i);
+            msg++;
+            if (msg % itv != 0) continue;
+            msg = 0;
+            if (inputs.n >= len) {
+                emit_window(&d, &ob, 0, 0, inputs.a + (inputs.n - len), len);  /* wall-clock range: not comparable */
+                v_erase_front(&inputs, inputs.n - len + 1);
+            }
+        }
+        free(inputs.a);
+    }
+
+    out->r.n_windows = ob.ws.n;
+    out->r.n_rows = ob.key.n;
+    out->r.n_aggs = p->n_aggs;
+    out->r.memory = EK_MEM_HOST;
+    v_push(&ob.moff, ob.mem.n);
+    out->r.win_start = take(&ob.ws);
+    out->r.win_end = take(&ob.we);
+    out->r.win_row_offset = take(&ob.roff);
+    out->r.win_row_count = take(&ob.rcnt);
+    out->r.win_member_count = take(&ob.mcnt);
+    out->r.win_member_hash = (uint64_t*)take(&ob.mhash);
+    {
+        int64_t* st = take(&ob.st);
+        out->r.win_status = (int32_t*)calloc((size_t)(out->r.n_windows ? out->r.n_windows : 1), 4);
+        for (int64_t w = 0; w < out->r.n_windows; ++w) out->r.win_status[w] = (int32_t)st[w];
+        free(st);
+    }
+    {
+        int64_t* k = take(&ob.key);
+        out->r.key = (uint32_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 4);
+        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.key[r] = (uint32_t)k[r];
+        free(k);
+    }
+    for (int a = 0; a < p->n_aggs; ++a) {
+        out->r.agg_value[a] = take(&ob.aval[a]);
+        int64_t* t = take(&ob.atag[a]);
+        out->r.agg_tag[a] = (uint8_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 1);
+        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.agg_tag[a][r] = (uint8_t)t[r];
+        free(t);
+    }
+    out->member_offset = take(&ob.moff);
+    out->members = take(&ob.mem);
+    out->win_error = ob.werr ? ob.werr : (char*)calloc(1, 128);
+    return 0;
+}
+
+void eko_free(eko_output* o) {
+    if (!o) return;
+    free(o->r.win_start); free(o->r.win_end); free(o->r.win_row_offset); free(o->r.win_row_count);
+    free(o->r.win_status); free(o->r.win_member_count); free(o->r.win_member_hash); free(o->r.key);
+    for (int a = 0; a < EK_MAX_AGGS; ++a) { free(o->r.agg_value[a]); free(o->r.agg_tag[a]); }
+    free(o->member_offset); free(o->members); free(o->win_error);
+    memset(o, 0, sizeof *o);
+}

@@ -1,0 +1,106 @@
+"""Pin the CPU oracle against the reference's own known-answer tests (tests/golden/*.json)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ekgpu import abi as A
+from ekgpu.rule import compile_rule
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FN = {"avg": A.EK_AGG_AVG, "max": A.EK_AGG_MAX, "min": A.EK_AGG_MIN, "stddev": A.EK_AGG_STDDEV,
+      "stddevs": A.EK_AGG_STDDEVS, "var": A.EK_AGG_VAR, "vars": A.EK_AGG_VARS, "sum": A.EK_AGG_SUM,
+      "count": A.EK_AGG_COUNT, "count_star": A.EK_AGG_COUNT_STAR,
+      "percentile_cont": A.EK_AGG_PERCENTILE_CONT, "percentile_disc": A.EK_AGG_PERCENTILE_DISC}
+TYPES = {"i64": A.EK_COL_I64, "f64": A.EK_COL_F64}
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def _check(got, exp):
+    if exp is None:
+        assert got is None
+        return
+    t, v = exp
+    if t == "i64":
+        assert isinstance(got, int) and got == v
+    else:
+        assert isinstance(got, float) and got == v  # bit-exact: same IEEE ops as Go
+
+
+@pytest.mark.parametrize("case", _load("kat_functions.json")["agg_exec"], ids=lambda c: c["case"])
+def test_agg_exec_kat(oracle, case):
+    for fname, exp in case["expect"].items():
+        got = oracle.agg_exec(FN[fname], TYPES[case["type"]], case["values"], case["valid"])
+        _check(got, exp)
+
+
+@pytest.mark.parametrize("case", _load("kat_functions.json")["percentile"], ids=lambda c: c["case"])
+def test_percentile_kat(oracle, case):
+    for fname, exp in case["expect"].items():
+        got = oracle.agg_exec(FN[fname], TYPES[case["type"]], case["values"], case["valid"], case["p"])
+        _check(got, exp)
+
+
+@pytest.mark.parametrize("case", _load("kat_functions.json")["median"], ids=lambda c: c["case"])
+def test_median_kat(oracle, case):
+    got = oracle.agg_exec(A.EK_AGG_MEDIAN, TYPES[case["type"]], case["values"])
+    _check(got, case["expect"])
+
+
+@pytest.mark.parametrize("case", _load("kat_functions.json")["project_agg"], ids=lambda c: c["case"])
+def test_project_agg_kat(oracle, case):
+    for fname, exp in case["expect"].items():
+        got = oracle.agg_exec(FN[fname], TYPES[case["type"]], case["values"], case["valid"])
+        _check(got, exp)
+
+
+def test_percentile_bounds_errors(oracle):
+    # stats v0.7.1 BoundsErr surfaced with the reference's messages (funcs_agg.go:326,362)
+    with pytest.raises(ValueError, match="percentile exec with error: Input is outside of range."):
+        oracle.agg_exec(A.EK_AGG_PERCENTILE_CONT, A.EK_COL_F64, [1.0, 2.0], None, 1.5)
+    with pytest.raises(ValueError, match="Input is outside of range."):
+        oracle.agg_exec(A.EK_AGG_PERCENTILE_DISC, A.EK_COL_F64, [1.0, 2.0], None, -0.1)
+    # n == 1 returns the element before the bounds check (stats.Percentile)
+    assert oracle.agg_exec(A.EK_AGG_PERCENTILE_CONT, A.EK_COL_F64, [7.0], None, 5.0) == 7.0
+
+
+def test_alignment_kat(oracle):
+    g = _load("kat_alignment.json")
+    for c in g["cases"]:
+        got = oracle.aligned_window_end(g["ts"], c["interval"], A.UNIT_BY_NAME[c["unit"]], g["tz_offset_s"])
+        assert got == c["end"], c
+
+
+def _stream_cols(s):
+    rows = np.array(s["rows"], dtype=object)
+    return [np.array(rows[:, 0], dtype=np.int64), np.array(rows[:, 1], dtype=np.int64),
+            np.array(rows[:, 2], dtype=np.uint32), np.array(rows[:, 3], dtype=np.float64)]
+
+
+SCHEMA = {"ts": "bigint", "size": "bigint", "color": "key", "temp": "float"}
+
+
+@pytest.mark.parametrize("case", _load("kat_window_rules.json")["tests"], ids=lambda c: c["name"])
+def test_window_rule_kat(oracle, case):
+    g = _load("kat_window_rules.json")
+    cols = _stream_cols(g["streams"][case["stream"]])
+    rule = compile_rule(case["sql"], SCHEMA, is_event_time=True, late_tolerance_ms=1000, num_keys=4)
+    run = oracle.run(rule.plan, cols)
+    assert len(run.windows) == case["windows_out"]
+    assert run.records_late == case["late"]
+    outs = [(w, run.members[i]) for i, w in enumerate(run.windows) if len(w.keys) > 0]
+    assert len(outs) == len(case["outputs"])
+    where_sizes = cols[1]
+    for (w, members), exp in zip(outs, case["outputs"]):
+        kept = [int(m) for m in members]
+        if "WHERE size > 2" in case["sql"]:
+            kept = [m for m in kept if where_sizes[m] > 2]
+        assert sorted(kept) == sorted(exp["members"])
+        assert w.value(0, 0) == len(exp["members"])  # count(*)
+        if "window_start" in exp:
+            assert w.start == exp["window_start"] and w.end == exp["window_end"]
