@@ -1,0 +1,197 @@
+// ek_device.h — device-side plan descriptor and helpers shared by the gfx950 kernels.
+//
+// Semantics restated from the reference:
+//   expression evaluation      internal/xsql/valuer.go:574-660 (evalBinaryExpr), :823-1000 (SimpleDataEval)
+//   aggregate finalisation     internal/binder/function/funcs_agg.go:28-297, common_array_funcs.go:27-247
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ekgpu.h"
+
+namespace ek {
+
+constexpr int kBlock = 256;       // 4 wave64s per workgroup
+constexpr int kMaxVC = 8;         // value columns referenced by aggregates
+
+// fields kept per (pane, key) in the pane-partial state and per key in LDS tables
+enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32 };
+
+struct DPlan {
+    int32_t n_columns;
+    int32_t col_type[EK_MAX_COLUMNS];
+    int32_t ts_col;
+    int32_t key_col;
+    uint32_t num_keys;
+    int32_t n_where, n_having, n_trigger;
+    ek_instr where_prog[EK_MAX_PROG];
+    ek_instr having_prog[EK_MAX_PROG];
+    ek_instr trigger_prog[EK_MAX_PROG];
+    int32_t n_vc;                 // distinct value columns used by aggregates
+    int32_t vc_col[kMaxVC];       // -> plan column
+    int32_t vc_flags[kMaxVC];     // NEED_*
+    int32_t vc_is_float[kMaxVC];
+    int32_t n_aggs;
+    int32_t agg_fn[EK_MAX_AGGS];
+    int32_t agg_vc[EK_MAX_AGGS];  // -1 for count(*)
+    double agg_p[EK_MAX_AGGS];
+};
+
+// Columns of one micro-batch (device pointers).
+struct DBatch {
+    const void* col[EK_MAX_COLUMNS];
+    const uint8_t* valid[EK_MAX_COLUMNS];
+    int64_t n;
+};
+
+// Pane-partial state: SoA field arrays of [slots * K] entries.
+struct DState {
+    int64_t* cnt;                 // count(*) of rows passing WHERE
+    int64_t* vcnt[kMaxVC];        // non-nil count per value column
+    int64_t* sum[kMaxVC];         // i64 sum or f64 bits
+    int64_t* mn[kMaxVC];          // i64 or f64 bits
+    int64_t* mx[kMaxVC];
+    double* m2[kMaxVC];           // Σ (x - mean)^2 (two-pass per partial, Chan merge across partials)
+    double* fsum[kMaxVC];         // f64 sum of an int column (for var on int columns)
+    int64_t K;                    // keys per slot (padded)
+};
+
+// ---------------------------------------------------------------- ordered bits for f64 min/max
+__device__ __forceinline__ uint64_t f64_to_ord(double d) {
+    uint64_t u = (uint64_t)__double_as_longlong(d);
+    return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord_to_f64(uint64_t o) {
+    uint64_t u = (o & 0x8000000000000000ull) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+    return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ uint64_t i64_to_ord(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ull; }
+__device__ __forceinline__ int64_t ord_to_i64(uint64_t o) { return (int64_t)(o ^ 0x8000000000000000ull); }
+
+// ---------------------------------------------------------------- column access
+__device__ __forceinline__ bool col_valid(const DBatch& b, int c, int64_t i) {
+    return b.valid[c] == nullptr || b.valid[c][i] != 0;
+}
+__device__ __forceinline__ int64_t col_i64(const DPlan& p, const DBatch& b, int c, int64_t i) {
+    return p.col_type[c] == EK_COL_U32 ? (int64_t)((const uint32_t*)b.col[c])[i] : ((const int64_t*)b.col[c])[i];
+}
+__device__ __forceinline__ double col_f64(const DBatch& b, int c, int64_t i) { return ((const double*)b.col[c])[i]; }
+
+// ---------------------------------------------------------------- expression interpreter
+enum : int { V_NULL = 0, V_BOOL = 1, V_I64 = 2, V_F64 = 3, V_ERR = 4 };
+struct Val {
+    int tag;
+    int64_t i;
+    double f;
+};
+__device__ __forceinline__ Val mkb(bool b) { return Val{V_BOOL, b ? 1 : 0, 0.0}; }
+
+// valuer.go:823-1000 SimpleDataEval over the plan ISA
+__device__ inline Val simple_eval(Val l, Val r, int op) {
+    if (l.tag == V_NULL || r.tag == V_NULL) {
+        if (op >= EK_OP_EQ && op <= EK_OP_OR) return mkb(false);
+        return Val{V_NULL, 0, 0.0};
+    }
+    if (l.tag == V_BOOL || r.tag == V_BOOL) {
+        if (l.tag != V_BOOL || r.tag != V_BOOL) return Val{V_ERR, 0, 0.0};
+        switch (op) {
+        case EK_OP_AND: return mkb(l.i && r.i);
+        case EK_OP_OR: return mkb(l.i || r.i);
+        case EK_OP_EQ: return mkb(l.i == r.i);
+        case EK_OP_NEQ: return mkb(l.i != r.i);
+        default: return Val{V_ERR, 0, 0.0};
+        }
+    }
+    if (l.tag == V_F64 || r.tag == V_F64) {
+        double a = l.tag == V_F64 ? l.f : (double)l.i;
+        double c = r.tag == V_F64 ? r.f : (double)r.i;
+        switch (op) {
+        case EK_OP_EQ: return mkb(a == c);
+        case EK_OP_NEQ: return mkb(a != c);
+        case EK_OP_LT: return mkb(a < c);
+        case EK_OP_LTE: return mkb(a <= c);
+        case EK_OP_GT: return mkb(a > c);
+        case EK_OP_GTE: return mkb(a >= c);
+        case EK_OP_ADD: return Val{V_F64, 0, __dadd_rn(a, c)};
+        case EK_OP_SUB: return Val{V_F64, 0, __dsub_rn(a, c)};
+        case EK_OP_MUL: return Val{V_F64, 0, __dmul_rn(a, c)};
+        case EK_OP_DIV: return c == 0 ? Val{V_ERR, 0, 0.0} : Val{V_F64, 0, __ddiv_rn(a, c)};
+        case EK_OP_MOD: return c == 0 ? Val{V_ERR, 0, 0.0} : Val{V_F64, 0, fmod(a, c)};
+        default: return Val{V_ERR, 0, 0.0};
+        }
+    }
+    int64_t a = l.i, c = r.i;
+    switch (op) {
+    case EK_OP_EQ: return mkb(a == c);
+    case EK_OP_NEQ: return mkb(a != c);
+    case EK_OP_LT: return mkb(a < c);
+    case EK_OP_LTE: return mkb(a <= c);
+    case EK_OP_GT: return mkb(a > c);
+    case EK_OP_GTE: return mkb(a >= c);
+    case EK_OP_ADD: return Val{V_I64, (int64_t)((uint64_t)a + (uint64_t)c), 0.0};
+    case EK_OP_SUB: return Val{V_I64, (int64_t)((uint64_t)a - (uint64_t)c), 0.0};
+    case EK_OP_MUL: return Val{V_I64, (int64_t)((uint64_t)a * (uint64_t)c), 0.0};
+    case EK_OP_DIV: return c == 0 ? Val{V_ERR, 0, 0.0} : Val{V_I64, (a == INT64_MIN && c == -1) ? a : a / c, 0.0};
+    case EK_OP_MOD: return c == 0 ? Val{V_ERR, 0, 0.0} : Val{V_I64, (c == -1) ? 0 : a % c, 0.0};
+    default: return Val{V_ERR, 0, 0.0};
+    }
+}
+
+// Postfix program over one row (aggs != nullptr for HAVING). Mirrors evalBinaryExpr's
+// short-circuit: a decided lhs of AND/OR wins over an error on the rhs.
+__device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, const DBatch* b, int64_t row,
+                                const Val* aggs) {
+    Val st[16];
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        const ek_instr in = prog[k];
+        if (in.op == EK_OP_COL) {
+            int c = in.arg;
+            Val v{V_NULL, 0, 0.0};
+            if (b && col_valid(*b, c, row)) {
+                if (p.col_type[c] == EK_COL_F64) v = Val{V_F64, 0, col_f64(*b, c, row)};
+                else v = Val{V_I64, col_i64(p, *b, c, row), 0.0};
+            }
+            st[sp++] = v;
+        } else if (in.op == EK_OP_AGG) {
+            st[sp++] = aggs ? aggs[in.arg] : Val{V_NULL, 0, 0.0};
+        } else if (in.op == EK_OP_CONST_I64) {
+            st[sp++] = Val{V_I64, in.i64, 0.0};
+        } else if (in.op == EK_OP_CONST_F64) {
+            st[sp++] = Val{V_F64, 0, in.f64};
+        } else {
+            Val r = st[--sp], l = st[--sp], res;
+            if (l.tag == V_ERR) res = l;
+            else if (in.op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mkb(false);
+            else if (in.op == EK_OP_OR && l.tag == V_BOOL && l.i) res = mkb(true);
+            else if (r.tag == V_ERR) res = r;
+            else res = simple_eval(l, r, in.op);
+            st[sp++] = res;
+        }
+    }
+    return sp ? st[sp - 1] : Val{V_NULL, 0, 0.0};
+}
+
+// WHERE decision: 1 keep, 0 drop, -1 error (filter_operator.go:63-77: nil -> drop, non-bool -> error)
+__device__ __forceinline__ int where_decide(const DPlan& p, const DBatch& b, int64_t row) {
+    if (p.n_where <= 0) return 1;
+    Val v = eval_prog(p.where_prog, p.n_where, p, &b, row, nullptr);
+    if (v.tag == V_BOOL) return v.i ? 1 : 0;
+    if (v.tag == V_NULL) return 0;
+    return -1;
+}
+
+__device__ __forceinline__ uint64_t d_mix64(uint64_t x) {  // == ek_mix64 (ekgpu.h)
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ int64_t floordiv64(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b) != 0 && ((a < 0) != (b < 0))) q--;
+    return q;
+}
+
+}  // namespace ek

@@ -1,0 +1,1112 @@
+// ek_engine.hip — host side of the MI355X window/aggregate engine: the C ABI of include/ekgpu.h.
+//
+// Replaces, for one rule, the reference's per-tuple operator chain
+//   WatermarkOp (internal/topo/node/watermark_op.go:144-225)
+//   WindowOperator event-time trigger (event_window_trigger.go:112-209, window_op.go:194-227,605-739)
+//   FilterOp / AggregateOp / HavingOp / ProjectOp aggregate fields (internal/topo/operator/*.go)
+// with columnar micro-batches processed by the gfx950 kernels of ek_kernels.h.
+//
+// Event-time semantics kept exactly (see DESIGN.md §2 for the derivation):
+//   * late drop: event i accepted iff ts_i >= max(ts_<i) - lateTol            watermark_op.go:144-155
+//   * watermark after a batch W = max ts - lateTol; windows with end <= W are emitted in order, none at EOF
+//   * first window end E1 = getAlignedWindowEndTime(min accepted ts)         event_window_trigger.go:57-75
+//   * tumbling window j: ts < E1 (j = 0) or [E_{j-1}, E_j); hopping j: [E_j - L, E_j)
+//   * window_start quirks of scan()                                          window_op.go:697-707
+// Aggregation is pane-based: each (pane, key) keeps a partial (count, sum, min, max, M2), windows
+// merge their panes when they close.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ek_kernels.h"
+
+using namespace ek;
+
+namespace {
+
+constexpr int64_t kMinTs = INT64_MIN;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct WinInfo {
+    int64_t j;           // window index (0 = first)
+    int64_t start, end;
+    int64_t out_base;    // first row of the window's result region
+    int32_t slot;        // index into win_cnt / win_err device arrays
+    int64_t member_count;
+    uint64_t member_hash;
+};
+
+int64_t floordiv_h(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b) != 0 && ((a < 0) != (b < 0))) q--;
+    return q;
+}
+
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+
+int64_t unit_ms(int32_t u) {
+    switch (u) {
+    case EK_UNIT_DD: return 86400000LL;
+    case EK_UNIT_HH: return 3600000LL;
+    case EK_UNIT_MI: return 60000LL;
+    case EK_UNIT_SS: return 1000LL;
+    case EK_UNIT_MS: return 1LL;
+    }
+    return 0;
+}
+
+// window_op.go:194-227 getAlignedWindowEndTime (time.Local = UTC + tz_offset_s, no DST)
+int64_t aligned_end(int64_t ts, int32_t interval, int32_t unit, int32_t tz) {
+    int64_t off = (int64_t)tz * 1000;
+    int64_t local = ts + off;
+    int64_t day0 = floordiv_h(local, 86400000LL) * 86400000LL;
+    int64_t gap = interval;
+    switch (unit) {
+    case EK_UNIT_DD: return day0 + (int64_t)interval * 86400000LL - off;
+    case EK_UNIT_HH: {
+        int64_t hour = (local - day0) / 3600000LL;
+        if (hour > interval) gap = (int64_t)interval * (hour / interval + 1);
+        return day0 + gap * 3600000LL - off;
+    }
+    case EK_UNIT_MI: {
+        int64_t h0 = floordiv_h(local, 3600000LL) * 3600000LL;
+        int64_t minute = (local - h0) / 60000LL;
+        if (minute > interval) gap = (int64_t)interval * (minute / interval + 1);
+        return h0 + gap * 60000LL - off;
+    }
+    case EK_UNIT_SS: {
+        int64_t m0 = floordiv_h(local, 60000LL) * 60000LL;
+        int64_t sec = (local - m0) / 1000LL;
+        if (sec > interval) gap = (int64_t)interval * (sec / interval + 1);
+        return m0 + gap * 1000LL - off;
+    }
+    case EK_UNIT_MS: {
+        int64_t s0 = floordiv_h(local, 1000LL) * 1000LL;
+        int64_t milli = local - s0;
+        if (milli > interval) gap = (int64_t)interval * (milli / interval + 1);
+        return s0 + gap - off;
+    }
+    }
+    return ts;
+}
+
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
+int prog_depth_ok(const ek_instr* prog, int n) {
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        int op = prog[k].op;
+        if (op == EK_OP_COL || op == EK_OP_AGG || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) sp++;
+        else if (op >= EK_OP_EQ && op <= EK_OP_MOD) { if (sp < 2) return 0; sp--; }
+        else return 0;
+        if (sp > 16) return 0;
+    }
+    return n == 0 || sp == 1;
+}
+
+}  // namespace
+
+struct Engine {
+    ek_plan plan{};
+    DPlan dp{};
+    DPlan* d_plan = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    // ---- derived configuration
+    int wtype = 0;
+    int64_t L = 0, H = 0, P = 0;       // ms
+    int64_t ppw = 1, hpp = 1;          // panes per window, panes per hop
+    int32_t raw_interval = 0;
+    uint32_t K = 1;                    // keys
+    int kbits = 0, NB = 1;
+    int64_t Kpad = 1;
+    int ring = 16;
+    int max_panes_group = 8;
+    int64_t group_events = 8 << 20;
+    int chunk = 16384;
+    LdsLayout lay{};
+    int np_max = 8192;
+
+    // ---- stream state
+    bool has_M = false;
+    int64_t M = kMinTs;                // max ts over all arrivals
+    bool has_W = false;
+    int64_t W = kMinTs;                // last watermark
+    bool e1_known = false;
+    int64_t E1 = 0, first_ts = 0;
+    int64_t next_win = 0;              // next window index to emit
+    int64_t arrivals = 0;
+    std::vector<int64_t> slot_pane;    // pane id held by each ring slot (INT64_MIN = free)
+    PaneGrid grid{};
+    ek_stats stats{};
+
+    // ---- device memory
+    DevBuf state_buf, pane_err, pane_mcnt, pane_mhash;
+    DState dstate{};
+    DevBuf bstats;                     // BatchStats
+    BatchStats* h_stats = nullptr;     // pinned
+    int64_t* h_small = nullptr;        // pinned scratch (bounds)
+    size_t h_small_cap = 0;
+    DevBuf cmax, acc, bounds_val, bounds_idx, hist, offs, tiles;
+    DevBuf st_klo, st_val[kMaxVC], st_valid[kMaxVC];
+    int64_t st_cap = 0;
+    DevBuf in_cols[EK_MAX_COLUMNS], in_valid[EK_MAX_COLUMNS];   // H2D staging for host batches
+    // accepted events that arrived before the first watermark release (host copy, tiny)
+    DevBuf pend_cols[EK_MAX_COLUMNS], pend_valid[EK_MAX_COLUMNS], pend_arr_d;
+    std::vector<char> pend_host[EK_MAX_COLUMNS];
+    std::vector<uint8_t> pend_vhost[EK_MAX_COLUMNS];
+    std::vector<int64_t> pend_arr;
+    int64_t pend_n = 0, pend_min = INT64_MAX, pend_max = INT64_MIN;
+    bool pend_has_valid[EK_MAX_COLUMNS] = {};
+    DevBuf wdesc;                      // WinDesc array
+    WinDesc* h_wdesc = nullptr;        // pinned, bump-allocated per push (reset after the stats sync)
+    size_t h_wdesc_cap = 0, h_wdesc_used = 0;
+
+    // ---- results (device, accumulated until poll)
+    DevBuf r_key, r_val[EK_MAX_AGGS], r_tag[EK_MAX_AGGS], r_wcnt, r_werr, r_wmc, r_wmh;
+    int64_t r_rows_cap = 0, r_rows_used = 0;
+    int64_t r_win_cap = 0;
+    std::vector<WinInfo> wins;         // windows since last poll
+    // host copies handed out by poll (EK_MEM_HOST)
+    std::vector<int64_t> h_ws, h_we, h_off, h_cnt, h_mc;
+    std::vector<uint64_t> h_mh;
+    std::vector<int32_t> h_st;
+    std::vector<uint32_t> h_key;
+    std::vector<int64_t> h_val[EK_MAX_AGGS];
+    std::vector<uint8_t> h_tag[EK_MAX_AGGS];
+    std::vector<int64_t> d_off_host;   // offsets for device results
+
+    int fail(int code, const char* fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+
+    int ensure(DevBuf& b, size_t bytes) {
+        if (b.bytes >= bytes && b.p) return 0;
+        if (b.p) { hipStreamSynchronize(stream); hipFree(b.p); b.p = nullptr; b.bytes = 0; }
+        size_t nb = std::max(bytes, (size_t)256);
+        if (hipMalloc(&b.p, nb) != hipSuccess) return fail(EK_ERR_NOMEM, "hipMalloc(%zu) failed", nb);
+        b.bytes = nb;
+        return 0;
+    }
+    void release(DevBuf& b) {
+        if (b.p) hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+
+    // ------------------------------------------------------------------ create
+    int init(const ek_plan* p, int dev) {
+        plan = *p;
+        device = dev;
+        if (plan.abi_version != EKGPU_ABI_VERSION) return fail(EK_ERR_INVALID, "abi version %d != %d", plan.abi_version, EKGPU_ABI_VERSION);
+        if (plan.n_columns <= 0 || plan.n_columns > EK_MAX_COLUMNS) return fail(EK_ERR_INVALID, "bad n_columns");
+        if (plan.n_aggs < 0 || plan.n_aggs > EK_MAX_AGGS) return fail(EK_ERR_INVALID, "bad n_aggs");
+        if (plan.n_where < 0 || plan.n_where > EK_MAX_PROG || plan.n_having < 0 || plan.n_having > EK_MAX_PROG ||
+            plan.n_trigger < 0 || plan.n_trigger > EK_MAX_PROG)
+            return fail(EK_ERR_INVALID, "bad program length");
+        if (!prog_depth_ok(plan.where_prog, plan.n_where) || !prog_depth_ok(plan.having_prog, plan.n_having) ||
+            !prog_depth_ok(plan.trigger_prog, plan.n_trigger))
+            return fail(EK_ERR_INVALID, "malformed expression program");
+        for (int c = 0; c < plan.n_columns; ++c)
+            if (plan.column_type[c] < EK_COL_I64 || plan.column_type[c] > EK_COL_U32) return fail(EK_ERR_INVALID, "bad column type %d", c);
+        auto col_ok = [&](int c) { return c >= 0 && c < plan.n_columns; };
+        for (int k = 0; k < plan.n_where; ++k)
+            if (plan.where_prog[k].op == EK_OP_COL && !col_ok(plan.where_prog[k].arg)) return fail(EK_ERR_INVALID, "WHERE column out of range");
+            else if (plan.where_prog[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in WHERE");
+        for (int k = 0; k < plan.n_having; ++k) {
+            if (plan.having_prog[k].op == EK_OP_COL) return fail(EK_ERR_UNSUPPORTED, "non-aggregate column in HAVING");
+            if (plan.having_prog[k].op == EK_OP_AGG && (plan.having_prog[k].arg < 0 || plan.having_prog[k].arg >= plan.n_aggs))
+                return fail(EK_ERR_INVALID, "HAVING aggregate slot out of range");
+        }
+        wtype = plan.window_type;
+        if (plan.is_event_time) {
+            // NewEventTimeTrigger (event_window_trigger.go:35-53)
+            if (wtype < EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
+        }
+        if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING)
+            return fail(EK_ERR_UNSUPPORTED, "window type %d is not implemented by this engine build (tumbling/hopping only)", wtype);
+        if (!plan.is_event_time) return fail(EK_ERR_UNSUPPORTED, "processing-time time windows are not implemented (use event time)");
+        if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
+            return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
+        if (plan.key_column >= 0) {
+            if (!col_ok(plan.key_column) || plan.column_type[plan.key_column] != EK_COL_U32)
+                return fail(EK_ERR_INVALID, "GROUP BY key must be a u32 dictionary column");
+            if (plan.num_keys == 0) return fail(EK_ERR_INVALID, "num_keys must be > 0");
+            if (plan.nullable_mask & (1u << plan.key_column)) return fail(EK_ERR_UNSUPPORTED, "nullable GROUP BY key");
+        }
+        if (plan.nullable_mask & (1u << plan.ts_column)) return fail(EK_ERR_INVALID, "nullable timestamp column");
+        int64_t u = unit_ms(plan.time_unit);
+        if (u == 0) return fail(EK_ERR_INVALID, "bad time unit");
+        if (plan.length <= 0) return fail(EK_ERR_INVALID, "window length must be > 0");
+        L = (int64_t)plan.length * u;
+        if (plan.delay != 0) return fail(EK_ERR_UNSUPPORTED, "window delay is not supported for tumbling/hopping");
+        if (wtype == EK_WINDOW_TUMBLING) {
+            H = L; P = L; raw_interval = plan.length;
+        } else {
+            if (plan.interval <= 0) return fail(EK_ERR_INVALID, "hopping interval must be > 0");
+            H = (int64_t)plan.interval * u;
+            if (H > L) return fail(EK_ERR_UNSUPPORTED, "hopping interval larger than the window length");
+            P = gcd64(L, H);
+            raw_interval = plan.interval;
+        }
+        ppw = L / P;
+        hpp = H / P;
+
+        // ---- device plan + aggregate field needs
+        dp = DPlan{};
+        dp.n_columns = plan.n_columns;
+        for (int c = 0; c < plan.n_columns; ++c) dp.col_type[c] = plan.column_type[c];
+        dp.ts_col = plan.ts_column;
+        dp.key_col = plan.key_column;
+        dp.num_keys = plan.key_column >= 0 ? plan.num_keys : 1u;
+        dp.n_where = plan.n_where;
+        dp.n_having = plan.n_having;
+        dp.n_trigger = plan.n_trigger;
+        memcpy(dp.where_prog, plan.where_prog, sizeof plan.where_prog);
+        memcpy(dp.having_prog, plan.having_prog, sizeof plan.having_prog);
+        memcpy(dp.trigger_prog, plan.trigger_prog, sizeof plan.trigger_prog);
+        dp.n_aggs = plan.n_aggs;
+        for (int k = 0; k < plan.n_aggs; ++k) {
+            const ek_agg_spec& a = plan.aggs[k];
+            dp.agg_fn[k] = a.fn;
+            dp.agg_p[k] = a.param;
+            dp.agg_vc[k] = -1;
+            if (a.fn < EK_AGG_COUNT_STAR || a.fn > EK_AGG_PERCENTILE_DISC) return fail(EK_ERR_INVALID, "bad aggregate %d", a.fn);
+            if (a.fn == EK_AGG_MEDIAN || a.fn == EK_AGG_PERCENTILE_CONT || a.fn == EK_AGG_PERCENTILE_DISC)
+                return fail(EK_ERR_UNSUPPORTED, "median/percentile need the raw-event engine mode (not in this build)");
+            if (a.fn == EK_AGG_COUNT_STAR) continue;
+            if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "aggregate column out of range");
+            int v = -1;
+            for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == a.column) v = x;
+            if (v < 0) {
+                if (dp.n_vc >= kMaxVC) return fail(EK_ERR_UNSUPPORTED, "too many aggregated columns");
+                v = dp.n_vc++;
+                dp.vc_col[v] = a.column;
+                dp.vc_is_float[v] = plan.column_type[a.column] == EK_COL_F64;
+                dp.vc_flags[v] = 0;
+            }
+            dp.agg_vc[k] = v;
+            const bool nullable = (plan.nullable_mask >> a.column) & 1u;
+            const bool fl = dp.vc_is_float[v];
+            int f = 0;
+            switch (a.fn) {
+            case EK_AGG_COUNT: f = NEED_CNT; break;
+            case EK_AGG_SUM: f = NEED_SUM; break;
+            case EK_AGG_AVG: f = NEED_SUM | NEED_CNT; break;
+            case EK_AGG_MIN: f = NEED_MIN; break;
+            case EK_AGG_MAX: f = NEED_MAX; break;
+            default: f = NEED_M2 | NEED_CNT | (fl ? NEED_SUM : NEED_FSUM); break;   // var family
+            }
+            if (fl && (f & NEED_SUM) == 0 && (f & NEED_M2)) f |= NEED_SUM;
+            if (!nullable) f &= ~NEED_CNT;   // vcnt == count(*) when the column has no NULLs
+            dp.vc_flags[v] |= f;
+        }
+        for (int v = 0; v < dp.n_vc; ++v) {
+            // float sums feed the M2 merge and avg; int sums keep a float shadow only for var
+            if (!dp.vc_is_float[v] && (dp.vc_flags[v] & NEED_M2)) dp.vc_flags[v] |= NEED_FSUM;
+        }
+
+        // ---- key bucketing: keys per bucket (1 << kbits) sized so the LDS partial fits
+        K = dp.num_keys;
+        int bytes_per_key = 4;
+        for (int v = 0; v < dp.n_vc; ++v) {
+            int f = dp.vc_flags[v];
+            bytes_per_key += (f & NEED_CNT ? 4 : 0) + (f & NEED_SUM ? 8 : 0) + (f & NEED_MIN ? 8 : 0) + (f & NEED_MAX ? 8 : 0) +
+                             (f & NEED_M2 ? 8 : 0) + (f & NEED_FSUM ? 8 : 0);
+        }
+        int want = env_int("EKGPU_KBITS", 8);
+        kbits = 0;
+        while ((1u << kbits) < K && kbits < want) kbits++;
+        while (kbits > 0 && ((1 << kbits) * bytes_per_key) > 48 * 1024) kbits--;
+        NB = (int)((K + (1u << kbits) - 1) >> kbits);
+        Kpad = (int64_t)NB << kbits;
+        // LDS layout (8-byte fields first for alignment)
+        {
+            int kk = 1 << kbits;
+            int o = 0;
+            for (int v = 0; v < dp.n_vc; ++v) {
+                int f = dp.vc_flags[v];
+                if (f & NEED_SUM) { lay.off_sum[v] = o; o += 8 * kk; }
+                if (f & NEED_MIN) { lay.off_min[v] = o; o += 8 * kk; }
+                if (f & NEED_MAX) { lay.off_max[v] = o; o += 8 * kk; }
+                if (f & NEED_M2) { lay.off_m2[v] = o; o += 8 * kk; }
+                if (f & NEED_FSUM) { lay.off_fsum[v] = o; o += 8 * kk; }
+            }
+            lay.off_cnt = o; o += 4 * kk;
+            for (int v = 0; v < dp.n_vc; ++v) if (dp.vc_flags[v] & NEED_CNT) { lay.off_vcnt[v] = o; o += 4 * kk; }
+            lay.bytes = (o + 15) & ~15;
+        }
+        chunk = env_int("EKGPU_CHUNK", 16384);
+        group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 8 << 20);
+        np_max = env_int("EKGPU_NP_MAX", 8192);
+        int ppg = std::max(1, np_max / NB);
+        max_panes_group = (int)std::min<int64_t>(ppg, 64);
+        ring = (int)(2 * ppw + max_panes_group + 4);
+        if (NB > np_max) return fail(EK_ERR_UNSUPPORTED, "too many key buckets (%d)", NB);
+
+        // ---- HIP resources
+        if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(EK_ERR_DEVICE, "stream create failed");
+        own_stream = true;
+        hipEventCreate(&ev0);
+        hipEventCreate(&ev1);
+        if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
+        if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+        if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
+        if (int rc = ensure(bstats, sizeof(BatchStats))) return rc;
+        if (int rc = alloc_state()) return rc;
+        reset_state();
+        return 0;
+    }
+
+    int alloc_state() {
+        // SoA fields, each ring * Kpad entries of 8 bytes
+        int nf = 1;
+        for (int v = 0; v < dp.n_vc; ++v) {
+            int f = dp.vc_flags[v];
+            nf += !!(f & NEED_CNT) + !!(f & NEED_SUM) + !!(f & NEED_MIN) + !!(f & NEED_MAX) + !!(f & NEED_M2) + !!(f & NEED_FSUM);
+        }
+        size_t per = (size_t)ring * Kpad * 8;
+        if (int rc = ensure(state_buf, per * nf)) return rc;
+        char* b = (char*)state_buf.p;
+        dstate = DState{};
+        dstate.K = Kpad;
+        dstate.cnt = (int64_t*)b; b += per;
+        for (int v = 0; v < dp.n_vc; ++v) {
+            int f = dp.vc_flags[v];
+            if (f & NEED_CNT) { dstate.vcnt[v] = (int64_t*)b; b += per; }
+            if (f & NEED_SUM) { dstate.sum[v] = (int64_t*)b; b += per; }
+            if (f & NEED_MIN) { dstate.mn[v] = (int64_t*)b; b += per; }
+            if (f & NEED_MAX) { dstate.mx[v] = (int64_t*)b; b += per; }
+            if (f & NEED_M2) { dstate.m2[v] = (double*)b; b += per; }
+            if (f & NEED_FSUM) { dstate.fsum[v] = (double*)b; b += per; }
+        }
+        if (int rc = ensure(pane_err, (size_t)ring * 4)) return rc;
+        if (int rc = ensure(pane_mcnt, (size_t)ring * 8)) return rc;
+        if (int rc = ensure(pane_mhash, (size_t)ring * 8)) return rc;
+        return 0;
+    }
+
+    void reset_state() {
+        has_M = has_W = e1_known = false;
+        M = W = kMinTs;
+        E1 = first_ts = 0;
+        next_win = 0;
+        arrivals = 0;
+        pend_n = 0;
+        pend_min = INT64_MAX;
+        pend_max = INT64_MIN;
+        pend_arr.clear();
+        for (int c = 0; c < EK_MAX_COLUMNS; ++c) { pend_host[c].clear(); pend_vhost[c].clear(); pend_has_valid[c] = false; }
+        slot_pane.assign(ring, INT64_MIN);
+        wins.clear();
+        r_rows_used = 0;
+        stats = ek_stats{};
+    }
+
+    // ------------------------------------------------------------------ pane geometry
+    int64_t win_end(int64_t j) const { return E1 + j * H; }
+    int64_t win_first_pane(int64_t j) const { return wtype == EK_WINDOW_TUMBLING ? j : j * hpp; }
+    int64_t win_last_pane(int64_t j) const { return wtype == EK_WINDOW_TUMBLING ? j : j * hpp + ppw - 1; }
+    int64_t pane_host(int64_t ts) const {
+        if (wtype == EK_WINDOW_TUMBLING) return ts < E1 ? 0 : floordiv_h(ts - E1, P) + 1;
+        int64_t o = E1 - L;
+        return ts < o ? -1 : floordiv_h(ts - o, P);
+    }
+    int64_t pane_start(int64_t q) const {
+        if (wtype == EK_WINDOW_TUMBLING) return q == 0 ? INT64_MIN : E1 + (q - 1) * P;
+        return E1 - L + q * P;
+    }
+
+    int claim_slots(int64_t qa, int64_t qb) {
+        int64_t first_live = win_first_pane(next_win);
+        for (int64_t q = qa; q <= qb; ++q) {
+            int s = (int)(q % ring);
+            if (slot_pane[s] == q) continue;
+            if (slot_pane[s] != INT64_MIN && slot_pane[s] >= first_live)
+                return fail(EK_ERR_UNSUPPORTED, "pane ring overflow (pane %lld needs slot %d held by live pane %lld)",
+                            (long long)q, s, (long long)slot_pane[s]);
+            // zero the slot's partials
+            size_t per = (size_t)Kpad * 8;
+            hipMemsetAsync((char*)dstate.cnt + s * per, 0, per, stream);
+            for (int v = 0; v < dp.n_vc; ++v) {
+                if (dstate.vcnt[v]) hipMemsetAsync((char*)dstate.vcnt[v] + s * per, 0, per, stream);
+                if (dstate.sum[v]) hipMemsetAsync((char*)dstate.sum[v] + s * per, 0, per, stream);
+                if (dstate.mn[v]) hipMemsetAsync((char*)dstate.mn[v] + s * per, 0, per, stream);
+                if (dstate.mx[v]) hipMemsetAsync((char*)dstate.mx[v] + s * per, 0, per, stream);
+                if (dstate.m2[v]) hipMemsetAsync((char*)dstate.m2[v] + s * per, 0, per, stream);
+                if (dstate.fsum[v]) hipMemsetAsync((char*)dstate.fsum[v] + s * per, 0, per, stream);
+            }
+            hipMemsetAsync((char*)pane_err.p + s * 4, 0, 4, stream);
+            hipMemsetAsync((char*)pane_mcnt.p + s * 8, 0, 8, stream);
+            hipMemsetAsync((char*)pane_mhash.p + s * 8, 0, 8, stream);
+            slot_pane[s] = q;
+        }
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ results
+    int ensure_results(int64_t add_rows, int64_t add_wins) {
+        int64_t need_rows = r_rows_used + add_rows;
+        if (need_rows > r_rows_cap) {
+            int64_t cap = std::max<int64_t>(need_rows, r_rows_cap * 2);
+            cap = std::max<int64_t>(cap, 1024);
+            // grow with copy of the live rows
+            auto grow = [&](DevBuf& b, size_t esz) -> int {
+                DevBuf nb;
+                if (hipMalloc(&nb.p, (size_t)cap * esz) != hipSuccess) return fail(EK_ERR_NOMEM, "result alloc");
+                nb.bytes = (size_t)cap * esz;
+                if (b.p && r_rows_used) hipMemcpyAsync(nb.p, b.p, (size_t)r_rows_used * esz, hipMemcpyDeviceToDevice, stream);
+                if (b.p) { hipStreamSynchronize(stream); hipFree(b.p); }
+                b = nb;
+                return 0;
+            };
+            if (int rc = grow(r_key, 4)) return rc;
+            for (int k = 0; k < plan.n_aggs; ++k) {
+                if (int rc = grow(r_val[k], 8)) return rc;
+                if (int rc = grow(r_tag[k], 1)) return rc;
+            }
+            r_rows_cap = cap;
+        }
+        int64_t need_w = (int64_t)wins.size() + add_wins;
+        if (need_w > r_win_cap) {
+            int64_t cap = std::max<int64_t>(need_w, std::max<int64_t>(r_win_cap * 2, 256));
+            auto growz = [&](DevBuf& b, size_t esz) -> int {
+                DevBuf nb;
+                if (hipMalloc(&nb.p, (size_t)cap * esz) != hipSuccess) return fail(EK_ERR_NOMEM, "window alloc");
+                nb.bytes = (size_t)cap * esz;
+                hipMemsetAsync(nb.p, 0, (size_t)cap * esz, stream);
+                if (b.p && !wins.empty()) hipMemcpyAsync(nb.p, b.p, wins.size() * esz, hipMemcpyDeviceToDevice, stream);
+                if (b.p) { hipStreamSynchronize(stream); hipFree(b.p); }
+                b = nb;
+                return 0;
+            };
+            if (int rc = growz(r_wcnt, 8)) return rc;
+            if (int rc = growz(r_werr, 4)) return rc;
+            if (int rc = growz(r_wmc, 8)) return rc;
+            if (int rc = growz(r_wmh, 8)) return rc;
+            r_win_cap = cap;
+        }
+        return 0;
+    }
+
+    Results results_view() {
+        Results r{};
+        r.key = (uint32_t*)r_key.p;
+        for (int k = 0; k < plan.n_aggs; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
+        r.win_cnt = (int64_t*)r_wcnt.p;
+        r.win_err = (int32_t*)r_werr.p;
+        return r;
+    }
+
+    // window_op.go:688-716 scan(): windowStart by type, then the <= 0 fallback
+    int64_t window_start(int64_t j) const {
+        int64_t trig = j == 0 ? first_ts : win_end(j - 1);
+        int64_t ws = wtype == EK_WINDOW_TUMBLING ? trig : trig - H;
+        if (ws <= 0) ws = win_end(j) - L;
+        return ws;
+    }
+
+    // Emit every window j >= next_win with E_j <= W whose panes are complete (last pane <= q_done).
+    int finalize_ready(int64_t q_done) {
+        if (!e1_known || !has_W) return 0;
+        int64_t j0 = next_win, j1 = next_win;
+        while (win_end(j1) <= W && win_last_pane(j1) <= q_done) j1++;
+        if (j1 == j0) return 0;
+        int64_t n = j1 - j0;
+        // windows whose panes were never claimed hold no events: claim (zero) them so the merge reads zeros
+        if (int rc = claim_slots(std::max<int64_t>(0, win_first_pane(j0)), win_last_pane(j1 - 1))) return rc;
+        if (int rc = ensure_results(n * (int64_t)K, n)) return rc;
+        if (h_wdesc_used + n > h_wdesc_cap) {
+            hipStreamSynchronize(stream);  // every earlier descriptor upload has completed
+            if (h_wdesc_cap < (size_t)n) {
+                if (h_wdesc) hipHostFree(h_wdesc);
+                h_wdesc_cap = std::max<size_t>(n, 4096);
+                if (hipHostMalloc((void**)&h_wdesc, h_wdesc_cap * sizeof(WinDesc)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
+            }
+            h_wdesc_used = 0;
+        }
+        WinDesc* hd = h_wdesc + h_wdesc_used;
+        h_wdesc_used += n;
+        if (int rc = ensure(wdesc, (size_t)n * sizeof(WinDesc))) return rc;
+        for (int64_t j = j0; j < j1; ++j) {
+            WinInfo wi{};
+            wi.j = j;
+            wi.end = win_end(j);
+            wi.start = window_start(j);
+            wi.out_base = r_rows_used;
+            wi.slot = (int32_t)wins.size();
+            r_rows_used += K;
+            WinDesc& d = hd[j - j0];
+            d.q_first = std::max<int64_t>(0, win_first_pane(j));
+            d.q_last = win_last_pane(j);
+            d.out_base = wi.out_base;
+            d.idx = wi.slot;
+            wins.push_back(wi);
+        }
+        hipMemcpyAsync(wdesc.p, hd, (size_t)n * sizeof(WinDesc), hipMemcpyHostToDevice, stream);
+        dim3 grid((unsigned)((K + kBlock - 1) / kBlock), (unsigned)n);
+        hipLaunchKernelGGL(k_finalize, grid, dim3(kBlock), 0, stream, d_plan, (const WinDesc*)wdesc.p, dstate, ring,
+                           (const int32_t*)pane_err.p, results_view());
+        if (plan.debug_membership) {
+            hipLaunchKernelGGL(k_win_members, dim3((unsigned)n), dim3(64), 0, stream, (const WinDesc*)wdesc.p, ring,
+                               (const int64_t*)pane_mcnt.p, (const unsigned long long*)pane_mhash.p, (int64_t*)r_wmc.p,
+                               (unsigned long long*)r_wmh.p);
+        }
+        next_win = j1;
+        stats.windows_out += n;
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ batch processing
+    int process(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t min_acc, int64_t max_ts,
+                const int64_t* d_arrival) {
+        int64_t n = db.n;
+        int64_t q_lo = std::max<int64_t>(0, pane_host(min_acc));
+        int64_t q_hi = pane_host(max_ts);
+        if (q_hi < 0) return 0;   // every event precedes the first hopping window
+        int64_t first_live = win_first_pane(next_win);
+        q_lo = std::max(q_lo, first_live);
+
+        struct Grp { int64_t lo, hi, qa, qb; bool complete; };
+        std::vector<Grp> groups;
+        if (sorted) {
+            // pane boundaries by binary search on the sorted ts column
+            int64_t nq = q_hi - q_lo + 1;
+            int nb = (int)nq + 1;
+            if (h_small_cap < (size_t)(2 * nb)) {
+                if (h_small) { hipStreamSynchronize(stream); hipHostFree(h_small); }
+                h_small_cap = std::max<size_t>(2 * nb, 4096);
+                if (hipHostMalloc((void**)&h_small, h_small_cap * 8) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
+            }
+            for (int64_t k = 0; k < nq; ++k) h_small[k] = pane_start(q_lo + k);
+            if (h_small[0] == INT64_MIN) h_small[0] = INT64_MIN + 1;
+            h_small[nq] = INT64_MAX;
+            if (int rc = ensure(bounds_val, (size_t)nb * 8)) return rc;
+            if (int rc = ensure(bounds_idx, (size_t)nb * 8)) return rc;
+            hipMemcpyAsync(bounds_val.p, h_small, (size_t)nb * 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_lower_bound, dim3((nb + 255) / 256), dim3(256), 0, stream,
+                               (const int64_t*)db.col[dp.ts_col], start, n, (const int64_t*)bounds_val.p, nb,
+                               (int64_t*)bounds_idx.p);
+            hipMemcpyAsync(h_small + nb, bounds_idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "bounds sync failed");
+            const int64_t* b = h_small + nb;
+            // greedy grouping of consecutive panes; a pane larger than the target is split
+            int64_t k = 0;
+            while (k < nq) {
+                int64_t lo = b[k];
+                int64_t kk = k;
+                int64_t hi = b[k + 1];
+                if (hi - lo > group_events) {
+                    // split one big pane into several groups
+                    for (int64_t s = lo; s < hi; s += group_events) {
+                        int64_t e = std::min(hi, s + group_events);
+                        groups.push_back(Grp{s, e, q_lo + k, q_lo + k, e == hi});
+                    }
+                    k++;
+                    continue;
+                }
+                while (kk + 1 < nq && (b[kk + 2] - lo) <= group_events && (kk + 1 - k + 1) <= max_panes_group) {
+                    kk++;
+                    hi = b[kk + 1];
+                }
+                if (hi > lo) groups.push_back(Grp{lo, hi, q_lo + k, q_lo + kk, true});
+                else groups.push_back(Grp{lo, lo, q_lo + k, q_lo + kk, true});
+                k = kk + 1;
+            }
+        } else {
+            if (q_hi - q_lo + 1 > max_panes_group)
+                return fail(EK_ERR_UNSUPPORTED, "out-of-order batch spans %lld panes (max %d): split the batch",
+                            (long long)(q_hi - q_lo + 1), max_panes_group);
+            groups.push_back(Grp{start, n, q_lo, q_hi, true});
+        }
+
+        for (const Grp& g : groups) {
+            if (g.hi > g.lo) {
+                if (int rc = run_group(db, g.lo, g.hi, g.qa, g.qb, d_acc)) return rc;
+                if (plan.debug_membership) {
+                    hipLaunchKernelGGL(k_members, dim3(256), dim3(kBlock), 0, stream, d_plan, db, grid, d_acc,
+                                       (int)(d_acc != nullptr), g.lo, g.hi, arrivals, d_arrival, g.qa, g.qb, ring,
+                                       (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
+                }
+            }
+            int64_t q_done = g.complete ? g.qb : g.qb - 1;
+            if (int rc = finalize_ready(q_done)) return rc;
+        }
+        return finalize_ready(q_hi);
+    }
+
+    int run_group(const DBatch& db, int64_t lo, int64_t hi, int64_t qa, int64_t qb, const uint8_t* d_acc) {
+        if (int rc = claim_slots(qa, qb)) return rc;
+        GroupDesc gd{};
+        gd.lo = lo;
+        gd.hi = hi;
+        gd.q_lo = qa;
+        gd.n_panes = (int32_t)(qb - qa + 1);
+        gd.nb = NB;
+        gd.kbits = kbits;
+        gd.chunk = chunk;
+        gd.nch = (int32_t)((hi - lo + chunk - 1) / chunk);
+        gd.np = gd.n_panes * NB;
+        gd.ring = ring;
+        gd.has_accept = d_acc != nullptr;
+        if (gd.np > np_max) return fail(EK_ERR_UNSUPPORTED, "too many partitions in a group (%d)", gd.np);
+        int64_t nh = (int64_t)gd.np * gd.nch + 1;
+        if (int rc = ensure(hist, (size_t)nh * 4)) return rc;
+        if (int rc = ensure(offs, (size_t)nh * 4)) return rc;
+        int64_t ntile = (nh + kScanTile - 1) / kScanTile;
+        if (ntile > 1024 * 64) return fail(EK_ERR_UNSUPPORTED, "histogram too large");
+        if (int rc = ensure(tiles, (size_t)ntile * 4)) return rc;
+        int64_t ne = hi - lo;
+        if (ne > st_cap) {
+            if (int rc = ensure(st_klo, (size_t)ne * 2)) return rc;
+            for (int v = 0; v < dp.n_vc; ++v) {
+                if (int rc = ensure(st_val[v], (size_t)ne * 8)) return rc;
+                if ((plan.nullable_mask >> dp.vc_col[v]) & 1u)
+                    if (int rc = ensure(st_valid[v], (size_t)ne)) return rc;
+            }
+            st_cap = ne;
+        }
+        Staging st{};
+        st.klo = (uint16_t*)st_klo.p;
+        for (int v = 0; v < dp.n_vc; ++v) {
+            st.val[v] = (int64_t*)st_val[v].p;
+            if (db.valid[dp.vc_col[v]]) {
+                st.valid[v] = (uint8_t*)st_valid[v].p;
+                st.nullable_mask |= 1u << v;
+            }
+        }
+        size_t lds_np = (size_t)gd.np * 4;
+        hipMemsetAsync((char*)hist.p + (nh - 1) * 4, 0, 4, stream);
+        hipLaunchKernelGGL(k_hist, dim3(gd.nch), dim3(kBlock), lds_np, stream, d_plan, db, grid, gd, d_acc,
+                           (uint32_t*)hist.p, (int32_t*)pane_err.p);
+        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)ntile), dim3(kBlock), 0, stream, (const uint32_t*)hist.p, nh,
+                           (uint32_t*)tiles.p);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, (uint32_t*)tiles.p, (int)ntile);
+        hipLaunchKernelGGL(k_scan_down, dim3((unsigned)ntile), dim3(kBlock), 0, stream, (const uint32_t*)hist.p, nh,
+                           (const uint32_t*)tiles.p, (uint32_t*)offs.p);
+        hipLaunchKernelGGL(k_scatter, dim3(gd.nch), dim3(kBlock), lds_np, stream, d_plan, db, grid, gd, d_acc,
+                           (const uint32_t*)offs.p, st);
+        hipLaunchKernelGGL(k_agg, dim3(gd.np), dim3(kBlock), (size_t)lay.bytes, stream, d_plan, gd, lay,
+                           (const uint32_t*)offs.p, st, dstate);
+        if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
+        return 0;
+    }
+
+    // Accepted events that arrived before the first watermark release are kept (host side, tiny:
+    // at most lateTolerance worth of events) until the first window end can be aligned
+    // (getNextWindow on the first released event, event_window_trigger.go:57-75).
+    int append_pending(const DBatch& db, const uint8_t* d_acc, int64_t arrival_base) {
+        int64_t n = db.n;
+        std::vector<uint8_t> acc_h;
+        if (d_acc) {
+            acc_h.resize(n);
+            hipMemcpyAsync(acc_h.data(), d_acc, n, hipMemcpyDeviceToHost, stream);
+        }
+        std::vector<char> colh[EK_MAX_COLUMNS];
+        std::vector<uint8_t> valh[EK_MAX_COLUMNS];
+        for (int c = 0; c < plan.n_columns; ++c) {
+            size_t es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
+            colh[c].resize(n * es);
+            hipMemcpyAsync(colh[c].data(), db.col[c], n * es, hipMemcpyDeviceToHost, stream);
+            if (db.valid[c]) {
+                valh[c].resize(n);
+                hipMemcpyAsync(valh[c].data(), db.valid[c], n, hipMemcpyDeviceToHost, stream);
+            }
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "pending copy failed");
+        const int64_t* ts = (const int64_t*)colh[dp.ts_col].data();
+        for (int64_t i = 0; i < n; ++i) {
+            if (d_acc && !acc_h[i]) continue;
+            for (int c = 0; c < plan.n_columns; ++c) {
+                size_t es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
+                pend_host[c].insert(pend_host[c].end(), colh[c].data() + i * es, colh[c].data() + (i + 1) * es);
+                if (db.valid[c] && !pend_has_valid[c]) { pend_vhost[c].assign(pend_n, 1); pend_has_valid[c] = true; }
+                if (pend_has_valid[c]) pend_vhost[c].push_back(db.valid[c] ? valh[c][i] : 1);
+            }
+            pend_arr.push_back(arrival_base + i);
+            pend_min = std::min(pend_min, ts[i]);
+            pend_max = std::max(pend_max, ts[i]);
+            pend_n++;
+        }
+        return 0;
+    }
+
+    int flush_pending() {
+        DBatch pb{};
+        pb.n = pend_n;
+        for (int c = 0; c < plan.n_columns; ++c) {
+            size_t es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
+            if (int rc = ensure(pend_cols[c], pend_n * es)) return rc;
+            hipMemcpyAsync(pend_cols[c].p, pend_host[c].data(), pend_n * es, hipMemcpyHostToDevice, stream);
+            pb.col[c] = pend_cols[c].p;
+            if (pend_has_valid[c]) {
+                if (int rc = ensure(pend_valid[c], pend_n)) return rc;
+                hipMemcpyAsync(pend_valid[c].p, pend_vhost[c].data(), pend_n, hipMemcpyHostToDevice, stream);
+                pb.valid[c] = (const uint8_t*)pend_valid[c].p;
+            }
+        }
+        if (int rc = ensure(pend_arr_d, pend_n * 8)) return rc;
+        hipMemcpyAsync(pend_arr_d.p, pend_arr.data(), pend_n * 8, hipMemcpyHostToDevice, stream);
+        int rc = process(pb, false, 0, nullptr, pend_min, pend_max, (const int64_t*)pend_arr_d.p);
+        hipStreamSynchronize(stream);   // host vectors may be released now
+        pend_n = 0;
+        pend_arr.clear();
+        for (int c = 0; c < EK_MAX_COLUMNS; ++c) { pend_host[c].clear(); pend_vhost[c].clear(); pend_has_valid[c] = false; }
+        return rc;
+    }
+
+    int push(const ek_batch* b) {
+        if (!b) return fail(EK_ERR_INVALID, "null batch");
+        int64_t n = b->n_rows;
+        if (n < 0) return fail(EK_ERR_INVALID, "negative row count");
+        if (n == 0) return 0;
+        if (n > ((int64_t)1 << 31) - 1) return fail(EK_ERR_UNSUPPORTED, "batch larger than 2^31-1 rows");
+        for (int c = 0; c < plan.n_columns; ++c) {
+            if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
+            if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
+        }
+        hipEventRecord(ev0, stream);
+        DBatch db{};
+        db.n = n;
+        if (b->memory == EK_MEM_HOST) {
+            for (int c = 0; c < plan.n_columns; ++c) {
+                size_t es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
+                if (int rc = ensure(in_cols[c], (size_t)n * es)) return rc;
+                hipMemcpyAsync(in_cols[c].p, b->columns[c], (size_t)n * es, hipMemcpyHostToDevice, stream);
+                db.col[c] = in_cols[c].p;
+                if (b->validity[c]) {
+                    if (int rc = ensure(in_valid[c], (size_t)n)) return rc;
+                    hipMemcpyAsync(in_valid[c].p, b->validity[c], (size_t)n, hipMemcpyHostToDevice, stream);
+                    db.valid[c] = (const uint8_t*)in_valid[c].p;
+                }
+            }
+        } else {
+            for (int c = 0; c < plan.n_columns; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
+        }
+        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+        stats.records_in += n;
+
+        // ---- 1. batch statistics (one pass over ts)
+        BatchStats init{INT64_MAX, INT64_MIN, 0, INT64_MAX, 0, 0};
+        *h_stats = init;
+        hipMemcpyAsync(bstats.p, h_stats, sizeof(BatchStats), hipMemcpyHostToDevice, stream);
+        int sblocks = (int)std::min<int64_t>(2048, (n + 2 * kBlock - 1) / (2 * kBlock));
+        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats.p);
+        hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
+        BatchStats s = *h_stats;
+        const int64_t T = plan.late_tolerance_ms;
+
+        // ---- 2. late-event drop (watermark_op.go:144-155)
+        bool sorted = !s.unsorted;
+        int64_t start = 0, n_acc = n, min_acc = s.min_ts;
+        const uint8_t* d_acc = nullptr;
+        if (sorted && has_M && s.min_ts < M - T) {
+            // sorted batch below the carried watermark: the late events are a prefix
+            int64_t bound = M - T;
+            if (int rc = ensure(bounds_val, 8)) return rc;
+            if (int rc = ensure(bounds_idx, 8)) return rc;
+            hipMemcpyAsync(bounds_val.p, &bound, 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(64), 0, stream, ts, (int64_t)0, n, (const int64_t*)bounds_val.p, 1,
+                               (int64_t*)bounds_idx.p);
+            hipMemcpyAsync(&start, bounds_idx.p, 8, hipMemcpyDeviceToHost, stream);
+            hipStreamSynchronize(stream);
+            n_acc = n - start;
+            if (n_acc > 0) {
+                hipMemcpyAsync(&min_acc, ts + start, 8, hipMemcpyDeviceToHost, stream);
+                hipStreamSynchronize(stream);
+            }
+        } else if (!sorted) {
+            int nch = (int)((n + kAccChunk - 1) / kAccChunk);
+            if (int rc = ensure(cmax, (size_t)nch * 8)) return rc;
+            if (int rc = ensure(acc, (size_t)n)) return rc;
+            hipLaunchKernelGGL(k_chunk_max, dim3(nch), dim3(kBlock), 0, stream, ts, n, (int64_t*)cmax.p);
+            hipLaunchKernelGGL(k_scan_max, dim3(1), dim3(1024), 0, stream, (int64_t*)cmax.p, nch, has_M ? M : kMinTs);
+            hipLaunchKernelGGL(k_accept, dim3(nch), dim3(kBlock), 0, stream, ts, n, (const int64_t*)cmax.p, T,
+                               (uint8_t*)acc.p, (BatchStats*)bstats.p);
+            hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "accept kernel failed");
+            n_acc = h_stats->n_accepted;
+            min_acc = h_stats->min_accepted;
+            d_acc = (const uint8_t*)acc.p;
+        }
+        stats.records_late += n - n_acc;
+        int64_t arrival_base = arrivals;
+        arrivals += n;
+        h_wdesc_used = 0;   // the stats sync above drained every earlier descriptor upload
+
+        // ---- 3. watermark advance (watermark_op.go:157-214): W = max ts - lateTol
+        if (!has_M || s.max_ts > M) {
+            M = s.max_ts;
+            has_M = true;
+            W = M - T;
+            has_W = true;
+        }
+        if (n_acc == 0) return record_time();
+
+        // ---- 4. first window alignment once the first event is released
+        if (!e1_known) {
+            int64_t mn = std::min(min_acc, pend_min);
+            if (!(has_W && W >= mn)) {
+                int rc = append_pending(db, d_acc, arrival_base);
+                return rc ? rc : record_time();
+            }
+            e1_known = true;
+            first_ts = mn;
+            E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
+            grid.tumbling = wtype == EK_WINDOW_TUMBLING;
+            grid.origin = grid.tumbling ? E1 : E1 - L;
+            grid.P = P;
+            if (pend_n) {
+                if (int rc = flush_pending()) return rc;
+            }
+        }
+        {
+            int64_t save = arrivals;
+            arrivals = arrival_base;
+            int rc = process(db, sorted, start, d_acc, min_acc, s.max_ts, nullptr);
+            arrivals = save;
+            if (rc) return rc;
+        }
+        return record_time();
+    }
+
+    int record_time() {
+        hipEventRecord(ev1, stream);
+        if (hipEventSynchronize(ev1) == hipSuccess) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, ev0, ev1);
+            stats.last_batch_device_ms = ms;
+        }
+        return 0;
+    }
+
+    // ------------------------------------------------------------------ poll
+    int poll(int32_t memory, ek_result* out) {
+        memset(out, 0, sizeof *out);
+        int64_t nw = (int64_t)wins.size();
+        out->n_windows = nw;
+        out->n_aggs = plan.n_aggs;
+        out->memory = memory;
+        std::vector<int64_t> wc(nw);
+        std::vector<int32_t> we(nw);
+        std::vector<int64_t> wmc(nw);
+        std::vector<uint64_t> wmh(nw);
+        if (nw) {
+            hipMemcpyAsync(wc.data(), r_wcnt.p, nw * 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(we.data(), r_werr.p, nw * 4, hipMemcpyDeviceToHost, stream);
+            if (plan.debug_membership) {
+                hipMemcpyAsync(wmc.data(), r_wmc.p, nw * 8, hipMemcpyDeviceToHost, stream);
+                hipMemcpyAsync(wmh.data(), r_wmh.p, nw * 8, hipMemcpyDeviceToHost, stream);
+            }
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "poll sync failed");
+        h_ws.assign(nw, 0); h_we.assign(nw, 0); h_off.assign(nw, 0); h_cnt.assign(nw, 0); h_st.assign(nw, 0);
+        h_mc.assign(nw, 0); h_mh.assign(nw, 0);
+        int64_t total = 0;
+        for (int64_t w = 0; w < nw; ++w) {
+            h_ws[w] = wins[w].start;
+            h_we[w] = wins[w].end;
+            h_st[w] = we[w];
+            h_cnt[w] = we[w] ? 0 : wc[w];   // an errored window emits only its error (operations.go:108-113)
+            h_mc[w] = wmc[w];
+            h_mh[w] = wmh[w];
+            total += h_cnt[w];
+        }
+        stats.rows_out += total;
+        out->win_start = h_ws.data();
+        out->win_end = h_we.data();
+        out->win_row_count = h_cnt.data();
+        out->win_status = h_st.data();
+        out->win_member_count = h_mc.data();
+        out->win_member_hash = h_mh.data();
+        if (memory == EK_MEM_DEVICE) {
+            for (int64_t w = 0; w < nw; ++w) h_off[w] = wins[w].out_base;
+            out->win_row_offset = h_off.data();
+            out->n_rows = r_rows_used;
+            out->key = (uint32_t*)r_key.p;
+            for (int k = 0; k < plan.n_aggs; ++k) {
+                out->agg_value[k] = (int64_t*)r_val[k].p;
+                out->agg_tag[k] = (uint8_t*)r_tag[k].p;
+            }
+            return 0;
+        }
+        h_key.resize(total);
+        for (int k = 0; k < plan.n_aggs; ++k) { h_val[k].resize(total); h_tag[k].resize(total); }
+        int64_t o = 0;
+        for (int64_t w = 0; w < nw; ++w) {
+            h_off[w] = o;
+            int64_t c = h_cnt[w];
+            if (c) {
+                int64_t base = wins[w].out_base;
+                hipMemcpyAsync(h_key.data() + o, (uint32_t*)r_key.p + base, c * 4, hipMemcpyDeviceToHost, stream);
+                for (int k = 0; k < plan.n_aggs; ++k) {
+                    hipMemcpyAsync(h_val[k].data() + o, (int64_t*)r_val[k].p + base, c * 8, hipMemcpyDeviceToHost, stream);
+                    hipMemcpyAsync(h_tag[k].data() + o, (uint8_t*)r_tag[k].p + base, c, hipMemcpyDeviceToHost, stream);
+                }
+            }
+            o += c;
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "poll copy failed");
+        out->win_row_offset = h_off.data();
+        out->n_rows = total;
+        out->key = h_key.data();
+        for (int k = 0; k < plan.n_aggs; ++k) { out->agg_value[k] = h_val[k].data(); out->agg_tag[k] = h_tag[k].data(); }
+        return 0;
+    }
+
+    int release_results() {
+        // windows handed out are dropped; device regions are recycled
+        int64_t nw = (int64_t)wins.size();
+        if (nw && r_wcnt.p) {
+            hipMemsetAsync(r_wcnt.p, 0, nw * 8, stream);
+            hipMemsetAsync(r_werr.p, 0, nw * 4, stream);
+            hipMemsetAsync(r_wmc.p, 0, nw * 8, stream);
+            hipMemsetAsync(r_wmh.p, 0, nw * 8, stream);
+        }
+        wins.clear();
+        r_rows_used = 0;
+        return 0;
+    }
+
+    int reset() {
+        hipStreamSynchronize(stream);
+        release_results();
+        reset_state();
+        return hipStreamSynchronize(stream) == hipSuccess ? 0 : fail(EK_ERR_DEVICE, "reset sync failed");
+    }
+
+    ~Engine() {
+        if (stream) hipStreamSynchronize(stream);
+        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash); release(bstats);
+        release(cmax); release(acc); release(bounds_val); release(bounds_idx); release(hist); release(offs); release(tiles);
+        release(st_klo);
+        for (int v = 0; v < kMaxVC; ++v) { release(st_val[v]); release(st_valid[v]); }
+        for (int c = 0; c < EK_MAX_COLUMNS; ++c) { release(in_cols[c]); release(in_valid[c]); release(pend_cols[c]); release(pend_valid[c]); }
+        release(pend_arr_d);
+        release(wdesc); release(r_key); release(r_wcnt); release(r_werr); release(r_wmc); release(r_wmh);
+        for (int k = 0; k < EK_MAX_AGGS; ++k) { release(r_val[k]); release(r_tag[k]); }
+        if (d_plan) hipFree(d_plan);
+        if (h_stats) hipHostFree(h_stats);
+        if (h_small) hipHostFree(h_small);
+        if (h_wdesc) hipHostFree(h_wdesc);
+        if (ev0) hipEventDestroy(ev0);
+        if (ev1) hipEventDestroy(ev1);
+        if (stream && own_stream) hipStreamDestroy(stream);
+    }
+};
+
+// ---------------------------------------------------------------------- C ABI
+static thread_local std::string g_create_error;
+
+extern "C" {
+
+int ek_abi_version(void) { return EKGPU_ABI_VERSION; }
+
+int ek_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ek_create(const ek_plan* plan, int device, void** out_handle) {
+    if (!plan || !out_handle) return EK_ERR_INVALID;
+    *out_handle = nullptr;
+    Engine* e = new (std::nothrow) Engine();
+    if (!e) return EK_ERR_NOMEM;
+    int rc = e->init(plan, device);
+    if (rc) {
+        g_create_error = e->err;
+        delete e;
+        return rc;
+    }
+    *out_handle = e;
+    return 0;
+}
+
+int ek_push_batch(void* h, const ek_batch* batch) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->push(batch);
+}
+
+int ek_poll_results(void* h, int32_t memory, ek_result* out) {
+    if (!h || !out) return EK_ERR_INVALID;
+    return ((Engine*)h)->poll(memory, out);
+}
+
+int ek_release_results(void* h, ek_result* res) {
+    if (!h) return EK_ERR_INVALID;
+    if (res) memset(res, 0, sizeof *res);
+    return ((Engine*)h)->release_results();
+}
+
+int ek_reset(void* h) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->reset();
+}
+
+int ek_sync(void* h) {
+    if (!h) return EK_ERR_INVALID;
+    return hipStreamSynchronize(((Engine*)h)->stream) == hipSuccess ? 0 : EK_ERR_DEVICE;
+}
+
+int ek_set_stream(void* h, void* s) {
+    if (!h) return EK_ERR_INVALID;
+    Engine* e = (Engine*)h;
+    hipStreamSynchronize(e->stream);
+    if (s) {
+        if (e->own_stream) hipStreamDestroy(e->stream);
+        e->stream = (hipStream_t)s;
+        e->own_stream = false;
+    } else if (!e->own_stream) {
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+        e->own_stream = true;
+    }
+    return 0;
+}
+
+int ek_get_stats(void* h, ek_stats* out) {
+    if (!h || !out) return EK_ERR_INVALID;
+    *out = ((Engine*)h)->stats;
+    return 0;
+}
+
+const char* ek_last_error(void* h) {
+    if (!h) return g_create_error.c_str();
+    return ((Engine*)h)->err.c_str();
+}
+
+int ek_destroy(void* h) {
+    delete (Engine*)h;
+    return 0;
+}
+
+}  // extern "C"

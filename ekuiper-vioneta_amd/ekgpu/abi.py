@@ -64,6 +64,7 @@ class ek_plan(C.Structure):
         ("key_column", C.c_int32),
         ("num_keys", C.c_uint32),
         ("debug_membership", C.c_int32),
+        ("nullable_mask", C.c_uint32),
         ("n_aggs", C.c_int32),
         ("aggs", ek_agg_spec * EK_MAX_AGGS),
         ("n_where", C.c_int32),

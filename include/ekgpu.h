@@ -109,6 +109,7 @@ typedef struct {
     int32_t key_column;           /* GROUP BY dimension as dense u32 id; -1 = no GROUP BY       */
     uint32_t num_keys;            /* exclusive bound of key ids                                 */
     int32_t debug_membership;     /* 1: report per-window member count + member-set hash        */
+    uint32_t nullable_mask;       /* bit c: column c may carry a validity array (NULLs)         */
     int32_t n_aggs;
     ek_agg_spec aggs[EK_MAX_AGGS];
     int32_t n_where;
@@ -195,6 +196,10 @@ int ek_push_batch(void* h, const ek_batch* batch);
  * the engine; EK_MEM_DEVICE hands out device pointers. Valid until ek_release_results. */
 int ek_poll_results(void* h, int32_t memory, ek_result* out);
 int ek_release_results(void* h, ek_result* res);
+
+/* Forget all stream state (watermark, open windows, unpolled results) but keep the device
+ * allocations, so that a new stream can be pushed without re-creating the handle. */
+int ek_reset(void* h);
 
 /* Wait for all work queued on the handle's stream. */
 int ek_sync(void* h);

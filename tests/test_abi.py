@@ -1,0 +1,98 @@
+"""CPU-side checks of the boundary: the C-ABI library loads and exports every declared symbol; the
+ctypes mirror matches the header; the rule compiler builds the plans the configs need."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from ekgpu import abi as A
+from ekgpu.rule import RuleError, compile_rule
+from ekgpu.synth import IOT_SCHEMA
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ekgpu.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ek_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from ekgpu import engine
+    L = engine.lib()
+    names = declared_functions()
+    assert len(names) >= 12
+    for name in names:
+        assert hasattr(L, name), name
+    assert set(names) <= set(engine.EXPORTED_SYMBOLS)
+    assert L.ek_abi_version() == A.EKGPU_ABI_VERSION
+
+
+def test_header_constants_match_ctypes():
+    txt = open(HEADER).read()
+    for name in ("EK_MAX_COLUMNS", "EK_MAX_AGGS", "EK_MAX_PROG", "EKGPU_ABI_VERSION"):
+        m = re.search(rf"#define {name} (\d+)", txt)
+        assert int(m.group(1)) == getattr(A, name)
+    for name, val in re.findall(r"(EK_(?:WINDOW|AGG|OP|UNIT|COL|TAG|WIN|MEM)_[A-Z_]+)\s*=\s*(-?\d+)", txt):
+        assert getattr(A, name) == int(val), name
+
+
+def test_plan_struct_layout():
+    # offsets the C side sees (computed by the compiler through a tiny probe library)
+    import subprocess, tempfile
+    src = r'''
+#include <stddef.h>
+#include "ekgpu.h"
+size_t off_aggs(void){return offsetof(ek_plan,aggs);} size_t off_having(void){return offsetof(ek_plan,having_prog);}
+size_t size_plan(void){return sizeof(ek_plan);} size_t size_result(void){return sizeof(ek_result);}
+size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){return sizeof(ek_batch);}
+'''
+    d = tempfile.mkdtemp()
+    with open(os.path.join(d, "p.c"), "w") as f:
+        f.write(src)
+    so = os.path.join(d, "p.so")
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(d, "p.c")])
+    P = C.CDLL(so)
+    for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch"):
+        getattr(P, fn).restype = C.c_size_t
+    assert P.off_aggs() == A.ek_plan.aggs.offset
+    assert P.off_having() == A.ek_plan.having_prog.offset
+    assert P.size_plan() == C.sizeof(A.ek_plan)
+    assert P.size_result() == C.sizeof(A.ek_result)
+    assert P.off_rkey() == A.ek_result.key.offset
+    assert P.size_batch() == C.sizeof(A.ek_batch)
+
+
+def test_compile_baseline_configs():
+    r = compile_rule("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo "
+                     "GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", IOT_SCHEMA, num_keys=65536)
+    p = r.plan
+    assert (p.window_type, p.time_unit, p.length, p.key_column, p.n_aggs) == (A.EK_WINDOW_TUMBLING, A.EK_UNIT_SS, 10, 0, 3)
+    assert [p.aggs[k].fn for k in range(3)] == [A.EK_AGG_AVG, A.EK_AGG_MAX, A.EK_AGG_COUNT_STAR]
+    assert [f.name for f in r.fields] == ["deviceId", "avg", "max", "count"]
+    r = compile_rule("SELECT deviceId, sum(temperature), min(temperature), max(temperature) FROM demo "
+                     "GROUP BY deviceId, HOPPINGWINDOW(ss, 60, 5)", IOT_SCHEMA, num_keys=1 << 20)
+    assert (r.plan.window_type, r.plan.length, r.plan.interval) == (A.EK_WINDOW_HOPPING, 60, 5)
+    r = compile_rule("SELECT deviceId, stddev(temperature), var(temperature) FROM demo GROUP BY deviceId, "
+                     "COUNTWINDOW(1000) HAVING count(*) > 1", IOT_SCHEMA, num_keys=1 << 20, is_event_time=False)
+    assert (r.plan.window_type, r.plan.length, r.plan.n_having) == (A.EK_WINDOW_COUNT, 1000, 3)
+    assert r.plan.aggs[2].fn == A.EK_AGG_COUNT_STAR
+    r = compile_rule("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
+                     "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)", IOT_SCHEMA, num_keys=100)
+    assert r.plan.aggs[1].fn == A.EK_AGG_PERCENTILE_CONT and r.plan.aggs[1].param == 0.9
+    with pytest.raises(RuleError):
+        compile_rule("SELECT temperature FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", IOT_SCHEMA, num_keys=4)
+
+
+def test_engine_without_gpu_fails_loudly():
+    """No CPU fallback: creating an engine without a HIP device must raise, not silently compute."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ekgpu.engine import Engine, EngineError
+    r = compile_rule("SELECT deviceId, count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)",
+                     IOT_SCHEMA, num_keys=16)
+    with pytest.raises(EngineError):
+        Engine(r.plan)
