@@ -12,7 +12,7 @@
 namespace ek {
 
 constexpr int kBlock = 256;       // 4 wave64s per workgroup
-constexpr int kMaxVC = 8;         // value columns referenced by aggregates
+constexpr int kMaxVC = 4;         // value columns referenced by aggregates
 
 // fields kept per (pane, key) in the pane-partial state and per key in LDS tables
 enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32 };
@@ -173,8 +173,7 @@ __device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, con
 }
 
 // WHERE decision: 1 keep, 0 drop, -1 error (filter_operator.go:63-77: nil -> drop, non-bool -> error)
-__device__ __forceinline__ int where_decide(const DPlan& p, const DBatch& b, int64_t row) {
-    if (p.n_where <= 0) return 1;
+__device__ inline int where_decide_slow(const DPlan& p, const DBatch& b, int64_t row) {
     Val v = eval_prog(p.where_prog, p.n_where, p, &b, row, nullptr);
     if (v.tag == V_BOOL) return v.i ? 1 : 0;
     if (v.tag == V_NULL) return 0;

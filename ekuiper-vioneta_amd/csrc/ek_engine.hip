@@ -43,9 +43,19 @@ struct WinInfo {
     int64_t start, end;
     int64_t out_base;    // first row of the window's result region
     int32_t slot;        // index into win_cnt / win_err device arrays
-    int64_t member_count;
-    uint64_t member_hash;
+    bool direct;         // rows emitted by k_agg (whole tumbling pane inside one group)
 };
+
+// NVC-specialised launches (value columns referenced by aggregates: 1..kMaxVC)
+template <int N>
+void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLayout lay, const uint32_t* start,
+                const uint32_t* totals, Staging st, DState ds, Results res) {
+    hipLaunchKernelGGL(k_agg<N>, g, dim3(kAggBlock), lds, s, p, gd, lay, start, totals, st, ds, res);
+}
+template <int N>
+void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res) {
+    hipLaunchKernelGGL(k_finalize<N>, g, dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
+}
 
 int64_t floordiv_h(int64_t a, int64_t b) {
     int64_t q = a / b;
@@ -164,11 +174,11 @@ struct Engine {
     // ---- device memory
     DevBuf state_buf, pane_err, pane_mcnt, pane_mhash;
     DState dstate{};
-    DevBuf bstats;                     // BatchStats
+    DevBuf bstats, bstats_part;        // BatchStats, per-block partials of k_stats
     BatchStats* h_stats = nullptr;     // pinned
     int64_t* h_small = nullptr;        // pinned scratch (bounds)
     size_t h_small_cap = 0;
-    DevBuf cmax, acc, bounds_val, bounds_idx, hist, offs, tiles;
+    DevBuf cmax, acc, bounds_val, bounds_idx, chist, totals, pstart, pcursor, direct_d;
     DevBuf st_klo, st_val[kMaxVC], st_valid[kMaxVC];
     int64_t st_cap = 0;
     DevBuf in_cols[EK_MAX_COLUMNS], in_valid[EK_MAX_COLUMNS];   // H2D staging for host batches
@@ -341,7 +351,7 @@ struct Engine {
             bytes_per_key += (f & NEED_CNT ? 4 : 0) + (f & NEED_SUM ? 8 : 0) + (f & NEED_MIN ? 8 : 0) + (f & NEED_MAX ? 8 : 0) +
                              (f & NEED_M2 ? 8 : 0) + (f & NEED_FSUM ? 8 : 0);
         }
-        int want = env_int("EKGPU_KBITS", 8);
+        int want = env_int("EKGPU_KBITS", 10);
         kbits = 0;
         while ((1u << kbits) < K && kbits < want) kbits++;
         while (kbits > 0 && ((1 << kbits) * bytes_per_key) > 48 * 1024) kbits--;
@@ -419,6 +429,7 @@ struct Engine {
         M = W = kMinTs;
         E1 = first_ts = 0;
         next_win = 0;
+        reg_win = 0;
         arrivals = 0;
         pend_n = 0;
         pend_min = INT64_MAX;
@@ -445,32 +456,48 @@ struct Engine {
         return E1 - L + q * P;
     }
 
-    int claim_slots(int64_t qa, int64_t qb) {
+    // Bind panes [qa, qb] to ring slots. A pane new to its slot is "fresh": its partials are written
+    // (not merged) by the next k_agg, or zeroed here when `zero` (panes no group ever touched).
+    int claim_slots(int64_t qa, int64_t qb, uint64_t* fresh, bool zero) {
         int64_t first_live = win_first_pane(next_win);
+        if (fresh) *fresh = 0;
         for (int64_t q = qa; q <= qb; ++q) {
             int s = (int)(q % ring);
             if (slot_pane[s] == q) continue;
             if (slot_pane[s] != INT64_MIN && slot_pane[s] >= first_live)
                 return fail(EK_ERR_UNSUPPORTED, "pane ring overflow (pane %lld needs slot %d held by live pane %lld)",
                             (long long)q, s, (long long)slot_pane[s]);
-            // zero the slot's partials
+            slot_pane[s] = q;
+            if (fresh && q - qa < 64) *fresh |= 1ull << (q - qa);
+            if (!zero) continue;
             size_t per = (size_t)Kpad * 8;
             hipMemsetAsync((char*)dstate.cnt + s * per, 0, per, stream);
-            for (int v = 0; v < dp.n_vc; ++v) {
-                if (dstate.vcnt[v]) hipMemsetAsync((char*)dstate.vcnt[v] + s * per, 0, per, stream);
-                if (dstate.sum[v]) hipMemsetAsync((char*)dstate.sum[v] + s * per, 0, per, stream);
-                if (dstate.mn[v]) hipMemsetAsync((char*)dstate.mn[v] + s * per, 0, per, stream);
-                if (dstate.mx[v]) hipMemsetAsync((char*)dstate.mx[v] + s * per, 0, per, stream);
-                if (dstate.m2[v]) hipMemsetAsync((char*)dstate.m2[v] + s * per, 0, per, stream);
-                if (dstate.fsum[v]) hipMemsetAsync((char*)dstate.fsum[v] + s * per, 0, per, stream);
-            }
             hipMemsetAsync((char*)pane_err.p + s * 4, 0, 4, stream);
             hipMemsetAsync((char*)pane_mcnt.p + s * 8, 0, 8, stream);
             hipMemsetAsync((char*)pane_mhash.p + s * 8, 0, 8, stream);
-            slot_pane[s] = q;
         }
         return 0;
     }
+
+    // pinned host bump buffer for small per-launch descriptors (reset once per push, after a sync)
+    int64_t* h_desc = nullptr;
+    size_t h_desc_cap = 0, h_desc_used = 0;
+    int64_t* desc_alloc(size_t n) {
+        if (h_desc_used + n > h_desc_cap) {
+            hipStreamSynchronize(stream);
+            if (h_desc_cap < n) {
+                if (h_desc) hipHostFree(h_desc);
+                h_desc_cap = std::max<size_t>(n, 1 << 16);
+                if (hipHostMalloc((void**)&h_desc, h_desc_cap * 8) != hipSuccess) { h_desc = nullptr; h_desc_cap = 0; return nullptr; }
+            }
+            h_desc_used = 0;
+        }
+        int64_t* r = h_desc + h_desc_used;
+        h_desc_used += n;
+        return r;
+    }
+    DevBuf pbnd_d;
+    size_t pbnd_used = 0;
 
     // ------------------------------------------------------------------ results
     int ensure_results(int64_t add_rows, int64_t add_wins) {
@@ -534,6 +561,27 @@ struct Engine {
         return ws;
     }
 
+    // Windows are registered (result region + index) strictly in trigger order, possibly before
+    // their rows exist: a tumbling pane emitted directly by k_agg registers every earlier window first.
+    int64_t reg_win = 0;               // next window index to register
+    int register_until(int64_t j) {
+        while (reg_win <= j) {
+            if (int rc = ensure_results((int64_t)K, 1)) return rc;
+            WinInfo wi{};
+            wi.j = reg_win;
+            wi.end = win_end(reg_win);
+            wi.start = window_start(reg_win);
+            wi.out_base = r_rows_used;
+            wi.slot = (int32_t)wins.size();
+            wi.direct = false;
+            r_rows_used += K;
+            wins.push_back(wi);
+            reg_win++;
+        }
+        return 0;
+    }
+    WinInfo& win_info(int64_t j) { return wins[(size_t)(j - wins.front().j)]; }
+
     // Emit every window j >= next_win with E_j <= W whose panes are complete (last pane <= q_done).
     int finalize_ready(int64_t q_done) {
         if (!e1_known || !has_W) return 0;
@@ -541,9 +589,12 @@ struct Engine {
         while (win_end(j1) <= W && win_last_pane(j1) <= q_done) j1++;
         if (j1 == j0) return 0;
         int64_t n = j1 - j0;
-        // windows whose panes were never claimed hold no events: claim (zero) them so the merge reads zeros
-        if (int rc = claim_slots(std::max<int64_t>(0, win_first_pane(j0)), win_last_pane(j1 - 1))) return rc;
-        if (int rc = ensure_results(n * (int64_t)K, n)) return rc;
+        if (int rc = register_until(j1 - 1)) return rc;
+        // panes no group touched hold no events: bind and zero them so the merge reads empty partials
+        for (int64_t j = j0; j < j1; ++j) {
+            if (win_info(j).direct) continue;
+            if (int rc = claim_slots(std::max<int64_t>(0, win_first_pane(j)), win_last_pane(j), nullptr, true)) return rc;
+        }
         if (h_wdesc_used + n > h_wdesc_cap) {
             hipStreamSynchronize(stream);  // every earlier descriptor upload has completed
             if (h_wdesc_cap < (size_t)n) {
@@ -556,25 +607,34 @@ struct Engine {
         WinDesc* hd = h_wdesc + h_wdesc_used;
         h_wdesc_used += n;
         if (int rc = ensure(wdesc, (size_t)n * sizeof(WinDesc))) return rc;
-        for (int64_t j = j0; j < j1; ++j) {
-            WinInfo wi{};
-            wi.j = j;
-            wi.end = win_end(j);
-            wi.start = window_start(j);
-            wi.out_base = r_rows_used;
-            wi.slot = (int32_t)wins.size();
-            r_rows_used += K;
-            WinDesc& d = hd[j - j0];
-            d.q_first = std::max<int64_t>(0, win_first_pane(j));
-            d.q_last = win_last_pane(j);
-            d.out_base = wi.out_base;
-            d.idx = wi.slot;
-            wins.push_back(wi);
+        // descriptors: windows needing the pane merge first, then the direct ones (membership only)
+        int64_t nf = 0;
+        for (int64_t j = j0; j < j1; ++j) nf += win_info(j).direct ? 0 : 1;
+        int64_t k = 0;
+        for (int pass = 0; pass < 2; ++pass)
+            for (int64_t j = j0; j < j1; ++j) {
+                const WinInfo& wi = win_info(j);
+                if (wi.direct != (pass == 1)) continue;
+                WinDesc& d = hd[k++];
+                d.q_first = std::max<int64_t>(0, win_first_pane(j));
+                d.q_last = win_last_pane(j);
+                d.out_base = wi.out_base;
+                d.idx = wi.slot;
+            }
+        if (nf || plan.debug_membership)
+            hipMemcpyAsync(wdesc.p, hd, (size_t)n * sizeof(WinDesc), hipMemcpyHostToDevice, stream);
+        if (nf) {
+            dim3 grid_f((unsigned)((K + kBlock - 1) / kBlock), (unsigned)nf);
+            const int nvc = std::max(1, dp.n_vc);
+            Results rv = results_view();
+            const WinDesc* wd = (const WinDesc*)wdesc.p;
+            switch (nvc) {
+            case 1: launch_fin<1>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
+            case 2: launch_fin<2>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
+            case 3: launch_fin<3>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
+            default: launch_fin<4>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
+            }
         }
-        hipMemcpyAsync(wdesc.p, hd, (size_t)n * sizeof(WinDesc), hipMemcpyHostToDevice, stream);
-        dim3 grid((unsigned)((K + kBlock - 1) / kBlock), (unsigned)n);
-        hipLaunchKernelGGL(k_finalize, grid, dim3(kBlock), 0, stream, d_plan, (const WinDesc*)wdesc.p, dstate, ring,
-                           (const int32_t*)pane_err.p, results_view());
         if (plan.debug_membership) {
             hipLaunchKernelGGL(k_win_members, dim3((unsigned)n), dim3(64), 0, stream, (const WinDesc*)wdesc.p, ring,
                                (const int64_t*)pane_mcnt.p, (const unsigned long long*)pane_mhash.p, (int64_t*)r_wmc.p,
@@ -589,13 +649,18 @@ struct Engine {
     int process(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t min_acc, int64_t max_ts,
                 const int64_t* d_arrival) {
         int64_t n = db.n;
+        // size the result store once for every window this batch will close
+        if (W >= win_end(next_win)) {
+            int64_t nclose = (W - win_end(next_win)) / H + 1;
+            if (int rc = ensure_results(nclose * (int64_t)K, nclose)) return rc;
+        }
         int64_t q_lo = std::max<int64_t>(0, pane_host(min_acc));
         int64_t q_hi = pane_host(max_ts);
         if (q_hi < 0) return 0;   // every event precedes the first hopping window
         int64_t first_live = win_first_pane(next_win);
         q_lo = std::max(q_lo, first_live);
 
-        struct Grp { int64_t lo, hi, qa, qb; bool complete; };
+        struct Grp { int64_t lo, hi, qa, qb; bool complete; int64_t bk; };
         std::vector<Grp> groups;
         if (sorted) {
             // pane boundaries by binary search on the sorted ts column
@@ -606,15 +671,9 @@ struct Engine {
                 h_small_cap = std::max<size_t>(2 * nb, 4096);
                 if (hipHostMalloc((void**)&h_small, h_small_cap * 8) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
             }
-            for (int64_t k = 0; k < nq; ++k) h_small[k] = pane_start(q_lo + k);
-            if (h_small[0] == INT64_MIN) h_small[0] = INT64_MIN + 1;
-            h_small[nq] = INT64_MAX;
-            if (int rc = ensure(bounds_val, (size_t)nb * 8)) return rc;
             if (int rc = ensure(bounds_idx, (size_t)nb * 8)) return rc;
-            hipMemcpyAsync(bounds_val.p, h_small, (size_t)nb * 8, hipMemcpyHostToDevice, stream);
-            hipLaunchKernelGGL(k_lower_bound, dim3((nb + 255) / 256), dim3(256), 0, stream,
-                               (const int64_t*)db.col[dp.ts_col], start, n, (const int64_t*)bounds_val.p, nb,
-                               (int64_t*)bounds_idx.p);
+            hipLaunchKernelGGL(k_pane_bounds, dim3((nb + 255) / 256), dim3(256), 0, stream,
+                               (const int64_t*)db.col[dp.ts_col], start, n, grid, q_lo, nb, (int64_t*)bounds_idx.p);
             hipMemcpyAsync(h_small + nb, bounds_idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "bounds sync failed");
             const int64_t* b = h_small + nb;
@@ -628,7 +687,7 @@ struct Engine {
                     // split one big pane into several groups
                     for (int64_t s = lo; s < hi; s += group_events) {
                         int64_t e = std::min(hi, s + group_events);
-                        groups.push_back(Grp{s, e, q_lo + k, q_lo + k, e == hi});
+                        groups.push_back(Grp{s, e, q_lo + k, q_lo + k, e == hi, -1});
                     }
                     k++;
                     continue;
@@ -637,20 +696,31 @@ struct Engine {
                     kk++;
                     hi = b[kk + 1];
                 }
-                if (hi > lo) groups.push_back(Grp{lo, hi, q_lo + k, q_lo + kk, true});
-                else groups.push_back(Grp{lo, lo, q_lo + k, q_lo + kk, true});
+                groups.push_back(Grp{lo, std::max(lo, hi), q_lo + k, q_lo + kk, true, k});
                 k = kk + 1;
             }
         } else {
             if (q_hi - q_lo + 1 > max_panes_group)
                 return fail(EK_ERR_UNSUPPORTED, "out-of-order batch spans %lld panes (max %d): split the batch",
                             (long long)(q_hi - q_lo + 1), max_panes_group);
-            groups.push_back(Grp{start, n, q_lo, q_hi, true});
+            groups.push_back(Grp{start, n, q_lo, q_hi, true, -1});
         }
 
+        const int64_t* bidx = sorted ? h_small + (q_hi - q_lo + 2) : nullptr;
         for (const Grp& g : groups) {
             if (g.hi > g.lo) {
-                if (int rc = run_group(db, g.lo, g.hi, g.qa, g.qb, d_acc)) return rc;
+                // pane boundaries of the group (sorted batches): pbnd[k] = first event of pane qa + k
+                std::vector<int64_t> pb;
+                if (sorted) {
+                    int npn = (int)(g.qb - g.qa + 1);
+                    pb.resize(npn + 1);
+                    for (int k = 0; k <= npn; ++k) pb[k] = g.bk >= 0 ? bidx[g.bk + k] : (k == 0 ? g.lo : g.hi);
+                    pb[0] = g.lo;
+                    pb[npn] = g.hi;
+                }
+                // whole_panes: the group holds every event of this batch for each of its panes
+                if (int rc = run_group(db, g.lo, g.hi, g.qa, g.qb, d_acc, sorted ? pb.data() : nullptr,
+                                       !sorted || g.bk >= 0)) return rc;
                 if (plan.debug_membership) {
                     hipLaunchKernelGGL(k_members, dim3(256), dim3(kBlock), 0, stream, d_plan, db, grid, d_acc,
                                        (int)(d_acc != nullptr), g.lo, g.hi, arrivals, d_arrival, g.qa, g.qb, ring,
@@ -663,9 +733,11 @@ struct Engine {
         return finalize_ready(q_hi);
     }
 
-    int run_group(const DBatch& db, int64_t lo, int64_t hi, int64_t qa, int64_t qb, const uint8_t* d_acc) {
-        if (int rc = claim_slots(qa, qb)) return rc;
+    size_t direct_used = 0;
+    int run_group(const DBatch& db, int64_t lo, int64_t hi, int64_t qa, int64_t qb, const uint8_t* d_acc,
+                  const int64_t* pbnd_host, bool whole_panes) {
         GroupDesc gd{};
+        if (int rc = claim_slots(qa, qb, &gd.fresh, false)) return rc;
         gd.lo = lo;
         gd.hi = hi;
         gd.q_lo = qa;
@@ -673,18 +745,21 @@ struct Engine {
         gd.nb = NB;
         gd.kbits = kbits;
         gd.chunk = chunk;
-        gd.nch = (int32_t)((hi - lo + chunk - 1) / chunk);
+        gd.abase = lo & ~(int64_t)15;
+        gd.key_col = dp.key_col;
+        gd.ts_col = dp.ts_col;
+        gd.n_where = dp.n_where;
+        gd.num_keys = dp.num_keys;
+        gd.nbatch = db.n;
+        gd.nch = (int32_t)((hi - gd.abase + chunk - 1) / chunk);
         gd.np = gd.n_panes * NB;
         gd.ring = ring;
         gd.has_accept = d_acc != nullptr;
+        gd.sorted = pbnd_host != nullptr;
+        gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
+        if (gd.n_panes > kMaxGroupPanes) return fail(EK_ERR_UNSUPPORTED, "group spans %d panes", gd.n_panes);
         if (gd.np > np_max) return fail(EK_ERR_UNSUPPORTED, "too many partitions in a group (%d)", gd.np);
-        int64_t nh = (int64_t)gd.np * gd.nch + 1;
-        if (int rc = ensure(hist, (size_t)nh * 4)) return rc;
-        if (int rc = ensure(offs, (size_t)nh * 4)) return rc;
-        int64_t ntile = (nh + kScanTile - 1) / kScanTile;
-        if (ntile > 1024 * 64) return fail(EK_ERR_UNSUPPORTED, "histogram too large");
-        if (int rc = ensure(tiles, (size_t)ntile * 4)) return rc;
-        int64_t ne = hi - lo;
+        int64_t ne = (hi - lo) + 8LL * NB * gd.n_panes + 64;   // 8-aligned runs + vector over-read slack
         if (ne > st_cap) {
             if (int rc = ensure(st_klo, (size_t)ne * 2)) return rc;
             for (int v = 0; v < dp.n_vc; ++v) {
@@ -696,28 +771,99 @@ struct Engine {
         }
         Staging st{};
         st.klo = (uint16_t*)st_klo.p;
+        bool any_nullable = false;
         for (int v = 0; v < dp.n_vc; ++v) {
             st.val[v] = (int64_t*)st_val[v].p;
             if (db.valid[dp.vc_col[v]]) {
                 st.valid[v] = (uint8_t*)st_valid[v].p;
                 st.nullable_mask |= 1u << v;
+                any_nullable = true;
             }
         }
-        size_t lds_np = (size_t)gd.np * 4;
-        hipMemsetAsync((char*)hist.p + (nh - 1) * 4, 0, 4, stream);
-        hipLaunchKernelGGL(k_hist, dim3(gd.nch), dim3(kBlock), lds_np, stream, d_plan, db, grid, gd, d_acc,
-                           (uint32_t*)hist.p, (int32_t*)pane_err.p);
-        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)ntile), dim3(kBlock), 0, stream, (const uint32_t*)hist.p, nh,
-                           (uint32_t*)tiles.p);
-        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, stream, (uint32_t*)tiles.p, (int)ntile);
-        hipLaunchKernelGGL(k_scan_down, dim3((unsigned)ntile), dim3(kBlock), 0, stream, (const uint32_t*)hist.p, nh,
-                           (const uint32_t*)tiles.p, (uint32_t*)offs.p);
-        hipLaunchKernelGGL(k_scatter, dim3(gd.nch), dim3(kBlock), lds_np, stream, d_plan, db, grid, gd, d_acc,
-                           (const uint32_t*)offs.p, st);
-        hipLaunchKernelGGL(k_agg, dim3(gd.np), dim3(kBlock), (size_t)lay.bytes, stream, d_plan, gd, lay,
-                           (const uint32_t*)offs.p, st, dstate);
+        // pane boundary indices of this group (kernel argument)
+        for (int k = 0; k < 65; ++k) gd.pbnd[k] = 0;
+        if (pbnd_host) for (int k = 0; k <= gd.n_panes; ++k) gd.pbnd[k] = pbnd_host[k];
+        for (int r = 0; r < 64; ++r) { gd.dbase[r] = -1; gd.didx[r] = -1; }
+
+        // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
+        const int lp_stride = gd.sorted ? std::min(gd.np, NB * max_panes_in_chunk(pbnd_host, gd)) : gd.np;
+        size_t lds_h = (size_t)std::max(lp_stride, 1) * 4;
+        if (int rc = ensure(chist, (size_t)gd.nch * lp_stride * 4)) return rc;
+        if (int rc = ensure(totals, (size_t)gd.np * 4)) return rc;
+        if (int rc = ensure(pstart, (size_t)(gd.np + 1) * 4)) return rc;
+        if (int rc = ensure(pcursor, (size_t)gd.np * 4)) return rc;
+        hipLaunchKernelGGL(k_group_prep, dim3(1), dim3(1024), 0, stream, gd, (uint32_t*)totals.p, (int32_t*)pane_err.p,
+                           (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
+        const bool wh = dp.n_where > 0;
+#define EK_COUNT(S, W) hipLaunchKernelGGL((k_count<S, W>), dim3(gd.nch), dim3(kBlock), lds_h, stream, d_plan, db, grid, gd, d_acc, \
+                                          (uint32_t*)chist.p, lp_stride, (uint32_t*)totals.p, (int32_t*)pane_err.p)
+        if (gd.sorted) { if (wh) EK_COUNT(true, true); else EK_COUNT(true, false); }
+        else { if (wh) EK_COUNT(false, true); else EK_COUNT(false, false); }
+#undef EK_COUNT
+        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, stream, (const uint32_t*)totals.p, gd.np,
+                           (uint32_t*)pstart.p, (uint32_t*)pcursor.p);
+        if (lp_stride <= kMaxLocalParts) {
+            const int nvc = std::max(1, dp.n_vc);
+            size_t lds_s = scatter_lds_bytes(nvc, any_nullable);
+            const uint32_t* ch = (const uint32_t*)chist.p;
+            uint32_t* pc = (uint32_t*)pcursor.p;
+            dim3 gs(gd.nch);
+#define EK_SCATTER(S, W, N) hipLaunchKernelGGL((k_scatter<S, W, N>), gs, dim3(kBlock), lds_s, stream, d_plan, db, grid, gd, d_acc, ch, lp_stride, pc, st)
+#define EK_SCATTER_N(S, W) switch (nvc) { case 1: EK_SCATTER(S, W, 1); break; case 2: EK_SCATTER(S, W, 2); break; \
+                                          case 3: EK_SCATTER(S, W, 3); break; default: EK_SCATTER(S, W, 4); break; }
+            if (gd.sorted) { if (wh) { EK_SCATTER_N(true, true) } else { EK_SCATTER_N(true, false) } }
+            else { if (wh) { EK_SCATTER_N(false, true) } else { EK_SCATTER_N(false, false) } }
+#undef EK_SCATTER_N
+#undef EK_SCATTER
+        } else {
+#define EK_SD(S, W) hipLaunchKernelGGL((k_scatter_direct<S, W>), dim3(gd.nch), dim3(kBlock), lds_h, stream, d_plan, db, grid, gd, \
+                                       d_acc, (const uint32_t*)chist.p, lp_stride, (uint32_t*)pcursor.p, st)
+            if (gd.sorted) { if (wh) EK_SD(true, true); else EK_SD(true, false); }
+            else { if (wh) EK_SD(false, true); else EK_SD(false, false); }
+#undef EK_SD
+        }
+        // direct emission: a fresh tumbling pane whose whole content is in this group and whose window
+        // closes at this batch's watermark is finalised by k_agg itself (no pane-state round trip)
+        if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes) {
+            for (int r = 0; r < gd.n_panes && r < 64; ++r) {
+                int64_t q = qa + r;
+                if (!((gd.fresh >> r) & 1ull) || win_end(q) > W || q < next_win) continue;
+                if (int rc = register_until(q)) return rc;
+                WinInfo& wi = win_info(q);
+                wi.direct = true;
+                gd.dbase[r] = wi.out_base;
+                gd.didx[r] = wi.slot;
+            }
+        }
+        {
+            const int nvc = std::max(1, dp.n_vc);
+            Results rv = results_view();
+            dim3 ga(gd.np);
+            switch (nvc) {
+            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
+            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
+            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
+            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
+            }
+        }
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
         return 0;
+    }
+
+    // most panes any chunk of the group overlaps (sorted groups)
+    int max_panes_in_chunk(const int64_t* pb, const GroupDesc& gd) const {
+        if (!pb) return gd.n_panes;
+        int best = 1;
+        for (int64_t a0 = gd.abase; a0 < gd.hi; a0 += gd.chunk) {
+            int64_t c0 = std::max(gd.lo, a0);
+            int64_t c1 = std::min(gd.hi, a0 + gd.chunk);
+            int a = 0;
+            while (a + 1 < gd.n_panes && pb[a + 1] <= c0) a++;
+            int b = a;
+            while (b + 1 < gd.n_panes && pb[b + 1] < c1) b++;
+            best = std::max(best, b - a + 1);
+        }
+        return best;
     }
 
     // Accepted events that arrived before the first watermark release are kept (host side, tiny:
@@ -815,11 +961,11 @@ struct Engine {
         stats.records_in += n;
 
         // ---- 1. batch statistics (one pass over ts)
-        BatchStats init{INT64_MAX, INT64_MIN, 0, INT64_MAX, 0, 0};
-        *h_stats = init;
-        hipMemcpyAsync(bstats.p, h_stats, sizeof(BatchStats), hipMemcpyHostToDevice, stream);
-        int sblocks = (int)std::min<int64_t>(2048, (n + 2 * kBlock - 1) / (2 * kBlock));
-        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats.p);
+        int sblocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
+        if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
+        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats_part.p);
+        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
+                           (BatchStats*)bstats.p);
         hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
         BatchStats s = *h_stats;
@@ -862,6 +1008,9 @@ struct Engine {
         int64_t arrival_base = arrivals;
         arrivals += n;
         h_wdesc_used = 0;   // the stats sync above drained every earlier descriptor upload
+        h_desc_used = 0;
+        pbnd_used = 0;
+        direct_used = 0;
 
         // ---- 3. watermark advance (watermark_op.go:157-214): W = max ts - lateTol
         if (!has_M || s.max_ts > M) {
@@ -1006,8 +1155,9 @@ struct Engine {
 
     ~Engine() {
         if (stream) hipStreamSynchronize(stream);
-        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash); release(bstats);
-        release(cmax); release(acc); release(bounds_val); release(bounds_idx); release(hist); release(offs); release(tiles);
+        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash); release(bstats); release(bstats_part);
+        release(cmax); release(acc); release(bounds_val); release(bounds_idx); release(chist); release(totals);
+        release(pstart); release(pcursor); release(direct_d);
         release(st_klo);
         for (int v = 0; v < kMaxVC; ++v) { release(st_val[v]); release(st_valid[v]); }
         for (int c = 0; c < EK_MAX_COLUMNS; ++c) { release(in_cols[c]); release(in_valid[c]); release(pend_cols[c]); release(pend_valid[c]); }
@@ -1018,6 +1168,8 @@ struct Engine {
         if (h_stats) hipHostFree(h_stats);
         if (h_small) hipHostFree(h_small);
         if (h_wdesc) hipHostFree(h_wdesc);
+        if (h_desc) hipHostFree(h_desc);
+        release(pbnd_d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
         if (stream && own_stream) hipStreamDestroy(stream);

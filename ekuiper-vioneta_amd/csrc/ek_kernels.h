@@ -49,25 +49,75 @@ __device__ __forceinline__ int64_t wave_max64(int64_t v) {
 }
 
 // ---------------------------------------------------------------- k_stats
-__global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts, int64_t n, BatchStats* st) {
+// One streaming pass over ts (16 B per lane per load): min, max and "arrival order is non-decreasing".
+__global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts, int64_t n, BatchStats* part) {
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     int uns = 0;
-    const int64_t stride = (int64_t)gridDim.x * kBlock * 2;
-    for (int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2; i < n; i += stride) {
-        int64_t a = ts[i];
-        int64_t b = (i + 1 < n) ? ts[i + 1] : a;
-        int64_t p = (i > 0) ? ts[i - 1] : a;
-        uns |= (a < p) | (b < a);
-        mn = min(mn, min(a, b));
-        mx = max(mx, max(a, b));
+    const int64_t npair = n >> 1;
+    const longlong2* t2 = (const longlong2*)ts;
+    const int lane = threadIdx.x & 63;
+    constexpr int U = 4;   // pairs in flight per thread
+    const int64_t stride = (int64_t)gridDim.x * kBlock * U;
+    for (int64_t base = (int64_t)blockIdx.x * kBlock * U; base < npair; base += stride) {
+        longlong2 v[U];
+        int64_t lp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int64_t pi = base + u * kBlock + threadIdx.x;
+            v[u] = pi < npair ? t2[pi] : make_longlong2(INT64_MAX, INT64_MAX);
+            lp[u] = (lane == 0 && pi > 0 && pi < npair) ? ts[2 * pi - 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int64_t pi = base + u * kBlock + threadIdx.x;
+            // previous element of this pair = .y of the lane below; lane 0 reads it from memory
+            int64_t prev = __shfl_up(v[u].y, 1, 64);
+            if (lane == 0) prev = pi > 0 ? lp[u] : v[u].x;
+            if (pi < npair) {
+                uns |= (v[u].x < prev) | (v[u].y < v[u].x);
+                mn = min(mn, min(v[u].x, v[u].y));
+                mx = max(mx, max(v[u].x, v[u].y));
+            }
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd tail element
+        int64_t last = ts[n - 1];
+        mn = min(mn, last);
+        mx = max(mx, last);
+        if (n > 1) uns |= last < ts[n - 2];
     }
     mn = wave_min64(mn);
     mx = wave_max64(mx);
     uns = __any(uns);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin((long long*)&st->min_ts, (long long)mn);
-        atomicMax((long long*)&st->max_ts, (long long)mx);
-        if (uns) atomicOr(&st->unsorted, 1);
+    // one partial per block (same-address atomics from every wave would serialise at the memory side)
+    __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
+    __shared__ int suns[kBlock / 64];
+    if (lane == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; suns[threadIdx.x >> 6] = uns; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); uns |= suns[w]; }
+        part[blockIdx.x] = BatchStats{mn, mx, 0, INT64_MAX, uns, 0};
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    int uns = 0;
+    for (int k = threadIdx.x; k < nb; k += 1024) { mn = min(mn, part[k].min_ts); mx = max(mx, part[k].max_ts); uns |= part[k].unsorted; }
+    mn = wave_min64(mn);
+    mx = wave_max64(mx);
+    uns = __any(uns);
+    __shared__ int64_t smn[16], smx[16];
+    __shared__ int su[16];
+    if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; su[threadIdx.x >> 6] = uns; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); uns |= su[w]; }
+        st->min_ts = mn;
+        st->max_ts = mx;
+        st->unsorted = uns;
+        st->n_accepted = 0;
+        st->min_accepted = INT64_MAX;
     }
 }
 
@@ -147,6 +197,21 @@ __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ t
     }
 }
 
+// first index in [lo, hi) with ts >= start of pane q_lo + k (sorted batches; k = 0 -> lo for pane 0 of tumbling)
+__global__ void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, PaneGrid g, int64_t q_lo, int nb,
+                              int64_t* out) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nb) return;
+    int64_t q = q_lo + k;
+    if (k == nb - 1) { out[k] = hi; return; }
+    int64_t x;
+    if (g.tumbling) x = q == 0 ? INT64_MIN : g.origin + (q - 1) * g.P;
+    else x = g.origin + q * g.P;
+    int64_t a = lo, b = hi;
+    while (a < b) { int64_t m = (a + b) >> 1; if (ts[m] < x) a = m + 1; else b = m; }
+    out[k] = a;
+}
+
 // first index in [lo, hi) with ts >= bound[k] (sorted batches)
 __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
                               int64_t* out) {
@@ -169,64 +234,147 @@ struct GroupDesc {
     int32_t np;            // partitions = n_panes * nb
     int32_t ring;          // pane-slot ring size
     int32_t has_accept;    // acc[] valid
+    int32_t sorted;        // ts non-decreasing: pane of event i from the pane index boundaries pbnd[]
+    int32_t pad;           // diagnostic knobs (0 in production)
+    int64_t abase;         // chunk grid origin: lo rounded down to 16 rows (chunk k = [abase + k*chunk, +chunk) ∩ [lo, hi))
+    int64_t nbatch;        // rows in the batch (vector loads never read past it)
+    // hot plan scalars (kernel arguments stay in SGPRs; DPlan loads inside LDS-atomic loops re-issue)
+    int32_t key_col, ts_col, n_where;
+    uint32_t num_keys;
+    uint64_t fresh;        // bit r: pane q_lo + r was claimed for this group (its partials are written, not merged)
+    // small per-group descriptors travel in the kernel arguments (no tiny H2D copies per launch)
+    int64_t pbnd[65];      // sorted groups: pbnd[k] = first event of pane q_lo + k (k <= n_panes)
+    int64_t dbase[64];     // direct emission: result row base of pane r's window, or -1
+    int32_t didx[64];      // direct emission: window index of pane r
 };
 
-__device__ __forceinline__ int part_of(const DPlan& p, const DBatch& b, const PaneGrid& g, const GroupDesc& gd,
-                                       const uint8_t* acc, int64_t i, int64_t* q_out) {
-    if (gd.has_accept && !acc[i]) return -1;
-    int64_t q = pane_of(g, ((const int64_t*)b.col[p.ts_col])[i]);
-    int64_t rel = q - gd.q_lo;
-    if (q < 0 || rel < 0 || rel >= gd.n_panes) return -1;
-    uint32_t key = p.key_col >= 0 ? ((const uint32_t*)b.col[p.key_col])[i] : 0u;
-    if (key >= p.num_keys && p.key_col >= 0) return -1;
-    *q_out = q;
-    return (int)rel * gd.nb + (int)(key >> gd.kbits);
+constexpr int kMaxGroupPanes = 64;
+constexpr int kTile = 2048;                  // events staged and sorted in LDS per step of k_scatter
+constexpr int kTileE = kTile / kBlock;       // events per thread per tile
+constexpr int kMaxLocalParts = 2048;         // chunk-local partitions sorted through LDS
+
+__device__ __forceinline__ void chunk_range(const GroupDesc& gd, int64_t* a0, int64_t* c0, int64_t* c1) {
+    *a0 = gd.abase + (int64_t)blockIdx.x * gd.chunk;
+    *c0 = max(gd.lo, *a0);
+    *c1 = min(gd.hi, *a0 + gd.chunk);
 }
 
-__global__ __launch_bounds__(kBlock) void k_hist(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
-                                                 const uint8_t* __restrict__ acc, uint32_t* __restrict__ hist,
-                                                 int32_t* __restrict__ pane_err) {
+// Pane range [pa, pb] touched by the chunk [c0, c1). pbnd[k] = first event of pane q_lo + k (k <= n_panes).
+__device__ __forceinline__ void chunk_panes(const GroupDesc& gd, int64_t c0, int64_t c1, int* pa, int* pb) {
+    const int64_t* pbnd = gd.pbnd;
+    if (!gd.sorted) { *pa = 0; *pb = gd.n_panes - 1; return; }
+    int a = 0;
+    while (a + 1 < gd.n_panes && pbnd[a + 1] <= c0) a++;
+    int b = a;
+    while (b + 1 < gd.n_panes && pbnd[b + 1] < c1) b++;
+    *pa = a;
+    *pb = b;
+}
+
+constexpr int kMaxChunkBnd = 64;
+// boundaries strictly inside the chunk -> LDS (sorted groups): event i's pane is pa + #(lb <= i)
+__device__ __forceinline__ int chunk_bounds(const GroupDesc& gd, int pa, int pb, int64_t* lb) {
+    const int64_t* pbnd = gd.pbnd;
+    if (!gd.sorted) return 0;
+    const int n = min(pb - pa, kMaxChunkBnd);
+    for (int k = threadIdx.x; k < n; k += blockDim.x) lb[k] = pbnd[pa + 1 + k];
+    return n;
+}
+
+// Local partition of event i (-1: dropped: late, outside the group's panes, or filtered by WHERE).
+// For sorted groups the pane comes from the event index (cursor `k` advances monotonically per thread).
+template <bool SORTED, bool WHERE>
+__device__ __forceinline__ int local_part(const DPlan& p, const DBatch& b, const PaneGrid& g, const GroupDesc& gd,
+                                          const int64_t* lb, int nlb, const uint8_t* acc, int64_t i, int pa, uint32_t key,
+                                          int32_t* pane_err, bool check_where) {
+    int rel;
+    if (SORTED) {
+        rel = pa;
+        for (int k = 0; k < nlb; ++k) rel += (i >= lb[k]) ? 1 : 0;
+    } else {
+        if (gd.has_accept && !acc[i]) return -1;
+        int64_t q = pane_of(g, ((const int64_t*)b.col[gd.ts_col])[i]);
+        int64_t r = q - gd.q_lo;
+        if (q < 0 || r < 0 || r >= gd.n_panes) return -1;
+        rel = (int)r;
+    }
+    if (gd.key_col >= 0 && key >= gd.num_keys) return -1;
+    if (WHERE) {
+        int w = where_decide_slow(p, b, i);
+        if (w < 0) {
+            if (check_where) atomicOr(&pane_err[(gd.q_lo + rel) % gd.ring], EK_WIN_WHERE_ERROR);
+            return -1;
+        }
+        if (w == 0) return -1;
+    }
+    return (rel - pa) * gd.nb + (int)(key >> gd.kbits);
+}
+
+__device__ __forceinline__ uint32_t load_key(const DPlan& p, const DBatch& b, int64_t i) {
+    return p.key_col >= 0 ? ((const uint32_t*)b.col[p.key_col])[i] : 0u;
+}
+
+// Per chunk: histogram over its chunk-local partitions (pane, key bucket) of the rows that pass WHERE,
+// stored compactly as chist[chunk][lp] (lp < lp_stride), plus the group-wide totals per partition.
+template <bool SORTED, bool WHERE>
+__global__ __launch_bounds__(kBlock) void k_count(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
+                                                  const uint8_t* __restrict__ acc,
+                                                  uint32_t* __restrict__ chist, int lp_stride, uint32_t* __restrict__ totals,
+                                                  int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
     const DPlan& p = *pp;
-    for (int k = threadIdx.x; k < gd.np; k += kBlock) lh[k] = 0;
+    int64_t a0, c0, c1;
+    chunk_range(gd, &a0, &c0, &c1);
+    int pa, pb;
+    chunk_panes(gd, c0, c1, &pa, &pb);
+    const int lp_n = (pb - pa + 1) * gd.nb;
+    __shared__ int64_t lb[kMaxChunkBnd];
+    const int nlb = chunk_bounds(gd, pa, pb, lb);
+    for (int k = threadIdx.x; k < lp_n; k += kBlock) lh[k] = 0;
     __syncthreads();
-    int64_t c0 = gd.lo + (int64_t)blockIdx.x * gd.chunk;
-    int64_t c1 = min(gd.hi, c0 + gd.chunk);
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
-        int64_t q;
-        int pid = part_of(p, b, g, gd, acc, i, &q);
-        if (pid < 0) continue;
-        int w = where_decide(p, b, i);
-        if (w < 0) { atomicOr(&pane_err[q % gd.ring], EK_WIN_WHERE_ERROR); continue; }
-        if (w == 0) continue;
-        atomicAdd(&lh[pid], 1u);
+    const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
+    constexpr int V = 4;   // 16-byte key loads in flight per thread (16 keys)
+    for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
+        uint4 kv[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const int64_t i = base + (int64_t)u * kBlock * 4;
+            if (kcol && i + 3 < gd.nbatch && i < c1) kv[u] = *(const uint4*)(kcol + i);
+            else if (kcol && i < c1) {
+                kv[u].x = kcol[i];
+                kv[u].y = i + 1 < gd.nbatch ? kcol[i + 1] : 0u;
+                kv[u].z = i + 2 < gd.nbatch ? kcol[i + 2] : 0u;
+                kv[u].w = i + 3 < gd.nbatch ? kcol[i + 3] : 0u;
+            } else kv[u] = make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            const uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t i = base + (int64_t)u * kBlock * 4 + e;
+                if (i < c0 || i >= c1) continue;
+                const int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, kk[e], pane_err, true);
+                if (lp >= 0) atomicAdd(&lh[lp], 1u);
+            }
+        }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < gd.np; k += kBlock) hist[(int64_t)k * gd.nch + blockIdx.x] = lh[k];
-}
-
-// ---- exclusive scan (3 phase) over u32 counts -> u32 offsets
-constexpr int kScanTile = 4096;
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, int64_t n, uint32_t* tile_sum) {
-    int64_t base = (int64_t)blockIdx.x * kScanTile;
-    uint32_t s = 0;
-    for (int k = threadIdx.x; k < kScanTile; k += kBlock) {
-        int64_t i = base + k;
-        if (i < n) s += in[i];
+    for (int k = threadIdx.x; k < lp_stride; k += kBlock) {
+        uint32_t c = k < lp_n ? lh[k] : 0u;
+        chist[(int64_t)blockIdx.x * lp_stride + k] = c;
+        if (c) atomicAdd(&totals[pa * gd.nb + k], c);
     }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    __shared__ uint32_t w[4];
-    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) tile_sum[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
 }
 
-__global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* tile_sum, int nt) {
+// Exclusive scan of the np partition totals (single workgroup): start[p], and cursor[p] = start[p].
+__global__ __launch_bounds__(1024) void k_scan_parts(const uint32_t* __restrict__ totals, int np, uint32_t* start,
+                                                     uint32_t* cursor) {
     __shared__ uint32_t part[1024];
-    int per = (nt + 1023) / 1024;
-    int b = threadIdx.x * per, e = min(nt, b + per);
+    int per = (np + 1023) / 1024;
+    int b = threadIdx.x * per, e = min(np, b + per);
     uint32_t s = 0;
-    for (int i = b; i < e; ++i) s += tile_sum[i];
+    for (int i = b; i < e; ++i) s += (totals[i] + 7u) & ~7u;   // runs start 8-aligned
     part[threadIdx.x] = s;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -236,29 +384,8 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* tile_sum, int nt)
         __syncthreads();
     }
     uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = b; i < e; ++i) { uint32_t v = tile_sum[i]; tile_sum[i] = run; run += v; }
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t* __restrict__ in, int64_t n,
-                                                      const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ out) {
-    // each thread owns 16 consecutive elements of the 4096-element tile
-    __shared__ uint32_t ts[kBlock];
-    int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * 16;
-    uint32_t v[16];
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { int64_t i = base + k; v[k] = i < n ? in[i] : 0; s += v[k]; }
-    ts[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < kBlock; o <<= 1) {
-        uint32_t t = threadIdx.x >= o ? ts[threadIdx.x - o] : 0;
-        __syncthreads();
-        ts[threadIdx.x] += t;
-        __syncthreads();
-    }
-    uint32_t run = tile_off[blockIdx.x] + (threadIdx.x ? ts[threadIdx.x - 1] : 0);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { int64_t i = base + k; if (i < n) out[i] = run; run += v[k]; }
+    for (int i = b; i < e; ++i) { start[i] = run; cursor[i] = run; run += (totals[i] + 7u) & ~7u; }
+    if (threadIdx.x == 1023) start[np] = part[1023];
 }
 
 struct Staging {
@@ -268,23 +395,169 @@ struct Staging {
     uint32_t nullable_mask;   // bit v: staging carries validity for value column v
 };
 
+// Block-wide exclusive scan of cnt[0..n) in LDS (n <= kMaxLocalParts); cnt[n] receives the total.
+__device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
+    const int per = (n + kBlock - 1) / kBlock;
+    const int b = threadIdx.x * per, e = min(n, b + per);
+    uint32_t s = 0;
+    for (int k = b; k < e; ++k) s += cnt[k];
+    // inclusive scan of the per-thread sums across the wave, then across the 4 waves
+    uint32_t x = s;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < wv; ++w) wbase += wsum[w];
+    uint32_t run = wbase + x - s;
+    for (int k = b; k < e; ++k) { uint32_t c = cnt[k]; cnt[k] = run; run += c; }
+    if (threadIdx.x == kBlock - 1) cnt[n] = run;
+    __syncthreads();
+}
+
+// Route the chunk's rows into contiguous per-partition staging runs. Each tile of kTile rows is
+// loaded (all loads issued before any use), counting-sorted by chunk-local partition in LDS, then
+// written out so that consecutive lanes write consecutive addresses of a run (coalesced).
+template <bool SORTED, bool WHERE, int NVC>
 __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
-                                                    const uint8_t* __restrict__ acc, const uint32_t* __restrict__ off,
-                                                    Staging st) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+                                                    const uint8_t* __restrict__ acc,
+                                                    const uint32_t* __restrict__ chist, int lp_stride,
+                                                    uint32_t* __restrict__ cursor, Staging st) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DPlan& p = *pp;
-    for (int k = threadIdx.x; k < gd.np; k += kBlock) cur[k] = off[(int64_t)k * gd.nch + blockIdx.x];
+    int64_t a0, c0, c1;
+    chunk_range(gd, &a0, &c0, &c1);
+    int pa, pb;
+    chunk_panes(gd, c0, c1, &pa, &pb);
+    const int lp_n = (pb - pa + 1) * gd.nb;
+    __shared__ int64_t lb[kMaxChunkBnd];
+    const int nlb = chunk_bounds(gd, pa, pb, lb);
+    // LDS carve (16-byte aligned pieces)
+    int64_t* s_val = (int64_t*)smem;                                          // [NVC][kTile]
+    uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [kMaxLocalParts]
+    uint32_t* tcnt = cur + kMaxLocalParts;                                    // [kMaxLocalParts + 1]
+    uint16_t* s_klo = (uint16_t*)(tcnt + kMaxLocalParts + 4);                 // [kTile]
+    uint16_t* s_lp = s_klo + kTile;                                           // [kTile]
+    uint8_t* s_vd = (uint8_t*)(s_lp + kTile);                                 // [NVC][kTile]
+    __shared__ uint32_t wsum[4];
+    // reserve this chunk's run in every partition it feeds (runs of one partition land in any chunk order)
+    for (int k = threadIdx.x; k < lp_n; k += kBlock) {
+        uint32_t c = chist[(int64_t)blockIdx.x * lp_stride + k];
+        cur[k] = c ? atomicAdd(&cursor[pa * gd.nb + k], c) : 0u;
+    }
+    const uint32_t kmask = (1u << gd.kbits) - 1u;
+    const bool nullable = st.nullable_mask != 0;
+    const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
+    // row of (thread t, slot j) in a tile: t0 + (j/2)*2*kBlock + 2t + (j&1): lanes read 8-byte key pairs
+    // and 16-byte value pairs, each wave instruction one contiguous span
+    for (int64_t t0 = a0; t0 < c1; t0 += kTile) {
+        // issue every load of the tile first
+        uint32_t key[kTileE];
+        int64_t val[NVC][kTileE];
+#pragma unroll
+        for (int m = 0; m < kTileE / 2; ++m) {
+            const int64_t i = t0 + (int64_t)m * 2 * kBlock + 2 * threadIdx.x;
+            const bool full = i + 1 < gd.nbatch && i < c1;
+            if (full) {
+                uint2 kp = kcol ? *(const uint2*)(kcol + i) : make_uint2(0, 0);
+                key[2 * m] = kp.x;
+                key[2 * m + 1] = kp.y;
+            } else {
+                key[2 * m] = (kcol && i < gd.nbatch) ? kcol[i] : 0u;
+                key[2 * m + 1] = 0u;
+            }
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                if (v < p.n_vc && full) {
+                    longlong2 vp = *(const longlong2*)((const int64_t*)b.col[p.vc_col[v]] + i);
+                    val[v][2 * m] = vp.x;
+                    val[v][2 * m + 1] = vp.y;
+                } else {
+                    val[v][2 * m] = (v < p.n_vc && i < gd.nbatch) ? ((const int64_t*)b.col[p.vc_col[v]])[i] : 0;
+                    val[v][2 * m + 1] = 0;
+                }
+            }
+        }
+        for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
+        __syncthreads();
+        int lp[kTileE];
+        uint32_t rank[kTileE];
+#pragma unroll
+        for (int j = 0; j < kTileE; ++j) {
+            const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+            lp[j] = (i >= c0 && i < c1) ? local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, key[j], nullptr, false) : -1;
+            if (lp[j] >= 0) rank[j] = atomicAdd(&tcnt[lp[j]], 1u);
+        }
+        __syncthreads();
+        block_excl_scan(tcnt, lp_n, wsum);
+        // place rows at their sorted LDS position
+#pragma unroll
+        for (int j = 0; j < kTileE; ++j) {
+            if (lp[j] < 0) continue;
+            const uint32_t s = tcnt[lp[j]] + rank[j];
+            s_klo[s] = (uint16_t)(key[j] & kmask);
+            s_lp[s] = (uint16_t)lp[j];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) s_val[v * kTile + s] = val[v][j];
+            if (nullable) {
+                const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+#pragma unroll
+                for (int v = 0; v < NVC; ++v)
+                    if (st.nullable_mask & (1u << v)) s_vd[v * kTile + s] = col_valid(b, p.vc_col[v], i) ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        const uint32_t total = tcnt[lp_n];
+        for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
+            const int l = s_lp[s];
+            const uint32_t gpos = cur[l] + (s - tcnt[l]);
+            st.klo[gpos] = s_klo[s];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                if (v >= p.n_vc) break;
+                st.val[v][gpos] = s_val[v * kTile + s];
+                if (st.nullable_mask & (1u << v)) st.valid[v][gpos] = s_vd[v * kTile + s];
+            }
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] += tcnt[k + 1] - tcnt[k];
+        __syncthreads();
+    }
+}
+
+inline size_t scatter_lds_bytes(int nvc, bool nullable) {
+    return (size_t)nvc * kTile * 8 + (size_t)(2 * kMaxLocalParts + 4) * 4 + (size_t)kTile * 4 + (nullable ? (size_t)nvc * kTile : 0);
+}
+
+// Fallback for chunks touching more than kMaxLocalParts partitions: one scattered store per row.
+template <bool SORTED, bool WHERE>
+__global__ __launch_bounds__(kBlock) void k_scatter_direct(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
+                                                           const uint8_t* __restrict__ acc,
+                                                           const uint32_t* __restrict__ chist, int lp_stride,
+                                                           uint32_t* __restrict__ cursor, Staging st) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t curd[];
+    const DPlan& p = *pp;
+    int64_t a0, c0, c1;
+    chunk_range(gd, &a0, &c0, &c1);
+    int pa, pb;
+    chunk_panes(gd, c0, c1, &pa, &pb);
+    const int lp_n = (pb - pa + 1) * gd.nb;
+    __shared__ int64_t lb[kMaxChunkBnd];
+    const int nlb = chunk_bounds(gd, pa, pb, lb);
+    for (int k = threadIdx.x; k < lp_n; k += kBlock) {
+        uint32_t c = chist[(int64_t)blockIdx.x * lp_stride + k];
+        curd[k] = c ? atomicAdd(&cursor[pa * gd.nb + k], c) : 0u;
+    }
     __syncthreads();
     const uint32_t kmask = (1u << gd.kbits) - 1u;
-    int64_t c0 = gd.lo + (int64_t)blockIdx.x * gd.chunk;
-    int64_t c1 = min(gd.hi, c0 + gd.chunk);
     for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
-        int64_t q;
-        int pid = part_of(p, b, g, gd, acc, i, &q);
-        if (pid < 0) continue;
-        if (where_decide(p, b, i) != 1) continue;
-        uint32_t pos = atomicAdd(&cur[pid], 1u);
-        uint32_t key = p.key_col >= 0 ? ((const uint32_t*)b.col[p.key_col])[i] : 0u;
+        const uint32_t key = load_key(p, b, i);
+        int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, key, nullptr, false);
+        if (lp < 0) continue;
+        uint32_t pos = atomicAdd(&curd[lp], 1u);
         st.klo[pos] = (uint16_t)(key & kmask);
         for (int v = 0; v < p.n_vc; ++v) {
             int c = p.vc_col[v];
@@ -294,8 +567,22 @@ __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBat
     }
 }
 
+// per group: zero the partition totals and the per-pane scalars (WHERE error flag, membership
+// fingerprint) of freshly claimed ring slots
+__global__ void k_group_prep(GroupDesc gd, uint32_t* totals, int32_t* pane_err, int64_t* pane_mcnt,
+                             unsigned long long* pane_mhash) {
+    for (int k = threadIdx.x; k < gd.np; k += blockDim.x) totals[k] = 0;
+    int r = threadIdx.x;
+    if (r < gd.n_panes && ((gd.fresh >> r) & 1ull)) {
+        int64_t s = (gd.q_lo + r) % gd.ring;
+        pane_err[s] = 0;
+        pane_mcnt[s] = 0;
+        pane_mhash[s] = 0;
+    }
+}
+
 // ---------------------------------------------------------------- per-partition aggregation
-// LDS layout per partition (kk = 1 << kbits keys): cnt u32[kk], then per value column the fields it needs.
+// LDS layout per partition (kk = 1 << kbits keys): 8-byte fields first, then u32 counts.
 struct LdsLayout {
     int32_t off_cnt;
     int32_t off_vcnt[kMaxVC];
@@ -307,131 +594,6 @@ struct LdsLayout {
     int32_t bytes;
 };
 
-__global__ __launch_bounds__(kBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
-                                                const uint32_t* __restrict__ off, Staging st, DState ds) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const DPlan& p = *pp;
-    const int pid = blockIdx.x;
-    const int kk = 1 << gd.kbits;
-    const int rel = pid / gd.nb, bucket = pid % gd.nb;
-    const int64_t q = gd.q_lo + rel;
-    const int64_t slot = q % gd.ring;
-    const uint32_t s0 = off[(int64_t)pid * gd.nch];
-    const uint32_t s1 = off[(int64_t)(pid + 1) * gd.nch];   // off has np*nch+1 entries (last = total)
-    if (s1 == s0) return;   // nothing to merge
-
-    uint32_t* lcnt = (uint32_t*)(lds + lay.off_cnt);
-    for (int k = threadIdx.x; k < lay.bytes / 4; k += kBlock) ((uint32_t*)lds)[k] = 0;
-    __syncthreads();
-    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBlock) {
-        int kl = st.klo[i];
-        atomicAdd(&lcnt[kl], 1u);
-        for (int v = 0; v < p.n_vc; ++v) {
-            if ((st.nullable_mask & (1u << v)) && !st.valid[v][i]) continue;
-            const int f = p.vc_flags[v];
-            int64_t raw = st.val[v][i];
-            if (f & NEED_CNT) atomicAdd(&((uint32_t*)(lds + lay.off_vcnt[v]))[kl], 1u);
-            if (p.vc_is_float[v]) {
-                double x = __longlong_as_double(raw);
-                if (f & NEED_SUM) atomicAdd(&((double*)(lds + lay.off_sum[v]))[kl], x);
-                if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[v]))[kl], (unsigned long long)~f64_to_ord(x));
-                if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[v]))[kl], (unsigned long long)f64_to_ord(x));
-            } else {
-                if (f & NEED_SUM) atomicAdd(&((unsigned long long*)(lds + lay.off_sum[v]))[kl], (unsigned long long)raw);
-                if (f & NEED_FSUM) atomicAdd(&((double*)(lds + lay.off_fsum[v]))[kl], (double)raw);
-                if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[v]))[kl], (unsigned long long)~i64_to_ord(raw));
-                if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[v]))[kl], (unsigned long long)i64_to_ord(raw));
-            }
-        }
-    }
-    __syncthreads();
-    bool need_m2 = false;
-    for (int v = 0; v < p.n_vc; ++v) need_m2 |= (p.vc_flags[v] & NEED_M2) != 0;
-    if (need_m2) {
-        // second pass over the (L2-resident) run: Σ (x - mean)^2 with this partial's mean (stats._variance shape)
-        for (uint32_t i = s0 + threadIdx.x; i < s1; i += kBlock) {
-            int kl = st.klo[i];
-            for (int v = 0; v < p.n_vc; ++v) {
-                if (!(p.vc_flags[v] & NEED_M2)) continue;
-                if ((st.nullable_mask & (1u << v)) && !st.valid[v][i]) continue;
-                int64_t raw = st.val[v][i];
-                double x = p.vc_is_float[v] ? __longlong_as_double(raw) : (double)raw;
-                double n = (p.vc_flags[v] & NEED_CNT) ? (double)((uint32_t*)(lds + lay.off_vcnt[v]))[kl] : (double)lcnt[kl];
-                double s = p.vc_is_float[v] ? ((double*)(lds + lay.off_sum[v]))[kl] : ((double*)(lds + lay.off_fsum[v]))[kl];
-                double d = __dsub_rn(x, __ddiv_rn(s, n));
-                atomicAdd(&((double*)(lds + lay.off_m2[v]))[kl], __dmul_rn(d, d));
-            }
-        }
-        __syncthreads();
-    }
-    // merge this partial into the pane state (the workgroup owns these (pane, key) entries)
-    for (int kl = threadIdx.x; kl < kk; kl += kBlock) {
-        uint32_t c = lcnt[kl];
-        if (c == 0) continue;
-        int64_t key = (int64_t)bucket * kk + kl;
-        int64_t e = slot * ds.K + key;
-        int64_t cprev = ds.cnt[e];
-        ds.cnt[e] = cprev + c;
-        for (int v = 0; v < p.n_vc; ++v) {
-            const int f = p.vc_flags[v];
-            int64_t nb_ = (f & NEED_CNT) ? (int64_t)((uint32_t*)(lds + lay.off_vcnt[v]))[kl] : (int64_t)c;
-            if (nb_ == 0) continue;
-            int64_t na = (f & NEED_CNT) ? ds.vcnt[v][e] : cprev;
-            if (f & NEED_CNT) ds.vcnt[v][e] = na + nb_;
-            if (p.vc_is_float[v]) {
-                double sb = (f & (NEED_SUM | NEED_M2)) ? ((double*)(lds + lay.off_sum[v]))[kl] : 0.0;
-                double sa = (f & (NEED_SUM | NEED_M2)) && na ? __longlong_as_double(ds.sum[v][e]) : 0.0;
-                if (f & NEED_M2) {
-                    double m2b = ((double*)(lds + lay.off_m2[v]))[kl];
-                    if (na == 0) ds.m2[v][e] = m2b;
-                    else {
-                        double dlt = __dsub_rn(__ddiv_rn(sb, (double)nb_), __ddiv_rn(sa, (double)na));
-                        ds.m2[v][e] = ds.m2[v][e] + m2b + dlt * dlt * ((double)na * (double)nb_ / (double)(na + nb_));
-                    }
-                }
-                if (f & NEED_SUM) ds.sum[v][e] = __double_as_longlong(na ? __dadd_rn(sa, sb) : sb);
-                if (f & NEED_MIN) {
-                    uint64_t ob = ~((unsigned long long*)(lds + lay.off_min[v]))[kl];
-                    uint64_t oa = (uint64_t)ds.mn[v][e];
-                    ds.mn[v][e] = (int64_t)(na == 0 ? ob : (ob < oa ? ob : oa));
-                }
-                if (f & NEED_MAX) {
-                    uint64_t ob = ((unsigned long long*)(lds + lay.off_max[v]))[kl];
-                    uint64_t oa = (uint64_t)ds.mx[v][e];
-                    ds.mx[v][e] = (int64_t)(na == 0 ? ob : (ob > oa ? ob : oa));
-                }
-            } else {
-                if (f & NEED_SUM) {
-                    int64_t sb = (int64_t)((unsigned long long*)(lds + lay.off_sum[v]))[kl];
-                    ds.sum[v][e] = (int64_t)((uint64_t)(na ? ds.sum[v][e] : 0) + (uint64_t)sb);
-                }
-                double fb = (f & NEED_FSUM) ? ((double*)(lds + lay.off_fsum[v]))[kl] : 0.0;
-                double fa = (f & NEED_FSUM) && na ? ds.fsum[v][e] : 0.0;
-                if (f & NEED_M2) {
-                    double m2b = ((double*)(lds + lay.off_m2[v]))[kl];
-                    if (na == 0) ds.m2[v][e] = m2b;
-                    else {
-                        double dlt = __dsub_rn(__ddiv_rn(fb, (double)nb_), __ddiv_rn(fa, (double)na));
-                        ds.m2[v][e] = ds.m2[v][e] + m2b + dlt * dlt * ((double)na * (double)nb_ / (double)(na + nb_));
-                    }
-                }
-                if (f & NEED_FSUM) ds.fsum[v][e] = na ? fa + fb : fb;
-                if (f & NEED_MIN) {
-                    uint64_t ob = ~((unsigned long long*)(lds + lay.off_min[v]))[kl];
-                    uint64_t oa = (uint64_t)ds.mn[v][e];
-                    ds.mn[v][e] = (int64_t)(na == 0 ? ob : (ob < oa ? ob : oa));
-                }
-                if (f & NEED_MAX) {
-                    uint64_t ob = ((unsigned long long*)(lds + lay.off_max[v]))[kl];
-                    uint64_t oa = (uint64_t)ds.mx[v][e];
-                    ds.mx[v][e] = (int64_t)(na == 0 ? ob : (ob > oa ? ob : oa));
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------- finalize closed windows
 struct WinDesc {
     int64_t q_first, q_last;   // panes merged into the window
     int64_t out_base;          // first result row of this window's region
@@ -447,12 +609,328 @@ struct Results {
     int32_t* win_err;      // EK_WIN_* per window
 };
 
+// Merged partial aggregate of one (window, key), kept in registers (all indices compile-time).
+template <int NVC>
+struct Part {
+    int64_t cnt;
+    int64_t vcnt[NVC];
+    int64_t isum[NVC];
+    double fsum[NVC];    // f64 sum (float columns) or f64 shadow sum (int columns with var)
+    double m2[NVC];
+    uint64_t omn[NVC], omx[NVC];
+};
+
+template <int N, typename T>
+__device__ __forceinline__ T sel(const T (&a)[N], int v) {
+    T r = a[0];
+#pragma unroll
+    for (int u = 1; u < N; ++u) if (v == u) r = a[u];
+    return r;
+}
+
+__device__ __forceinline__ double chan_m2(double m2a, double sa, int64_t na, double m2b, double sb, int64_t nb) {
+    // Chan et al. pairwise merge of (n, sum, M2) partials
+    double d = __dsub_rn(__ddiv_rn(sb, (double)nb), __ddiv_rn(sa, (double)na));
+    double w = __ddiv_rn(__dmul_rn((double)na, (double)nb), (double)(na + nb));
+    return __dadd_rn(__dadd_rn(m2a, m2b), __dmul_rn(__dmul_rn(d, d), w));
+}
+
+// merge partial b (count c, fields from arrays) into a
+template <int NVC>
+__device__ __forceinline__ void part_merge(const DPlan& p, Part<NVC>& a, int64_t c, const int64_t (&vc)[NVC],
+                                           const int64_t (&is)[NVC], const double (&fs)[NVC], const double (&m2)[NVC],
+                                           const uint64_t (&mn)[NVC], const uint64_t (&mx)[NVC]) {
+    int64_t cprev = a.cnt;
+    a.cnt += c;
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) {
+        const int f = p.vc_flags[v];
+        int64_t nb = (f & NEED_CNT) ? vc[v] : c;
+        if (nb == 0) continue;
+        int64_t na = (f & NEED_CNT) ? a.vcnt[v] : cprev;
+        a.vcnt[v] = na + nb;
+        a.isum[v] = (int64_t)((uint64_t)a.isum[v] + (uint64_t)is[v]);
+        if (f & NEED_M2) a.m2[v] = na ? chan_m2(a.m2[v], a.fsum[v], na, m2[v], fs[v], nb) : m2[v];
+        a.fsum[v] = na ? __dadd_rn(a.fsum[v], fs[v]) : fs[v];
+        a.omn[v] = (na == 0 || mn[v] < a.omn[v]) ? mn[v] : a.omn[v];
+        a.omx[v] = (na == 0 || mx[v] > a.omx[v]) ? mx[v] : a.omx[v];
+    }
+}
+
+// funcs_agg.go: the value (and Go type) of aggregate slot k for a merged group partial
+template <int NVC>
+__device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int k) {
+    const int fn = p.agg_fn[k];
+    if (fn == EK_AGG_COUNT_STAR) return Val{V_I64, s.cnt, 0.0};
+    const int v = p.agg_vc[k];
+    const int64_t n = sel(s.vcnt, v);
+    if (fn == EK_AGG_COUNT) return Val{V_I64, n, 0.0};
+    if (n == 0) return Val{V_NULL, 0, 0.0};      // every value nil
+    const bool fl = p.vc_is_float[v];
+    switch (fn) {
+    case EK_AGG_SUM: return fl ? Val{V_F64, 0, sel(s.fsum, v)} : Val{V_I64, sel(s.isum, v), 0.0};
+    case EK_AGG_AVG: {   // funcs_agg.go:56-86: int -> truncating int64 division
+        if (fl) return Val{V_F64, 0, __ddiv_rn(sel(s.fsum, v), (double)n)};
+        int64_t t = sel(s.isum, v);
+        return Val{V_I64, (t == INT64_MIN && n == -1) ? t : t / n, 0.0};
+    }
+    case EK_AGG_MIN: return fl ? Val{V_F64, 0, ord_to_f64(sel(s.omn, v))} : Val{V_I64, ord_to_i64(sel(s.omn, v)), 0.0};
+    case EK_AGG_MAX: return fl ? Val{V_F64, 0, ord_to_f64(sel(s.omx, v))} : Val{V_I64, ord_to_i64(sel(s.omx, v)), 0.0};
+    case EK_AGG_VAR: return Val{V_F64, 0, __ddiv_rn(sel(s.m2, v), (double)n)};
+    case EK_AGG_VARS: return Val{V_F64, 0, __ddiv_rn(sel(s.m2, v), (double)(n - 1))};
+    case EK_AGG_STDDEV: return Val{V_F64, 0, __dsqrt_rn(__ddiv_rn(sel(s.m2, v), (double)n))};
+    case EK_AGG_STDDEVS: return Val{V_F64, 0, __dsqrt_rn(__ddiv_rn(sel(s.m2, v), (double)(n - 1)))};
+    }
+    return Val{V_NULL, 0, 0.0};
+}
+
+__device__ __noinline__ Val having_eval(const DPlan& p, const Val* aggs) {
+    return eval_prog(p.having_prog, p.n_having, p, nullptr, 0, aggs);
+}
+
+// HAVING (having_operator.go:41-56): true keeps the group, false drops it, anything else is an error.
+template <int NVC>
+__device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, int32_t* win_err) {
+    if (p.n_having <= 0) return true;
+    Val hv[EK_MAX_AGGS];
+    for (int k = 0; k < p.n_aggs; ++k) hv[k] = agg_value(p, s, k);
+    Val h = having_eval(p, hv);
+    if (h.tag != V_BOOL) { atomicOr(win_err, EK_WIN_HAVING_ERROR); return false; }
+    return h.i != 0;
+}
+
+// Block-compacted emission of result rows: ONE returning atomic per workgroup on the window's row
+// counter (per-wave atomics from thousands of waves on one address serialise for tens of µs).
+// Every thread of the block must call it (sh: >= 17 u32 of LDS).
+template <int NVC>
+__device__ __forceinline__ void emit_rows(const DPlan& p, bool present, const Part<NVC>& s, int64_t key, int64_t out_base,
+                                          int32_t widx, Results& res, uint32_t* sh) {
+    const unsigned long long mask = __ballot(present);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0) sh[wv] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < nw; ++w) { uint32_t c = sh[w]; sh[w] = run; run += c; }
+        sh[16] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[widx], (unsigned long long)run) : 0u;
+    }
+    __syncthreads();
+    const uint32_t wbase = sh[wv], bbase = sh[16];
+    __syncthreads();   // sh is reused by the caller's next round
+    if (!present) return;
+    const int64_t pos = out_base + (int64_t)bbase + wbase + __popcll(mask & ((1ull << lane) - 1ull));
+    res.key[pos] = (uint32_t)key;
+#pragma unroll
+    for (int k = 0; k < EK_MAX_AGGS; ++k) {
+        if (k >= p.n_aggs) break;
+        Val a = agg_value(p, s, k);
+        res.tag[k][pos] = a.tag == V_NULL ? EK_TAG_NULL : (a.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+        res.val[k][pos] = a.tag == V_F64 ? __double_as_longlong(a.f) : a.i;
+    }
+}
+
+constexpr int kAggBlock = 512;
+
+// One workgroup per partition (pane, key bucket): LDS aggregation of the partition's staged run,
+// then either (a) direct emission of the final rows when the pane is a whole tumbling window that
+// closes in this batch (direct[2*rel] = out_base >= 0), or (b) write / merge into the pane state.
+template <int NVC>
+__global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
+                                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ totals,
+                                                   Staging st, DState ds, Results res) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const DPlan& p = *pp;
+    const int pid = blockIdx.x;
+    const int kk = 1 << gd.kbits;
+    const int rel = pid / gd.nb, bucket = pid % gd.nb;
+    const int64_t q = gd.q_lo + rel;
+    const int64_t slot = q % gd.ring;
+    const uint32_t s0 = start[pid];
+    const uint32_t s1 = s0 + totals[pid];
+    const bool fresh = (gd.fresh >> rel) & 1ull;
+    const int64_t dbase = rel < 64 ? gd.dbase[rel] : -1;
+    if (s1 == s0 && (!fresh || dbase >= 0)) return;   // nothing to merge / no rows to emit
+
+    uint32_t* lcnt = (uint32_t*)(lds + lay.off_cnt);
+    for (int k = threadIdx.x; k < lay.bytes / 4; k += kAggBlock) ((uint32_t*)lds)[k] = 0;
+    // plan fields in registers (scalar reloads inside the atomic loop would serialise on lgkmcnt)
+    int fl[NVC];
+    bool isf[NVC];
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) { fl[v] = p.vc_flags[v]; isf[v] = p.vc_is_float[v] != 0; }
+    const uint32_t nullm = st.nullable_mask;
+    __syncthreads();
+    // the run [s0, s0 + n) starts 8-aligned: each lane reads 8 rows per step with 16-byte loads
+    const uint32_t s_end = s0 + totals[pid];
+    for (uint32_t base = s0 + threadIdx.x * 8; base < s_end; base += kAggBlock * 8) {
+        const uint4 kq = *(const uint4*)(st.klo + base);
+        longlong2 vq[NVC][4];
+        uint2 vdq[NVC];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            if (fl[v] == 0) continue;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) vq[v][m] = *(const longlong2*)(st.val[v] + base + 2 * m);
+            if (nullm & (1u << v)) vdq[v] = *(const uint2*)(st.valid[v] + base);
+        }
+        const uint32_t kw[4] = {kq.x, kq.y, kq.z, kq.w};
+        if (gd.pad & 1) {   // diagnostic build knob: loads only
+            uint64_t acc = kq.x ^ kq.y;
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) acc ^= (uint64_t)vq[v][0].x ^ (uint64_t)vq[v][1].y ^ (uint64_t)vq[v][2].x ^ (uint64_t)vq[v][3].y;
+            if (acc == 0x123456789ull) lcnt[0] = 1;
+            continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (base + e >= s_end) break;
+            const int kl = (int)((kw[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu);
+            atomicAdd(&lcnt[kl], 1u);
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                const int f = fl[v];
+                if (f == 0) continue;
+                if ((nullm & (1u << v)) && !((e < 4 ? vdq[v].x >> (8 * e) : vdq[v].y >> (8 * (e - 4))) & 0xFFu)) continue;
+                const int64_t raw = (e & 1) ? vq[v][e >> 1].y : vq[v][e >> 1].x;
+                if (f & NEED_CNT) atomicAdd(&((uint32_t*)(lds + lay.off_vcnt[v]))[kl], 1u);
+                if (isf[v]) {
+                    const double x = __longlong_as_double(raw);
+                    if (f & NEED_SUM) atomicAdd(&((double*)(lds + lay.off_sum[v]))[kl], x);
+                    if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[v]))[kl], (unsigned long long)~f64_to_ord(x));
+                    if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[v]))[kl], (unsigned long long)f64_to_ord(x));
+                } else {
+                    if (f & NEED_SUM) atomicAdd(&((unsigned long long*)(lds + lay.off_sum[v]))[kl], (unsigned long long)raw);
+                    if (f & NEED_FSUM) atomicAdd(&((double*)(lds + lay.off_fsum[v]))[kl], (double)raw);
+                    if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[v]))[kl], (unsigned long long)~i64_to_ord(raw));
+                    if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[v]))[kl], (unsigned long long)i64_to_ord(raw));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    bool need_m2 = false;
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) need_m2 |= (p.vc_flags[v] & NEED_M2) != 0;
+    if (need_m2) {
+        // second pass over the (L2-resident) run: Σ (x - mean)^2 with this partial's mean (stats._variance shape)
+        for (uint32_t i = s0 + threadIdx.x; i < s_end; i += kAggBlock) {
+            const int kl = st.klo[i];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                if (!(p.vc_flags[v] & NEED_M2)) continue;
+                if ((st.nullable_mask & (1u << v)) && !st.valid[v][i]) continue;
+                const int64_t raw = st.val[v][i];
+                const double x = p.vc_is_float[v] ? __longlong_as_double(raw) : (double)raw;
+                const double n = (p.vc_flags[v] & NEED_CNT) ? (double)((uint32_t*)(lds + lay.off_vcnt[v]))[kl] : (double)lcnt[kl];
+                const double sm = p.vc_is_float[v] ? ((double*)(lds + lay.off_sum[v]))[kl] : ((double*)(lds + lay.off_fsum[v]))[kl];
+                const double d = __dsub_rn(x, __ddiv_rn(sm, n));
+                atomicAdd(&((double*)(lds + lay.off_m2[v]))[kl], __dmul_rn(d, d));
+            }
+        }
+        __syncthreads();
+    }
+    // this partition's partial for key kl, read back from LDS
+    auto lds_part = [&](int kl, int64_t& c, int64_t (&vc)[NVC], int64_t (&is)[NVC], double (&fs)[NVC], double (&m2)[NVC],
+                        uint64_t (&mn)[NVC], uint64_t (&mx)[NVC]) {
+        c = lcnt[kl];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            const int f = p.vc_flags[v];
+            vc[v] = (f & NEED_CNT) ? (int64_t)((uint32_t*)(lds + lay.off_vcnt[v]))[kl] : c;
+            is[v] = (!p.vc_is_float[v] && (f & NEED_SUM)) ? ((int64_t*)(lds + lay.off_sum[v]))[kl] : 0;
+            fs[v] = p.vc_is_float[v] ? ((f & NEED_SUM) ? ((double*)(lds + lay.off_sum[v]))[kl] : 0.0)
+                                     : ((f & NEED_FSUM) ? ((double*)(lds + lay.off_fsum[v]))[kl] : 0.0);
+            m2[v] = (f & NEED_M2) ? ((double*)(lds + lay.off_m2[v]))[kl] : 0.0;
+            mn[v] = (f & NEED_MIN) ? ~((unsigned long long*)(lds + lay.off_min[v]))[kl] : 0ull;
+            mx[v] = (f & NEED_MAX) ? ((unsigned long long*)(lds + lay.off_max[v]))[kl] : 0ull;
+        }
+    };
+    if (gd.pad & 2) return;   // diagnostic build knob: no emission / merge
+    __shared__ uint32_t esh[20];
+    if (dbase >= 0) {
+        const int32_t widx = gd.didx[rel];
+        const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
+        for (int kb = 0; kb < kk; kb += kAggBlock) {
+            const int kl = kb + threadIdx.x;
+            const int64_t key = (int64_t)bucket * kk + kl;
+            Part<NVC> s{};
+            bool present = false;
+            if (kl < kk && key < K) {
+                int64_t c, vc[NVC], is[NVC];
+                double fs[NVC], m2[NVC];
+                uint64_t mn[NVC], mx[NVC];
+                lds_part(kl, c, vc, is, fs, m2, mn, mx);
+                if (c > 0) {
+                    part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+                    present = having_keep(p, s, &res.win_err[widx]);
+                }
+            }
+            emit_rows(p, present, s, key, dbase, widx, res, esh);
+        }
+        return;
+    }
+    // write (fresh pane) or merge into the pane state; the workgroup owns these (pane, key) entries
+    for (int kl = threadIdx.x; kl < kk; kl += kAggBlock) {
+        const int64_t e = slot * ds.K + (int64_t)bucket * kk + kl;
+        int64_t c, vc[NVC], is[NVC];
+        double fs[NVC], m2[NVC];
+        uint64_t mn[NVC], mx[NVC];
+        lds_part(kl, c, vc, is, fs, m2, mn, mx);
+        if (fresh) {
+            ds.cnt[e] = c;       // count 0 marks an absent key
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                const int f = p.vc_flags[v];
+                if (f & NEED_CNT) ds.vcnt[v][e] = vc[v];
+                if (f & NEED_SUM) ds.sum[v][e] = p.vc_is_float[v] ? __double_as_longlong(fs[v]) : is[v];
+                if (f & NEED_FSUM) ds.fsum[v][e] = fs[v];
+                if (f & NEED_M2) ds.m2[v][e] = m2[v];
+                if (f & NEED_MIN) ds.mn[v][e] = (int64_t)mn[v];
+                if (f & NEED_MAX) ds.mx[v][e] = (int64_t)mx[v];
+            }
+            continue;
+        }
+        if (c == 0) continue;
+        Part<NVC> a{};
+        int64_t avc[NVC], ais[NVC];
+        double afs[NVC], am2[NVC];
+        uint64_t amn[NVC], amx[NVC];
+        const int64_t ac = ds.cnt[e];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            const int f = p.vc_flags[v];
+            avc[v] = (f & NEED_CNT) ? ds.vcnt[v][e] : ac;
+            ais[v] = (!p.vc_is_float[v] && (f & NEED_SUM)) ? ds.sum[v][e] : 0;
+            afs[v] = p.vc_is_float[v] ? ((f & NEED_SUM) ? __longlong_as_double(ds.sum[v][e]) : 0.0) : ((f & NEED_FSUM) ? ds.fsum[v][e] : 0.0);
+            am2[v] = (f & NEED_M2) ? ds.m2[v][e] : 0.0;
+            amn[v] = (f & NEED_MIN) ? (uint64_t)ds.mn[v][e] : 0ull;
+            amx[v] = (f & NEED_MAX) ? (uint64_t)ds.mx[v][e] : 0ull;
+        }
+        if (ac) part_merge(p, a, ac, avc, ais, afs, am2, amn, amx);
+        part_merge(p, a, c, vc, is, fs, m2, mn, mx);
+        ds.cnt[e] = a.cnt;
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            const int f = p.vc_flags[v];
+            if (f & NEED_CNT) ds.vcnt[v][e] = a.vcnt[v];
+            if (f & NEED_SUM) ds.sum[v][e] = p.vc_is_float[v] ? __double_as_longlong(a.fsum[v]) : a.isum[v];
+            if (f & NEED_FSUM) ds.fsum[v][e] = a.fsum[v];
+            if (f & NEED_M2) ds.m2[v][e] = a.m2[v];
+            if (f & NEED_MIN) ds.mn[v][e] = (int64_t)a.omn[v];
+            if (f & NEED_MAX) ds.mx[v][e] = (int64_t)a.omx[v];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- finalize closed windows
+// Per (window, key): merge the window's panes from the pane state, finalise, HAVING, emit.
+template <int NVC>
 __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, const WinDesc* __restrict__ wins,
                                                      DState ds, int32_t ring, const int32_t* __restrict__ pane_err,
                                                      Results res) {
     const DPlan& p = *pp;
     const WinDesc w = wins[blockIdx.y];
-    int64_t key = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t key = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     int32_t werr = 0;
     for (int64_t q = w.q_first; q <= w.q_last; ++q) werr |= pane_err[q % ring];
     if (werr) {
@@ -460,83 +938,33 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
         return;
     }
     const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
-    if (key >= K) return;
-    // merge panes in time order
-    int64_t cnt = 0;
-    int64_t vcnt[kMaxVC], isum[kMaxVC];
-    double fsum[kMaxVC], m2[kMaxVC];
-    uint64_t omn[kMaxVC], omx[kMaxVC];
-    for (int v = 0; v < p.n_vc; ++v) { vcnt[v] = 0; isum[v] = 0; fsum[v] = 0; m2[v] = 0; omn[v] = ~0ull; omx[v] = 0; }
-    for (int64_t q = w.q_first; q <= w.q_last; ++q) {
-        int64_t e = (q % ring) * ds.K + key;
-        int64_t c = ds.cnt[e];
-        if (c == 0) continue;
-        int64_t cprev = cnt;
-        cnt += c;
-        for (int v = 0; v < p.n_vc; ++v) {
-            const int f = p.vc_flags[v];
-            int64_t nb_ = (f & NEED_CNT) ? ds.vcnt[v][e] : c;
-            if (nb_ == 0) continue;
-            int64_t na = (f & NEED_CNT) ? vcnt[v] : cprev;
-            vcnt[v] = na + nb_;
-            double sb = 0;
-            if (p.vc_is_float[v]) {
-                if (f & (NEED_SUM | NEED_M2)) sb = __longlong_as_double(ds.sum[v][e]);
-            } else {
-                if (f & NEED_SUM) isum[v] = (int64_t)((uint64_t)isum[v] + (uint64_t)ds.sum[v][e]);
-                if (f & NEED_FSUM) sb = ds.fsum[v][e];
+    Part<NVC> s{};
+    bool present = false;
+    if (key < K) {
+        for (int64_t q = w.q_first; q <= w.q_last; ++q) {
+            const int64_t e = (q % ring) * ds.K + key;
+            const int64_t c = ds.cnt[e];
+            if (c == 0) continue;
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                const int f = p.vc_flags[v];
+                vc[v] = (f & NEED_CNT) ? ds.vcnt[v][e] : c;
+                is[v] = (!p.vc_is_float[v] && (f & NEED_SUM)) ? ds.sum[v][e] : 0;
+                fs[v] = p.vc_is_float[v] ? ((f & NEED_SUM) ? __longlong_as_double(ds.sum[v][e]) : 0.0)
+                                         : ((f & NEED_FSUM) ? ds.fsum[v][e] : 0.0);
+                m2[v] = (f & NEED_M2) ? ds.m2[v][e] : 0.0;
+                mn[v] = (f & NEED_MIN) ? (uint64_t)ds.mn[v][e] : 0ull;
+                mx[v] = (f & NEED_MAX) ? (uint64_t)ds.mx[v][e] : 0ull;
             }
-            if (f & NEED_M2) {
-                double m2b = ds.m2[v][e];
-                if (na == 0) m2[v] = m2b;
-                else {
-                    double dlt = __dsub_rn(__ddiv_rn(sb, (double)nb_), __ddiv_rn(fsum[v], (double)na));
-                    m2[v] = m2[v] + m2b + dlt * dlt * ((double)na * (double)nb_ / (double)(na + nb_));
-                }
-            }
-            fsum[v] = na ? __dadd_rn(fsum[v], sb) : sb;
-            if (f & NEED_MIN) { uint64_t o = (uint64_t)ds.mn[v][e]; omn[v] = o < omn[v] ? o : omn[v]; }
-            if (f & NEED_MAX) { uint64_t o = (uint64_t)ds.mx[v][e]; omx[v] = o > omx[v] ? o : omx[v]; }
+            part_merge(p, s, c, vc, is, fs, m2, mn, mx);
         }
+        present = s.cnt > 0 && having_keep(p, s, &res.win_err[w.idx]);
     }
-    if (cnt == 0) return;  // group absent from this window
-    Val a[EK_MAX_AGGS];
-    for (int k = 0; k < p.n_aggs; ++k) {
-        const int fn = p.agg_fn[k];
-        const int v = p.agg_vc[k];
-        Val r{V_NULL, 0, 0.0};
-        if (fn == EK_AGG_COUNT_STAR) r = Val{V_I64, cnt, 0.0};
-        else if (fn == EK_AGG_COUNT) r = Val{V_I64, vcnt[v], 0.0};
-        else if (vcnt[v] > 0) {
-            const bool fl = p.vc_is_float[v];
-            switch (fn) {
-            case EK_AGG_SUM: r = fl ? Val{V_F64, 0, fsum[v]} : Val{V_I64, isum[v], 0.0}; break;
-            case EK_AGG_AVG:   // funcs_agg.go:56-86: int -> int64 truncating division
-                r = fl ? Val{V_F64, 0, __ddiv_rn(fsum[v], (double)vcnt[v])}
-                       : Val{V_I64, (isum[v] == INT64_MIN && vcnt[v] == -1) ? isum[v] : isum[v] / vcnt[v], 0.0};
-                break;
-            case EK_AGG_MIN: r = fl ? Val{V_F64, 0, ord_to_f64(omn[v])} : Val{V_I64, ord_to_i64(omn[v]), 0.0}; break;
-            case EK_AGG_MAX: r = fl ? Val{V_F64, 0, ord_to_f64(omx[v])} : Val{V_I64, ord_to_i64(omx[v]), 0.0}; break;
-            case EK_AGG_VAR: r = Val{V_F64, 0, __ddiv_rn(m2[v], (double)vcnt[v])}; break;
-            case EK_AGG_VARS: r = Val{V_F64, 0, __ddiv_rn(m2[v], (double)(vcnt[v] - 1))}; break;
-            case EK_AGG_STDDEV: r = Val{V_F64, 0, __dsqrt_rn(__ddiv_rn(m2[v], (double)vcnt[v]))}; break;
-            case EK_AGG_STDDEVS: r = Val{V_F64, 0, __dsqrt_rn(__ddiv_rn(m2[v], (double)(vcnt[v] - 1)))}; break;
-            default: break;
-            }
-        }
-        a[k] = r;
-    }
-    if (p.n_having > 0) {
-        Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, a);
-        if (h.tag != V_BOOL) { atomicOr(&res.win_err[w.idx], EK_WIN_HAVING_ERROR); return; }
-        if (!h.i) return;
-    }
-    int64_t pos = w.out_base + atomicAdd((unsigned long long*)&res.win_cnt[w.idx], 1ull);
-    res.key[pos] = (uint32_t)key;
-    for (int k = 0; k < p.n_aggs; ++k) {
-        res.tag[k][pos] = a[k].tag == V_NULL ? EK_TAG_NULL : (a[k].tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
-        res.val[k][pos] = a[k].tag == V_F64 ? __double_as_longlong(a[k].f) : a[k].i;
-    }
+    __shared__ uint32_t esh[20];
+    emit_rows(p, present, s, key, w.out_base, w.idx, res, esh);
 }
 
 // ---------------------------------------------------------------- debug: window membership fingerprint

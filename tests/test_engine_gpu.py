@@ -70,10 +70,10 @@ def _iot_cols(n, keys, seed=44, epm=100):
     return [key, ts, temp, hum]
 
 
-@pytest.mark.parametrize("n,keys,batches", [(300_000, 1000, 1), (300_000, 1000, 7), (120_000, 65536, 3)])
+@pytest.mark.parametrize("n,keys,batches", [(300_000, 1000, 1), (300_000, 1000, 7), (240_000, 65536, 3)])
 def test_c2_tumbling_parity(oracle, engine_mod, n, keys, batches):
     rule = compile_rule(C2_SQL, IOT_SCHEMA, num_keys=keys, debug_membership=True)
-    cols = _iot_cols(n, keys, epm=10)
+    cols = _iot_cols(n, keys, epm=10 if keys < 10000 else 5)
     got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
     assert len(got) >= 2
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
