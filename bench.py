@@ -26,6 +26,9 @@ EVENTS_PER_MS = 100
 BYTES_IN_PER_EVENT = 4 + 8 + 8 + 8      # key u32, ts i64, temperature f64, humidity f64
 BYTES_OUT_PER_ROW = 4 + 8 + 8 + 8       # key, avg, max, count
 HBM_PEAK_GBS = 8000.0                   # MI355X_MICROARCH.md: 8.0 TB/s spec
+PHASES = ("stats", "partition", "aggregate", "finalize")
+KERNEL_OF_PHASE = {"stats": "k_stats", "partition": "k_part", "aggregate": "k_agg", "finalize": "k_finalize"}
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
 def _tmix(x):
@@ -131,23 +134,43 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     dev_ms = 0.0
+    ph_ms = [0.0] * 4
+    ph_n = [0] * 4
     for _ in range(args.steps):
         step()
-        dev_ms += eng.stats().last_batch_device_ms
+        st = eng.stats()
+        dev_ms += st.last_batch_device_ms
+        for k in range(4):
+            ph_ms[k] += st.phase_ms[k]
+            ph_n[k] += st.phase_launches[k]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt, dev_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, dev_ms] + ph_ms, dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, dev_ms = float(t[0]), float(t[1])
+        ph_ms = [float(x) for x in t[2:]]
 
     ms_per_step = dt * 1000.0 / args.steps
     value = n * world * args.steps / dt
     dev_ms_step = dev_ms / args.steps
     alg_bytes = n * BYTES_IN_PER_EVENT + rows * BYTES_OUT_PER_ROW
-    achieved = alg_bytes / (dev_ms_step * 1e-3) / 1e9
+    path_gbs = alg_bytes / (dev_ms_step * 1e-3) / 1e9
+    # dominant kernel: k_part (one launch per push here); its algorithmic bytes are the input columns
+    # it must read once (28 B/event); staging writes are implementation traffic
+    part_launch_ms = ph_ms[1] / max(1, ph_n[1])
+    part_launches_per_step = ph_n[1] / args.steps
+    part_alg = n * BYTES_IN_PER_EVENT / max(1.0, part_launches_per_step)
+    achieved = part_alg / (part_launch_ms * 1e-3) / 1e9 if part_launch_ms > 0 else 0.0
+    traffic, traffic_src = None, None
+    if os.path.exists(PMC_SUMMARY):
+        pm = json.load(open(PMC_SUMMARY))
+        k = pm.get("kernels", {}).get("k_part")
+        if k and k.get("events_per_launch") == n:
+            traffic = k["hbm_bytes_per_launch"]
+            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
     out = {
         "metric": "events/sec (whole node) for windowed GROUP BY at 1/2/4/8 GPUs; % HBM peak",
         "value": value,
@@ -165,9 +188,14 @@ def main():
                    "event_rate": "100k ev/s event time (100 events per ms)", "windows_emitted": n_windows,
                    "rows_per_step": rows, "parallelism": f"key-hash shards x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "whole hot path of one ek_push_batch (all kernels, HIP events on the engine stream)",
-                     "algorithmic_bytes": alg_bytes, "device_ms": dev_ms_step},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_part (dominant kernel; HIP events around each launch on the engine stream)",
+                     "algorithmic_bytes_per_launch": part_alg, "launch_ms": part_launch_ms,
+                     "traffic_source": traffic_src,
+                     "phase_ms_per_step": {PHASES[k]: ph_ms[k] / args.steps for k in range(4)},
+                     "path": {"achieved": path_gbs, "frac": path_gbs / HBM_PEAK_GBS, "device_ms": dev_ms_step,
+                              "algorithmic_bytes": alg_bytes,
+                              "what": "whole ek_push_batch: 28 B/event in + 28 B/result row out over its device time"}},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample)

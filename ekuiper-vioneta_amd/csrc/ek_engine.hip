@@ -48,9 +48,9 @@ struct WinInfo {
 
 // NVC-specialised launches (value columns referenced by aggregates: 1..kMaxVC)
 template <int N>
-void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLayout lay, const uint32_t* start,
-                const uint32_t* totals, Staging st, DState ds, Results res) {
-    hipLaunchKernelGGL(k_agg<N>, g, dim3(kAggBlock), lds, s, p, gd, lay, start, totals, st, ds, res);
+void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLayout lay, const uint32_t* ctab, int ls,
+                int64_t rs, Staging st, DState ds, Results res, const int32_t* pane_err) {
+    hipLaunchKernelGGL(k_agg<N>, g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err);
 }
 template <int N>
 void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res) {
@@ -142,6 +142,22 @@ struct Engine {
     bool own_stream = false;
     std::string err;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // per-phase timing: event pairs recorded around launches, summed when the push completes
+    struct PhaseEv { hipEvent_t a, b; int phase; };
+    std::vector<PhaseEv> phase_ev;
+    size_t phase_used = 0;
+    int phase_begin(int ph) {
+        if (phase_used == phase_ev.size()) {
+            PhaseEv e{nullptr, nullptr, 0};
+            hipEventCreate(&e.a);
+            hipEventCreate(&e.b);
+            phase_ev.push_back(e);
+        }
+        phase_ev[phase_used].phase = ph;
+        hipEventRecord(phase_ev[phase_used].a, stream);
+        return (int)phase_used++;
+    }
+    void phase_end(int idx) { hipEventRecord(phase_ev[idx].b, stream); }
 
     // ---- derived configuration
     int wtype = 0;
@@ -374,12 +390,11 @@ struct Engine {
             lay.bytes = (o + 15) & ~15;
         }
         chunk = env_int("EKGPU_CHUNK", 16384);
-        group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 8 << 20);
+        // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
+        group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
         np_max = env_int("EKGPU_NP_MAX", 8192);
-        int ppg = std::max(1, np_max / NB);
-        max_panes_group = (int)std::min<int64_t>(ppg, 64);
-        ring = (int)(2 * ppw + max_panes_group + 4);
-        if (NB > np_max) return fail(EK_ERR_UNSUPPORTED, "too many key buckets (%d)", NB);
+        max_panes_group = env_int("EKGPU_MAX_GROUP_PANES", 4096);
+        ring = (int)(2 * ppw + 16);
 
         // ---- HIP resources
         if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
@@ -396,31 +411,82 @@ struct Engine {
         return 0;
     }
 
-    int alloc_state() {
-        // SoA fields, each ring * Kpad entries of 8 bytes
+    int n_state_fields() const {
         int nf = 1;
         for (int v = 0; v < dp.n_vc; ++v) {
             int f = dp.vc_flags[v];
             nf += !!(f & NEED_CNT) + !!(f & NEED_SUM) + !!(f & NEED_MIN) + !!(f & NEED_MAX) + !!(f & NEED_M2) + !!(f & NEED_FSUM);
         }
-        size_t per = (size_t)ring * Kpad * 8;
-        if (int rc = ensure(state_buf, per * nf)) return rc;
-        char* b = (char*)state_buf.p;
-        dstate = DState{};
-        dstate.K = Kpad;
-        dstate.cnt = (int64_t*)b; b += per;
+        return nf;
+    }
+    // SoA fields, each R * Kpad entries of 8 bytes, carved from one allocation
+    DState carve_state(void* base, int R) const {
+        size_t per = (size_t)R * Kpad * 8;
+        char* b = (char*)base;
+        DState d{};
+        d.K = Kpad;
+        d.cnt = (int64_t*)b; b += per;
         for (int v = 0; v < dp.n_vc; ++v) {
             int f = dp.vc_flags[v];
-            if (f & NEED_CNT) { dstate.vcnt[v] = (int64_t*)b; b += per; }
-            if (f & NEED_SUM) { dstate.sum[v] = (int64_t*)b; b += per; }
-            if (f & NEED_MIN) { dstate.mn[v] = (int64_t*)b; b += per; }
-            if (f & NEED_MAX) { dstate.mx[v] = (int64_t*)b; b += per; }
-            if (f & NEED_M2) { dstate.m2[v] = (double*)b; b += per; }
-            if (f & NEED_FSUM) { dstate.fsum[v] = (double*)b; b += per; }
+            if (f & NEED_CNT) { d.vcnt[v] = (int64_t*)b; b += per; }
+            if (f & NEED_SUM) { d.sum[v] = (int64_t*)b; b += per; }
+            if (f & NEED_MIN) { d.mn[v] = (int64_t*)b; b += per; }
+            if (f & NEED_MAX) { d.mx[v] = (int64_t*)b; b += per; }
+            if (f & NEED_M2) { d.m2[v] = (double*)b; b += per; }
+            if (f & NEED_FSUM) { d.fsum[v] = (double*)b; b += per; }
         }
+        return d;
+    }
+    int alloc_state() {
+        if (int rc = ensure(state_buf, (size_t)ring * Kpad * 8 * n_state_fields())) return rc;
+        dstate = carve_state(state_buf.p, ring);
         if (int rc = ensure(pane_err, (size_t)ring * 4)) return rc;
         if (int rc = ensure(pane_mcnt, (size_t)ring * 8)) return rc;
         if (int rc = ensure(pane_mhash, (size_t)ring * 8)) return rc;
+        return 0;
+    }
+    // Grow the pane ring to at least `need` slots, moving the partials of live panes.
+    int ensure_ring(int64_t need) {
+        if (need <= ring) return 0;
+        int R = (int)std::max<int64_t>(need, (int64_t)ring * 2);
+        hipStreamSynchronize(stream);
+        const int nf = n_state_fields();
+        DevBuf nsb, npe, npm, nph;
+        if (hipMalloc(&nsb.p, (size_t)R * Kpad * 8 * nf) != hipSuccess) return fail(EK_ERR_NOMEM, "pane state alloc (%d slots)", R);
+        nsb.bytes = (size_t)R * Kpad * 8 * nf;
+        if (hipMalloc(&npe.p, (size_t)R * 4) != hipSuccess || hipMalloc(&npm.p, (size_t)R * 8) != hipSuccess ||
+            hipMalloc(&nph.p, (size_t)R * 8) != hipSuccess)
+            return fail(EK_ERR_NOMEM, "pane scalar alloc");
+        npe.bytes = (size_t)R * 4; npm.bytes = nph.bytes = (size_t)R * 8;
+        DState nd = carve_state(nsb.p, R);
+        std::vector<int64_t> nslot(R, INT64_MIN);
+        const int64_t first_live = win_first_pane(next_win);
+        const size_t per = (size_t)Kpad * 8;
+        for (int so = 0; so < ring; ++so) {
+            int64_t q = slot_pane[so];
+            if (q == INT64_MIN || q < first_live) continue;
+            int sn = (int)(q % R);
+            nslot[sn] = q;
+            auto mv = [&](void* dst, void* src) { if (src) hipMemcpyAsync((char*)dst + sn * per, (char*)src + so * per, per, hipMemcpyDeviceToDevice, stream); };
+            mv(nd.cnt, dstate.cnt);
+            for (int v = 0; v < dp.n_vc; ++v) {
+                if (dstate.vcnt[v]) mv(nd.vcnt[v], dstate.vcnt[v]);
+                if (dstate.sum[v]) mv(nd.sum[v], dstate.sum[v]);
+                if (dstate.mn[v]) mv(nd.mn[v], dstate.mn[v]);
+                if (dstate.mx[v]) mv(nd.mx[v], dstate.mx[v]);
+                if (dstate.m2[v]) mv(nd.m2[v], dstate.m2[v]);
+                if (dstate.fsum[v]) mv(nd.fsum[v], dstate.fsum[v]);
+            }
+            hipMemcpyAsync((char*)npe.p + sn * 4, (char*)pane_err.p + so * 4, 4, hipMemcpyDeviceToDevice, stream);
+            hipMemcpyAsync((char*)npm.p + sn * 8, (char*)pane_mcnt.p + so * 8, 8, hipMemcpyDeviceToDevice, stream);
+            hipMemcpyAsync((char*)nph.p + sn * 8, (char*)pane_mhash.p + so * 8, 8, hipMemcpyDeviceToDevice, stream);
+        }
+        hipStreamSynchronize(stream);
+        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash);
+        state_buf = nsb; pane_err = npe; pane_mcnt = npm; pane_mhash = nph;
+        dstate = nd;
+        slot_pane = nslot;
+        ring = R;
         return 0;
     }
 
@@ -458,9 +524,10 @@ struct Engine {
 
     // Bind panes [qa, qb] to ring slots. A pane new to its slot is "fresh": its partials are written
     // (not merged) by the next k_agg, or zeroed here when `zero` (panes no group ever touched).
-    int claim_slots(int64_t qa, int64_t qb, uint64_t* fresh, bool zero) {
+    int claim_slots(int64_t qa, int64_t qb, uint8_t* fresh, bool zero) {
         int64_t first_live = win_first_pane(next_win);
-        if (fresh) *fresh = 0;
+        if (int rc = ensure_ring(qb - std::min(first_live, qa) + 3)) return rc;
+        if (fresh) memset(fresh, 0, (size_t)(qb - qa + 1));
         for (int64_t q = qa; q <= qb; ++q) {
             int s = (int)(q % ring);
             if (slot_pane[s] == q) continue;
@@ -468,7 +535,7 @@ struct Engine {
                 return fail(EK_ERR_UNSUPPORTED, "pane ring overflow (pane %lld needs slot %d held by live pane %lld)",
                             (long long)q, s, (long long)slot_pane[s]);
             slot_pane[s] = q;
-            if (fresh && q - qa < 64) *fresh |= 1ull << (q - qa);
+            if (fresh) fresh[q - qa] = 1;
             if (!zero) continue;
             size_t per = (size_t)Kpad * 8;
             hipMemsetAsync((char*)dstate.cnt + s * per, 0, per, stream);
@@ -496,8 +563,8 @@ struct Engine {
         h_desc_used += n;
         return r;
     }
-    DevBuf pbnd_d;
-    size_t pbnd_used = 0;
+    DevBuf aux_d;
+    size_t aux_used = 0;
 
     // ------------------------------------------------------------------ results
     int ensure_results(int64_t add_rows, int64_t add_wins) {
@@ -628,12 +695,14 @@ struct Engine {
             const int nvc = std::max(1, dp.n_vc);
             Results rv = results_view();
             const WinDesc* wd = (const WinDesc*)wdesc.p;
+            const int ph = phase_begin(EK_PHASE_FINALIZE);
             switch (nvc) {
             case 1: launch_fin<1>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
             case 2: launch_fin<2>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
             case 3: launch_fin<3>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
             default: launch_fin<4>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
             }
+            phase_end(ph);
         }
         if (plan.debug_membership) {
             hipLaunchKernelGGL(k_win_members, dim3((unsigned)n), dim3(64), 0, stream, (const WinDesc*)wdesc.p, ring,
@@ -660,7 +729,8 @@ struct Engine {
         int64_t first_live = win_first_pane(next_win);
         q_lo = std::max(q_lo, first_live);
 
-        struct Grp { int64_t lo, hi, qa, qb; bool complete; int64_t bk; };
+        struct Grp { int64_t lo, hi, qa, qb; int64_t q_done; int64_t bk; };
+        const int64_t pane_cap = (int64_t)(kMaxRuns - 2) * chunk;   // k_agg run list bound per pane
         std::vector<Grp> groups;
         if (sorted) {
             // pane boundaries by binary search on the sorted ts column
@@ -683,27 +753,34 @@ struct Engine {
                 int64_t lo = b[k];
                 int64_t kk = k;
                 int64_t hi = b[k + 1];
-                if (hi - lo > group_events) {
+                const int64_t cap = std::min(group_events, pane_cap);
+                if (hi - lo > cap) {
                     // split one big pane into several groups
-                    for (int64_t s = lo; s < hi; s += group_events) {
-                        int64_t e = std::min(hi, s + group_events);
-                        groups.push_back(Grp{s, e, q_lo + k, q_lo + k, e == hi, -1});
+                    for (int64_t s = lo; s < hi; s += cap) {
+                        int64_t e = std::min(hi, s + cap);
+                        groups.push_back(Grp{s, e, q_lo + k, q_lo + k, e == hi ? q_lo + k : q_lo + k - 1, -1});
                     }
                     k++;
                     continue;
                 }
-                while (kk + 1 < nq && (b[kk + 2] - lo) <= group_events && (kk + 1 - k + 1) <= max_panes_group) {
+                while (kk + 1 < nq && (b[kk + 2] - lo) <= group_events && (kk + 1 - k + 1) <= max_panes_group &&
+                       b[kk + 2] - b[kk + 1] <= pane_cap) {
                     kk++;
                     hi = b[kk + 1];
                 }
-                groups.push_back(Grp{lo, std::max(lo, hi), q_lo + k, q_lo + kk, true, k});
+                groups.push_back(Grp{lo, std::max(lo, hi), q_lo + k, q_lo + kk, q_lo + kk, k});
                 k = kk + 1;
             }
         } else {
-            if (q_hi - q_lo + 1 > max_panes_group)
+            if ((q_hi - q_lo + 1) * NB > np_max)
                 return fail(EK_ERR_UNSUPPORTED, "out-of-order batch spans %lld panes (max %d): split the batch",
-                            (long long)(q_hi - q_lo + 1), max_panes_group);
-            groups.push_back(Grp{start, n, q_lo, q_hi, true, -1});
+                            (long long)(q_hi - q_lo + 1), np_max / NB);
+            // every index range may hold events of any pane: finalise only after the last one
+            const int64_t cap = (int64_t)(kMaxRuns - 2) * chunk;
+            for (int64_t s = start; s < n; s += cap) {
+                int64_t e = std::min(n, s + cap);
+                groups.push_back(Grp{s, e, q_lo, q_hi, e == n ? q_hi : q_lo - 1, e == n && s == start ? 0 : -2});
+            }
         }
 
         const int64_t* bidx = sorted ? h_small + (q_hi - q_lo + 2) : nullptr;
@@ -720,15 +797,14 @@ struct Engine {
                 }
                 // whole_panes: the group holds every event of this batch for each of its panes
                 if (int rc = run_group(db, g.lo, g.hi, g.qa, g.qb, d_acc, sorted ? pb.data() : nullptr,
-                                       !sorted || g.bk >= 0)) return rc;
+                                       g.bk >= 0)) return rc;
                 if (plan.debug_membership) {
                     hipLaunchKernelGGL(k_members, dim3(256), dim3(kBlock), 0, stream, d_plan, db, grid, d_acc,
                                        (int)(d_acc != nullptr), g.lo, g.hi, arrivals, d_arrival, g.qa, g.qb, ring,
                                        (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
                 }
             }
-            int64_t q_done = g.complete ? g.qb : g.qb - 1;
-            if (int rc = finalize_ready(q_done)) return rc;
+            if (int rc = finalize_ready(g.q_done)) return rc;
         }
         return finalize_ready(q_hi);
     }
@@ -737,15 +813,35 @@ struct Engine {
     int run_group(const DBatch& db, int64_t lo, int64_t hi, int64_t qa, int64_t qb, const uint8_t* d_acc,
                   const int64_t* pbnd_host, bool whole_panes) {
         GroupDesc gd{};
-        if (int rc = claim_slots(qa, qb, &gd.fresh, false)) return rc;
+        const int npn = (int)(qb - qa + 1);
+        // per-pane descriptors: [pbnd n+1][dbase n][didx n (i32)][fresh n (u8)] in one pinned block -> one upload
+        const size_t aux_words = (size_t)(npn + 1) + npn + (npn + 1) / 2 + (npn + 7) / 8 + 2;
+        int64_t* aux = desc_alloc(aux_words);
+        if (!aux) return fail(EK_ERR_NOMEM, "pinned");
+        int64_t* h_pbnd = aux;
+        int64_t* h_dbase = h_pbnd + npn + 1;
+        int32_t* h_didx = (int32_t*)(h_dbase + npn);
+        uint8_t* h_fresh = (uint8_t*)(h_didx + 2 * ((npn + 1) / 2));
+        if (int rc = claim_slots(qa, qb, h_fresh, false)) return rc;
+        bool any_fresh = false;
+        for (int r = 0; r < npn; ++r) any_fresh |= h_fresh[r] != 0;
         gd.lo = lo;
         gd.hi = hi;
         gd.q_lo = qa;
         gd.n_panes = (int32_t)(qb - qa + 1);
         gd.nb = NB;
         gd.kbits = kbits;
-        gd.chunk = chunk;
         gd.abase = lo & ~(int64_t)15;
+        gd.hi = hi;
+        gd.n_panes = npn;
+        // chunk size of this group: halve while a chunk would span more panes than k_part sorts in LDS
+        int64_t csz = chunk;
+        int mp = max_panes_in_chunk(pbnd_host, gd, csz);
+        while (csz > 1024 && pbnd_host && (mp > kMaxChunkBnd + 1 || (int64_t)NB * mp > np_max)) {
+            csz >>= 1;
+            mp = max_panes_in_chunk(pbnd_host, gd, csz);
+        }
+        gd.chunk = csz;
         gd.key_col = dp.key_col;
         gd.ts_col = dp.ts_col;
         gd.n_where = dp.n_where;
@@ -757,9 +853,10 @@ struct Engine {
         gd.has_accept = d_acc != nullptr;
         gd.sorted = pbnd_host != nullptr;
         gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
-        if (gd.n_panes > kMaxGroupPanes) return fail(EK_ERR_UNSUPPORTED, "group spans %d panes", gd.n_panes);
-        if (gd.np > np_max) return fail(EK_ERR_UNSUPPORTED, "too many partitions in a group (%d)", gd.np);
-        int64_t ne = (hi - lo) + 8LL * NB * gd.n_panes + 64;   // 8-aligned runs + vector over-read slack
+
+
+        const int64_t rs = gd.chunk;                                // staging region per chunk
+        int64_t ne = (int64_t)gd.nch * rs + 64;
         if (ne > st_cap) {
             if (int rc = ensure(st_klo, (size_t)ne * 2)) return rc;
             for (int v = 0; v < dp.n_vc; ++v) {
@@ -780,90 +877,107 @@ struct Engine {
                 any_nullable = true;
             }
         }
-        // pane boundary indices of this group (kernel argument)
-        for (int k = 0; k < 65; ++k) gd.pbnd[k] = 0;
-        if (pbnd_host) for (int k = 0; k <= gd.n_panes; ++k) gd.pbnd[k] = pbnd_host[k];
-        for (int r = 0; r < 64; ++r) { gd.dbase[r] = -1; gd.didx[r] = -1; }
-
-        // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
-        const int lp_stride = gd.sorted ? std::min(gd.np, NB * max_panes_in_chunk(pbnd_host, gd)) : gd.np;
-        size_t lds_h = (size_t)std::max(lp_stride, 1) * 4;
-        if (int rc = ensure(chist, (size_t)gd.nch * lp_stride * 4)) return rc;
-        if (int rc = ensure(totals, (size_t)gd.np * 4)) return rc;
-        if (int rc = ensure(pstart, (size_t)(gd.np + 1) * 4)) return rc;
-        if (int rc = ensure(pcursor, (size_t)gd.np * 4)) return rc;
-        hipLaunchKernelGGL(k_group_prep, dim3(1), dim3(1024), 0, stream, gd, (uint32_t*)totals.p, (int32_t*)pane_err.p,
-                           (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
-        const bool wh = dp.n_where > 0;
-#define EK_COUNT(S, W) hipLaunchKernelGGL((k_count<S, W>), dim3(gd.nch), dim3(kBlock), lds_h, stream, d_plan, db, grid, gd, d_acc, \
-                                          (uint32_t*)chist.p, lp_stride, (uint32_t*)totals.p, (int32_t*)pane_err.p)
-        if (gd.sorted) { if (wh) EK_COUNT(true, true); else EK_COUNT(true, false); }
-        else { if (wh) EK_COUNT(false, true); else EK_COUNT(false, false); }
-#undef EK_COUNT
-        hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, stream, (const uint32_t*)totals.p, gd.np,
-                           (uint32_t*)pstart.p, (uint32_t*)pcursor.p);
-        if (lp_stride <= kMaxLocalParts) {
-            const int nvc = std::max(1, dp.n_vc);
-            size_t lds_s = scatter_lds_bytes(nvc, any_nullable);
-            const uint32_t* ch = (const uint32_t*)chist.p;
-            uint32_t* pc = (uint32_t*)pcursor.p;
-            dim3 gs(gd.nch);
-#define EK_SCATTER(S, W, N) hipLaunchKernelGGL((k_scatter<S, W, N>), gs, dim3(kBlock), lds_s, stream, d_plan, db, grid, gd, d_acc, ch, lp_stride, pc, st)
-#define EK_SCATTER_N(S, W) switch (nvc) { case 1: EK_SCATTER(S, W, 1); break; case 2: EK_SCATTER(S, W, 2); break; \
-                                          case 3: EK_SCATTER(S, W, 3); break; default: EK_SCATTER(S, W, 4); break; }
-            if (gd.sorted) { if (wh) { EK_SCATTER_N(true, true) } else { EK_SCATTER_N(true, false) } }
-            else { if (wh) { EK_SCATTER_N(false, true) } else { EK_SCATTER_N(false, false) } }
-#undef EK_SCATTER_N
-#undef EK_SCATTER
-        } else {
-#define EK_SD(S, W) hipLaunchKernelGGL((k_scatter_direct<S, W>), dim3(gd.nch), dim3(kBlock), lds_h, stream, d_plan, db, grid, gd, \
-                                       d_acc, (const uint32_t*)chist.p, lp_stride, (uint32_t*)pcursor.p, st)
-            if (gd.sorted) { if (wh) EK_SD(true, true); else EK_SD(true, false); }
-            else { if (wh) EK_SD(false, true); else EK_SD(false, false); }
-#undef EK_SD
-        }
+        for (int k = 0; k <= npn; ++k) h_pbnd[k] = pbnd_host ? pbnd_host[k] : 0;
+        for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
         // direct emission: a fresh tumbling pane whose whole content is in this group and whose window
         // closes at this batch's watermark is finalised by k_agg itself (no pane-state round trip)
         if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes) {
-            for (int r = 0; r < gd.n_panes && r < 64; ++r) {
+            for (int r = 0; r < npn; ++r) {
                 int64_t q = qa + r;
-                if (!((gd.fresh >> r) & 1ull) || win_end(q) > W || q < next_win) continue;
+                if (!h_fresh[r] || win_end(q) > W || q < next_win) continue;
                 if (int rc = register_until(q)) return rc;
                 WinInfo& wi = win_info(q);
                 wi.direct = true;
-                gd.dbase[r] = wi.out_base;
-                gd.didx[r] = wi.slot;
+                h_dbase[r] = wi.out_base;
+                h_didx[r] = wi.slot;
             }
+        }
+        {
+            size_t need = (aux_used + aux_words) * 8;
+            if (need > aux_d.bytes) {
+                hipStreamSynchronize(stream);
+                aux_used = 0;
+                if (int rc = ensure(aux_d, std::max<size_t>(aux_words * 8 * 4, 1 << 20))) return rc;
+            }
+            int64_t* dst = (int64_t*)aux_d.p + aux_used;
+            aux_used += aux_words;
+            hipMemcpyAsync(dst, aux, aux_words * 8, hipMemcpyHostToDevice, stream);
+            gd.pbnd = dst;
+            gd.dbase = dst + npn + 1;
+            gd.didx = (const int32_t*)(gd.dbase + npn);
+            gd.fresh = (const uint8_t*)(gd.didx + 2 * ((npn + 1) / 2));
+        }
+
+        // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
+        const int lp_stride = gd.sorted ? std::min(gd.np, NB * mp) : gd.np;
+        if (lp_stride > np_max || (gd.sorted && mp > kMaxChunkBnd + 1))
+            return fail(EK_ERR_UNSUPPORTED, "chunk spans %d partitions (split the batch)", lp_stride);
+        if (int mc = max_chunks_in_pane(pbnd_host, gd, gd.chunk); mc > kMaxRuns)
+            return fail(EK_ERR_UNSUPPORTED, "a pane spans %d chunks of one group (max %d)", mc, kMaxRuns);
+        const int ls = lp_stride + 1;
+        if (int rc = ensure(chist, (size_t)gd.nch * ls * 4)) return rc;
+        if (any_fresh)
+            hipLaunchKernelGGL(k_group_prep, dim3((npn + 255) / 256), dim3(256), 0, stream, gd, (int32_t*)pane_err.p,
+                               (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
+        const bool wh = dp.n_where > 0;
+        {
+            const int nvc = std::max(1, dp.n_vc);
+            const size_t lds_p = part_lds_bytes(nvc, lp_stride, any_nullable);
+            uint32_t* ct = (uint32_t*)chist.p;
+            dim3 gp(gd.nch);
+            const int ph = phase_begin(EK_PHASE_PARTITION);
+#define EK_PART(S, W, N) hipLaunchKernelGGL((k_part<S, W, N>), gp, dim3(kBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, (int32_t*)pane_err.p)
+#define EK_PART_N(S, W) switch (nvc) { case 1: EK_PART(S, W, 1); break; case 2: EK_PART(S, W, 2); break; \
+                                       case 3: EK_PART(S, W, 3); break; default: EK_PART(S, W, 4); break; }
+            if (gd.sorted) { if (wh) { EK_PART_N(true, true) } else { EK_PART_N(true, false) } }
+            else { if (wh) { EK_PART_N(false, true) } else { EK_PART_N(false, false) } }
+#undef EK_PART_N
+#undef EK_PART
+            phase_end(ph);
         }
         {
             const int nvc = std::max(1, dp.n_vc);
             Results rv = results_view();
             dim3 ga(gd.np);
+            const uint32_t* ct = (const uint32_t*)chist.p;
+            const int32_t* pe = (const int32_t*)pane_err.p;
+            const int ph = phase_begin(EK_PHASE_AGGREGATE);
             switch (nvc) {
-            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
-            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
-            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
-            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, (const uint32_t*)pstart.p, (const uint32_t*)totals.p, st, dstate, rv); break;
+            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
+            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
+            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
+            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
             }
+            phase_end(ph);
         }
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
         return 0;
     }
 
     // most panes any chunk of the group overlaps (sorted groups)
-    int max_panes_in_chunk(const int64_t* pb, const GroupDesc& gd) const {
+    // Largest number of panes one chunk of the aligned grid spans (sorted groups; cursors are monotone).
+    int max_panes_in_chunk(const int64_t* pb, const GroupDesc& gd, int64_t chunk_sz) const {
         if (!pb) return gd.n_panes;
-        int best = 1;
-        for (int64_t a0 = gd.abase; a0 < gd.hi; a0 += gd.chunk) {
+        int best = 1, a = 0, b = 0;
+        for (int64_t a0 = gd.abase; a0 < gd.hi; a0 += chunk_sz) {
             int64_t c0 = std::max(gd.lo, a0);
-            int64_t c1 = std::min(gd.hi, a0 + gd.chunk);
-            int a = 0;
+            int64_t c1 = std::min(gd.hi, a0 + chunk_sz);
             while (a + 1 < gd.n_panes && pb[a + 1] <= c0) a++;
-            int b = a;
+            b = std::max(a, b);
             while (b + 1 < gd.n_panes && pb[b + 1] < c1) b++;
             best = std::max(best, b - a + 1);
         }
         return best;
+    }
+    // Largest number of chunks one pane spans (bounded by k_agg's per-partition run list).
+    int max_chunks_in_pane(const int64_t* pb, const GroupDesc& gd, int64_t chunk_sz) const {
+        if (!pb) return (int)((gd.hi - gd.abase + chunk_sz - 1) / chunk_sz);
+        int64_t best = 0;
+        for (int k = 0; k < gd.n_panes; ++k) {
+            if (pb[k + 1] <= pb[k]) continue;
+            best = std::max(best, (pb[k + 1] - 1 - gd.abase) / chunk_sz - (pb[k] - gd.abase) / chunk_sz + 1);
+        }
+        return (int)best;
     }
 
     // Accepted events that arrived before the first watermark release are kept (host side, tiny:
@@ -939,6 +1053,7 @@ struct Engine {
             if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
             if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
         }
+        phase_used = 0;
         hipEventRecord(ev0, stream);
         DBatch db{};
         db.n = n;
@@ -963,9 +1078,11 @@ struct Engine {
         // ---- 1. batch statistics (one pass over ts)
         int sblocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
         if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
+        const int ph_s = phase_begin(EK_PHASE_STATS);
         hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats_part.p);
         hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
                            (BatchStats*)bstats.p);
+        phase_end(ph_s);
         hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
         BatchStats s = *h_stats;
@@ -1009,8 +1126,7 @@ struct Engine {
         arrivals += n;
         h_wdesc_used = 0;   // the stats sync above drained every earlier descriptor upload
         h_desc_used = 0;
-        pbnd_used = 0;
-        direct_used = 0;
+        aux_used = 0;
 
         // ---- 3. watermark advance (watermark_op.go:157-214): W = max ts - lateTol
         if (!has_M || s.max_ts > M) {
@@ -1054,7 +1170,16 @@ struct Engine {
             float ms = 0;
             hipEventElapsedTime(&ms, ev0, ev1);
             stats.last_batch_device_ms = ms;
+            for (int k = 0; k < 4; ++k) { stats.phase_ms[k] = 0; stats.phase_launches[k] = 0; }
+            for (size_t k = 0; k < phase_used; ++k) {
+                float t = 0;
+                if (hipEventElapsedTime(&t, phase_ev[k].a, phase_ev[k].b) == hipSuccess) {
+                    stats.phase_ms[phase_ev[k].phase] += t;
+                    stats.phase_launches[phase_ev[k].phase]++;
+                }
+            }
         }
+        phase_used = 0;
         return 0;
     }
 
@@ -1169,9 +1294,11 @@ struct Engine {
         if (h_small) hipHostFree(h_small);
         if (h_wdesc) hipHostFree(h_wdesc);
         if (h_desc) hipHostFree(h_desc);
-        release(pbnd_d);
+        release(aux_d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
+        for (auto& e : phase_ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+        phase_ev.clear();
         if (stream && own_stream) hipStreamDestroy(stream);
     }
 };

@@ -241,11 +241,11 @@ struct GroupDesc {
     // hot plan scalars (kernel arguments stay in SGPRs; DPlan loads inside LDS-atomic loops re-issue)
     int32_t key_col, ts_col, n_where;
     uint32_t num_keys;
-    uint64_t fresh;        // bit r: pane q_lo + r was claimed for this group (its partials are written, not merged)
-    // small per-group descriptors travel in the kernel arguments (no tiny H2D copies per launch)
-    int64_t pbnd[65];      // sorted groups: pbnd[k] = first event of pane q_lo + k (k <= n_panes)
-    int64_t dbase[64];     // direct emission: result row base of pane r's window, or -1
-    int32_t didx[64];      // direct emission: window index of pane r
+    // per-pane descriptors (device arrays, one upload per group)
+    const int64_t* pbnd;   // sorted groups: pbnd[k] = first event of pane q_lo + k (k <= n_panes)
+    const int64_t* dbase;  // direct emission: result row base of pane r's window, or -1
+    const int32_t* didx;   // direct emission: window index of pane r
+    const uint8_t* fresh;  // 1: pane r was claimed for this group (its partials are written, not merged)
 };
 
 constexpr int kMaxGroupPanes = 64;
@@ -263,12 +263,13 @@ __device__ __forceinline__ void chunk_range(const GroupDesc& gd, int64_t* a0, in
 __device__ __forceinline__ void chunk_panes(const GroupDesc& gd, int64_t c0, int64_t c1, int* pa, int* pb) {
     const int64_t* pbnd = gd.pbnd;
     if (!gd.sorted) { *pa = 0; *pb = gd.n_panes - 1; return; }
-    int a = 0;
-    while (a + 1 < gd.n_panes && pbnd[a + 1] <= c0) a++;
-    int b = a;
-    while (b + 1 < gd.n_panes && pbnd[b + 1] < c1) b++;
-    *pa = a;
-    *pb = b;
+    // pa = last pane whose first row <= c0; pb = last pane whose first row < c1 (binary searches)
+    int lo = 0, hi = gd.n_panes - 1;
+    while (lo < hi) { int m = (lo + hi + 1) >> 1; if (pbnd[m] <= c0) lo = m; else hi = m - 1; }
+    *pa = lo;
+    hi = gd.n_panes - 1;
+    while (lo < hi) { int m = (lo + hi + 1) >> 1; if (pbnd[m] < c1) lo = m; else hi = m - 1; }
+    *pb = lo;
 }
 
 constexpr int kMaxChunkBnd = 64;
@@ -316,78 +317,6 @@ __device__ __forceinline__ uint32_t load_key(const DPlan& p, const DBatch& b, in
 
 // Per chunk: histogram over its chunk-local partitions (pane, key bucket) of the rows that pass WHERE,
 // stored compactly as chist[chunk][lp] (lp < lp_stride), plus the group-wide totals per partition.
-template <bool SORTED, bool WHERE>
-__global__ __launch_bounds__(kBlock) void k_count(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
-                                                  const uint8_t* __restrict__ acc,
-                                                  uint32_t* __restrict__ chist, int lp_stride, uint32_t* __restrict__ totals,
-                                                  int32_t* __restrict__ pane_err) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lh[];
-    const DPlan& p = *pp;
-    int64_t a0, c0, c1;
-    chunk_range(gd, &a0, &c0, &c1);
-    int pa, pb;
-    chunk_panes(gd, c0, c1, &pa, &pb);
-    const int lp_n = (pb - pa + 1) * gd.nb;
-    __shared__ int64_t lb[kMaxChunkBnd];
-    const int nlb = chunk_bounds(gd, pa, pb, lb);
-    for (int k = threadIdx.x; k < lp_n; k += kBlock) lh[k] = 0;
-    __syncthreads();
-    const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
-    constexpr int V = 4;   // 16-byte key loads in flight per thread (16 keys)
-    for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
-        uint4 kv[V];
-#pragma unroll
-        for (int u = 0; u < V; ++u) {
-            const int64_t i = base + (int64_t)u * kBlock * 4;
-            if (kcol && i + 3 < gd.nbatch && i < c1) kv[u] = *(const uint4*)(kcol + i);
-            else if (kcol && i < c1) {
-                kv[u].x = kcol[i];
-                kv[u].y = i + 1 < gd.nbatch ? kcol[i + 1] : 0u;
-                kv[u].z = i + 2 < gd.nbatch ? kcol[i + 2] : 0u;
-                kv[u].w = i + 3 < gd.nbatch ? kcol[i + 3] : 0u;
-            } else kv[u] = make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < V; ++u) {
-            const uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t i = base + (int64_t)u * kBlock * 4 + e;
-                if (i < c0 || i >= c1) continue;
-                const int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, kk[e], pane_err, true);
-                if (lp >= 0) atomicAdd(&lh[lp], 1u);
-            }
-        }
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < lp_stride; k += kBlock) {
-        uint32_t c = k < lp_n ? lh[k] : 0u;
-        chist[(int64_t)blockIdx.x * lp_stride + k] = c;
-        if (c) atomicAdd(&totals[pa * gd.nb + k], c);
-    }
-}
-
-// Exclusive scan of the np partition totals (single workgroup): start[p], and cursor[p] = start[p].
-__global__ __launch_bounds__(1024) void k_scan_parts(const uint32_t* __restrict__ totals, int np, uint32_t* start,
-                                                     uint32_t* cursor) {
-    __shared__ uint32_t part[1024];
-    int per = (np + 1023) / 1024;
-    int b = threadIdx.x * per, e = min(np, b + per);
-    uint32_t s = 0;
-    for (int i = b; i < e; ++i) s += (totals[i] + 7u) & ~7u;   // runs start 8-aligned
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = b; i < e; ++i) { start[i] = run; cursor[i] = run; run += (totals[i] + 7u) & ~7u; }
-    if (threadIdx.x == 1023) start[np] = part[1023];
-}
-
 struct Staging {
     uint16_t* klo;
     int64_t* val[kMaxVC];
@@ -395,13 +324,12 @@ struct Staging {
     uint32_t nullable_mask;   // bit v: staging carries validity for value column v
 };
 
-// Block-wide exclusive scan of cnt[0..n) in LDS (n <= kMaxLocalParts); cnt[n] receives the total.
+// Block-wide exclusive scan of cnt[0..n) in LDS; cnt[n] receives the total.
 __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
     const int per = (n + kBlock - 1) / kBlock;
     const int b = threadIdx.x * per, e = min(n, b + per);
     uint32_t s = 0;
     for (int k = b; k < e; ++k) s += cnt[k];
-    // inclusive scan of the per-thread sums across the wave, then across the 4 waves
     uint32_t x = s;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int o = 1; o < 64; o <<= 1) {
@@ -418,14 +346,21 @@ __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
     __syncthreads();
 }
 
-// Route the chunk's rows into contiguous per-partition staging runs. Each tile of kTile rows is
-// loaded (all loads issued before any use), counting-sorted by chunk-local partition in LDS, then
-// written out so that consecutive lanes write consecutive addresses of a run (coalesced).
+// LDS bytes of k_part for `nvc` value columns and `lp` chunk-local partitions
+inline size_t part_lds_bytes(int nvc, int lp, bool nullable) {
+    size_t lpp = ((size_t)lp + 4 + 3) & ~(size_t)3;
+    return (size_t)nvc * kTile * 8 + 2 * lpp * 4 + (size_t)kTile * 4 + (nullable ? (size_t)nvc * kTile : 0);
+}
+
+// One workgroup per chunk: partition the chunk's rows by (pane, key bucket) into the chunk's OWN
+// staging region [chunk * rs, chunk * rs + rows): (1) count rows per chunk-local partition (16-byte
+// key loads), (2) exclusive scan -> run offsets, published in ctab[chunk][0..lp_n], (3) per tile of
+// kTile rows: load, counting-sort by partition in LDS, write runs with consecutive lanes on
+// consecutive addresses. No global atomics, no global scan: k_agg walks the per-chunk runs.
 template <bool SORTED, bool WHERE, int NVC>
-__global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
-                                                    const uint8_t* __restrict__ acc,
-                                                    const uint32_t* __restrict__ chist, int lp_stride,
-                                                    uint32_t* __restrict__ cursor, Staging st) {
+__global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
+                                                 const uint8_t* __restrict__ acc, Staging st, uint32_t* __restrict__ ctab,
+                                                 int ls, int64_t rs, int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const DPlan& p = *pp;
     int64_t a0, c0, c1;
@@ -434,27 +369,59 @@ __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBat
     chunk_panes(gd, c0, c1, &pa, &pb);
     const int lp_n = (pb - pa + 1) * gd.nb;
     __shared__ int64_t lb[kMaxChunkBnd];
+    __shared__ uint32_t wsum[4];
     const int nlb = chunk_bounds(gd, pa, pb, lb);
-    // LDS carve (16-byte aligned pieces)
+    const int lpp = (lp_n + 4 + 3) & ~3;
     int64_t* s_val = (int64_t*)smem;                                          // [NVC][kTile]
-    uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [kMaxLocalParts]
-    uint32_t* tcnt = cur + kMaxLocalParts;                                    // [kMaxLocalParts + 1]
-    uint16_t* s_klo = (uint16_t*)(tcnt + kMaxLocalParts + 4);                 // [kTile]
+    uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [lpp]
+    uint32_t* tcnt = cur + lpp;                                               // [lpp]
+    uint16_t* s_klo = (uint16_t*)(tcnt + lpp);                                // [kTile]
     uint16_t* s_lp = s_klo + kTile;                                           // [kTile]
     uint8_t* s_vd = (uint8_t*)(s_lp + kTile);                                 // [NVC][kTile]
-    __shared__ uint32_t wsum[4];
-    // reserve this chunk's run in every partition it feeds (runs of one partition land in any chunk order)
-    for (int k = threadIdx.x; k < lp_n; k += kBlock) {
-        uint32_t c = chist[(int64_t)blockIdx.x * lp_stride + k];
-        cur[k] = c ? atomicAdd(&cursor[pa * gd.nb + k], c) : 0u;
+    const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
+    const int64_t region = (int64_t)blockIdx.x * rs;
+
+    // ---- (1) count
+    for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
+    __syncthreads();
+    {
+        constexpr int V = 4;   // 16-byte key loads in flight per thread
+        for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
+            uint4 kv[V];
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const int64_t i = base + (int64_t)u * kBlock * 4;
+                if (kcol && i + 3 < gd.nbatch && i < c1) kv[u] = *(const uint4*)(kcol + i);
+                else if (kcol && i < c1) {
+                    kv[u].x = kcol[i];
+                    kv[u].y = i + 1 < gd.nbatch ? kcol[i + 1] : 0u;
+                    kv[u].z = i + 2 < gd.nbatch ? kcol[i + 2] : 0u;
+                    kv[u].w = i + 3 < gd.nbatch ? kcol[i + 3] : 0u;
+                } else kv[u] = make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < V; ++u) {
+                const uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t i = base + (int64_t)u * kBlock * 4 + e;
+                    if (i < c0 || i >= c1) continue;
+                    const int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, kk[e], pane_err, true);
+                    if (lp >= 0) atomicAdd(&tcnt[lp], 1u);
+                }
+            }
+        }
     }
+    __syncthreads();
+    // ---- (2) run offsets of this chunk
+    block_excl_scan(tcnt, lp_n, wsum);
+    for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
+    for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] = tcnt[k];
+    __syncthreads();
+    // ---- (3) tiles: load, LDS counting sort, coalesced run writes
     const uint32_t kmask = (1u << gd.kbits) - 1u;
     const bool nullable = st.nullable_mask != 0;
-    const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
-    // row of (thread t, slot j) in a tile: t0 + (j/2)*2*kBlock + 2t + (j&1): lanes read 8-byte key pairs
-    // and 16-byte value pairs, each wave instruction one contiguous span
     for (int64_t t0 = a0; t0 < c1; t0 += kTile) {
-        // issue every load of the tile first
         uint32_t key[kTileE];
         int64_t val[NVC][kTileE];
 #pragma unroll
@@ -493,7 +460,6 @@ __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBat
         }
         __syncthreads();
         block_excl_scan(tcnt, lp_n, wsum);
-        // place rows at their sorted LDS position
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
             if (lp[j] < 0) continue;
@@ -513,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBat
         const uint32_t total = tcnt[lp_n];
         for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
             const int l = s_lp[s];
-            const uint32_t gpos = cur[l] + (s - tcnt[l]);
+            const int64_t gpos = region + cur[l] + (s - tcnt[l]);
             st.klo[gpos] = s_klo[s];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
@@ -528,52 +494,11 @@ __global__ __launch_bounds__(kBlock) void k_scatter(DPlan* __restrict__ pp, DBat
     }
 }
 
-inline size_t scatter_lds_bytes(int nvc, bool nullable) {
-    return (size_t)nvc * kTile * 8 + (size_t)(2 * kMaxLocalParts + 4) * 4 + (size_t)kTile * 4 + (nullable ? (size_t)nvc * kTile : 0);
-}
-
-// Fallback for chunks touching more than kMaxLocalParts partitions: one scattered store per row.
-template <bool SORTED, bool WHERE>
-__global__ __launch_bounds__(kBlock) void k_scatter_direct(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
-                                                           const uint8_t* __restrict__ acc,
-                                                           const uint32_t* __restrict__ chist, int lp_stride,
-                                                           uint32_t* __restrict__ cursor, Staging st) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t curd[];
-    const DPlan& p = *pp;
-    int64_t a0, c0, c1;
-    chunk_range(gd, &a0, &c0, &c1);
-    int pa, pb;
-    chunk_panes(gd, c0, c1, &pa, &pb);
-    const int lp_n = (pb - pa + 1) * gd.nb;
-    __shared__ int64_t lb[kMaxChunkBnd];
-    const int nlb = chunk_bounds(gd, pa, pb, lb);
-    for (int k = threadIdx.x; k < lp_n; k += kBlock) {
-        uint32_t c = chist[(int64_t)blockIdx.x * lp_stride + k];
-        curd[k] = c ? atomicAdd(&cursor[pa * gd.nb + k], c) : 0u;
-    }
-    __syncthreads();
-    const uint32_t kmask = (1u << gd.kbits) - 1u;
-    for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
-        const uint32_t key = load_key(p, b, i);
-        int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, key, nullptr, false);
-        if (lp < 0) continue;
-        uint32_t pos = atomicAdd(&curd[lp], 1u);
-        st.klo[pos] = (uint16_t)(key & kmask);
-        for (int v = 0; v < p.n_vc; ++v) {
-            int c = p.vc_col[v];
-            st.val[v][pos] = ((const int64_t*)b.col[c])[i];
-            if (st.nullable_mask & (1u << v)) st.valid[v][pos] = col_valid(b, c, i) ? 1 : 0;
-        }
-    }
-}
-
-// per group: zero the partition totals and the per-pane scalars (WHERE error flag, membership
-// fingerprint) of freshly claimed ring slots
-__global__ void k_group_prep(GroupDesc gd, uint32_t* totals, int32_t* pane_err, int64_t* pane_mcnt,
-                             unsigned long long* pane_mhash) {
-    for (int k = threadIdx.x; k < gd.np; k += blockDim.x) totals[k] = 0;
-    int r = threadIdx.x;
-    if (r < gd.n_panes && ((gd.fresh >> r) & 1ull)) {
+// per group: zero the per-pane scalars (WHERE error flag, membership fingerprint) of freshly
+// claimed ring slots
+__global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < gd.n_panes && gd.fresh[r]) {
         int64_t s = (gd.q_lo + r) % gd.ring;
         pane_err[s] = 0;
         pane_mcnt[s] = 0;
@@ -734,10 +659,12 @@ constexpr int kAggBlock = 512;
 // One workgroup per partition (pane, key bucket): LDS aggregation of the partition's staged run,
 // then either (a) direct emission of the final rows when the pane is a whole tumbling window that
 // closes in this batch (direct[2*rel] = out_base >= 0), or (b) write / merge into the pane state.
+constexpr int kMaxRuns = 2048;
+
 template <int NVC>
 __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
-                                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ totals,
-                                                   Staging st, DState ds, Results res) {
+                                                   const uint32_t* __restrict__ ctab, int ls, int64_t rs,
+                                                   Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const DPlan& p = *pp;
     const int pid = blockIdx.x;
@@ -745,11 +672,50 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     const int rel = pid / gd.nb, bucket = pid % gd.nb;
     const int64_t q = gd.q_lo + rel;
     const int64_t slot = q % gd.ring;
-    const uint32_t s0 = start[pid];
-    const uint32_t s1 = s0 + totals[pid];
-    const bool fresh = (gd.fresh >> rel) & 1ull;
-    const int64_t dbase = rel < 64 ? gd.dbase[rel] : -1;
-    if (s1 == s0 && (!fresh || dbase >= 0)) return;   // nothing to merge / no rows to emit
+    const bool fresh = gd.fresh[rel] != 0;
+    const int64_t dbase = gd.dbase[rel];
+    // ---- the partition's rows are one run per chunk that holds rows of this pane (k_part)
+    __shared__ int64_t r_start[kMaxRuns];
+    __shared__ uint32_t r_pre[kMaxRuns + 1];
+    __shared__ uint32_t r_wsum[kAggBlock / 64];
+    int c_lo = 0, c_hi = gd.nch - 1;
+    if (gd.sorted) {
+        const int64_t e0 = gd.pbnd[rel], e1 = gd.pbnd[rel + 1];
+        if (e1 <= e0) { c_lo = 0; c_hi = -1; }
+        else { c_lo = (int)((e0 - gd.abase) / gd.chunk); c_hi = (int)((e1 - 1 - gd.abase) / gd.chunk); }
+    }
+    const int nruns = min(c_hi - c_lo + 1, kMaxRuns);
+    for (int j = threadIdx.x; j < nruns; j += kAggBlock) {
+        const int c = c_lo + j;
+        const int64_t a0 = gd.abase + (int64_t)c * gd.chunk;
+        int pa, pb;
+        chunk_panes(gd, max(gd.lo, a0), min(gd.hi, a0 + gd.chunk), &pa, &pb);
+        const int lp = (rel - pa) * gd.nb + bucket;
+        uint32_t o0 = 0, o1 = 0;
+        if (rel >= pa && rel <= pb) { o0 = ctab[(int64_t)c * ls + lp]; o1 = ctab[(int64_t)c * ls + lp + 1]; }
+        r_start[j] = (int64_t)c * rs + o0;
+        r_pre[j] = o1 - o0;
+    }
+    __syncthreads();
+    {   // exclusive prefix of run lengths (512 threads)
+        const int per = (nruns + kAggBlock - 1) / kAggBlock;
+        const int b0 = threadIdx.x * per, b1 = min(nruns, b0 + per);
+        uint32_t sm = 0;
+        for (int k = b0; k < b1; ++k) sm += r_pre[k];
+        uint32_t x = sm;
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        for (int o = 1; o < 64; o <<= 1) { uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+        if (lane == 63) r_wsum[wv] = x;
+        __syncthreads();
+        uint32_t wb = 0;
+        for (int w = 0; w < wv; ++w) wb += r_wsum[w];
+        uint32_t run = wb + x - sm;
+        for (int k = b0; k < b1; ++k) { uint32_t c = r_pre[k]; r_pre[k] = run; run += c; }
+        if (threadIdx.x == kAggBlock - 1) r_pre[nruns] = run;
+        __syncthreads();
+    }
+    const uint32_t total = nruns > 0 ? r_pre[nruns] : 0u;
+    if (total == 0 && (!fresh || dbase >= 0)) return;   // nothing to merge / no rows to emit
 
     uint32_t* lcnt = (uint32_t*)(lds + lay.off_cnt);
     for (int k = threadIdx.x; k < lay.bytes / 4; k += kAggBlock) ((uint32_t*)lds)[k] = 0;
@@ -760,38 +726,42 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     for (int v = 0; v < NVC; ++v) { fl[v] = p.vc_flags[v]; isf[v] = p.vc_is_float[v] != 0; }
     const uint32_t nullm = st.nullable_mask;
     __syncthreads();
-    // the run [s0, s0 + n) starts 8-aligned: each lane reads 8 rows per step with 16-byte loads
-    const uint32_t s_end = s0 + totals[pid];
-    for (uint32_t base = s0 + threadIdx.x * 8; base < s_end; base += kAggBlock * 8) {
-        const uint4 kq = *(const uint4*)(st.klo + base);
-        longlong2 vq[NVC][4];
-        uint2 vdq[NVC];
+    // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}
+    constexpr int U = 4;   // rows in flight per thread
+    for (uint32_t base = threadIdx.x; base < total; base += kAggBlock * U) {
+        int64_t pos[U];
+        int klu[U];
+        int64_t rv[NVC][U];
+        uint8_t vd[NVC][U];
 #pragma unroll
-        for (int v = 0; v < NVC; ++v) {
-            if (fl[v] == 0) continue;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) vq[v][m] = *(const longlong2*)(st.val[v] + base + 2 * m);
-            if (nullm & (1u << v)) vdq[v] = *(const uint2*)(st.valid[v] + base);
-        }
-        const uint32_t kw[4] = {kq.x, kq.y, kq.z, kq.w};
-        if (gd.pad & 1) {   // diagnostic build knob: loads only
-            uint64_t acc = kq.x ^ kq.y;
-#pragma unroll
-            for (int v = 0; v < NVC; ++v) acc ^= (uint64_t)vq[v][0].x ^ (uint64_t)vq[v][1].y ^ (uint64_t)vq[v][2].x ^ (uint64_t)vq[v][3].y;
-            if (acc == 0x123456789ull) lcnt[0] = 1;
-            continue;
+        for (int u = 0; u < U; ++u) {
+            const uint32_t v = base + u * kAggBlock;
+            pos[u] = -1;
+            if (v < total) {
+                int lo = 0, hi = nruns - 1;
+                while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= v) lo = m; else hi = m - 1; }
+                pos[u] = r_start[lo] + (v - r_pre[lo]);
+            }
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            if (base + e >= s_end) break;
-            const int kl = (int)((kw[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu);
+        for (int u = 0; u < U; ++u) {
+            klu[u] = pos[u] >= 0 ? (int)st.klo[pos[u]] : -1;
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                rv[v][u] = (pos[u] >= 0 && fl[v]) ? st.val[v][pos[u]] : 0;
+                vd[v][u] = (pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int kl = klu[u];
+            if (kl < 0) break;
             atomicAdd(&lcnt[kl], 1u);
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
                 const int f = fl[v];
-                if (f == 0) continue;
-                if ((nullm & (1u << v)) && !((e < 4 ? vdq[v].x >> (8 * e) : vdq[v].y >> (8 * (e - 4))) & 0xFFu)) continue;
-                const int64_t raw = (e & 1) ? vq[v][e >> 1].y : vq[v][e >> 1].x;
+                if (f == 0 || !vd[v][u]) continue;
+                const int64_t raw = rv[v][u];
                 if (f & NEED_CNT) atomicAdd(&((uint32_t*)(lds + lay.off_vcnt[v]))[kl], 1u);
                 if (isf[v]) {
                     const double x = __longlong_as_double(raw);
@@ -813,7 +783,10 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     for (int v = 0; v < NVC; ++v) need_m2 |= (p.vc_flags[v] & NEED_M2) != 0;
     if (need_m2) {
         // second pass over the (L2-resident) run: Σ (x - mean)^2 with this partial's mean (stats._variance shape)
-        for (uint32_t i = s0 + threadIdx.x; i < s_end; i += kAggBlock) {
+        for (uint32_t vv = threadIdx.x; vv < total; vv += kAggBlock) {
+            int lo = 0, hi = nruns - 1;
+            while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= vv) lo = m; else hi = m - 1; }
+            const int64_t i = r_start[lo] + (vv - r_pre[lo]);
             const int kl = st.klo[i];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
@@ -849,6 +822,11 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     __shared__ uint32_t esh[20];
     if (dbase >= 0) {
         const int32_t widx = gd.didx[rel];
+        const int32_t perr = pane_err[slot];
+        if (perr) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
+            if (threadIdx.x == 0 && bucket == 0) atomicOr(&res.win_err[widx], perr);
+            return;
+        }
         const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
         for (int kb = 0; kb < kk; kb += kAggBlock) {
             const int kl = kb + threadIdx.x;

@@ -112,7 +112,12 @@ class ek_stats(C.Structure):
         ("windows_out", C.c_int64),
         ("rows_out", C.c_int64),
         ("last_batch_device_ms", C.c_double),
+        ("phase_ms", C.c_double * 4),
+        ("phase_launches", C.c_int64 * 4),
     ]
+
+
+EK_PHASE_STATS, EK_PHASE_PARTITION, EK_PHASE_AGGREGATE, EK_PHASE_FINALIZE = 0, 1, 2, 3
 
 
 def mix64(x: int) -> int:

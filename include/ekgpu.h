@@ -164,7 +164,14 @@ typedef struct {
     int64_t windows_out;      /* windows triggered                              */
     int64_t rows_out;         /* result rows                                    */
     double last_batch_device_ms; /* device time of the last push (HIP events)   */
+    /* Device time of the last push per phase (HIP events on the engine stream around each launch):
+     * [EK_PHASE_STATS] batch statistics + pane bounds, [EK_PHASE_PARTITION] k_part,
+     * [EK_PHASE_AGGREGATE] k_agg, [EK_PHASE_FINALIZE] k_finalize. */
+    double phase_ms[4];
+    int64_t phase_launches[4];
 } ek_stats;
+
+enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };
 
 /* Error codes. */
 enum {

@@ -16,6 +16,14 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 @pytest.fixture(scope="module")
 def engine_mod():
+    # torch ships its own HIP/HSA runtime copy: it must open the device before libekgpu's runtime
+    # does, or torch reports no GPUs ("sharing a process with PyTorch")
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     from ekgpu import engine
     if engine.lib().ek_device_count() < 1:
         pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
