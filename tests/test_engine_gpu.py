@@ -168,3 +168,41 @@ def test_full_size_c2_properties(engine_mod):
         avg = w.values[0].view(np.float64)
         assert (avg >= 0).all() and (avg < 100).all()
     eng.close()
+
+
+def test_key_sharded_engines_union(oracle, engine_mod):
+    """Two engine handles as two key-hash shards on one device: the union of their
+    rows equals the single-stream oracle result; the handles share nothing."""
+    from ekgpu.shard import ShardDictionary, shard_batch
+    sql = "SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)"
+    keys, world = 4000, 2
+    cols = _iot_cols(300_000, keys, seed=52, epm=10)
+    ref = {w.end: w.rows() for w in oracle.run(compile_rule(sql, IOT_SCHEMA, num_keys=keys).plan, cols).windows}
+    shards = []
+    for r in range(world):
+        d = ShardDictionary()
+        local, _ = shard_batch(cols, 0, world, r, d)
+        eng = engine_mod.Engine(compile_rule(sql, IOT_SCHEMA, num_keys=len(d.global_of)).plan)
+        for lo in range(0, len(local[0]), 50_000):
+            eng.push_host([c[lo:lo + 50_000] for c in local])
+        wins = eng.poll()
+        eng.close()
+        rows = {}
+        for w in wins:
+            rr = w.rows()
+            g = d.decode(np.fromiter(rr.keys(), dtype=np.int64, count=len(rr)))
+            rows[w.end] = {int(k): v for k, v in zip(g, rr.values())}
+        shards.append((rows, int(local[1].max())))
+    closed = min(m for _, m in shards)
+    ends = [e for e in ref if e <= closed]
+    assert len(ends) >= 2
+    for e in ends:
+        union = {}
+        for rows, _ in shards:
+            part = rows.get(e, {})
+            assert not (set(part) & set(union))
+            union.update(part)
+        assert set(union) == set(ref[e])
+        for k, v in ref[e].items():
+            g = union[k]
+            assert g[1:] == v[1:] and abs(g[0] - v[0]) <= 1e-6 * abs(v[0])
