@@ -367,7 +367,7 @@ struct Engine {
             bytes_per_key += (f & NEED_CNT ? 4 : 0) + (f & NEED_SUM ? 8 : 0) + (f & NEED_MIN ? 8 : 0) + (f & NEED_MAX ? 8 : 0) +
                              (f & NEED_M2 ? 8 : 0) + (f & NEED_FSUM ? 8 : 0);
         }
-        int want = env_int("EKGPU_KBITS", 10);
+        int want = env_int("EKGPU_KBITS", 11);
         kbits = 0;
         while ((1u << kbits) < K && kbits < want) kbits++;
         while (kbits > 0 && ((1 << kbits) * bytes_per_key) > 48 * 1024) kbits--;
@@ -389,7 +389,7 @@ struct Engine {
             for (int v = 0; v < dp.n_vc; ++v) if (dp.vc_flags[v] & NEED_CNT) { lay.off_vcnt[v] = o; o += 4 * kk; }
             lay.bytes = (o + 15) & ~15;
         }
-        chunk = env_int("EKGPU_CHUNK", 16384);
+        chunk = env_int("EKGPU_CHUNK", 8192);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
         np_max = env_int("EKGPU_NP_MAX", 8192);

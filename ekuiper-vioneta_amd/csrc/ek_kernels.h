@@ -384,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     // ---- (1) count
     for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
     __syncthreads();
-    {
+    if (!(gd.pad & 4)) {   // (diagnostic knob 4: skip the count pass; timing only)
         constexpr int V = 4;   // 16-byte key loads in flight per thread
         for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
             uint4 kv[V];
@@ -421,6 +421,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     // ---- (3) tiles: load, LDS counting sort, coalesced run writes
     const uint32_t kmask = (1u << gd.kbits) - 1u;
     const bool nullable = st.nullable_mask != 0;
+    if (gd.pad & 16) return;   // diagnostic knob 16: count pass only
     for (int64_t t0 = a0; t0 < c1; t0 += kTile) {
         uint32_t key[kTileE];
         int64_t val[NVC][kTileE];
@@ -476,10 +477,10 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
             }
         }
         __syncthreads();
-        const uint32_t total = tcnt[lp_n];
+        const uint32_t total = (gd.pad & 8) ? 0u : tcnt[lp_n];   // diagnostic knob 8: no global stores
         for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
             const int l = s_lp[s];
-            const int64_t gpos = region + cur[l] + (s - tcnt[l]);
+            const int64_t gpos = (gd.pad & 64) ? region + (t0 - a0) + s : region + cur[l] + (s - tcnt[l]);  // 64: experiment
             st.klo[gpos] = s_klo[s];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
@@ -659,7 +660,7 @@ constexpr int kAggBlock = 512;
 // One workgroup per partition (pane, key bucket): LDS aggregation of the partition's staged run,
 // then either (a) direct emission of the final rows when the pane is a whole tumbling window that
 // closes in this batch (direct[2*rel] = out_base >= 0), or (b) write / merge into the pane state.
-constexpr int kMaxRuns = 2048;
+constexpr int kMaxRuns = 1024;
 
 template <int NVC>
 __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
@@ -675,7 +676,7 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     const bool fresh = gd.fresh[rel] != 0;
     const int64_t dbase = gd.dbase[rel];
     // ---- the partition's rows are one run per chunk that holds rows of this pane (k_part)
-    __shared__ int64_t r_start[kMaxRuns];
+    __shared__ uint32_t r_start[kMaxRuns];   // staging index of each run (staging < 2^32 rows, host-checked)
     __shared__ uint32_t r_pre[kMaxRuns + 1];
     __shared__ uint32_t r_wsum[kAggBlock / 64];
     int c_lo = 0, c_hi = gd.nch - 1;
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
         const int lp = (rel - pa) * gd.nb + bucket;
         uint32_t o0 = 0, o1 = 0;
         if (rel >= pa && rel <= pb) { o0 = ctab[(int64_t)c * ls + lp]; o1 = ctab[(int64_t)c * ls + lp + 1]; }
-        r_start[j] = (int64_t)c * rs + o0;
+        r_start[j] = (uint32_t)((int64_t)c * rs + o0);
         r_pre[j] = o1 - o0;
     }
     __syncthreads();
@@ -726,21 +727,29 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     for (int v = 0; v < NVC; ++v) { fl[v] = p.vc_flags[v]; isf[v] = p.vc_is_float[v] != 0; }
     const uint32_t nullm = st.nullable_mask;
     __syncthreads();
-    // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}
-    constexpr int U = 4;   // rows in flight per thread
-    for (uint32_t base = threadIdx.x; base < total; base += kAggBlock * U) {
+    // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}.
+    // Each wave takes a span of 64*U consecutive rows (coalesced loads); its first run is found by
+    // one binary search, and every lane then advances its run pointer monotonically.
+    constexpr int U = 4;   // rows in flight per lane
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    auto run_of = [&](uint32_t v) {
+        int lo = 0, hi = nruns - 1;
+        while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= v) lo = m; else hi = m - 1; }
+        return lo;
+    };
+    for (uint32_t span = (uint32_t)wave * 64u * U; span < total; span += (uint32_t)kAggBlock * U) {
+        int j = run_of(span);
         int64_t pos[U];
         int klu[U];
         int64_t rv[NVC][U];
         uint8_t vd[NVC][U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t v = base + u * kAggBlock;
+            const uint32_t v = span + u * 64 + lane;
             pos[u] = -1;
             if (v < total) {
-                int lo = 0, hi = nruns - 1;
-                while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= v) lo = m; else hi = m - 1; }
-                pos[u] = r_start[lo] + (v - r_pre[lo]);
+                while (j + 1 < nruns && r_pre[j + 1] <= v) ++j;
+                pos[u] = (int64_t)r_start[j] + (v - r_pre[j]);
             }
         }
 #pragma unroll
@@ -783,10 +792,12 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     for (int v = 0; v < NVC; ++v) need_m2 |= (p.vc_flags[v] & NEED_M2) != 0;
     if (need_m2) {
         // second pass over the (L2-resident) run: Σ (x - mean)^2 with this partial's mean (stats._variance shape)
-        for (uint32_t vv = threadIdx.x; vv < total; vv += kAggBlock) {
-            int lo = 0, hi = nruns - 1;
-            while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= vv) lo = m; else hi = m - 1; }
-            const int64_t i = r_start[lo] + (vv - r_pre[lo]);
+        for (uint32_t span = (uint32_t)wave * 64u; span < total; span += (uint32_t)kAggBlock) {
+            const uint32_t vv = span + lane;
+            if (vv >= total) continue;
+            int lo = run_of(span);
+            while (lo + 1 < nruns && r_pre[lo + 1] <= vv) ++lo;
+            const int64_t i = (int64_t)r_start[lo] + (vv - r_pre[lo]);
             const int kl = st.klo[i];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
