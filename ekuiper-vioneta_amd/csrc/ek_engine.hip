@@ -26,6 +26,8 @@
 #include <vector>
 
 #include "ek_kernels.h"
+#include "ek_lib.h"
+#include "ek_range.h"
 
 using namespace ek;
 
@@ -272,35 +274,56 @@ struct Engine {
                 return fail(EK_ERR_INVALID, "HAVING aggregate slot out of range");
         }
         wtype = plan.window_type;
+        bool sort_aggs = false;
+        for (int k = 0; k < plan.n_aggs; ++k)
+            sort_aggs |= plan.aggs[k].fn == EK_AGG_MEDIAN || plan.aggs[k].fn == EK_AGG_PERCENTILE_CONT ||
+                         plan.aggs[k].fn == EK_AGG_PERCENTILE_DISC;
         if (plan.is_event_time) {
-            // NewEventTimeTrigger (event_window_trigger.go:35-53)
-            if (wtype < EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
+            // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time
+            if (wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
+        } else if (wtype != EK_WINDOW_COUNT) {
+            return fail(EK_ERR_UNSUPPORTED, "processing-time windows other than COUNTWINDOW are wall-clock driven (use event time)");
         }
-        if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING)
-            return fail(EK_ERR_UNSUPPORTED, "window type %d is not implemented by this engine build (tumbling/hopping only)", wtype);
-        if (!plan.is_event_time) return fail(EK_ERR_UNSUPPORTED, "processing-time time windows are not implemented (use event time)");
-        if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
-            return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
+        range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT || sort_aggs ||
+                     env_int("EKGPU_FORCE_RANGE", 0) != 0;
+        need_rel = wtype == EK_WINDOW_SLIDING;
+        if (plan.is_event_time) {
+            if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
+                return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
+            if (plan.nullable_mask & (1u << plan.ts_column)) return fail(EK_ERR_INVALID, "nullable timestamp column");
+        }
         if (plan.key_column >= 0) {
             if (!col_ok(plan.key_column) || plan.column_type[plan.key_column] != EK_COL_U32)
                 return fail(EK_ERR_INVALID, "GROUP BY key must be a u32 dictionary column");
             if (plan.num_keys == 0) return fail(EK_ERR_INVALID, "num_keys must be > 0");
             if (plan.nullable_mask & (1u << plan.key_column)) return fail(EK_ERR_UNSUPPORTED, "nullable GROUP BY key");
         }
-        if (plan.nullable_mask & (1u << plan.ts_column)) return fail(EK_ERR_INVALID, "nullable timestamp column");
-        int64_t u = unit_ms(plan.time_unit);
-        if (u == 0) return fail(EK_ERR_INVALID, "bad time unit");
-        if (plan.length <= 0) return fail(EK_ERR_INVALID, "window length must be > 0");
-        L = (int64_t)plan.length * u;
-        if (plan.delay != 0) return fail(EK_ERR_UNSUPPORTED, "window delay is not supported for tumbling/hopping");
-        if (wtype == EK_WINDOW_TUMBLING) {
-            H = L; P = L; raw_interval = plan.length;
+        if (plan.length <= 0) return fail(EK_ERR_INVALID, "Window size should not be less than zero.");
+        if (wtype == EK_WINDOW_COUNT) {
+            // window_op.go:100-103: CountInterval defaults to CountLength
+            if (plan.interval < 0) return fail(EK_ERR_INVALID, "count window interval must be >= 0");
+            L = plan.length;
+            H = plan.interval > 0 ? plan.interval : plan.length;
+            P = 1;
         } else {
-            if (plan.interval <= 0) return fail(EK_ERR_INVALID, "hopping interval must be > 0");
-            H = (int64_t)plan.interval * u;
-            if (H > L) return fail(EK_ERR_UNSUPPORTED, "hopping interval larger than the window length");
-            P = gcd64(L, H);
-            raw_interval = plan.interval;
+            int64_t u = unit_ms(plan.time_unit);
+            if (u == 0) return fail(EK_ERR_INVALID, "bad time unit");
+            L = (int64_t)plan.length * u;
+            if (plan.delay != 0 && wtype != EK_WINDOW_SLIDING) return fail(EK_ERR_UNSUPPORTED, "window delay is only defined for sliding windows");
+            if (plan.delay < 0) return fail(EK_ERR_INVALID, "negative window delay");
+            if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_SLIDING) {
+                H = L; P = L; raw_interval = plan.length;
+            } else if (wtype == EK_WINDOW_SESSION) {
+                // SESSIONWINDOW(unit, length, timeout): raw interval of the tick grid = length (planner.go:394-400)
+                if (plan.interval <= 0) return fail(EK_ERR_INVALID, "session timeout must be > 0");
+                H = (int64_t)plan.interval * u; P = L; raw_interval = plan.length;
+            } else {
+                if (plan.interval <= 0) return fail(EK_ERR_INVALID, "hopping interval must be > 0");
+                H = (int64_t)plan.interval * u;
+                if (H > L && !range_mode) return fail(EK_ERR_UNSUPPORTED, "hopping interval larger than the window length");
+                P = gcd64(L, H);
+                raw_interval = plan.interval;
+            }
         }
         ppw = L / P;
         hpp = H / P;
@@ -503,6 +526,20 @@ struct Engine {
         pend_arr.clear();
         for (int c = 0; c < EK_MAX_COLUMNS; ++c) { pend_host[c].clear(); pend_vhost[c].clear(); pend_has_valid[c] = false; }
         slot_pane.assign(ring, INT64_MIN);
+        // range mode
+        eb.n = 0;
+        eb_base = 0;
+        eb_rel = 0;
+        eb_floor = 0;
+        sW = -1;
+        range_wins = 0;
+        delayq.clear();
+        delayq_head = 0;
+        h_rts.clear();
+        h_rts_base = 0;
+        sess_last_ticked = sess_has_trigger = false;
+        sess_trigger = 0;
+        count_k = 1;
         wins.clear();
         r_rows_used = 0;
         stats = ek_stats{};
@@ -815,7 +852,7 @@ struct Engine {
         GroupDesc gd{};
         const int npn = (int)(qb - qa + 1);
         // per-pane descriptors: [pbnd n+1][dbase n][didx n (i32)][fresh n (u8)] in one pinned block -> one upload
-        const size_t aux_words = (size_t)(npn + 1) + npn + (npn + 1) / 2 + (npn + 7) / 8 + 2;
+        const size_t aux_words = aux_layout_words(npn);
         int64_t* aux = desc_alloc(aux_words);
         if (!aux) return fail(EK_ERR_NOMEM, "pinned");
         int64_t* h_pbnd = aux;
@@ -847,7 +884,7 @@ struct Engine {
         gd.n_where = dp.n_where;
         gd.num_keys = dp.num_keys;
         gd.nbatch = db.n;
-        gd.nch = (int32_t)((hi - gd.abase + chunk - 1) / chunk);
+        gd.nch = (int32_t)((hi - gd.abase + csz - 1) / csz);
         gd.np = gd.n_panes * NB;
         gd.ring = ring;
         gd.has_accept = d_acc != nullptr;
@@ -855,6 +892,56 @@ struct Engine {
         gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
 
 
+        for (int k = 0; k <= npn; ++k) h_pbnd[k] = pbnd_host ? pbnd_host[k] : 0;
+        for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
+        // direct emission: a fresh tumbling pane whose whole content is in this group and whose window
+        // closes at this batch's watermark is finalised by k_agg itself (no pane-state round trip)
+        if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes) {
+            for (int r = 0; r < npn; ++r) {
+                int64_t q = qa + r;
+                if (!h_fresh[r] || win_end(q) > W || q < next_win) continue;
+                if (int rc = register_until(q)) return rc;
+                WinInfo& wi = win_info(q);
+                wi.direct = true;
+                h_dbase[r] = wi.out_base;
+                h_didx[r] = wi.slot;
+            }
+        }
+        if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
+        // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
+        const int lp_stride = gd.sorted ? std::min(gd.np, NB * mp) : gd.np;
+        if (lp_stride > np_max || (gd.sorted && mp > kMaxChunkBnd + 1))
+            return fail(EK_ERR_UNSUPPORTED, "chunk spans %d partitions (split the batch)", lp_stride);
+        if (int mc = max_chunks_in_pane(pbnd_host, gd, gd.chunk); mc > kMaxRuns)
+            return fail(EK_ERR_UNSUPPORTED, "a pane spans %d chunks of one group (max %d)", mc, kMaxRuns);
+        return launch_part_agg(db, gd, gd.sorted ? 1 : 0, d_acc, (int32_t*)pane_err.p, (int64_t*)pane_mcnt.p,
+                               (unsigned long long*)pane_mhash.p, lp_stride, any_fresh);
+    }
+
+    // one pinned block [pbnd n+1][dbase n][didx n (i32)][fresh n (u8)][voff n] -> device, pointers into gd
+    int upload_aux(int64_t* aux, size_t aux_words, int npn, GroupDesc& gd) {
+        size_t need = (aux_used + aux_words) * 8;
+        if (need > aux_d.bytes) {
+            hipStreamSynchronize(stream);
+            aux_used = 0;
+            if (int rc = ensure(aux_d, std::max<size_t>(aux_words * 8 * 4, 1 << 20))) return rc;
+        }
+        int64_t* dst = (int64_t*)aux_d.p + aux_used;
+        aux_used += aux_words;
+        hipMemcpyAsync(dst, aux, aux_words * 8, hipMemcpyHostToDevice, stream);
+        gd.pbnd = dst;
+        gd.dbase = dst + npn + 1;
+        gd.didx = (const int32_t*)(gd.dbase + npn);
+        gd.fresh = (const uint8_t*)(gd.didx + 2 * ((npn + 1) / 2));
+        gd.voff = (const int64_t*)(dst + aux_layout_voff(npn));
+        return 0;
+    }
+    static size_t aux_layout_voff(int npn) { return (size_t)(npn + 1) + npn + (npn + 1) / 2 + (npn + 7) / 8; }
+    static size_t aux_layout_words(int npn) { return aux_layout_voff(npn) + npn + 2; }
+
+    // k_part (MODE 0 unsorted / 1 sorted / 2 virtual panes) + k_agg for one group
+    int launch_part_agg(const DBatch& db, const GroupDesc& gd, int mode, const uint8_t* d_acc, int32_t* perr,
+                        int64_t* pmc, unsigned long long* pmh, int lp_stride, bool any_fresh) {
         const int64_t rs = gd.chunk;                                // staging region per chunk
         int64_t ne = (int64_t)gd.nch * rs + 64;
         if (ne > st_cap) {
@@ -877,48 +964,10 @@ struct Engine {
                 any_nullable = true;
             }
         }
-        for (int k = 0; k <= npn; ++k) h_pbnd[k] = pbnd_host ? pbnd_host[k] : 0;
-        for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
-        // direct emission: a fresh tumbling pane whose whole content is in this group and whose window
-        // closes at this batch's watermark is finalised by k_agg itself (no pane-state round trip)
-        if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes) {
-            for (int r = 0; r < npn; ++r) {
-                int64_t q = qa + r;
-                if (!h_fresh[r] || win_end(q) > W || q < next_win) continue;
-                if (int rc = register_until(q)) return rc;
-                WinInfo& wi = win_info(q);
-                wi.direct = true;
-                h_dbase[r] = wi.out_base;
-                h_didx[r] = wi.slot;
-            }
-        }
-        {
-            size_t need = (aux_used + aux_words) * 8;
-            if (need > aux_d.bytes) {
-                hipStreamSynchronize(stream);
-                aux_used = 0;
-                if (int rc = ensure(aux_d, std::max<size_t>(aux_words * 8 * 4, 1 << 20))) return rc;
-            }
-            int64_t* dst = (int64_t*)aux_d.p + aux_used;
-            aux_used += aux_words;
-            hipMemcpyAsync(dst, aux, aux_words * 8, hipMemcpyHostToDevice, stream);
-            gd.pbnd = dst;
-            gd.dbase = dst + npn + 1;
-            gd.didx = (const int32_t*)(gd.dbase + npn);
-            gd.fresh = (const uint8_t*)(gd.didx + 2 * ((npn + 1) / 2));
-        }
-
-        // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
-        const int lp_stride = gd.sorted ? std::min(gd.np, NB * mp) : gd.np;
-        if (lp_stride > np_max || (gd.sorted && mp > kMaxChunkBnd + 1))
-            return fail(EK_ERR_UNSUPPORTED, "chunk spans %d partitions (split the batch)", lp_stride);
-        if (int mc = max_chunks_in_pane(pbnd_host, gd, gd.chunk); mc > kMaxRuns)
-            return fail(EK_ERR_UNSUPPORTED, "a pane spans %d chunks of one group (max %d)", mc, kMaxRuns);
         const int ls = lp_stride + 1;
         if (int rc = ensure(chist, (size_t)gd.nch * ls * 4)) return rc;
         if (any_fresh)
-            hipLaunchKernelGGL(k_group_prep, dim3((npn + 255) / 256), dim3(256), 0, stream, gd, (int32_t*)pane_err.p,
-                               (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
+            hipLaunchKernelGGL(k_group_prep, dim3((gd.n_panes + 255) / 256), dim3(256), 0, stream, gd, perr, pmc, pmh);
         const bool wh = dp.n_where > 0;
         {
             const int nvc = std::max(1, dp.n_vc);
@@ -926,11 +975,12 @@ struct Engine {
             uint32_t* ct = (uint32_t*)chist.p;
             dim3 gp(gd.nch);
             const int ph = phase_begin(EK_PHASE_PARTITION);
-#define EK_PART(S, W, N) hipLaunchKernelGGL((k_part<S, W, N>), gp, dim3(kBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, (int32_t*)pane_err.p)
-#define EK_PART_N(S, W) switch (nvc) { case 1: EK_PART(S, W, 1); break; case 2: EK_PART(S, W, 2); break; \
-                                       case 3: EK_PART(S, W, 3); break; default: EK_PART(S, W, 4); break; }
-            if (gd.sorted) { if (wh) { EK_PART_N(true, true) } else { EK_PART_N(true, false) } }
-            else { if (wh) { EK_PART_N(false, true) } else { EK_PART_N(false, false) } }
+#define EK_PART(M, W, N) hipLaunchKernelGGL((k_part<M, W, N>), gp, dim3(kBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, perr)
+#define EK_PART_N(M, W) switch (nvc) { case 1: EK_PART(M, W, 1); break; case 2: EK_PART(M, W, 2); break; \
+                                       case 3: EK_PART(M, W, 3); break; default: EK_PART(M, W, 4); break; }
+#define EK_PART_W(M) if (wh) { EK_PART_N(M, true) } else { EK_PART_N(M, false) }
+            if (mode == 0) { EK_PART_W(0) } else if (mode == 1) { EK_PART_W(1) } else { EK_PART_W(2) }
+#undef EK_PART_W
 #undef EK_PART_N
 #undef EK_PART
             phase_end(ph);
@@ -940,13 +990,12 @@ struct Engine {
             Results rv = results_view();
             dim3 ga(gd.np);
             const uint32_t* ct = (const uint32_t*)chist.p;
-            const int32_t* pe = (const int32_t*)pane_err.p;
             const int ph = phase_begin(EK_PHASE_AGGREGATE);
             switch (nvc) {
-            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
-            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
-            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
-            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, pe); break;
+            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
+            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
+            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
+            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
             }
             phase_end(ph);
         }
@@ -1043,6 +1092,595 @@ struct Engine {
         return rc;
     }
 
+    // ================================================================== RANGE mode
+    // The accepted events stay in a device-resident event buffer in the order the reference's
+    // WindowOperator holds them (`inputs`, window_op.go:576-739); each triggered window is an index range
+    // [a, b) of it, aggregated as one "virtual pane" (k_part MODE 2 + k_agg direct emission).
+    // Used for SLIDINGWINDOW, SESSIONWINDOW, COUNTWINDOW, and for tumbling/hopping windows whose
+    // aggregates need the raw values (median, percentile_*).
+    bool range_mode = false;
+    struct EvBuf {
+        DevBuf col[EK_MAX_COLUMNS], valid[EK_MAX_COLUMNS], arr, rel;
+        int64_t cap = 0, n = 0;
+    };
+    EvBuf eb, eb_alt;
+    int64_t eb_base = 0;               // absolute stream position of buffer index 0
+    bool eb_valid_on[EK_MAX_COLUMNS] = {};
+    bool need_rel = false;             // sliding windows: per-event release step (closed right boundary)
+    int64_t eb_rel = 0;                // released prefix (buffer index)
+    int64_t eb_floor = 0;              // smallest buffer index a future window can start at
+    int64_t sW = -1;                   // arrival index at which the watermark reached W
+    int64_t range_wins = 0;            // windows triggered so far
+    // sliding windows with delay: queued triggers (event_window_trigger.go:129-135,156-161)
+    struct DelayTrig { int64_t pos_abs, ts, w_rel; };
+    std::vector<DelayTrig> delayq;
+    size_t delayq_head = 0;
+    // session windows: host mirror of the released timestamps [h_rts_base, h_rts_base + size)
+    std::vector<int64_t> h_rts;
+    int64_t h_rts_base = 0;
+    bool sess_last_ticked = false, sess_has_trigger = false;
+    int64_t sess_trigger = 0;
+    int64_t count_k = 1;               // COUNTWINDOW: next window index
+    DevBuf rq_d, ab_d, slot_d, trig_d, flags_d, cnts_d, runmax_d, runcm_d, mrg_keys[2], mrg_src[2], mrg_tmp, mrg_tail,
+        mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh;
+    std::vector<int64_t> h_ab;
+
+    size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
+
+    DBatch buffer_view() const {
+        DBatch d{};
+        d.n = eb.n;
+        for (int c = 0; c < plan.n_columns; ++c) {
+            d.col[c] = eb.col[c].p;
+            d.valid[c] = eb_valid_on[c] ? (const uint8_t*)eb.valid[c].p : nullptr;
+        }
+        return d;
+    }
+
+    // Make room for `add` more rows: drop the consumed prefix [0, eb_floor) and/or grow (double buffer).
+    int eb_reserve(int64_t add) {
+        const int64_t drop = std::max<int64_t>(0, std::min(eb_floor, eb.n));
+        const bool compact = drop > 0 && (drop >= (eb.n >> 1) || eb.n + add > eb.cap);
+        if (eb.n + add <= eb.cap && !compact) return 0;
+        const int64_t live = eb.n - (compact ? drop : 0);
+        int64_t cap = eb.cap;
+        if (live + add > cap) cap = std::max<int64_t>(2 * (live + add), (int64_t)1 << 16);
+        const int64_t d = compact ? drop : 0;
+        auto mv = [&](DevBuf& dst, DevBuf& src, size_t es) -> int {
+            if (dst.bytes < (size_t)cap * es) {
+                release(dst);
+                if (int rc = ensure(dst, (size_t)cap * es)) return rc;
+            }
+            if (src.p && live) hipMemcpyAsync(dst.p, (char*)src.p + d * es, (size_t)live * es, hipMemcpyDeviceToDevice, stream);
+            return 0;
+        };
+        for (int c = 0; c < plan.n_columns; ++c) {
+            if (int rc = mv(eb_alt.col[c], eb.col[c], col_es(c))) return rc;
+            if (eb_valid_on[c]) if (int rc = mv(eb_alt.valid[c], eb.valid[c], 1)) return rc;
+        }
+        if (int rc = mv(eb_alt.arr, eb.arr, 8)) return rc;
+        if (need_rel) if (int rc = mv(eb_alt.rel, eb.rel, 8)) return rc;
+        std::swap(eb, eb_alt);
+        eb.cap = cap;
+        eb.n = live;
+        eb_alt.n = 0;
+        eb_base += d;
+        eb_rel -= d;
+        eb_floor -= d;
+        return 0;
+    }
+
+    void fill_valid_ones(int c, int64_t from, int64_t cnt) {
+        if (cnt > 0) hipMemsetAsync((uint8_t*)eb.valid[c].p + from, 1, (size_t)cnt, stream);
+    }
+    // a batch brings validity for column c the buffer has not carried so far: all earlier rows are valid
+    int eb_enable_valid(int c) {
+        if (eb_valid_on[c]) return 0;
+        if (int rc = ensure(eb.valid[c], (size_t)std::max<int64_t>(eb.cap, 1))) return rc;
+        fill_valid_ones(c, 0, eb.n);
+        eb_valid_on[c] = true;
+        return 0;
+    }
+
+    // Append rows [start, start + cnt) of a batch (already in buffer order) to the buffer.
+    int eb_append(const DBatch& db, int64_t start, int64_t cnt, int64_t arr_base) {
+        for (int c = 0; c < plan.n_columns; ++c)
+            if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
+        if (int rc = eb_reserve(cnt)) return rc;
+        for (int c = 0; c < plan.n_columns; ++c) {
+            const size_t es = col_es(c);
+            hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
+                           hipMemcpyDeviceToDevice, stream);
+            if (eb_valid_on[c]) {
+                if (db.valid[c]) hipMemcpyAsync((uint8_t*)eb.valid[c].p + eb.n, db.valid[c] + start, (size_t)cnt, hipMemcpyDeviceToDevice, stream);
+                else fill_valid_ones(c, eb.n, cnt);
+            }
+        }
+        const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
+        hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
+        if (need_rel) hipMemsetAsync((int64_t*)eb.rel.p + eb.n, 0x7f, (size_t)cnt * 8, stream);   // "not released"
+        eb.n += cnt;
+        return 0;
+    }
+
+    // Merge the accepted rows of an out-of-order batch (or one that starts below the buffer's tail) into the
+    // ts-ordered buffer: the buffer rows with ts >= min_acc and the new rows are stably sorted by ts
+    // (buffer rows first on ties, then arrival order = watermark_op.go:158-168 insertion "after equal").
+    int eb_merge(const DBatch& db, int64_t start, const uint8_t* d_acc, int64_t n_acc, int64_t min_acc, int64_t max_acc,
+                 int64_t arr_base) {
+        const int64_t n = db.n;
+        const int tsc = dp.ts_col;
+        for (int c = 0; c < plan.n_columns; ++c)
+            if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
+        if (int rc = eb_reserve(n_acc)) return rc;
+        // accepted row indices of the batch, in arrival order
+        if (int rc = ensure(mrg_bidx, (size_t)std::max<int64_t>(n, 1) * 8)) return rc;
+        int64_t* bidx = (int64_t*)mrg_bidx.p;
+        if (d_acc) {
+            const int nb = (int)((n + kCompactTile - 1) / kCompactTile);
+            if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+            hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, d_acc, n, (int64_t*)cnts_d.p);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+            hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, d_acc, n, (const int64_t*)cnts_d.p, (int64_t)0, bidx);
+        } else {
+            const int g = (int)std::min<int64_t>(4096, (n_acc + 255) / 256);
+            hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, bidx, start, n_acc);
+        }
+        // tail of the buffer that interleaves with the batch
+        if (int rc = ensure(bounds_val, 8)) return rc;
+        if (int rc = ensure(bounds_idx, 8)) return rc;
+        hipMemcpyAsync(bounds_val.p, &min_acc, 8, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[tsc].p, (int64_t)0, eb.n,
+                           (const int64_t*)bounds_val.p, 1, (int64_t*)bounds_idx.p);
+        int64_t p = 0;
+        hipMemcpyAsync(&p, bounds_idx.p, 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "merge bound failed");
+        const int64_t ntail = eb.n - p, nm = ntail + n_acc;
+        // saved tail (every column + arrivals + release steps), 8-byte slots
+        const int nsv = plan.n_columns + 1 + (need_rel ? 1 : 0);
+        if (int rc = ensure(mrg_tail, (size_t)std::max<int64_t>(ntail, 1) * 8 * (nsv + plan.n_columns))) return rc;
+        auto tail_slot = [&](int k) { return (char*)mrg_tail.p + (size_t)k * std::max<int64_t>(ntail, 1) * 8; };
+        for (int c = 0; c < plan.n_columns; ++c) {
+            hipMemcpyAsync(tail_slot(c), (char*)eb.col[c].p + p * col_es(c), (size_t)ntail * col_es(c), hipMemcpyDeviceToDevice, stream);
+            if (eb_valid_on[c]) hipMemcpyAsync(tail_slot(nsv + c), (uint8_t*)eb.valid[c].p + p, (size_t)ntail, hipMemcpyDeviceToDevice, stream);
+        }
+        hipMemcpyAsync(tail_slot(plan.n_columns), (int64_t*)eb.arr.p + p, (size_t)ntail * 8, hipMemcpyDeviceToDevice, stream);
+        if (need_rel) hipMemcpyAsync(tail_slot(plan.n_columns + 1), (int64_t*)eb.rel.p + p, (size_t)ntail * 8, hipMemcpyDeviceToDevice, stream);
+        // sort keys = ts - min_acc (the tail starts at ts >= min_acc), stable
+        for (int k = 0; k < 2; ++k) {
+            if (int rc = ensure(mrg_keys[k], (size_t)nm * 8)) return rc;
+            if (int rc = ensure(mrg_src[k], (size_t)nm * 8)) return rc;
+        }
+        const int g = (int)std::min<int64_t>(8192, (nm + 255) / 256);
+        hipLaunchKernelGGL(k_merge_keys, dim3(g), dim3(256), 0, stream, (const int64_t*)tail_slot(tsc), ntail,
+                           (const int64_t*)db.col[tsc], (const int64_t*)bidx, n_acc, min_acc, (uint64_t*)mrg_keys[0].p,
+                           (int64_t*)mrg_src[0].p);
+        int64_t hi_ts = std::max(max_acc, M);
+        uint64_t range = (uint64_t)(hi_ts - min_acc);
+        int end_bit = 1;
+        while (end_bit < 64 && (range >> end_bit)) end_bit++;
+        size_t tb = 0;
+        ekl_sort_pairs_u64(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, nm, end_bit, stream);
+        if (int rc = ensure(mrg_tmp, tb + 256)) return rc;
+        tb = mrg_tmp.bytes;
+        if (ekl_sort_pairs_u64(mrg_tmp.p, &tb, (const uint64_t*)mrg_keys[0].p, (uint64_t*)mrg_keys[1].p,
+                               (const int64_t*)mrg_src[0].p, (int64_t*)mrg_src[1].p, nm, end_bit, stream))
+            return fail(EK_ERR_DEVICE, "radix sort failed");
+        const int64_t* perm = (const int64_t*)mrg_src[1].p;
+        for (int c = 0; c < plan.n_columns; ++c) {
+            if (col_es(c) == 4)
+                hipLaunchKernelGGL(k_gather4, dim3(g), dim3(256), 0, stream, perm, nm, ntail, (const uint32_t*)tail_slot(c),
+                                   (const uint32_t*)db.col[c], (const int64_t*)bidx, (uint32_t*)eb.col[c].p + p);
+            else
+                hipLaunchKernelGGL(k_gather8, dim3(g), dim3(256), 0, stream, perm, nm, ntail, (const int64_t*)tail_slot(c),
+                                   (const int64_t*)db.col[c], (const int64_t*)bidx, (int64_t*)eb.col[c].p + p);
+            if (eb_valid_on[c])
+                hipLaunchKernelGGL(k_gather1, dim3(g), dim3(256), 0, stream, perm, nm, ntail, (const uint8_t*)tail_slot(nsv + c),
+                                   db.valid[c], (const int64_t*)bidx, (uint8_t*)eb.valid[c].p + p);
+        }
+        // arrivals of the batch rows: arr_base + row
+        if (int rc = ensure(mrg_col, (size_t)std::max<int64_t>(n, 1) * 8)) return rc;
+        hipLaunchKernelGGL(k_iota64, dim3((int)std::min<int64_t>(4096, (n + 255) / 256)), dim3(256), 0, stream,
+                           (int64_t*)mrg_col.p, arr_base, n);
+        hipLaunchKernelGGL(k_gather8, dim3(g), dim3(256), 0, stream, perm, nm, ntail, (const int64_t*)tail_slot(plan.n_columns),
+                           (const int64_t*)mrg_col.p, (const int64_t*)bidx, (int64_t*)eb.arr.p + p);
+        if (need_rel) {
+            hipMemsetAsync(mrg_col.p, 0x7f, (size_t)n * 8, stream);
+            hipLaunchKernelGGL(k_gather8, dim3(g), dim3(256), 0, stream, perm, nm, ntail,
+                               (const int64_t*)tail_slot(plan.n_columns + 1), (const int64_t*)mrg_col.p,
+                               (const int64_t*)bidx, (int64_t*)eb.rel.p + p);
+        }
+        eb.n = p + nm;
+        return 0;
+    }
+
+    // Per-event running max of the batch (arrival order) -> runmax_d
+    int batch_runmax(const int64_t* ts, int64_t n, int64_t seed) {
+        int nch = (int)((n + kAccChunk - 1) / kAccChunk);
+        if (int rc = ensure(runcm_d, (size_t)nch * 8)) return rc;
+        if (int rc = ensure(runmax_d, (size_t)n * 8)) return rc;
+        hipLaunchKernelGGL(k_chunk_max, dim3(nch), dim3(kBlock), 0, stream, ts, n, (int64_t*)runcm_d.p);
+        hipLaunchKernelGGL(k_scan_max, dim3(1), dim3(1024), 0, stream, (int64_t*)runcm_d.p, nch, seed);
+        hipLaunchKernelGGL(k_runmax, dim3(nch), dim3(kBlock), 0, stream, ts, n, (const int64_t*)runcm_d.p, (int64_t*)runmax_d.p);
+        return 0;
+    }
+
+    // one scalar device -> host (synchronous)
+    int64_t fetch_i64(const void* dptr) {
+        int64_t v = 0;
+        hipMemcpyAsync(&v, dptr, 8, hipMemcpyDeviceToHost, stream);
+        hipStreamSynchronize(stream);
+        return v;
+    }
+
+    // A triggered window before its range is resolved
+    struct PendWin { RangeQ q; int64_t start, end; };
+
+    // Resolve the ranges of `pw` on the device, register the windows, launch their aggregation.
+    int fire_windows(std::vector<PendWin>& pw) {
+        const int nq = (int)pw.size();
+        if (nq == 0) return 0;
+        if (int rc = ensure(rq_d, (size_t)nq * sizeof(RangeQ))) return rc;
+        if (int rc = ensure(ab_d, (size_t)nq * 16)) return rc;
+        std::vector<RangeQ> hq(nq);
+        for (int w = 0; w < nq; ++w) hq[w] = pw[w].q;
+        hipMemcpyAsync(rq_d.p, hq.data(), (size_t)nq * sizeof(RangeQ), hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_window_ranges, dim3((nq + 255) / 256), dim3(256), 0, stream, (const int64_t*)eb.col[std::max(0, dp.ts_col)].p,
+                           need_rel ? (const int64_t*)eb.rel.p : nullptr, eb_rel, (const RangeQ*)rq_d.p, nq, (int64_t*)ab_d.p);
+        h_ab.resize((size_t)nq * 2);
+        hipMemcpyAsync(h_ab.data(), ab_d.p, (size_t)nq * 16, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window range kernel failed");
+        // register in trigger order; rows reserved = min(K, members)
+        int64_t rows = 0;
+        for (int w = 0; w < nq; ++w) rows += std::min<int64_t>(K, h_ab[2 * w + 1] - h_ab[2 * w]);
+        if (int rc = ensure_results(rows, nq)) return rc;
+        std::vector<int32_t> slots(nq);
+        std::vector<int64_t> obase(nq);
+        for (int w = 0; w < nq; ++w) {
+            WinInfo wi{};
+            wi.j = range_wins++;
+            wi.start = pw[w].start;
+            wi.end = pw[w].end;
+            wi.out_base = r_rows_used;
+            wi.slot = (int32_t)wins.size();
+            wi.direct = true;
+            r_rows_used += std::min<int64_t>(K, h_ab[2 * w + 1] - h_ab[2 * w]);
+            wins.push_back(wi);
+            slots[w] = wi.slot;
+            obase[w] = wi.out_base;
+        }
+        stats.windows_out += nq;
+        if (plan.debug_membership) {
+            if (int rc = ensure(slot_d, (size_t)nq * 4)) return rc;
+            hipMemcpyAsync(slot_d.p, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)eb.arr.p,
+                               (const int64_t*)ab_d.p, (const int32_t*)slot_d.p, (int64_t*)r_wmc.p,
+                               (unsigned long long*)r_wmh.p);
+            hipStreamSynchronize(stream);   // slots/ab host vectors are reused
+        }
+        // virtual-pane groups of consecutive non-empty windows
+        const int64_t vcap = (int64_t)env_int("EKGPU_RANGE_GROUP_EVENTS", 1 << 26);
+        int w = 0;
+        while (w < nq) {
+            std::vector<int> members;
+            int64_t V = 0;
+            while (w < nq && (int)members.size() < max_panes_group) {
+                const int64_t sz = h_ab[2 * w + 1] - h_ab[2 * w];
+                if (sz == 0) { w++; continue; }       // empty window: no output (aggregate_operator.go:66-75)
+                if (!members.empty() && V + sz > vcap) break;
+                members.push_back(w);
+                V += sz;
+                w++;
+            }
+            if (members.empty()) continue;
+            if (int rc = run_vgroup(members, V, obase, slots)) return rc;
+        }
+        // windows never start below the last fired one's start (overlapping) or end (disjoint)
+        const bool overlap = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_COUNT;
+        eb_floor = std::max(eb_floor, overlap ? h_ab[2 * (nq - 1)] : h_ab[2 * (nq - 1) + 1]);
+        return 0;
+    }
+
+    int run_vgroup(const std::vector<int>& members, int64_t V, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots) {
+        const int npn = (int)members.size();
+        const size_t aux_words = aux_layout_words(npn);
+        int64_t* aux = desc_alloc(aux_words);
+        if (!aux) return fail(EK_ERR_NOMEM, "pinned");
+        int64_t* h_pbnd = aux;
+        int64_t* h_dbase = h_pbnd + npn + 1;
+        int32_t* h_didx = (int32_t*)(h_dbase + npn);
+        uint8_t* h_fresh = (uint8_t*)(h_didx + 2 * ((npn + 1) / 2));
+        int64_t* h_voff = aux + aux_layout_voff(npn);
+        int64_t v = 0;
+        for (int r = 0; r < npn; ++r) {
+            const int w = members[r];
+            const int64_t a = h_ab[2 * w], b = h_ab[2 * w + 1];
+            h_pbnd[r] = v;
+            h_voff[r] = a - v;
+            h_dbase[r] = obase[w];
+            h_didx[r] = slots[w];
+            h_fresh[r] = 1;
+            v += b - a;
+        }
+        h_pbnd[npn] = v;
+        GroupDesc gd{};
+        gd.lo = 0;
+        gd.hi = V;
+        gd.q_lo = 0;
+        gd.n_panes = npn;
+        gd.nb = NB;
+        gd.kbits = kbits;
+        gd.abase = 0;
+        gd.sorted = 1;
+        gd.ring = npn;
+        // chunk size: small windows -> shorter chunks (a chunk sorts at most kMaxChunkBnd+1 panes in LDS);
+        // big windows -> longer chunks (k_agg walks at most kMaxRuns chunk runs per pane)
+        int64_t csz = chunk;
+        int mp = max_panes_in_chunk(h_pbnd, gd, csz);
+        while (csz > 256 && (mp > kMaxChunkBnd + 1 || (int64_t)NB * mp > np_max)) { csz >>= 1; mp = max_panes_in_chunk(h_pbnd, gd, csz); }
+        while (max_chunks_in_pane(h_pbnd, gd, csz) > kMaxRuns && csz < (1 << 22)) { csz <<= 1; mp = max_panes_in_chunk(h_pbnd, gd, csz); }
+        const int lp_stride = std::min(npn * NB, NB * mp);
+        if (mp > kMaxChunkBnd + 1 || lp_stride > np_max || max_chunks_in_pane(h_pbnd, gd, csz) > kMaxRuns)
+            return fail(EK_ERR_UNSUPPORTED, "window sizes in one launch too uneven (%d windows per chunk, %lld events)",
+                        mp, (long long)V);
+        gd.chunk = (int32_t)csz;
+        gd.key_col = dp.key_col;
+        gd.ts_col = dp.ts_col;
+        gd.n_where = dp.n_where;
+        gd.num_keys = dp.num_keys;
+        gd.nbatch = eb.n;
+        gd.nch = (int32_t)((V + csz - 1) / csz);
+        gd.np = npn * NB;
+        gd.has_accept = 0;
+        gd.pad = 0;
+        if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
+        if (int rc = ensure(vp_err, (size_t)npn * 4)) return rc;
+        if (int rc = ensure(vp_mc, (size_t)npn * 8)) return rc;
+        if (int rc = ensure(vp_mh, (size_t)npn * 8)) return rc;
+        return launch_part_agg(buffer_view(), gd, 2, nullptr, (int32_t*)vp_err.p, (int64_t*)vp_mc.p,
+                               (unsigned long long*)vp_mh.p, lp_stride, true);
+    }
+
+    // ---- triggers per window type (host side of event_window_trigger.go:112-209 over the buffer)
+    int range_triggers(int64_t rel_prev) {
+        std::vector<PendWin> pw;
+        const int64_t n_new = eb_rel - rel_prev;
+        if (wtype == EK_WINDOW_SLIDING) {
+            const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
+            if (n_new > 0) {
+                // trigger events among the newly released rows (OVER (WHEN ...)), in release order
+                if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
+                if (int rc = ensure(trig_d, (size_t)n_new * 8)) return rc;
+                const int nb = (int)((n_new + kCompactTile - 1) / kCompactTile);
+                if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+                const DBatch bv = buffer_view();
+                hipLaunchKernelGGL(k_trigger_flags, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
+                                   d_plan, bv, rel_prev, eb_rel, (uint8_t*)flags_d.p);
+                hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new, (int64_t*)cnts_d.p);
+                hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+                hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new,
+                                   (const int64_t*)cnts_d.p, rel_prev, (int64_t*)trig_d.p);
+                const int64_t nt = fetch_i64((const int64_t*)cnts_d.p + nb);
+                if (nt > 0) {
+                    std::vector<int64_t> pos(nt), tts(nt), trel(nt);
+                    hipMemcpyAsync(pos.data(), trig_d.p, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                    if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger list failed");
+                    // ts and release step of each trigger (device gathers, then one copy each)
+                    if (int rc = ensure(mrg_col, (size_t)nt * 16)) return rc;
+                    int64_t* g_ts = (int64_t*)mrg_col.p;
+                    const int gg = (int)std::min<int64_t>(4096, (nt + 255) / 256);
+                    hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, (const int64_t*)trig_d.p, nt, INT64_MAX,
+                                       (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)nullptr, (const int64_t*)nullptr, g_ts);
+                    hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, (const int64_t*)trig_d.p, nt, INT64_MAX,
+                                       (const int64_t*)eb.rel.p, (const int64_t*)nullptr, (const int64_t*)nullptr, g_ts + nt);
+                    hipMemcpyAsync(tts.data(), g_ts, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                    hipMemcpyAsync(trel.data(), g_ts + nt, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                    if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+                    for (int64_t k = 0; k < nt; ++k) {
+                        const int64_t i = pos[k], t = tts[k], r = trel[k];
+                        if (D == 0) {
+                            PendWin p{};
+                            p.q.kind = RB_SLIDE;
+                            p.q.lo_ts = t - L;
+                            p.q.hi_ts = t;
+                            p.q.pos = i;
+                            p.q.rstep = r;
+                            p.q.floor = eb_floor;
+                            p.start = t - L;   // scan(): windowStart = t - length (window_op.go:697-707)
+                            p.end = t;
+                            pw.push_back(p);
+                        } else {
+                            // W at the release step: the delayed window fires at a LATER watermark advance
+                            delayq.push_back(DelayTrig{eb_base + i, t, r == INT64_MAX ? W : relstep_w(r)});
+                        }
+                    }
+                }
+            }
+            if (D > 0) {
+                while (delayq_head < delayq.size()) {
+                    const DelayTrig& d = delayq[delayq_head];
+                    if (!(W >= d.ts + D && W > d.w_rel)) break;
+                    PendWin p{};
+                    p.q.kind = RB_LB;
+                    p.q.lo_ts = d.ts - L;
+                    p.q.hi_ts = d.ts + D;
+                    p.q.floor = eb_floor;
+                    p.start = 0;     // second-part scan leaves WindowRange unset
+                    p.end = 0;
+                    pw.push_back(p);
+                    delayq_head++;
+                }
+                if (delayq_head > 4096 && delayq_head * 2 > delayq.size()) {
+                    delayq.erase(delayq.begin(), delayq.begin() + (int64_t)delayq_head);
+                    delayq_head = 0;
+                }
+            }
+        } else if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_HOPPING) {
+            if (!e1_known && eb_rel > 0) {
+                e1_known = true;
+                first_ts = fetch_i64(eb.col[dp.ts_col].p);
+                E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
+            }
+            if (e1_known && has_W) {
+                while (win_end(next_win) <= W) {
+                    const int64_t j = next_win++;
+                    PendWin p{};
+                    p.q.kind = RB_LB;
+                    p.q.lo_ts = wtype == EK_WINDOW_TUMBLING ? (j == 0 ? INT64_MIN : win_end(j - 1)) : win_end(j) - L;
+                    p.q.hi_ts = win_end(j);
+                    p.q.floor = eb_floor;
+                    p.start = window_start(j);
+                    p.end = win_end(j);
+                    pw.push_back(p);
+                }
+            }
+        } else if (wtype == EK_WINDOW_SESSION) {
+            if (int rc = session_triggers(rel_prev, pw)) return rc;
+        }
+        return fire_windows(pw);
+    }
+
+    // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
+    int64_t cur_arr_base = 0;
+    int64_t relstep_w(int64_t r) {
+        const int64_t j = r - cur_arr_base;
+        if (j < 0 || !runmax_d.p) return W;
+        return fetch_i64((const int64_t*)runmax_d.p + j) - plan.late_tolerance_ms;
+    }
+
+    // SESSIONWINDOW(unit, L, timeout): getNextSessionWindow (event_window_trigger.go:77-110) over the released
+    // timestamps, evaluated at the batch's final watermark.
+    int session_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
+        // mirror the newly released timestamps
+        const int64_t n_new = eb_rel - rel_prev;
+        if (h_rts.empty()) h_rts_base = eb_base + rel_prev;
+        if (n_new > 0) {
+            const size_t o = h_rts.size();
+            h_rts.resize(o + n_new);
+            hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "session mirror copy failed");
+        }
+        const int64_t timeout = H, duration = L;
+        int64_t floor_abs = eb_base + eb_floor;
+        auto next_session = [&](int64_t from_abs, bool* ticked) -> int64_t {
+            *ticked = false;
+            const int64_t i0 = from_abs - h_rts_base, i1 = (int64_t)h_rts.size();
+            if (i0 >= i1) return INT64_MAX;
+            const int64_t et = h_rts[i0];
+            int64_t tick = aligned_end(et, raw_interval, plan.time_unit, plan.tz_offset_s);
+            int64_t p = INT64_MIN;
+            for (int64_t i = i0; i < i1; ++i) {
+                const int64_t t = h_rts[i];
+                int64_t r = INT64_MAX;
+                if (p != INT64_MIN && t - p > timeout) r = p + timeout;
+                if (t > tick) {
+                    if (tick - duration > et && tick < r) { r = tick; *ticked = true; }
+                    tick += duration;
+                }
+                if (r < INT64_MAX) return r;
+                p = t;
+            }
+            if (p != INT64_MIN && W - p > timeout) return p + timeout;
+            *ticked = false;
+            return INT64_MAX;
+        };
+        bool ticked = false;
+        int64_t we = next_session(floor_abs, &ticked);
+        while (we != INT64_MAX && we <= W) {
+            const int64_t i0 = floor_abs - h_rts_base;
+            const bool has_inputs = i0 < (int64_t)h_rts.size();
+            if (!sess_last_ticked && has_inputs) { sess_trigger = h_rts[i0]; sess_has_trigger = true; }
+            // content: remaining inputs with ts < we
+            const int64_t b_abs = h_rts_base + (std::lower_bound(h_rts.begin() + i0, h_rts.end(), we) - h_rts.begin());
+            PendWin p{};
+            p.q.kind = RB_FIXED;
+            p.q.pos = floor_abs - eb_base;
+            p.q.rstep = b_abs - eb_base;
+            int64_t ws = sess_has_trigger ? sess_trigger : 0;
+            if (ws <= 0) ws = we - L;
+            p.start = ws;
+            p.end = we;
+            pw.push_back(p);
+            floor_abs = b_abs;
+            sess_trigger = we;
+            sess_has_trigger = true;
+            sess_last_ticked = ticked;
+            we = next_session(floor_abs, &ticked);
+        }
+        // trim the mirror below the floor
+        const int64_t drop = floor_abs - h_rts_base;
+        if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
+            h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+            h_rts_base = floor_abs;
+        }
+        return 0;
+    }
+
+    // Event-time push in range mode, after the shared late-drop / watermark steps.
+    int push_range(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t n_acc, int64_t min_acc,
+                   int64_t max_ts, int64_t arrival_base, int64_t M_prev, bool had_M) {
+        const int64_t n = db.n;
+        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+        cur_arr_base = arrival_base;
+        // running max of the batch: release steps (sliding) and the step at which W was reached
+        if (int rc = batch_runmax(ts, n, had_M ? M_prev : INT64_MIN)) return rc;
+        if (n_acc > 0) {
+            if (sorted && (eb.n == 0 || !had_M || min_acc >= M_prev)) {
+                if (int rc = eb_append(db, start, n_acc, arrival_base)) return rc;
+            } else {
+                int64_t max_acc = max_ts;
+                if (int rc = eb_merge(db, start, d_acc, n_acc, min_acc, max_acc, arrival_base)) return rc;
+            }
+        }
+        // the watermark's step: first arrival whose running max reached M (only if M advanced in this batch)
+        if (!had_M || max_ts > M_prev) {
+            if (int rc = ensure(bounds_idx, 8)) return rc;
+            hipLaunchKernelGGL(k_first_ge, dim3(1), dim3(64), 0, stream, (const int64_t*)runmax_d.p, n, max_ts, (int64_t*)bounds_idx.p);
+            sW = arrival_base + fetch_i64(bounds_idx.p);
+        }
+        const int64_t rel_prev = eb_rel;
+        if (eb.n > 0) {
+            if (int rc = ensure(bounds_idx, 8)) return rc;
+            hipLaunchKernelGGL(k_rel_end, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
+                               (const int64_t*)eb.arr.p, eb.n, W, sW, (int64_t*)bounds_idx.p);
+            eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
+        }
+        if (need_rel && eb_rel > rel_prev) {
+            const int g = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
+            hipLaunchKernelGGL(k_release_step, dim3(g), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
+                               (const int64_t*)eb.arr.p, rel_prev, eb_rel, (const int64_t*)runmax_d.p, n, arrival_base,
+                               had_M ? M_prev : INT64_MIN, plan.late_tolerance_ms, (int64_t*)eb.rel.p);
+        }
+        return range_triggers(rel_prev);
+    }
+
+    // COUNTWINDOW(n[, m]) in processing time (window_op.go:390-418, TupleList 502-551): every m-th arrival
+    // emits the last n arrivals when at least n are buffered; arrival order, no watermark.
+    int push_count(const DBatch& db) {
+        const int64_t n = db.n;
+        const int64_t arrival_base = arrivals;
+        if (int rc = eb_append(db, 0, n, arrival_base)) return rc;
+        arrivals += n;
+        eb_rel = eb.n;
+        const int64_t len = plan.length, itv = plan.interval > 0 ? plan.interval : plan.length;
+        std::vector<PendWin> pw;
+        for (; count_k * itv <= arrivals; ++count_k) {
+            const int64_t e = count_k * itv;
+            if (e < len) continue;
+            PendWin p{};
+            p.q.kind = RB_FIXED;
+            p.q.pos = e - len - eb_base;
+            p.q.rstep = e - eb_base;
+            p.start = 0;   // wall-clock WindowRange (not reproducible): reported as 0
+            p.end = 0;
+            pw.push_back(p);
+        }
+        int rc = fire_windows(pw);
+        // the next window starts at (count_k * itv - len)
+        eb_floor = std::max(eb_floor, count_k * itv - len - eb_base);
+        return rc;
+    }
+
     int push(const ek_batch* b) {
         if (!b) return fail(EK_ERR_INVALID, "null batch");
         int64_t n = b->n_rows;
@@ -1072,8 +1710,12 @@ struct Engine {
         } else {
             for (int c = 0; c < plan.n_columns; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
         }
-        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
         stats.records_in += n;
+        if (wtype == EK_WINDOW_COUNT) {
+            const int rc = push_count(db);
+            return rc ? rc : record_time();
+        }
+        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
 
         // ---- 1. batch statistics (one pass over ts)
         int sblocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
@@ -1129,11 +1771,17 @@ struct Engine {
         aux_used = 0;
 
         // ---- 3. watermark advance (watermark_op.go:157-214): W = max ts - lateTol
+        const int64_t M_prev = M;
+        const bool had_M = has_M;
         if (!has_M || s.max_ts > M) {
             M = s.max_ts;
             has_M = true;
             W = M - T;
             has_W = true;
+        }
+        if (range_mode) {
+            const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M);
+            return rc ? rc : record_time();
         }
         if (n_acc == 0) return record_time();
 
@@ -1295,6 +1943,14 @@ struct Engine {
         if (h_wdesc) hipHostFree(h_wdesc);
         if (h_desc) hipHostFree(h_desc);
         release(aux_d);
+        for (EvBuf* e : {&eb, &eb_alt}) {
+            for (int c = 0; c < EK_MAX_COLUMNS; ++c) { release(e->col[c]); release(e->valid[c]); }
+            release(e->arr);
+            release(e->rel);
+        }
+        for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
+                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh})
+            release(*d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
         for (auto& e : phase_ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }

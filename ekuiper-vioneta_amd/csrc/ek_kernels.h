@@ -246,6 +246,7 @@ struct GroupDesc {
     const int64_t* dbase;  // direct emission: result row base of pane r's window, or -1
     const int32_t* didx;   // direct emission: window index of pane r
     const uint8_t* fresh;  // 1: pane r was claimed for this group (its partials are written, not merged)
+    const int64_t* voff;   // range mode (virtual panes): physical row of virtual row v in pane r = v + voff[r]
 };
 
 constexpr int kMaxGroupPanes = 64;
@@ -282,17 +283,21 @@ __device__ __forceinline__ int chunk_bounds(const GroupDesc& gd, int pa, int pb,
     return n;
 }
 
-// Local partition of event i (-1: dropped: late, outside the group's panes, or filtered by WHERE).
-// For sorted groups the pane comes from the event index (cursor `k` advances monotonically per thread).
-template <bool SORTED, bool WHERE>
+// Pane (group-relative) of virtual row v inside a sorted chunk: pa + #(boundaries <= v).
+__device__ __forceinline__ int chunk_rel(const int64_t* lb, int nlb, int pa, int64_t v) {
+    int rel = pa;
+    for (int k = 0; k < nlb; ++k) rel += (v >= lb[k]) ? 1 : 0;
+    return rel;
+}
+
+// Local partition of event row `i` (-1: dropped: late, outside the group's panes, or filtered by WHERE).
+// MODE 0 (unsorted): the pane comes from the event's ts. MODE 1 (sorted) / 2 (virtual panes): the
+// caller passes the pane `rel` derived from the (virtual) row index; `i` is the physical row.
+template <int MODE, bool WHERE>
 __device__ __forceinline__ int local_part(const DPlan& p, const DBatch& b, const PaneGrid& g, const GroupDesc& gd,
-                                          const int64_t* lb, int nlb, const uint8_t* acc, int64_t i, int pa, uint32_t key,
+                                          int rel, const uint8_t* acc, int64_t i, int pa, uint32_t key,
                                           int32_t* pane_err, bool check_where) {
-    int rel;
-    if (SORTED) {
-        rel = pa;
-        for (int k = 0; k < nlb; ++k) rel += (i >= lb[k]) ? 1 : 0;
-    } else {
+    if (MODE == 0) {
         if (gd.has_accept && !acc[i]) return -1;
         int64_t q = pane_of(g, ((const int64_t*)b.col[gd.ts_col])[i]);
         int64_t r = q - gd.q_lo;
@@ -357,7 +362,10 @@ inline size_t part_lds_bytes(int nvc, int lp, bool nullable) {
 // key loads), (2) exclusive scan -> run offsets, published in ctab[chunk][0..lp_n], (3) per tile of
 // kTile rows: load, counting-sort by partition in LDS, write runs with consecutive lanes on
 // consecutive addresses. No global atomics, no global scan: k_agg walks the per-chunk runs.
-template <bool SORTED, bool WHERE, int NVC>
+// MODE 0: unsorted batch (pane from ts); 1: ts-sorted batch (pane from the row index);
+// 2: virtual panes (range mode): the group's rows are the concatenation of possibly overlapping
+//    index ranges of the event buffer, virtual row v of pane r lives at physical row v + voff[r].
+template <int MODE, bool WHERE, int NVC>
 __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
                                                  const uint8_t* __restrict__ acc, Staging st, uint32_t* __restrict__ ctab,
                                                  int ls, int64_t rs, int32_t* __restrict__ pane_err) {
@@ -369,8 +377,11 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     chunk_panes(gd, c0, c1, &pa, &pb);
     const int lp_n = (pb - pa + 1) * gd.nb;
     __shared__ int64_t lb[kMaxChunkBnd];
+    __shared__ int64_t loff[kMaxChunkBnd + 1];
     __shared__ uint32_t wsum[4];
     const int nlb = chunk_bounds(gd, pa, pb, lb);
+    if (MODE == 2)
+        for (int k = threadIdx.x; k <= pb - pa; k += kBlock) loff[k] = gd.voff[pa + k];
     const int lpp = (lp_n + 4 + 3) & ~3;
     int64_t* s_val = (int64_t*)smem;                                          // [NVC][kTile]
     uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [lpp]
@@ -384,7 +395,16 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     // ---- (1) count
     for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
     __syncthreads();
-    if (!(gd.pad & 4)) {   // (diagnostic knob 4: skip the count pass; timing only)
+    if (MODE == 2) {
+        // physical rows are contiguous only inside one pane: scalar (still coalesced) key loads
+        for (int64_t v = c0 + threadIdx.x; v < c1; v += kBlock) {
+            const int rel = chunk_rel(lb, nlb, pa, v);
+            const int64_t i = v + loff[rel - pa];
+            const uint32_t key = kcol ? kcol[i] : 0u;
+            const int lp = local_part<MODE, WHERE>(p, b, g, gd, rel, acc, i, pa, key, pane_err, true);
+            if (lp >= 0) atomicAdd(&tcnt[lp], 1u);
+        }
+    } else if (!(gd.pad & 4)) {   // (diagnostic knob 4: skip the count pass; timing only)
         constexpr int V = 4;   // 16-byte key loads in flight per thread
         for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
             uint4 kv[V];
@@ -406,7 +426,8 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
                 for (int e = 0; e < 4; ++e) {
                     const int64_t i = base + (int64_t)u * kBlock * 4 + e;
                     if (i < c0 || i >= c1) continue;
-                    const int lp = local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, kk[e], pane_err, true);
+                    const int rel = MODE == 1 ? chunk_rel(lb, nlb, pa, i) : 0;
+                    const int lp = local_part<MODE, WHERE>(p, b, g, gd, rel, acc, i, pa, kk[e], pane_err, true);
                     if (lp >= 0) atomicAdd(&tcnt[lp], 1u);
                 }
             }
@@ -425,27 +446,46 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     for (int64_t t0 = a0; t0 < c1; t0 += kTile) {
         uint32_t key[kTileE];
         int64_t val[NVC][kTileE];
+        int64_t phys[kTileE];   // MODE 2: physical row of each element (-1 outside the chunk)
+        int rel[kTileE];
+        if (MODE == 2) {
 #pragma unroll
-        for (int m = 0; m < kTileE / 2; ++m) {
-            const int64_t i = t0 + (int64_t)m * 2 * kBlock + 2 * threadIdx.x;
-            const bool full = i + 1 < gd.nbatch && i < c1;
-            if (full) {
-                uint2 kp = kcol ? *(const uint2*)(kcol + i) : make_uint2(0, 0);
-                key[2 * m] = kp.x;
-                key[2 * m + 1] = kp.y;
-            } else {
-                key[2 * m] = (kcol && i < gd.nbatch) ? kcol[i] : 0u;
-                key[2 * m + 1] = 0u;
+            for (int j = 0; j < kTileE; ++j) {
+                const int64_t v = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+                rel[j] = 0;
+                phys[j] = -1;
+                if (v >= c0 && v < c1) {
+                    rel[j] = chunk_rel(lb, nlb, pa, v);
+                    phys[j] = v + loff[rel[j] - pa];
+                }
+                key[j] = (kcol && phys[j] >= 0) ? kcol[phys[j]] : 0u;
+#pragma unroll
+                for (int c = 0; c < NVC; ++c)
+                    val[c][j] = (c < p.n_vc && phys[j] >= 0) ? ((const int64_t*)b.col[p.vc_col[c]])[phys[j]] : 0;
             }
+        } else {
 #pragma unroll
-            for (int v = 0; v < NVC; ++v) {
-                if (v < p.n_vc && full) {
-                    longlong2 vp = *(const longlong2*)((const int64_t*)b.col[p.vc_col[v]] + i);
-                    val[v][2 * m] = vp.x;
-                    val[v][2 * m + 1] = vp.y;
+            for (int m = 0; m < kTileE / 2; ++m) {
+                const int64_t i = t0 + (int64_t)m * 2 * kBlock + 2 * threadIdx.x;
+                const bool full = i + 1 < gd.nbatch && i < c1;
+                if (full) {
+                    uint2 kp = kcol ? *(const uint2*)(kcol + i) : make_uint2(0, 0);
+                    key[2 * m] = kp.x;
+                    key[2 * m + 1] = kp.y;
                 } else {
-                    val[v][2 * m] = (v < p.n_vc && i < gd.nbatch) ? ((const int64_t*)b.col[p.vc_col[v]])[i] : 0;
-                    val[v][2 * m + 1] = 0;
+                    key[2 * m] = (kcol && i < gd.nbatch) ? kcol[i] : 0u;
+                    key[2 * m + 1] = 0u;
+                }
+#pragma unroll
+                for (int v = 0; v < NVC; ++v) {
+                    if (v < p.n_vc && full) {
+                        longlong2 vp = *(const longlong2*)((const int64_t*)b.col[p.vc_col[v]] + i);
+                        val[v][2 * m] = vp.x;
+                        val[v][2 * m + 1] = vp.y;
+                    } else {
+                        val[v][2 * m] = (v < p.n_vc && i < gd.nbatch) ? ((const int64_t*)b.col[p.vc_col[v]])[i] : 0;
+                        val[v][2 * m + 1] = 0;
+                    }
                 }
             }
         }
@@ -456,7 +496,12 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
             const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
-            lp[j] = (i >= c0 && i < c1) ? local_part<SORTED, WHERE>(p, b, g, gd, lb, nlb, acc, i, pa, key[j], nullptr, false) : -1;
+            if (MODE == 2) {
+                lp[j] = phys[j] >= 0 ? local_part<MODE, WHERE>(p, b, g, gd, rel[j], acc, phys[j], pa, key[j], nullptr, false) : -1;
+            } else {
+                const int r = (MODE == 1 && i >= c0 && i < c1) ? chunk_rel(lb, nlb, pa, i) : 0;
+                lp[j] = (i >= c0 && i < c1) ? local_part<MODE, WHERE>(p, b, g, gd, r, acc, i, pa, key[j], nullptr, false) : -1;
+            }
             if (lp[j] >= 0) rank[j] = atomicAdd(&tcnt[lp[j]], 1u);
         }
         __syncthreads();
@@ -470,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
 #pragma unroll
             for (int v = 0; v < NVC; ++v) s_val[v * kTile + s] = val[v][j];
             if (nullable) {
-                const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+                const int64_t i = MODE == 2 ? phys[j] : t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
 #pragma unroll
                 for (int v = 0; v < NVC; ++v)
                     if (st.nullable_mask & (1u << v)) s_vd[v * kTile + s] = col_valid(b, p.vc_col[v], i) ? 1 : 0;
@@ -480,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
         const uint32_t total = (gd.pad & 8) ? 0u : tcnt[lp_n];   // diagnostic knob 8: no global stores
         for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
             const int l = s_lp[s];
-            const int64_t gpos = (gd.pad & 64) ? region + (t0 - a0) + s : region + cur[l] + (s - tcnt[l]);  // 64: experiment
+            const int64_t gpos = region + cur[l] + (s - tcnt[l]);
             st.klo[gpos] = s_klo[s];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {

@@ -1,0 +1,9 @@
+// ek_lib.h — host wrappers implemented in ek_lib.hip (library-backed, off the hot path).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// Stable ascending sort of (key, value) pairs on the low end_bit bits of the keys. With tmp == nullptr
+// only *tmp_bytes is computed. Returns 0 on success.
+int ekl_sort_pairs_u64(void* tmp, size_t* tmp_bytes, const uint64_t* kin, uint64_t* kout, const int64_t* vin,
+                       int64_t* vout, int64_t n, int end_bit, hipStream_t s);

@@ -1,0 +1,15 @@
+// ek_lib.hip — library-backed helpers off the hot path (separate translation unit: hipCUB headers are heavy).
+//
+// Used only by RANGE mode when an out-of-order batch must be merged into the ts-ordered event buffer
+// (the release order of WatermarkOp, watermark_op.go:157-168: stable in arrival order for equal ts).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "ek_lib.h"
+
+int ekl_sort_pairs_u64(void* tmp, size_t* tmp_bytes, const uint64_t* kin, uint64_t* kout, const int64_t* vin,
+                       int64_t* vout, int64_t n, int end_bit, hipStream_t s) {
+    // LSD radix sort: stable, so equal timestamps keep their input order (buffer tail first, then arrival)
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}

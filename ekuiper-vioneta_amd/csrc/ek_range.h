@@ -1,0 +1,270 @@
+// ek_range.h — gfx950 kernels of the engine's RANGE mode.
+//
+// Range mode keeps the accepted events of the stream in a device-resident event buffer, ordered the way
+// the reference's WindowOperator sees them (its `inputs` slice, window_op.go:576-739):
+//   event time:  release order of WatermarkOp = stable ts order (ties in arrival order)  watermark_op.go:157-214
+//   count window: arrival order                                                         window_op.go:390-418
+// Every triggered window is then an index range [a, b) of that buffer, so windows of any type
+// (sliding, session, count, and tumbling/hopping when an aggregate needs the raw values) are
+// aggregated by the same partition/aggregate kernels as "virtual panes" (k_part MODE 2 + k_agg).
+#pragma once
+#include "ek_kernels.h"
+
+namespace ek {
+
+__global__ void k_iota64(int64_t* __restrict__ out, int64_t base, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = base + i;
+}
+
+// Inclusive running max of ts in arrival order (the stream max M_j of watermark_op.go:217-225 after
+// event j), seeded per kAccChunk chunk with the exclusive prefix max from k_chunk_max + k_scan_max.
+__global__ __launch_bounds__(kBlock) void k_runmax(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+                                                   int64_t* __restrict__ out) {
+    __shared__ int64_t tmax[kBlock];
+    const int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
+    int64_t v[kAccPerThread];
+    int64_t lm = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < kAccPerThread; ++k) {
+        const int64_t i = base + k;
+        v[k] = i < n ? ts[i] : INT64_MIN;
+        lm = max(lm, v[k]);
+    }
+    tmax[threadIdx.x] = lm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = excl[blockIdx.x];
+        for (int t = 0; t < kBlock; ++t) { int64_t x = tmax[t]; tmax[t] = run; run = max(run, x); }
+    }
+    __syncthreads();
+    int64_t run = tmax[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < kAccPerThread; ++k) {
+        const int64_t i = base + k;
+        run = max(run, v[k]);
+        if (i < n) out[i] = run;
+    }
+}
+
+// first j in [lo, hi) with a[j] >= x (hi if none); a non-decreasing
+__device__ __forceinline__ int64_t lb_i64(const int64_t* a, int64_t lo, int64_t hi, int64_t x) {
+    while (lo < hi) { int64_t m = (lo + hi) >> 1; if (a[m] < x) lo = m + 1; else hi = m; }
+    return lo;
+}
+// first j in [lo, hi) with a[j] > x
+__device__ __forceinline__ int64_t ub_i64(const int64_t* a, int64_t lo, int64_t hi, int64_t x) {
+    while (lo < hi) { int64_t m = (lo + hi) >> 1; if (a[m] <= x) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+// Release step of buffered events [i0, i1): the arrival index of the watermark advance that released the
+// event (watermark_op.go:157-214: released at the first advance W_j > W_{j-1} at or after its arrival with
+// W_j >= ts). runmax[0..nb) = batch running max (arrival arr_base + j), prevmax = stream max before the
+// batch (INT64_MIN if none), W_j = runmax[j] - late_tol. Events not released in this batch get INT64_MAX.
+__global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t i0,
+                               int64_t i1, const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base,
+                               int64_t prevmax, int64_t late_tol, int64_t* __restrict__ brel) {
+    for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = bts[i] + late_tol;
+        const int64_t ls = max((int64_t)0, barr[i] - arr_base);
+        int64_t r = INT64_MAX;
+        if (ls < nb) {
+            const int64_t j0 = lb_i64(runmax, ls, nb, x);
+            if (j0 < nb) {
+                const int64_t prev = j0 > 0 ? runmax[j0 - 1] : prevmax;
+                if (runmax[j0] > prev) r = arr_base + j0;
+                else {
+                    const int64_t j1 = ub_i64(runmax, j0 + 1, nb, runmax[j0]);
+                    if (j1 < nb) r = arr_base + j1;
+                }
+            }
+        }
+        brel[i] = r;
+    }
+}
+
+// Released prefix of the buffer after a batch (single thread): events with ts < W, plus those with
+// ts == W that arrived no later than the step sW at which the watermark reached W.
+__global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n, int64_t W,
+                          int64_t sW, int64_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t p = lb_i64(bts, 0, n, W);
+    const int64_t q = ub_i64(bts, p, n, W);
+    out[0] = ub_i64(barr, p, q, sW);   // arrivals are increasing inside one ts run
+}
+
+// first j in [0, n) with runmax[j] >= x (n if none) — the step at which the stream max reached x
+__global__ void k_first_ge(const int64_t* __restrict__ a, int64_t n, int64_t x, int64_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    out[0] = lb_i64(a, 0, n, x);
+}
+
+// SLIDINGWINDOW trigger flags over buffer rows [i0, i1): 1 when OVER (WHEN cond) holds
+// (window_op.go:741-768: nil, error or non-bool -> no trigger); every row triggers without OVER.
+__global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {
+    const DPlan& p = *pp;
+    for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
+        uint8_t f = 1;
+        if (p.n_trigger > 0) {
+            Val v = eval_prog(p.trigger_prog, p.n_trigger, p, &b, i, nullptr);
+            f = (v.tag == V_BOOL && v.i) ? 1 : 0;
+        }
+        flags[i - i0] = f;
+    }
+}
+
+// Per-block counts of set flags (stable compaction, pass 1)
+constexpr int kCompactTile = 4096;
+__global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict__ flags, int64_t n, int64_t* cnt) {
+    const int64_t base = (int64_t)blockIdx.x * kCompactTile;
+    int64_t c = 0;
+    for (int k = threadIdx.x; k < kCompactTile; k += kBlock) {
+        const int64_t i = base + k;
+        if (i < n && flags[i]) c++;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ int64_t s[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+// exclusive scan of nb block counts (single workgroup); cnt[nb] = total
+__global__ __launch_bounds__(1024) void k_scan_counts(int64_t* cnt, int nb) {
+    __shared__ int64_t part[1024];
+    const int per = (nb + 1023) / 1024;
+    const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    int64_t s = 0;
+    for (int k = b0; k < b1; ++k) s += cnt[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int t = 0; t < 1024; ++t) { int64_t x = part[t]; part[t] = run; run += x; }
+        cnt[nb] = run;
+    }
+    __syncthreads();
+    int64_t run = part[threadIdx.x];
+    for (int k = b0; k < b1; ++k) { int64_t x = cnt[k]; cnt[k] = run; run += x; }
+}
+
+// pass 2: write base + i of every set flag, in order (one wave-ordered sweep per block)
+__global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict__ flags, int64_t n, const int64_t* cnt,
+                                                       int64_t base_idx, int64_t* __restrict__ out) {
+    const int64_t base = (int64_t)blockIdx.x * kCompactTile;
+    __shared__ uint32_t wsum[kBlock / 64];
+    int64_t run = cnt[blockIdx.x];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k0 = 0; k0 < kCompactTile; k0 += kBlock) {
+        const int64_t i = base + k0 + threadIdx.x;
+        const bool f = i < n && flags[i];
+        const unsigned long long m = __ballot(f);
+        if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) { if (w < wv) wb += wsum[w]; tot += wsum[w]; }
+        if (f) out[run + wb + __popcll(m & ((1ull << lane) - 1ull))] = base_idx + i;
+        run += tot;
+        __syncthreads();
+    }
+}
+
+// Window range descriptor (host -> device): content = [max(floor, lo(lo_ts)), hi(...)) of the buffer.
+enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2 };
+struct RangeQ {
+    int64_t lo_ts;      // lower bound ts: content starts at the first row with ts >= lo_ts (INT64_MIN: from floor)
+    int64_t hi_ts;      // RB_LB: first row with ts >= hi_ts; RB_SLIDE: ts <= hi_ts and release step <= rstep
+    int64_t pos;        // RB_SLIDE: buffer index of the trigger event; RB_FIXED: a (index)
+    int64_t rstep;      // RB_SLIDE: release step of the trigger event; RB_FIXED: b (index)
+    int64_t floor;      // smallest buffer index a window may start at
+    int32_t kind;
+    int32_t pad;
+};
+
+__global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* __restrict__ brel, int64_t n_rel,
+                                const RangeQ* __restrict__ q, int nq, int64_t* __restrict__ ab) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nq) return;
+    const RangeQ d = q[w];
+    int64_t a, b;
+    if (d.kind == RB_FIXED) {
+        a = d.pos;
+        b = d.rstep;
+    } else {
+        a = d.lo_ts == INT64_MIN ? d.floor : max(d.floor, lb_i64(bts, d.floor, n_rel, d.lo_ts));
+        if (d.kind == RB_LB) {
+            b = lb_i64(bts, a, n_rel, d.hi_ts);
+        } else {
+            // sliding (window_op.go:605-655 with ts <= t): rows after the trigger with the same ts that were
+            // released at the same watermark step belong to the window; later ones do not
+            int64_t lo = d.pos + 1, hi = n_rel;
+            while (lo < hi) {
+                int64_t m = (lo + hi) >> 1;
+                if (bts[m] > d.hi_ts || brel[m] > d.rstep) hi = m; else lo = m + 1;
+            }
+            b = lo;
+        }
+        if (b < a) b = a;
+    }
+    ab[2 * w] = a;
+    ab[2 * w + 1] = b;
+}
+
+// debug_membership for range windows: count and Σ ek_mix64(arrival) over [a, b) (one block per window)
+__global__ __launch_bounds__(kBlock) void k_range_members(const int64_t* __restrict__ barr, const int64_t* __restrict__ ab,
+                                                          const int32_t* __restrict__ slot, int64_t* wmc,
+                                                          unsigned long long* wmh) {
+    const int64_t a = ab[2 * blockIdx.x], b = ab[2 * blockIdx.x + 1];
+    unsigned long long h = 0;
+    for (int64_t i = a + threadIdx.x; i < b; i += kBlock) h += d_mix64((uint64_t)barr[i]);
+    for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+    __shared__ unsigned long long s[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        wmc[slot[blockIdx.x]] = b - a;
+        wmh[slot[blockIdx.x]] = s[0] + s[1] + s[2] + s[3];
+    }
+}
+
+// Gather rows of the merge input (sources: [0, ntail) = saved buffer tail, [ntail, ..) = batch rows
+// listed in bidx) into the destination column in sorted order (perm from the radix sort).
+__global__ void k_gather8(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const int64_t* __restrict__ tail,
+                          const int64_t* __restrict__ batch, const int64_t* __restrict__ bidx, int64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = perm[k];
+        out[k] = s < ntail ? tail[s] : batch[bidx[s - ntail]];
+    }
+}
+__global__ void k_gather4(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const uint32_t* __restrict__ tail,
+                          const uint32_t* __restrict__ batch, const int64_t* __restrict__ bidx, uint32_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = perm[k];
+        out[k] = s < ntail ? tail[s] : batch[bidx[s - ntail]];
+    }
+}
+__global__ void k_gather1(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const uint8_t* __restrict__ tail,
+                          const uint8_t* __restrict__ batch, const int64_t* __restrict__ bidx, uint8_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = perm[k];
+        out[k] = s < ntail ? (tail ? tail[s] : (uint8_t)1) : (batch ? batch[bidx[s - ntail]] : (uint8_t)1);
+    }
+}
+// merge keys: ts of the saved tail rows and of the batch rows listed in bidx, and source ids 0..n-1
+__global__ void k_merge_keys(const int64_t* __restrict__ tail_ts, int64_t ntail, const int64_t* __restrict__ bts,
+                             const int64_t* __restrict__ bidx, int64_t nb, int64_t tmin, uint64_t* __restrict__ keys,
+                             int64_t* __restrict__ src) {
+    const int64_t n = ntail + nb;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = k < ntail ? tail_ts[k] : bts[bidx[k - ntail]];
+        keys[k] = (uint64_t)(t - tmin);
+        src[k] = k;
+    }
+}
+__global__ void k_arrivals_of(const int64_t* __restrict__ bidx, int64_t nb, int64_t arr_base, int64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = arr_base + bidx[k];
+}
+
+}  // namespace ek

@@ -27,7 +27,7 @@ class eko_output(C.Structure):
         ("r", A.ek_result),
         ("member_offset", C.POINTER(C.c_int64)),
         ("members", C.POINTER(C.c_int64)),
-        ("win_error", C.c_char_p),
+        ("win_error", C.c_void_p),
     ]
 
 

@@ -1,0 +1,172 @@
+"""GPU parity tests of RANGE mode (device event buffer, windows as index ranges): sliding, session and
+count windows, plus tumbling/hopping forced through range mode, against the CPU oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ekgpu import abi as A
+from ekgpu.rule import compile_rule
+from ekgpu.synth import IOT_SCHEMA, iot_stream
+from parity import assert_windows_equal
+from test_engine_gpu import engine_mod, run_both  # noqa: F401  (fixture + helper)
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kat_all():
+    g = json.load(open(os.path.join(GOLD, "kat_window_rules.json")))
+    return g["tests"]
+
+
+@pytest.fixture
+def force_range():
+    os.environ["EKGPU_FORCE_RANGE"] = "1"
+    yield
+    del os.environ["EKGPU_FORCE_RANGE"]
+
+
+def _kat_cols(case):
+    g = json.load(open(os.path.join(GOLD, "kat_window_rules.json")))
+    rows = np.array(g["streams"][case["stream"]]["rows"], dtype=object)
+    return [np.array(rows[:, 0], np.int64), np.array(rows[:, 1], np.int64), np.array(rows[:, 2], np.uint32),
+            np.array(rows[:, 3], np.float64)]
+
+
+KAT_SCHEMA = {"ts": "bigint", "size": "bigint", "color": "key", "temp": "float"}
+
+
+@pytest.mark.parametrize("case", _kat_all(), ids=lambda c: c["name"])
+def test_window_rule_kat_range(oracle, engine_mod, case, force_range):
+    """Every reference window KAT (window_rule_test.go) through range mode, whole stream and one event per push."""
+    cols = _kat_cols(case)
+    rule = compile_rule(case["sql"], KAT_SCHEMA, late_tolerance_ms=1000, num_keys=4, debug_membership=True)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols)
+    assert len(got) == case["windows_out"]
+    assert st.records_late == case["late"]
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+    got1, _, _ = run_both(oracle, engine_mod, rule, cols, batches=len(cols[0]))
+    assert_windows_equal(rule.plan, got1, exp.windows, check_members=True)
+
+
+def _iot(n, keys, seed, epm):
+    key, ts, temp, hum = iot_stream(n, keys, seed=seed, events_per_ms=epm)
+    return [key, ts, temp, hum]
+
+
+TRIG_SCHEMA = {"deviceId": "key", "ts": "bigint", "temperature": "float", "humidity": "float", "trig": "bigint"}
+
+
+def _with_trig(cols, every, seed=9):
+    rng = np.random.default_rng(seed)
+    trig = (rng.integers(0, every, len(cols[0])) == 0).astype(np.int64)
+    return cols + [trig]
+
+
+@pytest.mark.parametrize("batches", [1, 5])
+def test_sliding_over_when_c4a_shape(oracle, engine_mod, batches):
+    """C4a shape (reduced): SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1), stddev/var + HAVING."""
+    sql = ("SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=3000, debug_membership=True)
+    cols = _with_trig(_iot(200_000, 3000, seed=61, epm=10), 500)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert len(got) > 100
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_sliding_every_event(oracle, engine_mod):
+    """No OVER: one window per event (event_window_trigger.go:190-192), ties of ts inside the run."""
+    sql = "SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo GROUP BY deviceId, SLIDINGWINDOW(ms, 40)"
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=20, debug_membership=True)
+    cols = _iot(3000, 20, seed=62, epm=3)
+    for batches in (1, 7):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) == len(exp.windows) > 2900   # the last ts run stays unreleased
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_sliding_late_tolerance_out_of_order(oracle, engine_mod):
+    sql = ("SELECT deviceId, count(*), min(temperature), avg(humidity) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ms, 300) OVER (WHEN trig = 1)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=40, late_tolerance_ms=200, debug_membership=True)
+    cols = _with_trig(_iot(20_000, 40, seed=63, epm=2), 50)
+    rng = np.random.default_rng(5)
+    cols[1] = (cols[1] + rng.integers(-400, 400, len(cols[1]))).astype(np.int64)
+    for batches in (1, 9):
+        got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert exp.records_late > 0 and st.records_late == exp.records_late
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_sliding_with_delay(oracle, engine_mod):
+    sql = ("SELECT deviceId, count(*), sum(temperature) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ms, 200, 100) OVER (WHEN trig = 1)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=30, debug_membership=True)
+    cols = _with_trig(_iot(30_000, 30, seed=64, epm=3), 300)
+    for batches in (1, 6):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) > 10
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("n,m", [(1000, 0), (500, 200), (300, 700)])
+def test_count_window(oracle, engine_mod, n, m):
+    """COUNTWINDOW(n[, m]) in processing time (C4b shape, reduced) with stddev/var + HAVING."""
+    cw = f"COUNTWINDOW({n})" if m == 0 else f"COUNTWINDOW({n}, {m})"
+    sql = (f"SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+           f"GROUP BY deviceId, {cw} HAVING count(*) > 1")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=100, is_event_time=False, debug_membership=True)
+    cols = _iot(50_000, 100, seed=65, epm=10)
+    for batches in (1, 11):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) == len(exp.windows) > 10
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_count_window_rejected_in_event_time(engine_mod):
+    rule = compile_rule("SELECT count(*) FROM demo GROUP BY COUNTWINDOW(10)", IOT_SCHEMA)
+    with pytest.raises(engine_mod.EngineError) as e:
+        engine_mod.Engine(rule.plan)
+    assert e.value.code == A.EK_ERR_UNSUPPORTED
+
+
+def test_session_window(oracle, engine_mod):
+    sql = "SELECT deviceId, count(*), max(temperature) FROM demo GROUP BY deviceId, SESSIONWINDOW(ss, 10, 2)"
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=50, debug_membership=True)
+    key, ts, temp, hum = iot_stream(20_000, 50, seed=66, events_per_ms=1)
+    # bursts separated by gaps longer than the 2 s timeout
+    ts = ts + (np.arange(len(ts)) // 3000) * 3500
+    cols = [key, ts.astype(np.int64), temp, hum]
+    for batches in (1, 8):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) >= 3
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_tumbling_hopping_through_range_mode(oracle, engine_mod, force_range):
+    for sql, keys, epm in [
+        ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)", 4000, 5),
+        ("SELECT deviceId, sum(temperature), min(temperature), max(temperature) FROM demo "
+         "GROUP BY deviceId, HOPPINGWINDOW(ss, 6, 2)", 2000, 2),
+    ]:
+        rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys, debug_membership=True)
+        cols = _iot(300_000, keys, seed=67, epm=epm)
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=3)
+        assert len(got) >= 2
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_range_out_of_order_tumbling(oracle, engine_mod, force_range):
+    sql = "SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 2)"
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=50, late_tolerance_ms=700, debug_membership=True)
+    key, ts, temp, hum = iot_stream(20_000, 50, seed=47, events_per_ms=2)
+    rng = np.random.default_rng(7)
+    ts = ts + rng.integers(-1500, 1500, size=len(ts))
+    cols = [key, ts.astype(np.int64), temp, hum]
+    for batches in (1, 13):
+        got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert st.records_late == exp.records_late
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
