@@ -15,7 +15,9 @@ constexpr int kBlock = 256;       // 4 wave64s per workgroup
 constexpr int kMaxVC = 4;         // value columns referenced by aggregates
 
 // fields kept per (pane, key) in the pane-partial state and per key in LDS tables
-enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32 };
+enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32, NEED_SORT = 64 };
+constexpr int kMaxScol = 2;       // value columns of median / percentile_* (key-grouped scatter each)
+constexpr int kMaxSortAggs = 4;   // median / percentile_* calls per rule
 
 struct DPlan {
     int32_t n_columns;
@@ -35,6 +37,13 @@ struct DPlan {
     int32_t agg_fn[EK_MAX_AGGS];
     int32_t agg_vc[EK_MAX_AGGS];  // -1 for count(*)
     double agg_p[EK_MAX_AGGS];
+    // order-statistic aggregates (median, percentile_cont/disc): per sort slot s < n_sagg its column slot
+    int32_t n_scol;
+    int32_t scol_vc[kMaxScol];    // value column (vc index) of sort column slot
+    int32_t n_sagg;
+    int32_t agg_sidx[EK_MAX_AGGS];  // sort slot of aggregate k (-1 otherwise)
+    int32_t sagg_scol[kMaxSortAggs];
+    int32_t sagg_agg[kMaxSortAggs];
 };
 
 // Columns of one micro-batch (device pointers).

@@ -51,8 +51,14 @@ struct WinInfo {
 // NVC-specialised launches (value columns referenced by aggregates: 1..kMaxVC)
 template <int N>
 void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLayout lay, const uint32_t* ctab, int ls,
-                int64_t rs, Staging st, DState ds, Results res, const int32_t* pane_err) {
-    hipLaunchKernelGGL(k_agg<N>, g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err);
+                int64_t rs, Staging st, DState ds, Results res, const int32_t* pane_err, const int64_t* pbase,
+                uint64_t* scratch, int64_t scr_stride) {
+    if (pbase)
+        hipLaunchKernelGGL((k_agg<N, true>), g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err,
+                           pbase, scratch, scr_stride);
+    else
+        hipLaunchKernelGGL((k_agg<N, false>), g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err,
+                           pbase, scratch, scr_stride);
 }
 template <int N>
 void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res) {
@@ -347,9 +353,8 @@ struct Engine {
             dp.agg_fn[k] = a.fn;
             dp.agg_p[k] = a.param;
             dp.agg_vc[k] = -1;
+            dp.agg_sidx[k] = -1;
             if (a.fn < EK_AGG_COUNT_STAR || a.fn > EK_AGG_PERCENTILE_DISC) return fail(EK_ERR_INVALID, "bad aggregate %d", a.fn);
-            if (a.fn == EK_AGG_MEDIAN || a.fn == EK_AGG_PERCENTILE_CONT || a.fn == EK_AGG_PERCENTILE_DISC)
-                return fail(EK_ERR_UNSUPPORTED, "median/percentile need the raw-event engine mode (not in this build)");
             if (a.fn == EK_AGG_COUNT_STAR) continue;
             if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "aggregate column out of range");
             int v = -1;
@@ -371,6 +376,25 @@ struct Engine {
             case EK_AGG_AVG: f = NEED_SUM | NEED_CNT; break;
             case EK_AGG_MIN: f = NEED_MIN; break;
             case EK_AGG_MAX: f = NEED_MAX; break;
+            case EK_AGG_MEDIAN: case EK_AGG_PERCENTILE_CONT: case EK_AGG_PERCENTILE_DISC: {
+                // order statistics over the group's values (range mode, k_agg sort pass)
+                if (a.fn == EK_AGG_MEDIAN && nullable)
+                    return fail(EK_ERR_UNSUPPORTED, "median over a nullable column (nil first element is a type error)");
+                if (dp.n_sagg >= kMaxSortAggs) return fail(EK_ERR_UNSUPPORTED, "too many median/percentile calls");
+                int sc = -1;
+                for (int x = 0; x < dp.n_scol; ++x) if (dp.scol_vc[x] == v) sc = x;
+                if (sc < 0) {
+                    if (dp.n_scol >= kMaxScol) return fail(EK_ERR_UNSUPPORTED, "median/percentile over more than %d columns", kMaxScol);
+                    sc = dp.n_scol++;
+                    dp.scol_vc[sc] = v;
+                }
+                dp.agg_sidx[k] = dp.n_sagg;
+                dp.sagg_scol[dp.n_sagg] = sc;
+                dp.sagg_agg[dp.n_sagg] = k;
+                dp.n_sagg++;
+                f = NEED_SORT | NEED_CNT;
+                break;
+            }
             default: f = NEED_M2 | NEED_CNT | (fl ? NEED_SUM : NEED_FSUM); break;   // var family
             }
             if (fl && (f & NEED_SUM) == 0 && (f & NEED_M2)) f |= NEED_SUM;
@@ -390,6 +414,7 @@ struct Engine {
             bytes_per_key += (f & NEED_CNT ? 4 : 0) + (f & NEED_SUM ? 8 : 0) + (f & NEED_MIN ? 8 : 0) + (f & NEED_MAX ? 8 : 0) +
                              (f & NEED_M2 ? 8 : 0) + (f & NEED_FSUM ? 8 : 0);
         }
+        if (dp.n_sagg > 0) bytes_per_key += 8 + 9 * dp.n_sagg;   // key offsets + cursors, results + tags
         int want = env_int("EKGPU_KBITS", 11);
         kbits = 0;
         while ((1u << kbits) < K && kbits < want) kbits++;
@@ -408,8 +433,14 @@ struct Engine {
                 if (f & NEED_M2) { lay.off_m2[v] = o; o += 8 * kk; }
                 if (f & NEED_FSUM) { lay.off_fsum[v] = o; o += 8 * kk; }
             }
+            if (dp.n_sagg > 0) { lay.off_sres = o; o += 8 * kk * dp.n_sagg; }
             lay.off_cnt = o; o += 4 * kk;
             for (int v = 0; v < dp.n_vc; ++v) if (dp.vc_flags[v] & NEED_CNT) { lay.off_vcnt[v] = o; o += 4 * kk; }
+            if (dp.n_sagg > 0) {
+                lay.off_koff = o; o += 4 * (kk + 1);
+                lay.off_kcur = o; o += 4 * kk;
+                lay.off_stag = o; o += dp.n_sagg * kk;
+            }
             lay.bytes = (o + 15) & ~15;
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
@@ -991,11 +1022,23 @@ struct Engine {
             dim3 ga(gd.np);
             const uint32_t* ct = (const uint32_t*)chist.p;
             const int ph = phase_begin(EK_PHASE_AGGREGATE);
+            // order statistics: scratch region per partition = exclusive prefix of the partition sizes
+            const int64_t* pbase = nullptr;
+            uint64_t* scr = nullptr;
+            const int64_t scr_stride = gd.hi - gd.lo;
+            if (dp.n_sagg > 0) {
+                if (int rc = ensure(sort_pbase, (size_t)(gd.np + 1) * 8)) return rc;
+                if (int rc = ensure(sort_scr, (size_t)std::max<int64_t>(scr_stride, 1) * 8 * dp.n_scol)) return rc;
+                hipLaunchKernelGGL(k_part_sizes, dim3((gd.np + 255) / 256), dim3(256), 0, stream, gd, ct, ls, (int64_t*)sort_pbase.p);
+                hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)sort_pbase.p, gd.np);
+                pbase = (const int64_t*)sort_pbase.p;
+                scr = (uint64_t*)sort_scr.p;
+            }
             switch (nvc) {
-            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
-            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
-            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
-            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr); break;
+            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
+            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
+            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
+            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
             }
             phase_end(ph);
         }
@@ -1122,7 +1165,7 @@ struct Engine {
     int64_t sess_trigger = 0;
     int64_t count_k = 1;               // COUNTWINDOW: next window index
     DevBuf rq_d, ab_d, slot_d, trig_d, flags_d, cnts_d, runmax_d, runcm_d, mrg_keys[2], mrg_src[2], mrg_tmp, mrg_tail,
-        mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh;
+        mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh, sort_pbase, sort_scr;
     std::vector<int64_t> h_ab;
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
@@ -1949,7 +1992,7 @@ struct Engine {
             release(e->rel);
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
-                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh})
+                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr})
             release(*d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);

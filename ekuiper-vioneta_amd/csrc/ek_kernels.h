@@ -562,6 +562,7 @@ struct LdsLayout {
     int32_t off_max[kMaxVC];
     int32_t off_m2[kMaxVC];
     int32_t off_fsum[kMaxVC];
+    int32_t off_koff, off_kcur, off_sres, off_stag;   // sort aggregates: key offsets/cursors, results, tags
     int32_t bytes;
 };
 
@@ -629,10 +630,27 @@ __device__ __forceinline__ void part_merge(const DPlan& p, Part<NVC>& a, int64_t
 }
 
 // funcs_agg.go: the value (and Go type) of aggregate slot k for a merged group partial
+// Order-statistic results (median / percentile_*) come from the per-key LDS table of k_agg's sort pass:
+// sres[slot * kk + kl] value bits, stag[...] EK_TAG_* or kTagErr.
+constexpr uint8_t kTagErr = 0xFF;
+struct SortRes {
+    const uint64_t* sres;
+    const uint8_t* stag;
+    int kl, kk;
+};
 template <int NVC>
-__device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int k) {
+__device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int k, const SortRes* sr = nullptr) {
     const int fn = p.agg_fn[k];
     if (fn == EK_AGG_COUNT_STAR) return Val{V_I64, s.cnt, 0.0};
+    if (fn >= EK_AGG_MEDIAN) {
+        if (!sr) return Val{V_ERR, 0, 0.0};
+        const int e = p.agg_sidx[k] * sr->kk + sr->kl;
+        const uint8_t t = sr->stag[e];
+        if (t == kTagErr) return Val{V_ERR, 0, 0.0};
+        if (t == EK_TAG_NULL) return Val{V_NULL, 0, 0.0};
+        if (t == EK_TAG_I64) return Val{V_I64, (int64_t)sr->sres[e], 0.0};
+        return Val{V_F64, 0, __longlong_as_double((long long)sr->sres[e])};
+    }
     const int v = p.agg_vc[k];
     const int64_t n = sel(s.vcnt, v);
     if (fn == EK_AGG_COUNT) return Val{V_I64, n, 0.0};
@@ -661,10 +679,10 @@ __device__ __noinline__ Val having_eval(const DPlan& p, const Val* aggs) {
 
 // HAVING (having_operator.go:41-56): true keeps the group, false drops it, anything else is an error.
 template <int NVC>
-__device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, int32_t* win_err) {
+__device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, int32_t* win_err, const SortRes* sr = nullptr) {
     if (p.n_having <= 0) return true;
     Val hv[EK_MAX_AGGS];
-    for (int k = 0; k < p.n_aggs; ++k) hv[k] = agg_value(p, s, k);
+    for (int k = 0; k < p.n_aggs; ++k) hv[k] = agg_value(p, s, k, sr);
     Val h = having_eval(p, hv);
     if (h.tag != V_BOOL) { atomicOr(win_err, EK_WIN_HAVING_ERROR); return false; }
     return h.i != 0;
@@ -675,7 +693,7 @@ __device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, 
 // Every thread of the block must call it (sh: >= 17 u32 of LDS).
 template <int NVC>
 __device__ __forceinline__ void emit_rows(const DPlan& p, bool present, const Part<NVC>& s, int64_t key, int64_t out_base,
-                                          int32_t widx, Results& res, uint32_t* sh) {
+                                          int32_t widx, Results& res, uint32_t* sh, const SortRes* sr = nullptr) {
     const unsigned long long mask = __ballot(present);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if (lane == 0) sh[wv] = (uint32_t)__popcll(mask);
@@ -694,7 +712,7 @@ __device__ __forceinline__ void emit_rows(const DPlan& p, bool present, const Pa
 #pragma unroll
     for (int k = 0; k < EK_MAX_AGGS; ++k) {
         if (k >= p.n_aggs) break;
-        Val a = agg_value(p, s, k);
+        Val a = agg_value(p, s, k, sr);
         res.tag[k][pos] = a.tag == V_NULL ? EK_TAG_NULL : (a.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
         res.val[k][pos] = a.tag == V_F64 ? __double_as_longlong(a.f) : a.i;
     }
@@ -707,10 +725,138 @@ constexpr int kAggBlock = 512;
 // closes in this batch (direct[2*rel] = out_base >= 0), or (b) write / merge into the pane state.
 constexpr int kMaxRuns = 1024;
 
-template <int NVC>
+// Runs of partition (rel, bucket): chunk c in [c_lo, c_hi] holds ctab[c][lp .. lp+1) of it.
+__device__ __forceinline__ void part_chunks(const GroupDesc& gd, int rel, int* c_lo, int* c_hi) {
+    *c_lo = 0;
+    *c_hi = gd.nch - 1;
+    if (gd.sorted) {
+        const int64_t e0 = gd.pbnd[rel], e1 = gd.pbnd[rel + 1];
+        if (e1 <= e0) { *c_lo = 0; *c_hi = -1; }
+        else { *c_lo = (int)((e0 - gd.abase) / gd.chunk); *c_hi = (int)((e1 - 1 - gd.abase) / gd.chunk); }
+    }
+}
+__device__ __forceinline__ void part_run(const GroupDesc& gd, const uint32_t* ctab, int ls, int rel, int bucket, int c,
+                                         uint32_t* o0, uint32_t* o1) {
+    const int64_t a0 = gd.abase + (int64_t)c * gd.chunk;
+    int pa, pb;
+    chunk_panes(gd, max(gd.lo, a0), min(gd.hi, a0 + gd.chunk), &pa, &pb);
+    const int lp = (rel - pa) * gd.nb + bucket;
+    *o0 = *o1 = 0;
+    if (rel >= pa && rel <= pb) { *o0 = ctab[(int64_t)c * ls + lp]; *o1 = ctab[(int64_t)c * ls + lp + 1]; }
+}
+
+// Rows per partition (sort aggregates: the key-grouped scratch region of each partition), one thread each.
+__global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restrict__ ctab, int ls, int64_t* __restrict__ out) {
+    const int pid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pid >= gd.np) return;
+    const int rel = pid / gd.nb, bucket = pid % gd.nb;
+    int c_lo, c_hi;
+    part_chunks(gd, rel, &c_lo, &c_hi);
+    int64_t t = 0;
+    for (int c = c_lo; c <= c_hi; ++c) {
+        uint32_t o0, o1;
+        part_run(gd, ctab, ls, rel, bucket, c, &o0, &o1);
+        t += o1 - o0;
+    }
+    out[pid] = t;
+}
+
+// ---------------------------------------------------------------- order statistics (median, percentile_*)
+// Element of rank r (0-based, ascending) of a short segment of ordered keys: O(n^2) counting, one thread.
+__device__ __forceinline__ uint64_t seg_select(const uint64_t* seg, int n, int r) {
+    for (int i = 0; i < n; ++i) {
+        const uint64_t x = seg[i];
+        int less = 0, eq = 0;
+        for (int j = 0; j < n; ++j) { const uint64_t y = seg[j]; less += y < x; eq += y == x; }
+        if (less <= r && r < less + eq) return x;
+    }
+    return 0;
+}
+// Same for a long segment, by the whole workgroup: MSD radix select, 8 bits per pass (all threads call it).
+__device__ inline uint64_t block_select(const uint64_t* seg, int64_t n, int64_t r, uint32_t* hist, uint64_t* sh) {
+    uint64_t prefix = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int d = threadIdx.x; d < 256; d += blockDim.x) hist[d] = 0;
+        __syncthreads();
+        const uint64_t hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t x = seg[i];
+            if ((x & hm) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t c = 0;
+            for (int d = 0; d < 256; ++d) {
+                if (r < c + hist[d]) { prefix |= (uint64_t)d << shift; r -= c; break; }
+                c += hist[d];
+            }
+            sh[0] = prefix;
+            sh[1] = (uint64_t)r;
+        }
+        __syncthreads();
+        prefix = sh[0];
+        r = (int64_t)sh[1];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+// funcs_agg.go:29-55 (median), :298-370 with stats v0.7.1 Percentile / PercentileNearestRank over the n
+// values of one group; sel(r) returns the ordered bits of the rank-r value. Tag kTagErr = "Input is outside of range".
+template <typename SEL>
+__device__ __forceinline__ void order_stat(int fn, bool isf, double param, int64_t n, SEL sel, uint64_t* out, uint8_t* tag) {
+    auto val = [&](uint64_t o) { return isf ? ord_to_f64(o) : (double)ord_to_i64(o); };
+    *out = 0;
+    if (n <= 0) { *tag = EK_TAG_NULL; return; }
+    if (fn == EK_AGG_MEDIAN) {
+        if (n & 1) {
+            const uint64_t o = sel(n / 2);
+            *tag = isf ? EK_TAG_F64 : EK_TAG_I64;
+            *out = isf ? (uint64_t)__double_as_longlong(ord_to_f64(o)) : (uint64_t)ord_to_i64(o);
+        } else {
+            const uint64_t a = sel(n / 2 - 1), b = sel(n / 2);
+            double m;
+            if (isf) m = __ddiv_rn(__dadd_rn(ord_to_f64(a), ord_to_f64(b)), 2.0);
+            else m = __ddiv_rn((double)(int64_t)((uint64_t)ord_to_i64(a) + (uint64_t)ord_to_i64(b)), 2.0);
+            *tag = EK_TAG_F64;
+            *out = (uint64_t)__double_as_longlong(m);
+        }
+        return;
+    }
+    const double percent = __dmul_rn(param, 100.0);
+    double res;
+    if (fn == EK_AGG_PERCENTILE_CONT) {
+        if (n == 1) res = val(sel(0));
+        else {
+            if (percent <= 0 || percent > 100) { *tag = kTagErr; return; }
+            const double index = __dmul_rn(__ddiv_rn(percent, 100.0), (double)n);
+            const int64_t i = (int64_t)index;
+            if (index == (double)i) res = val(sel(i - 1));
+            else if (index > 1) {
+                const double a = val(sel(i - 1)), b = val(sel(i));
+                res = __ddiv_rn(__dadd_rn(__dadd_rn(0.0, a), b), 2.0);
+            } else { *tag = kTagErr; return; }
+        }
+    } else {
+        if (percent < 0 || percent > 100) { *tag = kTagErr; return; }
+        if (percent == 100.0) res = val(sel(n - 1));
+        else {
+            const int64_t r = (int64_t)ceil(__ddiv_rn(__dmul_rn((double)n, percent), 100.0));
+            res = val(sel(r == 0 ? 0 : r - 1));
+        }
+    }
+    *tag = EK_TAG_F64;
+    *out = (uint64_t)__double_as_longlong(res);
+}
+
+constexpr int kSmallSeg = 32;   // segments up to this length are selected by one thread
+
+template <int NVC, bool SORT>
 __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
-                                                   Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err) {
+                                                   Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err,
+                                                   const int64_t* __restrict__ pbase, uint64_t* __restrict__ scratch,
+                                                   int64_t scr_stride) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const DPlan& p = *pp;
     const int pid = blockIdx.x;
@@ -724,21 +870,13 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     __shared__ uint32_t r_start[kMaxRuns];   // staging index of each run (staging < 2^32 rows, host-checked)
     __shared__ uint32_t r_pre[kMaxRuns + 1];
     __shared__ uint32_t r_wsum[kAggBlock / 64];
-    int c_lo = 0, c_hi = gd.nch - 1;
-    if (gd.sorted) {
-        const int64_t e0 = gd.pbnd[rel], e1 = gd.pbnd[rel + 1];
-        if (e1 <= e0) { c_lo = 0; c_hi = -1; }
-        else { c_lo = (int)((e0 - gd.abase) / gd.chunk); c_hi = (int)((e1 - 1 - gd.abase) / gd.chunk); }
-    }
+    int c_lo, c_hi;
+    part_chunks(gd, rel, &c_lo, &c_hi);
     const int nruns = min(c_hi - c_lo + 1, kMaxRuns);
     for (int j = threadIdx.x; j < nruns; j += kAggBlock) {
         const int c = c_lo + j;
-        const int64_t a0 = gd.abase + (int64_t)c * gd.chunk;
-        int pa, pb;
-        chunk_panes(gd, max(gd.lo, a0), min(gd.hi, a0 + gd.chunk), &pa, &pb);
-        const int lp = (rel - pa) * gd.nb + bucket;
-        uint32_t o0 = 0, o1 = 0;
-        if (rel >= pa && rel <= pb) { o0 = ctab[(int64_t)c * ls + lp]; o1 = ctab[(int64_t)c * ls + lp + 1]; }
+        uint32_t o0, o1;
+        part_run(gd, ctab, ls, rel, bucket, c, &o0, &o1);
         r_start[j] = (uint32_t)((int64_t)c * rs + o0);
         r_pre[j] = o1 - o0;
     }
@@ -858,6 +996,90 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
         }
         __syncthreads();
     }
+    // ---- order statistics: group the partition's values by key into its scratch region, then select
+    if constexpr (SORT) {
+        uint32_t* koff = (uint32_t*)(lds + lay.off_koff);   // [kk + 1]
+        uint32_t* kcur = (uint32_t*)(lds + lay.off_kcur);   // [kk]
+        uint64_t* sres = (uint64_t*)(lds + lay.off_sres);   // [n_sagg][kk]
+        uint8_t* stag = (uint8_t*)(lds + lay.off_stag);     // [n_sagg][kk]
+        __shared__ uint32_t s_hist[256];
+        __shared__ uint64_t s_sel[2];
+        __shared__ uint32_t s_nbig;
+        __shared__ uint32_t s_wsum[kAggBlock / 64];
+        const int64_t pbs = pbase[pid];
+        for (int sc = 0; sc < p.n_scol; ++sc) {
+            const int v = p.scol_vc[sc];
+            const bool vnull = (nullm >> v) & 1u;
+            uint64_t* seg0 = scratch + (int64_t)sc * scr_stride + pbs;
+            // values per key (nil values are ignored, cast.ToFloat64Slice IGNORE_NIL) -> exclusive offsets
+            for (int k = threadIdx.x; k < kk; k += kAggBlock)
+                koff[k] = (p.vc_flags[v] & NEED_CNT) ? ((uint32_t*)(lds + lay.off_vcnt[v]))[k] : lcnt[k];
+            if (threadIdx.x == 0) s_nbig = 0;
+            __syncthreads();
+            {
+                const int per = (kk + kAggBlock - 1) / kAggBlock;
+                const int b0 = threadIdx.x * per, b1 = min(kk, b0 + per);
+                uint32_t sm = 0;
+                for (int k = b0; k < b1; ++k) sm += koff[k];
+                uint32_t x = sm;
+                for (int o = 1; o < 64; o <<= 1) { uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+                if (lane == 63) s_wsum[wave] = x;
+                __syncthreads();
+                uint32_t wb = 0;
+                for (int w = 0; w < wave; ++w) wb += s_wsum[w];
+                uint32_t run = wb + x - sm;
+                for (int k = b0; k < b1; ++k) { uint32_t c = koff[k]; koff[k] = run; kcur[k] = 0; run += c; }
+                if (threadIdx.x == kAggBlock - 1) koff[kk] = run;
+                __syncthreads();
+            }
+            // scatter the ordered bits of every valid value to its key's segment
+            for (uint32_t span = (uint32_t)wave * 64u; span < total; span += (uint32_t)kAggBlock) {
+                const uint32_t vv = span + lane;
+                if (vv >= total) continue;
+                int j = run_of(span);
+                while (j + 1 < nruns && r_pre[j + 1] <= vv) ++j;
+                const int64_t i = (int64_t)r_start[j] + (vv - r_pre[j]);
+                if (vnull && !st.valid[v][i]) continue;
+                const int kl = st.klo[i];
+                const int64_t raw = st.val[v][i];
+                const uint64_t o = isf[v] ? f64_to_ord(__longlong_as_double(raw)) : i64_to_ord(raw);
+                seg0[koff[kl] + atomicAdd(&kcur[kl], 1u)] = o;
+            }
+            __threadfence();
+            __syncthreads();
+            // short segments: one thread per key; long ones are queued for the whole workgroup
+            for (int kl = threadIdx.x; kl < kk; kl += kAggBlock) {
+                const int n = (int)(koff[kl + 1] - koff[kl]);
+                const uint64_t* seg = seg0 + koff[kl];
+                const bool big = n > kSmallSeg;
+                for (int a = 0; a < p.n_sagg; ++a) {
+                    if (p.sagg_scol[a] != sc) continue;
+                    const int k = p.sagg_agg[a];
+                    if (big) continue;
+                    order_stat(p.agg_fn[k], isf[v], p.agg_p[k], n, [&](int64_t r) { return seg_select(seg, n, (int)r); },
+                               &sres[a * kk + kl], &stag[a * kk + kl]);
+                }
+                if (big) kcur[atomicAdd(&s_nbig, 1u)] = (uint32_t)kl;
+            }
+            __syncthreads();
+            const uint32_t nbig = s_nbig;
+            for (uint32_t t = 0; t < nbig; ++t) {
+                const int kl = (int)kcur[t];
+                const int64_t n = koff[kl + 1] - koff[kl];
+                const uint64_t* seg = seg0 + koff[kl];
+                for (int a = 0; a < p.n_sagg; ++a) {
+                    if (p.sagg_scol[a] != sc) continue;
+                    const int k = p.sagg_agg[a];
+                    uint64_t o;
+                    uint8_t tg;
+                    order_stat(p.agg_fn[k], isf[v], p.agg_p[k], n,
+                               [&](int64_t r) { return block_select(seg, n, r, s_hist, s_sel); }, &o, &tg);
+                    if (threadIdx.x == 0) { sres[a * kk + kl] = o; stag[a * kk + kl] = tg; }
+                }
+            }
+            __syncthreads();
+        }
+    }
     // this partition's partial for key kl, read back from LDS
     auto lds_part = [&](int kl, int64_t& c, int64_t (&vc)[NVC], int64_t (&is)[NVC], double (&fs)[NVC], double (&m2)[NVC],
                         uint64_t (&mn)[NVC], uint64_t (&mx)[NVC]) {
@@ -896,10 +1118,19 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
                 lds_part(kl, c, vc, is, fs, m2, mn, mx);
                 if (c > 0) {
                     part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-                    present = having_keep(p, s, &res.win_err[widx]);
+                    bool err = false;
+                    if constexpr (SORT) {
+                        for (int a = 0; a < p.n_sagg; ++a) err |= ((uint8_t*)(lds + lay.off_stag))[a * kk + kl] == kTagErr;
+                    }
+                    if (err) atomicOr(&res.win_err[widx], EK_WIN_AGG_ERROR);   // "run Select error: ..." replaces the window
+                    else {
+                        const SortRes sr{(const uint64_t*)(lds + lay.off_sres), (const uint8_t*)(lds + lay.off_stag), kl, kk};
+                        present = having_keep(p, s, &res.win_err[widx], SORT ? &sr : nullptr);
+                    }
                 }
             }
-            emit_rows(p, present, s, key, dbase, widx, res, esh);
+            const SortRes sr{(const uint64_t*)(lds + lay.off_sres), (const uint8_t*)(lds + lay.off_stag), kl, kk};
+            emit_rows(p, present, s, key, dbase, widx, res, esh, SORT ? &sr : nullptr);
         }
         return;
     }

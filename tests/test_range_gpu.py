@@ -170,3 +170,70 @@ def test_range_out_of_order_tumbling(oracle, engine_mod, force_range):
         got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
         assert st.records_late == exp.records_late
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+# ------------------------------------------------------------------ order statistics (median, percentile_*)
+MED_SQL = ("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9), percentile_disc(humidity, 0.5), "
+           "count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)")
+
+
+@pytest.mark.parametrize("keys", [4000, 3])
+def test_median_percentile_tumbling(oracle, engine_mod, keys):
+    """Short groups (one thread selects) and long groups (whole-workgroup radix select)."""
+    rule = compile_rule(MED_SQL, IOT_SCHEMA, num_keys=keys, debug_membership=True)
+    cols = _iot(300_000, keys, seed=71, epm=5)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=2)
+    assert len(got) >= 4
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_median_percentile_int_columns_nulls(oracle, engine_mod):
+    schema = {"k": "key", "ts": "bigint", "a": "bigint", "b": "bigint"}
+    sql = ("SELECT k, median(a), percentile_cont(b, 0.5), percentile_disc(b, 0.25), percentile_cont(a, 1), count(b) "
+           "FROM s GROUP BY k, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, schema, num_keys=37, nullable=("b",), debug_membership=True)
+    n = 40_000
+    rng = np.random.default_rng(4)
+    k = rng.integers(0, 37, n).astype(np.uint32)
+    ts = (1541152480000 + np.arange(n) // 4).astype(np.int64)
+    a = rng.integers(-50, 50, n).astype(np.int64)          # many ties
+    b = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    vb = (rng.random(n) > 0.4).astype(np.uint8)
+    got, exp, _ = run_both(oracle, engine_mod, rule, [k, ts, a, b], batches=3, validity=[None, None, None, vb])
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_percentile_out_of_range_is_window_error(oracle, engine_mod):
+    """stats.Percentile: index < 1 and not integral -> "Input is outside of range" -> the window errors."""
+    sql = "SELECT deviceId, percentile_cont(temperature, 0.05), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)"
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=500, debug_membership=True)
+    cols = _iot(40_000, 500, seed=72, epm=5)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols)
+    assert any(w.status == A.EK_WIN_AGG_ERROR for w in exp.windows)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_c5_shape_high_cardinality_median(oracle, engine_mod):
+    """C5 shape (reduced): ~10 events per key over many keys in one 60 s tumbling window + a sentinel."""
+    keys = 200_000
+    sql = ("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
+           "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys)
+    n = 2_000_000
+    key, ts, temp, hum = iot_stream(n, keys, seed=73, events_per_ms=40)
+    t_min = 1541152440000                      # a minute boundary: the first 60 s window is [t_min, t_min + 60 s)
+    ts = np.minimum(ts - 40_000, t_min + 59_000)
+    ts[-1] = t_min + 60_000                    # sentinel: closes the window
+    got, exp, _ = run_both(oracle, engine_mod, rule, [key, ts, temp, hum], batches=2)
+    assert len(got) == 1 and len(got[0].keys) > 0.99 * keys
+    assert_windows_equal(rule.plan, got, exp.windows)
+
+
+def test_sliding_median(oracle, engine_mod):
+    sql = ("SELECT deviceId, median(temperature), percentile_disc(temperature, 0.75) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 2) OVER (WHEN trig = 1)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=64, debug_membership=True)
+    cols = _with_trig(_iot(60_000, 64, seed=74, epm=5), 400)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=4)
+    assert len(got) > 50
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
