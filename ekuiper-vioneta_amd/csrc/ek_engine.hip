@@ -169,6 +169,7 @@ struct Engine {
 
     // ---- derived configuration
     int wtype = 0;
+    int n_out = 0;                     // value arrays per result row: aggregates, or every column (filter rules)
     int64_t L = 0, H = 0, P = 0;       // ms
     int64_t ppw = 1, hpp = 1;          // panes per window, panes per hop
     int32_t raw_interval = 0;
@@ -284,6 +285,31 @@ struct Engine {
         for (int k = 0; k < plan.n_aggs; ++k)
             sort_aggs |= plan.aggs[k].fn == EK_AGG_MEDIAN || plan.aggs[k].fn == EK_AGG_PERCENTILE_CONT ||
                          plan.aggs[k].fn == EK_AGG_PERCENTILE_DISC;
+        n_out = plan.n_aggs;
+        if (wtype == EK_WINDOW_NONE) {
+            // a rule without window and aggregates: FilterOp (WHERE) + SELECT * per event (C1 shape)
+            if (plan.n_aggs != 0 || plan.key_column >= 0 || plan.n_having)
+                return fail(EK_ERR_UNSUPPORTED, "aggregates need a window in GROUP BY");
+            if (plan.is_event_time) return fail(EK_ERR_UNSUPPORTED, "event-time ordering of a window-less rule is not on this path");
+            n_out = plan.n_columns;
+            if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
+            if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(EK_ERR_DEVICE, "stream create failed");
+            own_stream = true;
+            hipEventCreate(&ev0);
+            hipEventCreate(&ev1);
+            dp = DPlan{};
+            dp.n_columns = plan.n_columns;
+            for (int c = 0; c < plan.n_columns; ++c) dp.col_type[c] = plan.column_type[c];
+            dp.ts_col = plan.ts_column;
+            dp.key_col = -1;
+            dp.n_where = plan.n_where;
+            memcpy(dp.where_prog, plan.where_prog, sizeof plan.where_prog);
+            if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
+            if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+            if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
+            reset_state();
+            return 0;
+        }
         if (plan.is_event_time) {
             // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time
             if (wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
@@ -651,7 +677,7 @@ struct Engine {
                 return 0;
             };
             if (int rc = grow(r_key, 4)) return rc;
-            for (int k = 0; k < plan.n_aggs; ++k) {
+            for (int k = 0; k < n_out; ++k) {
                 if (int rc = grow(r_val[k], 8)) return rc;
                 if (int rc = grow(r_tag[k], 1)) return rc;
             }
@@ -682,7 +708,7 @@ struct Engine {
     Results results_view() {
         Results r{};
         r.key = (uint32_t*)r_key.p;
-        for (int k = 0; k < plan.n_aggs; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
+        for (int k = 0; k < n_out; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
         r.win_cnt = (int64_t*)r_wcnt.p;
         r.win_err = (int32_t*)r_werr.p;
         return r;
@@ -1697,6 +1723,49 @@ struct Engine {
         return range_triggers(rel_prev);
     }
 
+    // Window-less rule (SELECT * ... WHERE): FilterOp.Apply per event (filter_operator.go:36-90). Each push
+    // yields one result segment whose rows are the events that passed, in arrival order: key = row index
+    // in the batch, value k = column k (SELECT *). A row whose WHERE errors is dropped and counted
+    // (the reference forwards that event's error instead of the event).
+    int push_filter(const DBatch& db) {
+        const int64_t n = db.n;
+        if (int rc = ensure(flags_d, (size_t)n)) return rc;
+        if (int rc = ensure(trig_d, (size_t)n * 8)) return rc;
+        const int nb = (int)((n + kCompactTile - 1) / kCompactTile);
+        if (int rc = ensure(cnts_d, (size_t)(nb + 2) * 8)) return rc;
+        hipMemsetAsync((int64_t*)cnts_d.p + nb + 1, 0, 8, stream);
+        const int ph = phase_begin(EK_PHASE_PARTITION);
+        hipLaunchKernelGGL(k_filter_flags, dim3((int)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, stream, d_plan, db,
+                           (uint8_t*)flags_d.p, (unsigned long long*)((int64_t*)cnts_d.p + nb + 1));
+        hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (int64_t*)cnts_d.p);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+        hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (const int64_t*)cnts_d.p,
+                           (int64_t)0, (int64_t*)trig_d.p);
+        phase_end(ph);
+        int64_t sel_err[2] = {0, 0};
+        hipMemcpyAsync(sel_err, (int64_t*)cnts_d.p + nb, 16, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "filter kernel failed");
+        const int64_t ns = sel_err[0];
+        stats.records_filter_error += sel_err[1];
+        if (int rc = ensure_results(ns, 1)) return rc;
+        WinInfo wi{};
+        wi.j = range_wins++;
+        wi.out_base = r_rows_used;
+        wi.slot = (int32_t)wins.size();
+        wi.direct = true;
+        wins.push_back(wi);
+        r_rows_used += ns;
+        stats.windows_out++;
+        if (ns > 0) {
+            Results rv = results_view();
+            const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
+            hipLaunchKernelGGL(k_filter_emit, dim3((int)std::min<int64_t>(8192, (ns + 255) / 256)), dim3(256), 0, stream, d_plan, db,
+                               (const int64_t*)trig_d.p, ns, wi.out_base, wi.slot, rv);
+            phase_end(ph2);
+        }
+        return 0;
+    }
+
     // COUNTWINDOW(n[, m]) in processing time (window_op.go:390-418, TupleList 502-551): every m-th arrival
     // emits the last n arrivals when at least n are buffered; arrival order, no watermark.
     int push_count(const DBatch& db) {
@@ -1754,6 +1823,10 @@ struct Engine {
             for (int c = 0; c < plan.n_columns; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
         }
         stats.records_in += n;
+        if (wtype == EK_WINDOW_NONE) {
+            const int rc = push_filter(db);
+            return rc ? rc : record_time();
+        }
         if (wtype == EK_WINDOW_COUNT) {
             const int rc = push_count(db);
             return rc ? rc : record_time();
@@ -1879,7 +1952,7 @@ struct Engine {
         memset(out, 0, sizeof *out);
         int64_t nw = (int64_t)wins.size();
         out->n_windows = nw;
-        out->n_aggs = plan.n_aggs;
+        out->n_aggs = n_out;
         out->memory = memory;
         std::vector<int64_t> wc(nw);
         std::vector<int32_t> we(nw);
@@ -1918,14 +1991,14 @@ struct Engine {
             out->win_row_offset = h_off.data();
             out->n_rows = r_rows_used;
             out->key = (uint32_t*)r_key.p;
-            for (int k = 0; k < plan.n_aggs; ++k) {
+            for (int k = 0; k < n_out; ++k) {
                 out->agg_value[k] = (int64_t*)r_val[k].p;
                 out->agg_tag[k] = (uint8_t*)r_tag[k].p;
             }
             return 0;
         }
         h_key.resize(total);
-        for (int k = 0; k < plan.n_aggs; ++k) { h_val[k].resize(total); h_tag[k].resize(total); }
+        for (int k = 0; k < n_out; ++k) { h_val[k].resize(total); h_tag[k].resize(total); }
         int64_t o = 0;
         for (int64_t w = 0; w < nw; ++w) {
             h_off[w] = o;
@@ -1933,7 +2006,7 @@ struct Engine {
             if (c) {
                 int64_t base = wins[w].out_base;
                 hipMemcpyAsync(h_key.data() + o, (uint32_t*)r_key.p + base, c * 4, hipMemcpyDeviceToHost, stream);
-                for (int k = 0; k < plan.n_aggs; ++k) {
+                for (int k = 0; k < n_out; ++k) {
                     hipMemcpyAsync(h_val[k].data() + o, (int64_t*)r_val[k].p + base, c * 8, hipMemcpyDeviceToHost, stream);
                     hipMemcpyAsync(h_tag[k].data() + o, (uint8_t*)r_tag[k].p + base, c, hipMemcpyDeviceToHost, stream);
                 }
@@ -1944,7 +2017,7 @@ struct Engine {
         out->win_row_offset = h_off.data();
         out->n_rows = total;
         out->key = h_key.data();
-        for (int k = 0; k < plan.n_aggs; ++k) { out->agg_value[k] = h_val[k].data(); out->agg_tag[k] = h_tag[k].data(); }
+        for (int k = 0; k < n_out; ++k) { out->agg_value[k] = h_val[k].data(); out->agg_tag[k] = h_tag[k].data(); }
         return 0;
     }
 

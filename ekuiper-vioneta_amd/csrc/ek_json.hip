@@ -1,0 +1,674 @@
+// ek_json.hip — columnar JSON ingest on the GPU (north-star item 1).
+//
+// Replaces, for flat JSON objects with numeric fields, the reference's per-message decode
+//   FastJsonConverter.Decode -> decodeWithSchema -> decodeObject   internal/converter/json/converter.go:92-171,246-410
+//   extractNumberValue (schema BIGINT -> Int64, FLOAT -> Float64)  converter.go:429-460
+// A micro-batch of messages (concatenated payload bytes + offsets) is parsed by one thread per message
+// straight into the columns of an ek_batch in device memory (one pass, no per-message maps).
+//
+// Semantics kept from the reference for a schema-typed stream:
+//   * a field outside the schema is skipped (checkSchema: not added), null -> nil (validity 0),
+//     an absent field -> nil; for duplicate keys the last one wins (obj.Visit + map assignment)
+//   * BIGINT: the number must be an integer literal that fits int64 (fastfloat.ParseInt64), else error
+//   * FLOAT: the number as float64, correctly rounded (fastfloat.Parse / strconv.ParseFloat)
+//   * a string / bool / object / array value for a numeric schema field -> "has wrong type" error
+//   * any syntax error -> the message fails to decode; the message is dropped and its error reported
+//     (DecodeOp forwards the error, node/decode_op.go:146-193)
+// Numbers are converted exactly on the Clinger fast path (mantissa <= 2^53, |exp10| <= 22: one IEEE
+// multiply/divide by an exact power of ten), else by Eisel-Lemire with a 128-bit power-of-five table,
+// whose undecided cases are settled by an exact big-integer midpoint comparison. Not decided on the GPU
+// (reported as EK_JSON_ERR_NUMBER, never guessed): subnormal / overflowing results, and mantissas beyond
+// 19 significant digits whose truncation straddles a rounding boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ekgpu.h"
+#include "ek_json_pow5.h"
+
+namespace {
+
+constexpr int kJBlock = 256;
+
+struct JSchema {
+    int32_t n;
+    int32_t type[EK_MAX_COLUMNS];
+    int32_t len[EK_MAX_COLUMNS];
+    uint64_t hash[EK_MAX_COLUMNS];
+    char name[EK_MAX_COLUMNS][EK_JSON_MAX_NAME];
+};
+
+struct JOut {
+    void* col[EK_MAX_COLUMNS];
+    uint8_t* valid[EK_MAX_COLUMNS];
+    uint8_t* err;
+    unsigned int* nulls;   // [EK_MAX_COLUMNS]: decoded messages with column c nil (0 -> no validity array)
+};
+
+__device__ __forceinline__ bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+__device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Eisel-Lemire core (Go's strconv eiselLemire64 with its bail-outs reported instead of taken): the
+// binary64 bits of w * 10^q from a truncated 128-bit product. *ambiguous: the product could not decide
+// the rounding (the true value is then either the candidate or the next double up, since truncation
+// only underestimates). Returns false for results outside the normal range.
+__device__ bool el_core(uint64_t w, int64_t q, uint64_t* bits, bool* ambiguous) {
+    *ambiguous = false;
+    const int clz = __clzll((long long)w);
+    w <<= clz;
+    int64_t exp2 = ((217706 * q) >> 16) + 64 + 1023 - clz;
+    const uint64_t hi5 = kPow5Hi[q + 342], lo5 = kPow5Lo[q + 342];
+    uint64_t xhi = __umul64hi(w, hi5), xlo = w * hi5;
+    if ((xhi & 0x1FF) == 0x1FF && xlo + w < w) {
+        const uint64_t yhi = __umul64hi(w, lo5), ylo = w * lo5;
+        uint64_t mhi = xhi;
+        const uint64_t mlo = xlo + yhi;
+        if (mlo < xlo) mhi++;
+        if ((mhi & 0x1FF) == 0x1FF && mlo + 1 == 0 && ylo + w < w) *ambiguous = true;
+        xhi = mhi;
+        xlo = mlo;
+    }
+    const uint64_t msb = xhi >> 63;
+    uint64_t mant = xhi >> (msb + 9);
+    exp2 -= (int64_t)(1 ^ msb);
+    if (xlo == 0 && (xhi & 0x1FF) == 0 && (mant & 3) == 1) *ambiguous = true;   // half-way at the truncated level
+    mant += mant & 1;
+    mant >>= 1;
+    if ((mant >> 53) > 0) { mant >>= 1; exp2 += 1; }
+    if (exp2 <= 0 || exp2 >= 0x7FF) return false;   // subnormal / overflow (ParseFloat range error)
+    *bits = ((uint64_t)exp2 << 52) | (mant & 0x000FFFFFFFFFFFFFull);
+    return true;
+}
+
+// Exact decision for an ambiguous product: compare w * 10^q with the midpoint between the candidate c0
+// and the next double up, in big-integer arithmetic (32-bit limbs, values up to ~900 bits).
+constexpr int kLimbs = 42;   // 1344 bits: 100 decimal digits (333 bits) times 5^342 (795 bits) plus shifts
+struct Big {
+    uint32_t d[kLimbs];
+};
+__device__ void big_set(Big& a, uint64_t v) {
+    for (int k = 0; k < kLimbs; ++k) a.d[k] = 0;
+    a.d[0] = (uint32_t)v;
+    a.d[1] = (uint32_t)(v >> 32);
+}
+__device__ void big_mul_small(Big& a, uint32_t m) {
+    uint64_t carry = 0;
+    for (int k = 0; k < kLimbs; ++k) {
+        const uint64_t t = (uint64_t)a.d[k] * m + carry;
+        a.d[k] = (uint32_t)t;
+        carry = t >> 32;
+    }
+}
+__device__ void big_mul_pow5(Big& a, int64_t k) {
+    while (k >= 13) { big_mul_small(a, 1220703125u); k -= 13; }   // 5^13 < 2^32
+    uint32_t m = 1;
+    while (k-- > 0) m *= 5;
+    if (m != 1) big_mul_small(a, m);
+}
+__device__ void big_shl(Big& a, int64_t s) {
+    const int w = (int)(s >> 5), b = (int)(s & 31);
+    for (int k = kLimbs - 1; k >= 0; --k) {
+        const int src = k - w;
+        uint32_t v = src >= 0 ? a.d[src] << b : 0u;
+        if (b && src - 1 >= 0) v |= a.d[src - 1] >> (32 - b);
+        a.d[k] = v;
+    }
+}
+__device__ int big_cmp(const Big& a, const Big& b) {
+    for (int k = kLimbs - 1; k >= 0; --k)
+        if (a.d[k] != b.d[k]) return a.d[k] < b.d[k] ? -1 : 1;
+    return 0;
+}
+// A (the decimal mantissa) * 10^q vs the midpoint above c0: returns c0 or the next double up
+__device__ uint64_t decide_exact_big(Big& A, int64_t q, uint64_t c0) {
+    const int64_t e = (int64_t)((c0 >> 52) & 0x7FF);
+    const uint64_t m = (c0 & 0x000FFFFFFFFFFFFFull) | (1ull << 52);   // c0 = m * 2^(e - 1075)
+    const int64_t E = e - 1076;                                        // midpoint = (2m + 1) * 2^E
+    Big B;
+    big_set(B, 2 * m + 1);
+    // w * 10^q  vs  (2m+1) * 2^E   <=>   A vs B * 2^(E - q), with the power of five on the proper side
+    if (q >= 0) big_mul_pow5(A, q); else big_mul_pow5(B, -q);
+    const int64_t s = E - q;
+    if (s >= 0) big_shl(B, s); else big_shl(A, -s);
+    const int c = big_cmp(A, B);
+    if (c > 0 || (c == 0 && (m & 1))) return c0 + 1;   // above the midpoint, or a tie to the even neighbour
+    return c0;
+}
+__device__ uint64_t decide_exact(uint64_t w, int64_t q, uint64_t c0) {
+    Big A;
+    big_set(A, w);
+    return decide_exact_big(A, q, c0);
+}
+
+// w * 10^q correctly rounded (|w| < 2^64, normal results); false for out-of-range results.
+__device__ bool dec_to_f64(uint64_t w, int64_t q, bool neg, double* out) {
+    if (w == 0 || q < -342) { *out = neg ? -0.0 : 0.0; return true; }   // below 2^-1075 for any 64-bit w
+    if (q > 308) return false;
+    uint64_t bits;
+    bool amb;
+    if (!el_core(w, q, &bits, &amb)) return false;
+    if (amb) bits = decide_exact(w, q, bits);
+    if (((bits >> 52) & 0x7FF) == 0x7FF) return false;
+    if (neg) bits |= 1ull << 63;
+    *out = __longlong_as_double((long long)bits);
+    return true;
+}
+
+// Parse a JSON number at p (p < e). Returns the position after it, or nullptr on a syntax error.
+struct Num {
+    bool neg, is_int, fits_i64, exact, trunc;
+    uint64_t mant;       // first <= 19 significant digits
+    int64_t exp10;       // value = mant * 10^exp10 (when !trunc)
+    int64_t i64;
+    double f64;
+};
+
+__device__ const uint8_t* parse_number(const uint8_t* p, const uint8_t* e, Num* n) {
+    n->neg = false;
+    n->is_int = true;
+    n->trunc = false;
+    n->mant = 0;
+    n->exp10 = 0;
+    if (p < e && *p == '-') { n->neg = true; ++p; }
+    if (p >= e || *p < '0' || *p > '9') return nullptr;
+    int nd = 0;            // significant digits kept in mant
+    int64_t drop = 0;      // integer digits dropped (beyond 19)
+    const uint8_t* ds = p;
+    const uint8_t *fs = nullptr, *fe = nullptr;   // fraction digits [fs, fe)
+    if (*p == '0') ++p;
+    else
+        while (p < e && *p >= '0' && *p <= '9') {
+            if (nd < 19) { n->mant = n->mant * 10 + (*p - '0'); if (n->mant) nd++; }
+            else { drop++; if (*p != '0') n->trunc = true; }
+            ++p;
+        }
+    const int int_digits = (int)(p - ds);
+    int64_t frac_exp = 0;
+    if (p < e && *p == '.') {
+        n->is_int = false;
+        ++p;
+        if (p >= e || *p < '0' || *p > '9') return nullptr;
+        fs = p;
+        while (p < e && *p >= '0' && *p <= '9') {
+            if (nd < 19) { n->mant = n->mant * 10 + (*p - '0'); frac_exp--; if (n->mant) nd++; }
+            else if (*p != '0') n->trunc = true;
+            ++p;
+        }
+        fe = p;
+    }
+    int64_t ex = 0;
+    if (p < e && (*p == 'e' || *p == 'E')) {
+        n->is_int = false;
+        ++p;
+        bool eneg = false;
+        if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
+        if (p >= e || *p < '0' || *p > '9') return nullptr;
+        while (p < e && *p >= '0' && *p <= '9') { if (ex < 100000) ex = ex * 10 + (*p - '0'); ++p; }
+        if (eneg) ex = -ex;
+    }
+    n->exp10 = drop + frac_exp + ex;
+    // int64 (fastfloat.ParseInt64): plain integer literal without overflow
+    n->fits_i64 = false;
+    if (n->is_int && !n->trunc && drop == 0 && int_digits <= 19) {
+        const uint64_t lim = n->neg ? (1ull << 63) : ((1ull << 63) - 1);
+        if (n->mant <= lim) { n->fits_i64 = true; n->i64 = n->neg ? (int64_t)(0 - n->mant) : (int64_t)n->mant; }
+    }
+    // float64
+    n->exact = true;
+    if (!n->trunc && n->mant <= (1ull << 53) && n->exp10 >= -22 && n->exp10 <= 22) {
+        double v = (double)n->mant;
+        v = n->exp10 < 0 ? __ddiv_rn(v, kPow10[-n->exp10]) : __dmul_rn(v, kPow10[n->exp10]);
+        n->f64 = n->neg ? -v : v;
+    } else if (!dec_to_f64(n->mant, n->exp10, n->neg, &n->f64)) {
+        n->exact = false;   // outside the normal range of binary64
+    } else if (n->trunc) {
+        // more than 19 significant digits: mant and mant + 1 usually round alike (strconv atof.go); if not,
+        // the full digit string (up to 100 significant digits) decides against the midpoint
+        double up;
+        if (!dec_to_f64(n->mant + 1, n->exp10, n->neg, &up)) n->exact = false;
+        else if (up != n->f64) {
+            Big A;
+            big_set(A, 0);
+            int sig = 0;
+            int64_t q = ex;
+            const uint8_t* ie = fs ? fs - 1 : (fe ? fe : p);
+            if (!fs) ie = ds + int_digits;
+            for (const uint8_t* c = ds; c < ie; ++c) {
+                if (sig == 0 && *c == '0') continue;
+                if (sig >= 100) { q++; continue; }
+                big_mul_small(A, 10);
+                A.d[0] += *c - '0';   // no carry: the low limb is a multiple of 10 after the multiply
+                sig++;
+            }
+            for (const uint8_t* c = fs; fs && c < fe; ++c) {
+                if (sig == 0 && *c == '0') { q--; continue; }
+                if (sig >= 100) { if (*c != '0') { n->exact = false; break; } continue; }
+                big_mul_small(A, 10);
+                A.d[0] += *c - '0';
+                sig++;
+                q--;
+            }
+            if (n->exact) {
+                // any nonzero integer digit beyond the 100th makes the 100-digit mantissa inexact as well
+                int seen = 0;
+                for (const uint8_t* c = ds; c < ie; ++c) {
+                    if (seen == 0 && *c == '0') continue;
+                    if (++seen > 100 && *c != '0') n->exact = false;
+                }
+            }
+            if (n->exact) {
+                uint64_t c0 = (uint64_t)__double_as_longlong(n->f64) & ~(1ull << 63);
+                const uint64_t b = decide_exact_big(A, q, c0);
+                n->f64 = __longlong_as_double((long long)(b | (n->neg ? (1ull << 63) : 0)));
+            }
+        }
+    }
+    return p;
+}
+
+// skip a JSON string starting at the opening quote; returns the position after the closing quote
+__device__ const uint8_t* skip_string(const uint8_t* p, const uint8_t* e) {
+    ++p;
+    while (p < e) {
+        if (*p == '\\') { p += 2; continue; }
+        if (*p == '"') return p + 1;
+        ++p;
+    }
+    return nullptr;
+}
+
+// skip any JSON value (nested objects/arrays string-aware): one flat scan, in-string state in a flag
+__device__ const uint8_t* skip_value(const uint8_t* p, const uint8_t* e) {
+    if (p >= e) return nullptr;
+    const uint8_t c = *p;
+    if (c == '"') return skip_string(p, e);
+    if (c == '{' || c == '[') {
+        int depth = 0;
+        bool in_str = false, esc = false;
+        for (; p < e; ++p) {
+            const uint8_t x = *p;
+            if (in_str) {
+                if (esc) esc = false;
+                else if (x == '\\') esc = true;
+                else if (x == '"') in_str = false;
+            } else if (x == '"') {
+                in_str = true;
+            } else if (x == '{' || x == '[') {
+                depth++;
+            } else if (x == '}' || x == ']') {
+                if (--depth == 0) return p + 1;
+            }
+        }
+        return nullptr;
+    }
+    if (c == 't') return (e - p >= 4 && p[1] == 'r' && p[2] == 'u' && p[3] == 'e') ? p + 4 : nullptr;
+    if (c == 'f') return (e - p >= 5 && p[1] == 'a' && p[2] == 'l' && p[3] == 's' && p[4] == 'e') ? p + 5 : nullptr;
+    if (c == 'n') return (e - p >= 4 && p[1] == 'u' && p[2] == 'l' && p[3] == 'l') ? p + 4 : nullptr;
+    Num n;
+    return parse_number(p, e, &n);
+}
+
+__device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint8_t c) { return (h ^ c) * 0x100000001B3ull; }
+
+// One thread per message: parse the object, scatter its schema fields into the columns.
+__global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
+                                                         int64_t n, const JSchema* __restrict__ sch, JOut out) {
+    const int64_t i = (int64_t)blockIdx.x * kJBlock + threadIdx.x;
+    if (i >= n) return;
+    const JSchema& S = *sch;
+    const uint8_t* p = bytes + off[i];
+    const uint8_t* e = bytes + off[i + 1];
+    int64_t ival[EK_MAX_COLUMNS];
+    uint32_t seen = 0, isnull = 0;
+    uint8_t err = EK_JSON_OK;
+    while (p < e && is_ws(*p)) ++p;
+    if (p >= e || *p != '{') err = (p < e && *p == '[') ? EK_JSON_ERR_UNSUPPORTED : EK_JSON_ERR_SYNTAX;
+    else {
+        ++p;
+        bool after_comma = false;
+        for (;;) {
+            while (p < e && is_ws(*p)) ++p;
+            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
+            if (*p == '}') {
+                if (after_comma) err = EK_JSON_ERR_SYNTAX;   // trailing comma
+                ++p;
+                break;
+            }
+            if (*p != '"') { err = EK_JSON_ERR_SYNTAX; break; }
+            // key
+            const uint8_t* ks = ++p;
+            uint64_t h = 0xCBF29CE484222325ull;
+            bool esc = false;
+            while (p < e && *p != '"') { if (*p == '\\') { esc = true; ++p; } h = fnv_step(h, *p); ++p; }
+            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
+            const int klen = (int)(p - ks);
+            ++p;
+            int col = -1;
+            if (!esc)
+                for (int c = 0; c < S.n; ++c) {
+                    if (S.hash[c] != h || S.len[c] != klen) continue;
+                    bool eq = true;
+                    for (int k = 0; k < klen; ++k) eq &= (uint8_t)S.name[c][k] == ks[k];
+                    if (eq) { col = c; break; }
+                }
+            while (p < e && is_ws(*p)) ++p;
+            if (p >= e || *p != ':') { err = EK_JSON_ERR_SYNTAX; break; }
+            ++p;
+            while (p < e && is_ws(*p)) ++p;
+            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
+            const uint8_t c0 = *p;
+            if (col < 0) {
+                p = skip_value(p, e);
+                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
+            } else if (c0 == 'n') {
+                p = skip_value(p, e);
+                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
+                seen |= 1u << col;
+                isnull |= 1u << col;
+            } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+                Num num;
+                p = parse_number(p, e, &num);
+                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
+                const int t = S.type[col];
+                if (t == EK_COL_F64) {
+                    if (!num.exact) { err = EK_JSON_ERR_NUMBER; break; }
+                    ival[col] = __double_as_longlong(num.f64);
+                } else {
+                    if (!num.fits_i64) { err = EK_JSON_ERR_NUMBER; break; }
+                    if (t == EK_COL_U32 && (num.i64 < 0 || num.i64 > 0xFFFFFFFFll)) { err = EK_JSON_ERR_NUMBER; break; }
+                    ival[col] = num.i64;
+                }
+                seen |= 1u << col;
+                isnull &= ~(1u << col);
+            } else {
+                // string / bool / object / array for a numeric schema field (converter.go checkSchema)
+                err = EK_JSON_ERR_TYPE;
+                break;
+            }
+            while (p < e && is_ws(*p)) ++p;
+            if (p < e && *p == ',') { ++p; after_comma = true; continue; }
+            if (p < e && *p == '}') { ++p; break; }
+            err = EK_JSON_ERR_SYNTAX;
+            break;
+        }
+        if (err == EK_JSON_OK) {
+            while (p < e && is_ws(*p)) ++p;
+            if (p != e) err = EK_JSON_ERR_SYNTAX;   // trailing bytes after the object
+        }
+    }
+    out.err[i] = err;
+    for (int c = 0; c < S.n; ++c) {
+        const bool ok = err == EK_JSON_OK && ((seen >> c) & 1u) && !((isnull >> c) & 1u);
+        if (err == EK_JSON_OK && !ok) atomicAdd(&out.nulls[c], 1u);
+        if (out.valid[c]) out.valid[c][i] = ok ? 1 : 0;
+        const int64_t v = ok ? ival[c] : 0;
+        if (S.type[c] == EK_COL_U32) ((uint32_t*)out.col[c])[i] = (uint32_t)v;
+        else ((int64_t*)out.col[c])[i] = v;
+    }
+}
+
+// stable compaction of the messages that decoded (same scheme as the range-mode trigger lists)
+constexpr int kTile = 4096;
+__global__ __launch_bounds__(kJBlock) void k_ok_count(const uint8_t* __restrict__ err, int64_t n, int64_t* cnt) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    int64_t c = 0;
+    for (int k = threadIdx.x; k < kTile; k += kJBlock) { const int64_t i = base + k; if (i < n && err[i] == 0) c++; }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ int64_t s[kJBlock / 64];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+__global__ __launch_bounds__(1024) void k_scan_cnt(int64_t* cnt, int nb) {
+    __shared__ int64_t part[1024];
+    const int per = (nb + 1023) / 1024;
+    const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    int64_t s = 0;
+    for (int k = b0; k < b1; ++k) s += cnt[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = 0;
+        for (int t = 0; t < 1024; ++t) { int64_t x = part[t]; part[t] = run; run += x; }
+        cnt[nb] = run;
+    }
+    __syncthreads();
+    int64_t run = part[threadIdx.x];
+    for (int k = b0; k < b1; ++k) { int64_t x = cnt[k]; cnt[k] = run; run += x; }
+}
+// move the decoded rows down to their compacted positions (row k -> dest <= k, processed in order per block)
+__global__ __launch_bounds__(kJBlock) void k_ok_pos(const uint8_t* __restrict__ err, int64_t n, const int64_t* cnt,
+                                                    int64_t* __restrict__ pos) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    __shared__ uint32_t wsum[kJBlock / 64];
+    int64_t run = cnt[blockIdx.x];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k0 = 0; k0 < kTile; k0 += kJBlock) {
+        const int64_t i = base + k0 + threadIdx.x;
+        const bool f = i < n && err[i] == 0;
+        const unsigned long long m = __ballot(f);
+        if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+        for (int w = 0; w < kJBlock / 64; ++w) { if (w < wv) wb += wsum[w]; tot += wsum[w]; }
+        if (i < n) pos[i] = f ? run + wb + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+        run += tot;
+        __syncthreads();
+    }
+}
+__global__ void k_compact_col(const int64_t* __restrict__ pos, int64_t n, const void* __restrict__ src, void* __restrict__ dst,
+                              int es) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = pos[i];
+        if (d < 0) continue;
+        if (es == 8) ((int64_t*)dst)[d] = ((const int64_t*)src)[i];
+        else if (es == 4) ((uint32_t*)dst)[d] = ((const uint32_t*)src)[i];
+        else ((uint8_t*)dst)[d] = ((const uint8_t*)src)[i];
+    }
+}
+
+struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct JsonDecoder {
+    JSchema sch{};
+    JSchema* d_sch = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    Buf in_bytes, in_off, raw_col[EK_MAX_COLUMNS], raw_valid[EK_MAX_COLUMNS], out_col[EK_MAX_COLUMNS],
+        out_valid[EK_MAX_COLUMNS], msg_err, pos, cnt, nulls;
+    std::vector<uint8_t> h_err;
+    int64_t last_n = 0, last_ok = 0;
+    ek_json_stats st{};
+
+    int fail(int code, const char* fmt, ...) {
+        char b[256];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(b, sizeof b, fmt, ap);
+        va_end(ap);
+        err = b;
+        return code;
+    }
+    int ensure(Buf& b, size_t bytes) {
+        if (b.p && b.bytes >= bytes) return 0;
+        if (b.p) { hipStreamSynchronize(stream); hipFree(b.p); b.p = nullptr; }
+        const size_t nb = std::max<size_t>(bytes, 256);
+        if (hipMalloc(&b.p, nb) != hipSuccess) return fail(EK_ERR_NOMEM, "hipMalloc(%zu) failed", nb);
+        b.bytes = nb;
+        return 0;
+    }
+    ~JsonDecoder() {
+        if (stream) hipStreamSynchronize(stream);
+        for (Buf* b : {&in_bytes, &in_off, &msg_err, &pos, &cnt, &nulls}) if (b->p) hipFree(b->p);
+        for (int c = 0; c < EK_MAX_COLUMNS; ++c)
+            for (Buf* b : {&raw_col[c], &raw_valid[c], &out_col[c], &out_valid[c]}) if (b->p) hipFree(b->p);
+        if (d_sch) hipFree(d_sch);
+        if (stream) hipStreamDestroy(stream);
+    }
+
+    int init(const ek_json_schema* s, int device) {
+        if (!s || s->n_fields <= 0 || s->n_fields > EK_MAX_COLUMNS) return fail(EK_ERR_INVALID, "bad schema field count");
+        sch.n = s->n_fields;
+        for (int c = 0; c < sch.n; ++c) {
+            const int t = s->column_type[c];
+            if (t != EK_COL_I64 && t != EK_COL_F64 && t != EK_COL_U32) return fail(EK_ERR_INVALID, "bad column type");
+            sch.type[c] = t;
+            const size_t L = strnlen(s->names[c], EK_JSON_MAX_NAME);
+            if (L == 0 || L >= EK_JSON_MAX_NAME) return fail(EK_ERR_INVALID, "bad field name %d", c);
+            memcpy(sch.name[c], s->names[c], L);
+            sch.len[c] = (int32_t)L;
+            uint64_t h = 0xCBF29CE484222325ull;
+            for (size_t k = 0; k < L; ++k) h = (h ^ (uint8_t)s->names[c][k]) * 0x100000001B3ull;
+            sch.hash[c] = h;
+        }
+        if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(EK_ERR_DEVICE, "stream");
+        if (hipMalloc((void**)&d_sch, sizeof(JSchema)) != hipSuccess) return fail(EK_ERR_NOMEM, "schema alloc");
+        if (hipMemcpy(d_sch, &sch, sizeof(JSchema), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "schema copy");
+        return 0;
+    }
+
+    int decode(const char* bytes, int64_t n_bytes, const int64_t* offsets, int64_t n, int32_t memory, ek_batch* out) {
+        if (!out || n < 0 || n_bytes < 0 || (n > 0 && (!bytes || !offsets))) return fail(EK_ERR_INVALID, "bad arguments");
+        memset(out, 0, sizeof *out);
+        out->memory = EK_MEM_DEVICE;
+        last_n = n;
+        last_ok = 0;
+        if (n == 0) return 0;
+        const uint8_t* d_bytes = (const uint8_t*)bytes;
+        const int64_t* d_off = offsets;
+        if (memory == EK_MEM_HOST) {
+            if (offsets[0] < 0 || offsets[n] > n_bytes) return fail(EK_ERR_INVALID, "offsets outside the payload");
+            if (int rc = ensure(in_bytes, (size_t)n_bytes + 1)) return rc;
+            if (int rc = ensure(in_off, (size_t)(n + 1) * 8)) return rc;
+            hipMemcpyAsync(in_bytes.p, bytes, (size_t)n_bytes, hipMemcpyHostToDevice, stream);
+            hipMemcpyAsync(in_off.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, stream);
+            d_bytes = (const uint8_t*)in_bytes.p;
+            d_off = (const int64_t*)in_off.p;
+        }
+        JOut jo{};
+        for (int c = 0; c < sch.n; ++c) {
+            const size_t es = sch.type[c] == EK_COL_U32 ? 4 : 8;
+            if (int rc = ensure(raw_col[c], (size_t)n * es)) return rc;
+            if (int rc = ensure(raw_valid[c], (size_t)n)) return rc;
+            jo.col[c] = raw_col[c].p;
+            jo.valid[c] = (uint8_t*)raw_valid[c].p;
+        }
+        if (int rc = ensure(msg_err, (size_t)n)) return rc;
+        if (int rc = ensure(nulls, EK_MAX_COLUMNS * 4)) return rc;
+        hipMemsetAsync(nulls.p, 0, EK_MAX_COLUMNS * 4, stream);
+        jo.err = (uint8_t*)msg_err.p;
+        jo.nulls = (unsigned int*)nulls.p;
+        hipLaunchKernelGGL(k_json_decode, dim3((unsigned)((n + kJBlock - 1) / kJBlock)), dim3(kJBlock), 0, stream, d_bytes,
+                           d_off, n, d_sch, jo);
+        const int nb = (int)((n + kTile - 1) / kTile);
+        if (int rc = ensure(cnt, (size_t)(nb + 1) * 8)) return rc;
+        hipLaunchKernelGGL(k_ok_count, dim3(nb), dim3(kJBlock), 0, stream, (const uint8_t*)msg_err.p, n, (int64_t*)cnt.p);
+        hipLaunchKernelGGL(k_scan_cnt, dim3(1), dim3(1024), 0, stream, (int64_t*)cnt.p, nb);
+        int64_t ok = 0;
+        unsigned int h_nulls[EK_MAX_COLUMNS];
+        hipMemcpyAsync(&ok, (int64_t*)cnt.p + nb, 8, hipMemcpyDeviceToHost, stream);
+        hipMemcpyAsync(h_nulls, nulls.p, sizeof h_nulls, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json decode kernel failed");
+        last_ok = ok;
+        st.messages += n;
+        st.errors += n - ok;
+        st.bytes += offsets && memory == EK_MEM_HOST ? (offsets[n] - offsets[0]) : 0;
+        out->n_rows = ok;
+        if (ok == n) {
+            for (int c = 0; c < sch.n; ++c) {
+                out->columns[c] = raw_col[c].p;
+                out->validity[c] = h_nulls[c] ? (const uint8_t*)raw_valid[c].p : nullptr;   // no nil: no validity array
+            }
+            return 0;
+        }
+        // drop the messages that failed to decode (their errors are kept for ek_json_errors)
+        if (int rc = ensure(pos, (size_t)n * 8)) return rc;
+        hipLaunchKernelGGL(k_ok_pos, dim3(nb), dim3(kJBlock), 0, stream, (const uint8_t*)msg_err.p, n, (const int64_t*)cnt.p,
+                           (int64_t*)pos.p);
+        const unsigned g = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+        for (int c = 0; c < sch.n; ++c) {
+            const int es = sch.type[c] == EK_COL_U32 ? 4 : 8;
+            if (int rc = ensure(out_col[c], (size_t)std::max<int64_t>(ok, 1) * es)) return rc;
+            if (int rc = ensure(out_valid[c], (size_t)std::max<int64_t>(ok, 1))) return rc;
+            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_col[c].p, out_col[c].p, es);
+            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_valid[c].p, out_valid[c].p, 1);
+            out->columns[c] = out_col[c].p;
+            out->validity[c] = h_nulls[c] ? (const uint8_t*)out_valid[c].p : nullptr;
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json compaction failed");
+        return 0;
+    }
+
+    int errors(int64_t* idx, uint8_t* code, int64_t cap, int64_t* n_out) {
+        h_err.resize((size_t)last_n);
+        if (last_n) {
+            hipMemcpyAsync(h_err.data(), msg_err.p, (size_t)last_n, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "error copy failed");
+        }
+        int64_t k = 0;
+        for (int64_t i = 0; i < last_n; ++i) {
+            if (!h_err[i]) continue;
+            if (k < cap) { if (idx) idx[k] = i; if (code) code[k] = h_err[i]; }
+            k++;
+        }
+        *n_out = k;
+        return 0;
+    }
+};
+
+thread_local std::string g_json_create_error;
+
+}  // namespace
+
+extern "C" {
+
+int ek_json_create(const ek_json_schema* schema, int device, void** out) {
+    if (!out) return EK_ERR_INVALID;
+    *out = nullptr;
+    JsonDecoder* d = new (std::nothrow) JsonDecoder();
+    if (!d) return EK_ERR_NOMEM;
+    if (int rc = d->init(schema, device)) {
+        g_json_create_error = d->err;
+        delete d;
+        return rc;
+    }
+    *out = d;
+    return 0;
+}
+
+int ek_json_decode(void* h, const char* bytes, int64_t n_bytes, const int64_t* offsets, int64_t n_msgs, int32_t memory,
+                   ek_batch* out) {
+    if (!h) return EK_ERR_INVALID;
+    return ((JsonDecoder*)h)->decode(bytes, n_bytes, offsets, n_msgs, memory, out);
+}
+
+int ek_json_errors(void* h, int64_t* msg_index, uint8_t* code, int64_t cap, int64_t* n_errors) {
+    if (!h || !n_errors) return EK_ERR_INVALID;
+    return ((JsonDecoder*)h)->errors(msg_index, code, cap, n_errors);
+}
+
+int ek_json_get_stats(void* h, ek_json_stats* out) {
+    if (!h || !out) return EK_ERR_INVALID;
+    *out = ((JsonDecoder*)h)->st;
+    return 0;
+}
+
+const char* ek_json_last_error(void* h) { return h ? ((JsonDecoder*)h)->err.c_str() : g_json_create_error.c_str(); }
+
+int ek_json_destroy(void* h) {
+    delete (JsonDecoder*)h;
+    return 0;
+}
+
+}  // extern "C"

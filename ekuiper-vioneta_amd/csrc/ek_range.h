@@ -114,6 +114,36 @@ __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, in
     }
 }
 
+// FilterOp over a window-less batch (filter_operator.go:36-90): 1 keep; nil/false drop; error drop + count
+__global__ void k_filter_flags(DPlan* __restrict__ pp, DBatch b, uint8_t* __restrict__ flags, unsigned long long* n_err) {
+    const DPlan& p = *pp;
+    unsigned long long e = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int w = p.n_where > 0 ? where_decide_slow(p, b, i) : 1;
+        flags[i] = w > 0 ? 1 : 0;
+        e += w < 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(n_err, e);
+}
+
+// SELECT * rows of the selected events: key = batch row, value c = column c (tag by type / validity)
+__global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ sel, int64_t ns, int64_t out_base,
+                              int32_t widx, Results res) {
+    const DPlan& p = *pp;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = sel[k], o = out_base + k;
+        res.key[o] = (uint32_t)i;
+        for (int c = 0; c < p.n_columns; ++c) {
+            const bool ok = col_valid(b, c, i);
+            const int t = p.col_type[c];
+            res.val[c][o] = !ok ? 0 : (t == EK_COL_U32 ? (int64_t)((const uint32_t*)b.col[c])[i] : ((const int64_t*)b.col[c])[i]);
+            res.tag[c][o] = !ok ? EK_TAG_NULL : (t == EK_COL_F64 ? EK_TAG_F64 : EK_TAG_I64);
+        }
+        if (k == 0) res.win_cnt[widx] = ns;
+    }
+}
+
 // Per-block counts of set flags (stable compaction, pass 1)
 constexpr int kCompactTile = 4096;
 __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict__ flags, int64_t n, int64_t* cnt) {

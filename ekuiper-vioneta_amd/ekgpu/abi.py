@@ -114,6 +114,7 @@ class ek_stats(C.Structure):
         ("last_batch_device_ms", C.c_double),
         ("phase_ms", C.c_double * 4),
         ("phase_launches", C.c_int64 * 4),
+        ("records_filter_error", C.c_int64),
     ]
 
 
@@ -127,3 +128,17 @@ def mix64(x: int) -> int:
     x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
     x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
     return x ^ (x >> 31)
+
+
+# columnar JSON ingest (ek_json_*)
+EK_JSON_MAX_NAME = 32
+EK_JSON_OK, EK_JSON_ERR_SYNTAX, EK_JSON_ERR_TYPE, EK_JSON_ERR_NUMBER, EK_JSON_ERR_UNSUPPORTED = range(5)
+
+
+class ek_json_schema(C.Structure):
+    _fields_ = [("n_fields", C.c_int32), ("column_type", C.c_int32 * EK_MAX_COLUMNS),
+                ("names", (C.c_char * EK_JSON_MAX_NAME) * EK_MAX_COLUMNS)]
+
+
+class ek_json_stats(C.Structure):
+    _fields_ = [("messages", C.c_int64), ("errors", C.c_int64), ("bytes", C.c_int64)]

@@ -52,6 +52,19 @@ def lib():
         L.ek_last_error.restype = C.c_char_p
         L.ek_destroy.argtypes = [C.c_void_p]
         L.ek_destroy.restype = C.c_int
+        L.ek_json_create.argtypes = [C.POINTER(A.ek_json_schema), C.c_int, C.POINTER(C.c_void_p)]
+        L.ek_json_create.restype = C.c_int
+        L.ek_json_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,
+                                     C.POINTER(A.ek_batch)]
+        L.ek_json_decode.restype = C.c_int
+        L.ek_json_errors.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.ek_json_errors.restype = C.c_int
+        L.ek_json_get_stats.argtypes = [C.c_void_p, C.POINTER(A.ek_json_stats)]
+        L.ek_json_get_stats.restype = C.c_int
+        L.ek_json_last_error.argtypes = [C.c_void_p]
+        L.ek_json_last_error.restype = C.c_char_p
+        L.ek_json_destroy.argtypes = [C.c_void_p]
+        L.ek_json_destroy.restype = C.c_int
         if L.ek_abi_version() != A.EKGPU_ABI_VERSION:
             raise EngineError(A.EK_ERR_INVALID, "libekgpu.so ABI version mismatch")
         _lib = L
@@ -60,7 +73,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_batch", "ek_poll_results",
                     "ek_release_results", "ek_reset", "ek_sync", "ek_set_stream", "ek_get_stats", "ek_last_error",
-                    "ek_destroy"]
+                    "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
+                    "ek_json_last_error", "ek_json_destroy"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -110,6 +124,10 @@ class Engine:
                     b.validity[k] = p
         self._check(lib().ek_push_batch(self.h, C.byref(b)))
 
+    def push_batch(self, batch: A.ek_batch):
+        """Push an ek_batch as is (e.g. the device columns returned by JsonDecoder.decode)."""
+        self._check(lib().ek_push_batch(self.h, C.byref(batch)))
+
     def poll(self):
         r = A.ek_result()
         self._check(lib().ek_poll_results(self.h, A.EK_MEM_HOST, C.byref(r)))
@@ -143,6 +161,67 @@ class Engine:
     def close(self):
         if self.h:
             lib().ek_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class JsonDecoder:
+    """Columnar JSON ingest on the GPU (include/ekgpu.h ek_json_*): a micro-batch of JSON messages ->
+    device columns of an ek_batch, ready for Engine.push_batch."""
+
+    def __init__(self, schema: dict, device: int = 0):
+        """schema: ordered {field: "bigint" | "float" | "key"} (same column order as the rule's schema)."""
+        from .rule import COLTYPES
+        L = lib()
+        s = A.ek_json_schema()
+        s.n_fields = len(schema)
+        for k, (name, t) in enumerate(schema.items()):
+            s.column_type[k] = COLTYPES[t]
+            s.names[k].value = name.encode()
+        self.h = C.c_void_p()
+        rc = L.ek_json_create(C.byref(s), device, C.byref(self.h))
+        if rc != 0:
+            raise EngineError(rc, L.ek_json_last_error(None).decode())
+
+    def decode(self, messages, offsets: Optional[np.ndarray] = None) -> A.ek_batch:
+        """messages: list of bytes, or one bytes blob with offsets (n+1, int64). Returns the device batch."""
+        if offsets is None:
+            lens = np.fromiter((len(m) for m in messages), dtype=np.int64, count=len(messages))
+            offsets = np.zeros(len(messages) + 1, dtype=np.int64)
+            np.cumsum(lens, out=offsets[1:])
+            blob = b"".join(messages)
+        else:
+            blob = messages
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        self._blob = np.frombuffer(blob, dtype=np.uint8) if len(blob) else np.zeros(1, np.uint8)
+        out = A.ek_batch()
+        rc = lib().ek_json_decode(self.h, self._blob.ctypes.data, len(blob), offsets.ctypes.data, len(offsets) - 1,
+                                  A.EK_MEM_HOST, C.byref(out))
+        if rc != 0:
+            raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
+        return out
+
+    def errors(self):
+        n = C.c_int64()
+        lib().ek_json_errors(self.h, None, None, 0, C.byref(n))
+        idx = np.zeros(max(n.value, 1), np.int64)
+        code = np.zeros(max(n.value, 1), np.uint8)
+        lib().ek_json_errors(self.h, idx.ctypes.data, code.ctypes.data, n.value, C.byref(n))
+        return idx[: n.value], code[: n.value]
+
+    def stats(self) -> A.ek_json_stats:
+        s = A.ek_json_stats()
+        lib().ek_json_get_stats(self.h, C.byref(s))
+        return s
+
+    def close(self):
+        if self.h:
+            lib().ek_json_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

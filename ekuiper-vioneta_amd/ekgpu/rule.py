@@ -257,6 +257,14 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
         t = p.peek()
         if t is None:
             raise RuleError("unexpected end of select list")
+        if t == "*":
+            p.i += 1
+            for c, name in enumerate(p.columns):
+                raw_select.append(OutputField(name, "column", c))
+            if p.peek() == ",":
+                p.i += 1
+                continue
+            break
         if p.peek(1) == "(" and t.lower() in ("window_start", "window_end"):
             p.i += 3
             name, kind, slot = t.lower(), t.lower(), -1
@@ -337,10 +345,20 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
         having = p.expr(True)
     if p.peek() is not None:
         raise RuleError(f"unexpected token {p.peek()!r}")
-    if wtype == A.EK_WINDOW_NONE:
-        raise RuleError("the GPU window engine needs a window in GROUP BY")
     plan.window_type = wtype
     plan.key_column = key_col
+    if wtype == A.EK_WINDOW_NONE:
+        # window-less rule: FilterOp + projection of every column (SELECT *, the C1 shape)
+        if p.aggs or key_col >= 0 or having:
+            raise RuleError("aggregates and GROUP BY need a window (the GPU engine's hot path)")
+        if [f.slot for f in raw_select] != list(range(len(p.columns))):
+            raise RuleError("window-less rules project every column (SELECT *)")
+        plan.n_where = _fill_prog(plan.where_prog, where)
+        plan.is_event_time = 0
+        plan.ts_column = -1
+        fields = [OutputField(f.name, "column", f.slot) for f in raw_select]
+        return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
+                            options=dict(isEventTime=False, lateTolerance=0))
     for f in raw_select:
         if f.kind == "column":
             if f.slot != key_col:

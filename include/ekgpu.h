@@ -169,6 +169,7 @@ typedef struct {
      * [EK_PHASE_AGGREGATE] k_agg, [EK_PHASE_FINALIZE] k_finalize. */
     double phase_ms[4];
     int64_t phase_launches[4];
+    int64_t records_filter_error; /* window-less rules: events whose WHERE evaluation errored      */
 } ek_stats;
 
 enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };
@@ -215,6 +216,47 @@ int ek_set_stream(void* h, void* hip_stream);
 int ek_get_stats(void* h, ek_stats* out);
 const char* ek_last_error(void* h);
 int ek_destroy(void* h);
+
+/* ---------------------------------------------------------------- columnar JSON ingest
+ * Replaces the per-message FastJsonConverter.Decode of a schema-typed stream
+ * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) for flat JSON objects
+ * with numeric fields: a micro-batch of messages (payload bytes concatenated, message i =
+ * bytes[offsets[i], offsets[i+1])) is decoded on the GPU straight into the columns of an ek_batch
+ * (device memory owned by the decoder, valid until its next decode), ready for ek_push_batch.
+ * Schema type BIGINT -> EK_COL_I64 (integer literal, fastfloat.ParseInt64), FLOAT -> EK_COL_F64
+ * (correctly rounded), a dense key id column -> EK_COL_U32 (integer literal in [0, 2^32)). null or an
+ * absent field -> validity 0; fields outside the schema are skipped. Messages that fail to decode are
+ * dropped from the batch and reported by ek_json_errors. */
+#define EK_JSON_MAX_NAME 32
+enum {
+    EK_JSON_OK = 0,
+    EK_JSON_ERR_SYNTAX = 1,      /* fastjson parse error                                        */
+    EK_JSON_ERR_TYPE = 2,        /* "%v has wrong type" (string/bool/object/array for a number)  */
+    EK_JSON_ERR_NUMBER = 3,      /* not an int64 literal for BIGINT / number out of range         */
+    EK_JSON_ERR_UNSUPPORTED = 4  /* top-level array payloads (decoded by the Go converter instead) */
+};
+
+typedef struct {
+    int32_t n_fields;
+    int32_t column_type[EK_MAX_COLUMNS];           /* EK_COL_* of column i                  */
+    char names[EK_MAX_COLUMNS][EK_JSON_MAX_NAME];  /* JSON key of column i (NUL-terminated)   */
+} ek_json_schema;
+
+typedef struct {
+    int64_t messages;
+    int64_t errors;
+    int64_t bytes;
+} ek_json_stats;
+
+int ek_json_create(const ek_json_schema* schema, int device, void** out_handle);
+/* memory: where bytes/offsets live (EK_MEM_HOST: copied to the device first). out: device columns. */
+int ek_json_decode(void* h, const char* bytes, int64_t n_bytes, const int64_t* offsets, int64_t n_msgs, int32_t memory,
+                   ek_batch* out);
+/* messages of the last decode that failed: their indices and EK_JSON_ERR_* codes (up to cap) */
+int ek_json_errors(void* h, int64_t* msg_index, uint8_t* code, int64_t cap, int64_t* n_errors);
+int ek_json_get_stats(void* h, ek_json_stats* out);
+const char* ek_json_last_error(void* h);
+int ek_json_destroy(void* h);
 
 /* Membership hash used by debug_membership (splitmix64 finaliser). */
 static inline uint64_t ek_mix64(uint64_t x) {

@@ -733,9 +733,37 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
     } else {
-        if (p->window_type != EK_WINDOW_COUNT) {
+        if (p->window_type == EK_WINDOW_NONE) {
+            /* window-less rule: FilterOp.Apply per event (filter_operator.go:36-90) + SELECT * projection.
+             * One output segment: rows = passing events in arrival order, key = row index, value c = column c. */
+            if (p->n_aggs != 0) { set_status(out, EK_ERR_UNSUPPORTED, "aggregates need a window"); return out->status; }
+            v_push(&ob.ws, 0); v_push(&ob.we, 0); v_push(&ob.roff, 0); v_push(&ob.moff, 0);
+            uint64_t h = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                v_push(&ob.mem, i);
+                h += ek_mix64((uint64_t)i);
+                if (p->n_where > 0) {
+                    val_t r = eval_prog(p->where_prog, p->n_where, &d, i, NULL);
+                    if (!(r.tag == V_BOOL && r.i)) continue;   /* nil/false dropped; an error drops the event */
+                }
+                v_push(&ob.key, i);
+                for (int c = 0; c < p->n_columns; ++c) {
+                    val_t v = col_val(&d, c, i);
+                    int64_t bits = v.i;
+                    if (v.tag == V_F64) memcpy(&bits, &v.f, 8);
+                    v_push(&ob.aval[c], v.tag == V_NULL ? 0 : bits);
+                    v_push(&ob.atag[c], v.tag == V_NULL ? EK_TAG_NULL : (v.tag == V_F64 ? EK_TAG_F64 : EK_TAG_I64));
+                }
+            }
+            v_push(&ob.mcnt, n);
+            v_push(&ob.mhash, (int64_t)h);
+            v_push(&ob.rcnt, ob.key.n);
+            v_push(&ob.st, EK_WIN_OK);
+            ob.werr = (char*)calloc(128, 1);
+            ob.werr_cap = 1;
+        } else if (p->window_type != EK_WINDOW_COUNT) {
             set_status(out, EK_ERR_UNSUPPORTED, "processing-time oracle supports COUNTWINDOW only"); return out->status;
-        }
+        } else {
         /* window_op.go:390-418 + TupleList 502-551; CountInterval defaults to CountLength (window_op.go:100-103) */
         int64_t len = p->length, itv = p->interval > 0 ? p->interval : p->length;
         if (len <= 0) { set_status(out, EK_ERR_INVALID, "Window size should not be less than zero."); return out->status; }
@@ -752,11 +780,12 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
             }
         }
         free(inputs.a);
+        }
     }
 
     out->r.n_windows = ob.ws.n;
     out->r.n_rows = ob.key.n;
-    out->r.n_aggs = p->n_aggs;
+    out->r.n_aggs = p->window_type == EK_WINDOW_NONE ? p->n_columns : p->n_aggs;
     out->r.memory = EK_MEM_HOST;
     v_push(&ob.moff, ob.mem.n);
     out->r.win_start = take(&ob.ws);
@@ -777,7 +806,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.key[r] = (uint32_t)k[r];
         free(k);
     }
-    for (int a = 0; a < p->n_aggs; ++a) {
+    for (int a = 0; a < out->r.n_aggs; ++a) {
         out->r.agg_value[a] = take(&ob.aval[a]);
         int64_t* t = take(&ob.atag[a]);
         out->r.agg_tag[a] = (uint8_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 1);
