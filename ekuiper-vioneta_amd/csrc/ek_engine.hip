@@ -929,8 +929,14 @@ struct Engine {
         gd.hi = hi;
         gd.n_panes = npn;
         // chunk size of this group: halve while a chunk would span more panes than k_part sorts in LDS
-        int64_t csz = chunk;
+        // sorted groups start from single-tile chunks (keys read once, k_part's count pass skipped) and
+        // grow the chunk only while a pane would span more chunk runs than k_agg walks
+        int64_t csz = pbnd_host ? std::min<int64_t>(kTile, chunk) : chunk;
         int mp = max_panes_in_chunk(pbnd_host, gd, csz);
+        while (pbnd_host && csz < chunk && max_chunks_in_pane(pbnd_host, gd, csz) > kMaxRuns) {
+            csz <<= 1;
+            mp = max_panes_in_chunk(pbnd_host, gd, csz);
+        }
         while (csz > 1024 && pbnd_host && (mp > kMaxChunkBnd + 1 || (int64_t)NB * mp > np_max)) {
             csz >>= 1;
             mp = max_panes_in_chunk(pbnd_host, gd, csz);
@@ -1028,7 +1034,7 @@ struct Engine {
         const bool wh = dp.n_where > 0;
         {
             const int nvc = std::max(1, dp.n_vc);
-            const size_t lds_p = part_lds_bytes(nvc, lp_stride, any_nullable);
+            const size_t lds_p = part_lds_bytes(nvc, lp_stride, any_nullable, gd.chunk <= kTile);
             uint32_t* ct = (uint32_t*)chist.p;
             dim3 gp(gd.nch);
             const int ph = phase_begin(EK_PHASE_PARTITION);
@@ -1484,7 +1490,7 @@ struct Engine {
         gd.ring = npn;
         // chunk size: small windows -> shorter chunks (a chunk sorts at most kMaxChunkBnd+1 panes in LDS);
         // big windows -> longer chunks (k_agg walks at most kMaxRuns chunk runs per pane)
-        int64_t csz = chunk;
+        int64_t csz = kTile;
         int mp = max_panes_in_chunk(h_pbnd, gd, csz);
         while (csz > 256 && (mp > kMaxChunkBnd + 1 || (int64_t)NB * mp > np_max)) { csz >>= 1; mp = max_panes_in_chunk(h_pbnd, gd, csz); }
         while (max_chunks_in_pane(h_pbnd, gd, csz) > kMaxRuns && csz < (1 << 22)) { csz <<= 1; mp = max_panes_in_chunk(h_pbnd, gd, csz); }

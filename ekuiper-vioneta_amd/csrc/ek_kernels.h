@@ -352,9 +352,10 @@ __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
 }
 
 // LDS bytes of k_part for `nvc` value columns and `lp` chunk-local partitions
-inline size_t part_lds_bytes(int nvc, int lp, bool nullable) {
+// (single-tile chunks need no per-row partition array: their runs come straight from the tile sort)
+inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
     size_t lpp = ((size_t)lp + 4 + 3) & ~(size_t)3;
-    return (size_t)nvc * kTile * 8 + 2 * lpp * 4 + (size_t)kTile * 4 + (nullable ? (size_t)nvc * kTile : 0);
+    return (size_t)nvc * kTile * 8 + 2 * lpp * 4 + (size_t)kTile * (single_tile ? 2 : 4) + (nullable ? (size_t)nvc * kTile : 0);
 }
 
 // One workgroup per chunk: partition the chunk's rows by (pane, key bucket) into the chunk's OWN
@@ -362,6 +363,8 @@ inline size_t part_lds_bytes(int nvc, int lp, bool nullable) {
 // key loads), (2) exclusive scan -> run offsets, published in ctab[chunk][0..lp_n], (3) per tile of
 // kTile rows: load, counting-sort by partition in LDS, write runs with consecutive lanes on
 // consecutive addresses. No global atomics, no global scan: k_agg walks the per-chunk runs.
+// A chunk of at most one tile skips (1)-(2): the tile's own sort yields its runs, so the keys are read
+// once and the tile is written as one block of runs at region + sorted position.
 // MODE 0: unsorted batch (pane from ts); 1: ts-sorted batch (pane from the row index);
 // 2: virtual panes (range mode): the group's rows are the concatenation of possibly overlapping
 //    index ranges of the event buffer, virtual row v of pane r lives at physical row v + voff[r].
@@ -386,16 +389,19 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     int64_t* s_val = (int64_t*)smem;                                          // [NVC][kTile]
     uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [lpp]
     uint32_t* tcnt = cur + lpp;                                               // [lpp]
+    const bool single = gd.chunk <= kTile;
     uint16_t* s_klo = (uint16_t*)(tcnt + lpp);                                // [kTile]
-    uint16_t* s_lp = s_klo + kTile;                                           // [kTile]
-    uint8_t* s_vd = (uint8_t*)(s_lp + kTile);                                 // [NVC][kTile]
+    uint16_t* s_lp = s_klo + kTile;                                           // [kTile] (multi-tile chunks)
+    uint8_t* s_vd = (uint8_t*)(s_klo + (single ? 1 : 2) * kTile);             // [NVC][kTile]
     const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
     const int64_t region = (int64_t)blockIdx.x * rs;
 
     // ---- (1) count
     for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
     __syncthreads();
-    if (MODE == 2) {
+    if (single) {
+        // runs come from the tile sort below
+    } else if (MODE == 2) {
         // physical rows are contiguous only inside one pane: scalar (still coalesced) key loads
         for (int64_t v = c0 + threadIdx.x; v < c1; v += kBlock) {
             const int rel = chunk_rel(lb, nlb, pa, v);
@@ -435,10 +441,12 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     }
     __syncthreads();
     // ---- (2) run offsets of this chunk
-    block_excl_scan(tcnt, lp_n, wsum);
-    for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
-    for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] = tcnt[k];
-    __syncthreads();
+    if (!single) {
+        block_excl_scan(tcnt, lp_n, wsum);
+        for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
+        for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] = tcnt[k];
+        __syncthreads();
+    }
     // ---- (3) tiles: load, LDS counting sort, coalesced run writes
     const uint32_t kmask = (1u << gd.kbits) - 1u;
     const bool nullable = st.nullable_mask != 0;
@@ -496,22 +504,25 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
             const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+            // (single-tile chunks flag WHERE errors here: there was no count pass)
             if (MODE == 2) {
-                lp[j] = phys[j] >= 0 ? local_part<MODE, WHERE>(p, b, g, gd, rel[j], acc, phys[j], pa, key[j], nullptr, false) : -1;
+                lp[j] = phys[j] >= 0 ? local_part<MODE, WHERE>(p, b, g, gd, rel[j], acc, phys[j], pa, key[j], pane_err, single) : -1;
             } else {
                 const int r = (MODE == 1 && i >= c0 && i < c1) ? chunk_rel(lb, nlb, pa, i) : 0;
-                lp[j] = (i >= c0 && i < c1) ? local_part<MODE, WHERE>(p, b, g, gd, r, acc, i, pa, key[j], nullptr, false) : -1;
+                lp[j] = (i >= c0 && i < c1) ? local_part<MODE, WHERE>(p, b, g, gd, r, acc, i, pa, key[j], pane_err, single) : -1;
             }
             if (lp[j] >= 0) rank[j] = atomicAdd(&tcnt[lp[j]], 1u);
         }
         __syncthreads();
         block_excl_scan(tcnt, lp_n, wsum);
+        if (single)
+            for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
             if (lp[j] < 0) continue;
             const uint32_t s = tcnt[lp[j]] + rank[j];
             s_klo[s] = (uint16_t)(key[j] & kmask);
-            s_lp[s] = (uint16_t)lp[j];
+            if (!single) s_lp[s] = (uint16_t)lp[j];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) s_val[v * kTile + s] = val[v][j];
             if (nullable) {
@@ -524,8 +535,11 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
         __syncthreads();
         const uint32_t total = (gd.pad & 8) ? 0u : tcnt[lp_n];   // diagnostic knob 8: no global stores
         for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
-            const int l = s_lp[s];
-            const int64_t gpos = region + cur[l] + (s - tcnt[l]);
+            int64_t gpos = region + s;
+            if (!single) {
+                const int l = s_lp[s];
+                gpos = region + cur[l] + (s - tcnt[l]);
+            }
             st.klo[gpos] = s_klo[s];
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
@@ -534,6 +548,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
                 if (st.nullable_mask & (1u << v)) st.valid[v][gpos] = s_vd[v * kTile + s];
             }
         }
+        if (single) break;
         __syncthreads();
         for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] += tcnt[k + 1] - tcnt[k];
         __syncthreads();
