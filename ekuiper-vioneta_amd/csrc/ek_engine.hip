@@ -1003,7 +1003,7 @@ struct Engine {
     static size_t aux_layout_words(int npn) { return aux_layout_voff(npn) + npn + 2; }
 
     // k_part (MODE 0 unsorted / 1 sorted / 2 virtual panes) + k_agg for one group
-    int launch_part_agg(const DBatch& db, const GroupDesc& gd, int mode, const uint8_t* d_acc, int32_t* perr,
+    int launch_part_agg(const DBatch& db, GroupDesc gd, int mode, const uint8_t* d_acc, int32_t* perr,
                         int64_t* pmc, unsigned long long* pmh, int lp_stride, bool any_fresh) {
         const int64_t rs = gd.chunk;                                // staging region per chunk
         int64_t ne = (int64_t)gd.nch * rs + 64;
@@ -1029,6 +1029,8 @@ struct Engine {
         }
         const int ls = lp_stride + 1;
         if (int rc = ensure(chist, (size_t)gd.nch * ls * 4)) return rc;
+        if (int rc = ensure(chunk_pa, (size_t)gd.nch * 4)) return rc;
+        gd.cpa = (int32_t*)chunk_pa.p;
         if (any_fresh)
             hipLaunchKernelGGL(k_group_prep, dim3((gd.n_panes + 255) / 256), dim3(256), 0, stream, gd, perr, pmc, pmh);
         const bool wh = dp.n_where > 0;
@@ -1197,7 +1199,7 @@ struct Engine {
     int64_t sess_trigger = 0;
     int64_t count_k = 1;               // COUNTWINDOW: next window index
     DevBuf rq_d, ab_d, slot_d, trig_d, flags_d, cnts_d, runmax_d, runcm_d, mrg_keys[2], mrg_src[2], mrg_tmp, mrg_tail,
-        mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh, sort_pbase, sort_scr;
+        mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh, sort_pbase, sort_scr, chunk_pa;
     std::vector<int64_t> h_ab;
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
@@ -2071,7 +2073,7 @@ struct Engine {
             release(e->rel);
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
-                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr})
+                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa})
             release(*d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);

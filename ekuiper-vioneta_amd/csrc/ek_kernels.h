@@ -247,6 +247,7 @@ struct GroupDesc {
     const int32_t* didx;   // direct emission: window index of pane r
     const uint8_t* fresh;  // 1: pane r was claimed for this group (its partials are written, not merged)
     const int64_t* voff;   // range mode (virtual panes): physical row of virtual row v in pane r = v + voff[r]
+    int32_t* cpa;          // first pane (group-relative) of every chunk, written by k_part for k_agg
 };
 
 constexpr int kMaxGroupPanes = 64;
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     __shared__ int64_t loff[kMaxChunkBnd + 1];
     __shared__ uint32_t wsum[4];
     const int nlb = chunk_bounds(gd, pa, pb, lb);
+    if (threadIdx.x == 0) gd.cpa[blockIdx.x] = pa;
     if (MODE == 2)
         for (int k = threadIdx.x; k <= pb - pa; k += kBlock) loff[k] = gd.voff[pa + k];
     const int lpp = (lp_n + 4 + 3) & ~3;
@@ -750,14 +752,14 @@ __device__ __forceinline__ void part_chunks(const GroupDesc& gd, int rel, int* c
         else { *c_lo = (int)((e0 - gd.abase) / gd.chunk); *c_hi = (int)((e1 - 1 - gd.abase) / gd.chunk); }
     }
 }
+// (k_part wrote the chunk's first pane pa into cpa[c]; ctab rows are padded with the chunk total past its
+// last local partition, so a pane beyond the chunk's last one reads an empty run)
 __device__ __forceinline__ void part_run(const GroupDesc& gd, const uint32_t* ctab, int ls, int rel, int bucket, int c,
                                          uint32_t* o0, uint32_t* o1) {
-    const int64_t a0 = gd.abase + (int64_t)c * gd.chunk;
-    int pa, pb;
-    chunk_panes(gd, max(gd.lo, a0), min(gd.hi, a0 + gd.chunk), &pa, &pb);
+    const int pa = gd.cpa[c];
     const int lp = (rel - pa) * gd.nb + bucket;
     *o0 = *o1 = 0;
-    if (rel >= pa && rel <= pb) { *o0 = ctab[(int64_t)c * ls + lp]; *o1 = ctab[(int64_t)c * ls + lp + 1]; }
+    if (rel >= pa && lp + 1 < ls) { *o0 = ctab[(int64_t)c * ls + lp]; *o1 = ctab[(int64_t)c * ls + lp + 1]; }
 }
 
 // Rows per partition (sort aggregates: the key-grouped scratch region of each partition), one thread each.
@@ -928,13 +930,14 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}.
     // Each wave takes a span of 64*U consecutive rows (coalesced loads); its first run is found by
     // one binary search, and every lane then advances its run pointer monotonically.
-    constexpr int U = 4;   // rows in flight per lane
+    constexpr int U = 8;   // rows in flight per lane
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto run_of = [&](uint32_t v) {
         int lo = 0, hi = nruns - 1;
         while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= v) lo = m; else hi = m - 1; }
         return lo;
     };
+    int64_t dbg_sink = 0;
     for (uint32_t span = (uint32_t)wave * 64u * U; span < total; span += (uint32_t)kAggBlock * U) {
         int j = run_of(span);
         int64_t pos[U];
@@ -958,6 +961,11 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
                 rv[v][u] = (pos[u] >= 0 && fl[v]) ? st.val[v][pos[u]] : 0;
                 vd[v][u] = (pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
             }
+        }
+        if (gd.pad & 32) {   // diagnostic knob 32: loads only, no LDS atomics (timing only)
+#pragma unroll
+            for (int u = 0; u < U; ++u) { dbg_sink += klu[u]; for (int v = 0; v < NVC; ++v) dbg_sink += rv[v][u]; }
+            continue;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -984,6 +992,7 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
             }
         }
     }
+    if ((gd.pad & 32) && dbg_sink == 0x5A5A5A5A5A5ALL) lcnt[0] = 1;   // keeps the knob-32 loads alive
     __syncthreads();
     bool need_m2 = false;
 #pragma unroll
