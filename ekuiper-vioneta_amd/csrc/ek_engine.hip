@@ -1040,7 +1040,7 @@ struct Engine {
             uint32_t* ct = (uint32_t*)chist.p;
             dim3 gp(gd.nch);
             const int ph = phase_begin(EK_PHASE_PARTITION);
-#define EK_PART(M, W, N) hipLaunchKernelGGL((k_part<M, W, N>), gp, dim3(kBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, perr)
+#define EK_PART(M, W, N) hipLaunchKernelGGL((k_part<M, W, N>), gp, dim3(kPartBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, perr)
 #define EK_PART_N(M, W) switch (nvc) { case 1: EK_PART(M, W, 1); break; case 2: EK_PART(M, W, 2); break; \
                                        case 3: EK_PART(M, W, 3); break; default: EK_PART(M, W, 4); break; }
 #define EK_PART_W(M) if (wh) { EK_PART_N(M, true) } else { EK_PART_N(M, false) }

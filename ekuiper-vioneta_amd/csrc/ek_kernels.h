@@ -251,8 +251,9 @@ struct GroupDesc {
 };
 
 constexpr int kMaxGroupPanes = 64;
-constexpr int kTile = 2048;                  // events staged and sorted in LDS per step of k_scatter
-constexpr int kTileE = kTile / kBlock;       // events per thread per tile
+constexpr int kPartBlock = 512;              // k_part workgroup (8 wave64s)
+constexpr int kTile = 4096;                  // events staged and sorted in LDS per k_part tile
+constexpr int kTileE = kTile / kPartBlock;   // events per thread per tile
 constexpr int kMaxLocalParts = 2048;         // chunk-local partitions sorted through LDS
 
 __device__ __forceinline__ void chunk_range(const GroupDesc& gd, int64_t* a0, int64_t* c0, int64_t* c1) {
@@ -330,9 +331,10 @@ struct Staging {
     uint32_t nullable_mask;   // bit v: staging carries validity for value column v
 };
 
-// Block-wide exclusive scan of cnt[0..n) in LDS; cnt[n] receives the total.
+// Block-wide exclusive scan of cnt[0..n) in LDS; cnt[n] receives the total (B threads, wsum[B / 64]).
+template <int B>
 __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
-    const int per = (n + kBlock - 1) / kBlock;
+    const int per = (n + B - 1) / B;
     const int b = threadIdx.x * per, e = min(n, b + per);
     uint32_t s = 0;
     for (int k = b; k < e; ++k) s += cnt[k];
@@ -348,15 +350,16 @@ __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
     for (int w = 0; w < wv; ++w) wbase += wsum[w];
     uint32_t run = wbase + x - s;
     for (int k = b; k < e; ++k) { uint32_t c = cnt[k]; cnt[k] = run; run += c; }
-    if (threadIdx.x == kBlock - 1) cnt[n] = run;
+    if (threadIdx.x == B - 1) cnt[n] = run;
     __syncthreads();
 }
 
 // LDS bytes of k_part for `nvc` value columns and `lp` chunk-local partitions
 // (single-tile chunks need no per-row partition array: their runs come straight from the tile sort)
+// (value columns are staged through LDS one at a time, so the footprint does not grow with their number)
 inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
     size_t lpp = ((size_t)lp + 4 + 3) & ~(size_t)3;
-    return (size_t)nvc * kTile * 8 + 2 * lpp * 4 + (size_t)kTile * (single_tile ? 2 : 4) + (nullable ? (size_t)nvc * kTile : 0);
+    return (size_t)kTile * 8 + 2 * lpp * 4 + (size_t)kTile * (single_tile ? 2 : 4) + (nullable ? (size_t)kTile : 0);
 }
 
 // One workgroup per chunk: partition the chunk's rows by (pane, key bucket) into the chunk's OWN
@@ -370,7 +373,7 @@ inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
 // 2: virtual panes (range mode): the group's rows are the concatenation of possibly overlapping
 //    index ranges of the event buffer, virtual row v of pane r lives at physical row v + voff[r].
 template <int MODE, bool WHERE, int NVC>
-__global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
+__global__ __launch_bounds__(kPartBlock) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
                                                  const uint8_t* __restrict__ acc, Staging st, uint32_t* __restrict__ ctab,
                                                  int ls, int64_t rs, int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -382,30 +385,30 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     const int lp_n = (pb - pa + 1) * gd.nb;
     __shared__ int64_t lb[kMaxChunkBnd];
     __shared__ int64_t loff[kMaxChunkBnd + 1];
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[kPartBlock / 64];
     const int nlb = chunk_bounds(gd, pa, pb, lb);
     if (threadIdx.x == 0) gd.cpa[blockIdx.x] = pa;
     if (MODE == 2)
-        for (int k = threadIdx.x; k <= pb - pa; k += kBlock) loff[k] = gd.voff[pa + k];
+        for (int k = threadIdx.x; k <= pb - pa; k += kPartBlock) loff[k] = gd.voff[pa + k];
     const int lpp = (lp_n + 4 + 3) & ~3;
-    int64_t* s_val = (int64_t*)smem;                                          // [NVC][kTile]
-    uint32_t* cur = (uint32_t*)(smem + (size_t)NVC * kTile * 8);              // [lpp]
+    int64_t* s_val = (int64_t*)smem;                                          // [kTile] one value column at a time
+    uint32_t* cur = (uint32_t*)(smem + (size_t)kTile * 8);                    // [lpp]
     uint32_t* tcnt = cur + lpp;                                               // [lpp]
     const bool single = gd.chunk <= kTile;
     uint16_t* s_klo = (uint16_t*)(tcnt + lpp);                                // [kTile]
     uint16_t* s_lp = s_klo + kTile;                                           // [kTile] (multi-tile chunks)
-    uint8_t* s_vd = (uint8_t*)(s_klo + (single ? 1 : 2) * kTile);             // [NVC][kTile]
+    uint8_t* s_vd = (uint8_t*)(s_klo + (single ? 1 : 2) * kTile);             // [kTile] validity of that column
     const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
     const int64_t region = (int64_t)blockIdx.x * rs;
 
     // ---- (1) count
-    for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
+    for (int k = threadIdx.x; k <= lp_n; k += kPartBlock) tcnt[k] = 0;
     __syncthreads();
     if (single) {
         // runs come from the tile sort below
     } else if (MODE == 2) {
         // physical rows are contiguous only inside one pane: scalar (still coalesced) key loads
-        for (int64_t v = c0 + threadIdx.x; v < c1; v += kBlock) {
+        for (int64_t v = c0 + threadIdx.x; v < c1; v += kPartBlock) {
             const int rel = chunk_rel(lb, nlb, pa, v);
             const int64_t i = v + loff[rel - pa];
             const uint32_t key = kcol ? kcol[i] : 0u;
@@ -414,11 +417,11 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
         }
     } else if (!(gd.pad & 4)) {   // (diagnostic knob 4: skip the count pass; timing only)
         constexpr int V = 4;   // 16-byte key loads in flight per thread
-        for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kBlock * 4 * V) {
+        for (int64_t base = a0 + (int64_t)threadIdx.x * 4; base < c1; base += (int64_t)kPartBlock * 4 * V) {
             uint4 kv[V];
 #pragma unroll
             for (int u = 0; u < V; ++u) {
-                const int64_t i = base + (int64_t)u * kBlock * 4;
+                const int64_t i = base + (int64_t)u * kPartBlock * 4;
                 if (kcol && i + 3 < gd.nbatch && i < c1) kv[u] = *(const uint4*)(kcol + i);
                 else if (kcol && i < c1) {
                     kv[u].x = kcol[i];
@@ -432,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
                 const uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int64_t i = base + (int64_t)u * kBlock * 4 + e;
+                    const int64_t i = base + (int64_t)u * kPartBlock * 4 + e;
                     if (i < c0 || i >= c1) continue;
                     const int rel = MODE == 1 ? chunk_rel(lb, nlb, pa, i) : 0;
                     const int lp = local_part<MODE, WHERE>(p, b, g, gd, rel, acc, i, pa, kk[e], pane_err, true);
@@ -444,14 +447,13 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
     __syncthreads();
     // ---- (2) run offsets of this chunk
     if (!single) {
-        block_excl_scan(tcnt, lp_n, wsum);
-        for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
-        for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] = tcnt[k];
+        block_excl_scan<kPartBlock>(tcnt, lp_n, wsum);
+        for (int k = threadIdx.x; k < ls; k += kPartBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
+        for (int k = threadIdx.x; k < lp_n; k += kPartBlock) cur[k] = tcnt[k];
         __syncthreads();
     }
     // ---- (3) tiles: load, LDS counting sort, coalesced run writes
     const uint32_t kmask = (1u << gd.kbits) - 1u;
-    const bool nullable = st.nullable_mask != 0;
     if (gd.pad & 16) return;   // diagnostic knob 16: count pass only
     for (int64_t t0 = a0; t0 < c1; t0 += kTile) {
         uint32_t key[kTileE];
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
         if (MODE == 2) {
 #pragma unroll
             for (int j = 0; j < kTileE; ++j) {
-                const int64_t v = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+                const int64_t v = t0 + (int64_t)(j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
                 rel[j] = 0;
                 phys[j] = -1;
                 if (v >= c0 && v < c1) {
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
         } else {
 #pragma unroll
             for (int m = 0; m < kTileE / 2; ++m) {
-                const int64_t i = t0 + (int64_t)m * 2 * kBlock + 2 * threadIdx.x;
+                const int64_t i = t0 + (int64_t)m * 2 * kPartBlock + 2 * threadIdx.x;
                 const bool full = i + 1 < gd.nbatch && i < c1;
                 if (full) {
                     uint2 kp = kcol ? *(const uint2*)(kcol + i) : make_uint2(0, 0);
@@ -499,13 +501,13 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
                 }
             }
         }
-        for (int k = threadIdx.x; k <= lp_n; k += kBlock) tcnt[k] = 0;
+        for (int k = threadIdx.x; k <= lp_n; k += kPartBlock) tcnt[k] = 0;
         __syncthreads();
         int lp[kTileE];
         uint32_t rank[kTileE];
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
-            const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
+            const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
             // (single-tile chunks flag WHERE errors here: there was no count pass)
             if (MODE == 2) {
                 lp[j] = phys[j] >= 0 ? local_part<MODE, WHERE>(p, b, g, gd, rel[j], acc, phys[j], pa, key[j], pane_err, single) : -1;
@@ -516,43 +518,50 @@ __global__ __launch_bounds__(kBlock) void k_part(DPlan* __restrict__ pp, DBatch 
             if (lp[j] >= 0) rank[j] = atomicAdd(&tcnt[lp[j]], 1u);
         }
         __syncthreads();
-        block_excl_scan(tcnt, lp_n, wsum);
+        block_excl_scan<kPartBlock>(tcnt, lp_n, wsum);
         if (single)
-            for (int k = threadIdx.x; k < ls; k += kBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
+            for (int k = threadIdx.x; k < ls; k += kPartBlock) ctab[(int64_t)blockIdx.x * ls + k] = k <= lp_n ? tcnt[k] : tcnt[lp_n];
+        uint32_t spos[kTileE];   // sorted position of each element (its partition run + rank)
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
             if (lp[j] < 0) continue;
-            const uint32_t s = tcnt[lp[j]] + rank[j];
-            s_klo[s] = (uint16_t)(key[j] & kmask);
-            if (!single) s_lp[s] = (uint16_t)lp[j];
-#pragma unroll
-            for (int v = 0; v < NVC; ++v) s_val[v * kTile + s] = val[v][j];
-            if (nullable) {
-                const int64_t i = MODE == 2 ? phys[j] : t0 + (int64_t)(j >> 1) * 2 * kBlock + 2 * threadIdx.x + (j & 1);
-#pragma unroll
-                for (int v = 0; v < NVC; ++v)
-                    if (st.nullable_mask & (1u << v)) s_vd[v * kTile + s] = col_valid(b, p.vc_col[v], i) ? 1 : 0;
-            }
+            spos[j] = tcnt[lp[j]] + rank[j];
+            s_klo[spos[j]] = (uint16_t)(key[j] & kmask);
+            if (!single) s_lp[spos[j]] = (uint16_t)lp[j];
         }
         __syncthreads();
         const uint32_t total = (gd.pad & 8) ? 0u : tcnt[lp_n];   // diagnostic knob 8: no global stores
-        for (uint32_t s = threadIdx.x; s < total; s += kBlock) {
-            int64_t gpos = region + s;
-            if (!single) {
-                const int l = s_lp[s];
-                gpos = region + cur[l] + (s - tcnt[l]);
-            }
-            st.klo[gpos] = s_klo[s];
+        auto gpos_of = [&](uint32_t s) -> int64_t {
+            if (single) return region + s;
+            const int l = s_lp[s];
+            return region + cur[l] + (s - tcnt[l]);
+        };
+        for (uint32_t s = threadIdx.x; s < total; s += kPartBlock) st.klo[gpos_of(s)] = s_klo[s];
+        // value columns: one LDS staging buffer, reused column by column
 #pragma unroll
-            for (int v = 0; v < NVC; ++v) {
-                if (v >= p.n_vc) break;
-                st.val[v][gpos] = s_val[v * kTile + s];
-                if (st.nullable_mask & (1u << v)) st.valid[v][gpos] = s_vd[v * kTile + s];
+        for (int v = 0; v < NVC; ++v) {
+            if (v >= p.n_vc) break;
+            const bool vnull = (st.nullable_mask >> v) & 1u;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kTileE; ++j) {
+                if (lp[j] < 0) continue;
+                s_val[spos[j]] = val[v][j];
+                if (vnull) {
+                    const int64_t i = MODE == 2 ? phys[j] : t0 + (int64_t)(j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
+                    s_vd[spos[j]] = col_valid(b, p.vc_col[v], i) ? 1 : 0;
+                }
+            }
+            __syncthreads();
+            for (uint32_t s = threadIdx.x; s < total; s += kPartBlock) {
+                const int64_t gp = gpos_of(s);
+                st.val[v][gp] = s_val[s];
+                if (vnull) st.valid[v][gp] = s_vd[s];
             }
         }
         if (single) break;
         __syncthreads();
-        for (int k = threadIdx.x; k < lp_n; k += kBlock) cur[k] += tcnt[k + 1] - tcnt[k];
+        for (int k = threadIdx.x; k < lp_n; k += kPartBlock) cur[k] += tcnt[k + 1] - tcnt[k];
         __syncthreads();
     }
 }
