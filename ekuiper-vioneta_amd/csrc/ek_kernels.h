@@ -373,7 +373,7 @@ inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
 // 2: virtual panes (range mode): the group's rows are the concatenation of possibly overlapping
 //    index ranges of the event buffer, virtual row v of pane r lives at physical row v + voff[r].
 template <int MODE, bool WHERE, int NVC>
-__global__ __launch_bounds__(kPartBlock) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
+__global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_PART_WAVES_PER_EU))) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
                                                  const uint8_t* __restrict__ acc, Staging st, uint32_t* __restrict__ ctab,
                                                  int ls, int64_t rs, int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -878,7 +878,7 @@ __device__ __forceinline__ void order_stat(int fn, bool isf, double param, int64
 constexpr int kSmallSeg = 32;   // segments up to this length are selected by one thread
 
 template <int NVC, bool SORT>
-__global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
+__global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AGG_WAVES_PER_EU))) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
                                                    Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err,
                                                    const int64_t* __restrict__ pbase, uint64_t* __restrict__ scratch,
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(kAggBlock) void k_agg(DPlan* __restrict__ pp, Group
     // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}.
     // Each wave takes a span of 64*U consecutive rows (coalesced loads); its first run is found by
     // one binary search, and every lane then advances its run pointer monotonically.
-    constexpr int U = 8;   // rows in flight per lane
+    constexpr int U = EK_AGG_U;   // rows in flight per lane
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto run_of = [&](uint32_t v) {
         int lo = 0, hi = nruns - 1;

@@ -12,7 +12,7 @@ from . import abi as A
 from .results import result_to_python
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libekgpu.so")
+LIB_PATH = os.environ.get("EKGPU_LIB") or os.path.join(HERE, "libekgpu.so")   # EKGPU_LIB: tuning builds
 
 _lib = None
 
