@@ -472,7 +472,8 @@ struct Engine {
         chunk = env_int("EKGPU_CHUNK", 8192);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
-        np_max = env_int("EKGPU_NP_MAX", 8192);
+        // chunk-local partitions k_part can sort through LDS: 8 B each next to the 4096-row staging (~13 K)
+        np_max = env_int("EKGPU_NP_MAX", 13000);
         max_panes_group = env_int("EKGPU_MAX_GROUP_PANES", 4096);
         ring = (int)(2 * ppw + 16);
 

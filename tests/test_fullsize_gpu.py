@@ -1,0 +1,140 @@
+"""BASELINE.json configs at their full per-GPU sizes on the device, checked through size-independent
+properties (the oracle cannot replay 1e7-1e8 events in test time). Each test prints its device time.
+
+  C3  HOPPINGWINDOW(ss,60,5) sum/min/max, 2e8 events / 1M keys over 8 GPUs -> one shard: 2.5e7 events, 131072 keys
+  C4a SLIDINGWINDOW(ss,30) OVER (WHEN trig = 1) stddev/var HAVING count(*) > 1: 1e7 events, 1M keys
+  C4b COUNTWINDOW(1000) stddev/var HAVING count(*) > 1 (processing time): 1e7 events of the 1e8 stream, 1M keys
+  C5  median + percentile_cont, 1e9 events / 100M keys over 8 GPUs -> one shard: 1.25e8 events, 12.5M keys
+"""
+import time
+
+import numpy as np
+import pytest
+
+from ekgpu import abi as A
+from ekgpu.rule import compile_rule
+from ekgpu.synth import IOT_SCHEMA
+from test_engine_gpu import engine_mod  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+T0 = 1541152480000
+
+
+def _stream(n, keys, epm, seed=91, t0=T0):
+    import torch
+    from bench import make_device_stream
+    cols = make_device_stream(n, keys, torch.device("cuda:0"), seed=seed, events_per_ms=epm, t0=t0)
+    torch.cuda.synchronize()
+    return cols
+
+
+def _push_time(eng, n, cols):
+    import torch
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    eng.push_device(n, [c.data_ptr() for c in cols])
+    dt = time.perf_counter() - t
+    return dt
+
+
+def test_c3_hopping_full_shard(engine_mod):
+    n, keys, epm = 25_000_000, 131072, 42           # 2e8 events / 8 shards over ~600 s
+    sql = ("SELECT deviceId, sum(temperature), min(temperature), max(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, HOPPINGWINDOW(ss, 60, 5)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys)
+    cols = _stream(n, keys, epm)
+    eng = engine_mod.Engine(rule.plan)
+    dt = _push_time(eng, n, cols)
+    wins = eng.poll()
+    st = eng.stats()
+    eng.close()
+    print(f"\nC3 shard: {n} events, {len(wins)} windows, {sum(len(w.keys) for w in wins)} rows, "
+          f"push {dt * 1e3:.1f} ms (device {st.last_batch_device_ms:.1f} ms) -> {n / dt / 1e9:.2f} G events/s")
+    last_ts = T0 + (n - 1) // epm
+    assert len(wins) >= 100
+    for k, w in enumerate(wins):
+        assert w.status == 0 and w.end <= last_ts
+        assert len(np.unique(w.keys)) == len(w.keys)
+        cnt = w.values[3]
+        lo, hi = max(w.end - 60_000, T0), w.end                   # events with ts in [end - 60 s, end)
+        assert cnt.sum() == (min(hi - T0, n // epm) - (lo - T0)) * epm
+        mn, mx = w.values[1].view(np.float64), w.values[2].view(np.float64)
+        assert (mn <= mx).all() and (mn >= 0).all() and (mx < 100).all()
+        s = w.values[0].view(np.float64)
+        assert (s >= mn * cnt - 1e-6).all() and (s <= mx * cnt + 1e-6).all()
+
+
+def test_c4a_sliding_full(engine_mod):
+    import torch
+    n, keys, epm = 10_000_000, 1_000_000, 10
+    schema = dict(IOT_SCHEMA, trig="bigint")
+    sql = ("SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 30) OVER (WHEN trig = 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, schema, num_keys=keys)
+    cols = _stream(n, keys, epm, seed=92)
+    i = torch.arange(n, device="cuda:0", dtype=torch.int64)
+    trig = (((i * 0x9E3779B1) >> 7) % 10_000 == 0).to(torch.int64)   # 1 in 1e4 events
+    n_trig = int(trig.sum())
+    eng = engine_mod.Engine(rule.plan)
+    dt = _push_time(eng, n, cols + [trig])
+    wins = eng.poll()
+    eng.close()
+    rows = sum(len(w.keys) for w in wins)
+    print(f"\nC4a: {n} events, {len(wins)} windows, {rows} rows, push {dt * 1e3:.1f} ms -> {n / dt / 1e6:.1f} M events/s")
+    assert n_trig - 1 <= len(wins) <= n_trig    # the last trigger may still be unreleased
+    for w in wins:
+        assert w.status == 0 and w.end - w.start == 30_000
+        cnt = w.values[2]
+        assert (cnt > 1).all()
+        sd, var = w.values[0].view(np.float64), w.values[1].view(np.float64)
+        assert (var >= 0).all() and np.allclose(sd * sd, var, rtol=1e-9, atol=1e-9)
+
+
+def test_c4b_count_window_full(engine_mod):
+    n, keys = 10_000_000, 1_000_000
+    sql = ("SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys, is_event_time=False)
+    cols = _stream(n, keys, 100, seed=93)
+    eng = engine_mod.Engine(rule.plan)
+    dt = _push_time(eng, n, cols)
+    wins = eng.poll()
+    eng.close()
+    rows = sum(len(w.keys) for w in wins)
+    print(f"\nC4b: {n} events, {len(wins)} windows, {rows} rows, push {dt * 1e3:.1f} ms -> {n / dt / 1e6:.1f} M events/s")
+    assert len(wins) == n // 1000
+    assert all(w.status == 0 and (w.values[2] > 1).all() for w in wins)
+    # keys repeated inside a 1000-event window over 1M keys: ~0.05 % of pairs
+    assert 0 < rows < 10 * len(wins)
+
+
+def test_c5_median_full_shard(engine_mod):
+    import torch
+    n, keys = 125_000_000, 12_500_000
+    t_min = 1541152440000                     # minute boundary: one 60 s tumbling window
+    sql = ("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
+           "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys)
+    cols = _stream(n, keys, 2084, seed=94, t0=t_min)   # 1.25e8 events inside [t_min, t_min + 60 s)
+    eng = engine_mod.Engine(rule.plan)
+    dt = _push_time(eng, n, cols)
+    sentinel = [torch.tensor([0], dtype=torch.int32, device="cuda:0"),
+                torch.tensor([t_min + 60_000], dtype=torch.int64, device="cuda:0"),
+                torch.tensor([50.0], dtype=torch.float64, device="cuda:0"),
+                torch.tensor([50.0], dtype=torch.float64, device="cuda:0")]
+    dt2 = _push_time(eng, 1, sentinel)
+    wins = eng.poll()
+    eng.close()
+    print(f"\nC5 shard: {n} events, {len(wins[0].keys) if wins else 0} groups, ingest {dt * 1e3:.1f} ms + "
+          f"window close {dt2 * 1e3:.1f} ms -> {n / (dt + dt2) / 1e6:.1f} M events/s")
+    assert len(wins) == 1 and wins[0].status == 0
+    w = wins[0]
+    assert len(np.unique(w.keys)) == len(w.keys) > 0.99 * keys
+    med = w.values[0]
+    tags = w.tags[0]
+    assert set(np.unique(tags)) <= {A.EK_TAG_F64}
+    med = med.view(np.float64)
+    p90 = w.values[1].view(np.float64)
+    assert (med >= 0).all() and (med < 100).all() and (p90 >= 0).all() and (p90 < 100).all()
+    # percentile_cont(0.9) of a group is never below its median except for the n <= 2 interpolation rules
+    assert (p90 >= med).mean() > 0.95
