@@ -467,7 +467,8 @@ struct Engine {
                 lay.off_kcur = o; o += 4 * kk;
                 lay.off_stag = o; o += dp.n_sagg * kk;
             }
-            lay.bytes = (o + 15) & ~15;
+            // the sparse-partition path of k_agg stages its rows in the same LDS
+            lay.bytes = (int32_t)std::max<size_t>((size_t)((o + 15) & ~15), (sparse_lds_bytes(dp.n_vc) + 15) & ~(size_t)15);
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg

@@ -877,6 +877,89 @@ __device__ __forceinline__ void order_stat(int fn, bool isf, double param, int64
 
 constexpr int kSmallSeg = 32;   // segments up to this length are selected by one thread
 
+// ---------------------------------------------------------------- sparse partitions
+// A directly emitted partition with at most kSparseRows rows (windows much smaller than the key space, e.g. a
+// 1000-event COUNTWINDOW over 1 M keys spreads ~2 rows over each 2048-key bucket): instead of zeroing and
+// scanning the dense 2^kbits-key LDS table, the rows are staged in LDS, the first row of every key leads its
+// group, and the leader folds the group's rows in staging order (exact two-pass M2 per group).
+constexpr int kSparseRows = kAggBlock;
+inline size_t sparse_lds_bytes(int nvc) { return (size_t)kSparseRows * (4 + 9 * (size_t)(nvc > 0 ? nvc : 1)); }
+
+template <int NVC>
+__device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Staging& st, unsigned char* lds,
+                                  const uint32_t* r_start, const uint32_t* r_pre, int nruns, uint32_t total, int bucket,
+                                  int kk, int64_t slot, int rel, int64_t dbase, const int32_t* pane_err, Results& res) {
+    uint32_t* s_klo = (uint32_t*)lds;                                  // [kSparseRows]
+    int64_t* s_val = (int64_t*)(lds + kSparseRows * 4);                // [NVC][kSparseRows]
+    uint8_t* s_vd = (uint8_t*)(s_val + (size_t)NVC * kSparseRows);     // [NVC][kSparseRows]
+    const int t = threadIdx.x;
+    if ((uint32_t)t < total) {
+        int lo = 0, hi = nruns - 1;
+        while (lo < hi) { int m = (lo + hi + 1) >> 1; if (r_pre[m] <= (uint32_t)t) lo = m; else hi = m - 1; }
+        const int64_t i = (int64_t)r_start[lo] + ((uint32_t)t - r_pre[lo]);
+        s_klo[t] = st.klo[i];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            s_val[v * kSparseRows + t] = v < p.n_vc ? st.val[v][i] : 0;
+            s_vd[v * kSparseRows + t] = (v < p.n_vc && ((st.nullable_mask >> v) & 1u)) ? st.valid[v][i] : (uint8_t)1;
+        }
+    }
+    __syncthreads();
+    const int32_t widx = gd.didx[rel];
+    const int32_t perr = pane_err[slot];
+    if (perr) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
+        if (t == 0 && bucket == 0) atomicOr(&res.win_err[widx], perr);
+        return;
+    }
+    Part<NVC> s{};
+    bool present = false;
+    uint32_t kl = 0;
+    if ((uint32_t)t < total) {
+        kl = s_klo[t];
+        bool leader = true;
+        for (int u = 0; u < t && leader; ++u) leader = s_klo[u] != kl;
+        if (leader) {
+            int64_t c = 0, vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
+            for (uint32_t u = t; u < total; ++u) {
+                if (s_klo[u] != kl) continue;
+                c++;
+#pragma unroll
+                for (int v = 0; v < NVC; ++v) {
+                    if (v >= p.n_vc || !s_vd[v * kSparseRows + u]) continue;
+                    const int64_t raw = s_val[v * kSparseRows + u];
+                    const bool fl = p.vc_is_float[v];
+                    const double x = fl ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = fl ? f64_to_ord(x) : i64_to_ord(raw);
+                    vc[v]++;
+                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+                    fs[v] = __dadd_rn(fs[v], x);
+                    mn[v] = o < mn[v] ? o : mn[v];
+                    mx[v] = o > mx[v] ? o : mx[v];
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {   // centred second pass (stats._variance shape)
+                if (v >= p.n_vc || !(p.vc_flags[v] & NEED_M2) || vc[v] == 0) continue;
+                const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+                for (uint32_t u = t; u < total; ++u) {
+                    if (s_klo[u] != kl || !s_vd[v * kSparseRows + u]) continue;
+                    const int64_t raw = s_val[v * kSparseRows + u];
+                    const double d = __dsub_rn(p.vc_is_float[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                    m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
+                }
+            }
+            part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+            present = having_keep(p, s, &res.win_err[widx]);
+        }
+    }
+    __shared__ uint32_t esh[20];
+    emit_rows(p, present, s, (int64_t)bucket * kk + kl, dbase, widx, res, esh);
+}
+
 template <int NVC, bool SORT>
 __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AGG_WAVES_PER_EU))) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
@@ -926,6 +1009,10 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
     }
     const uint32_t total = nruns > 0 ? r_pre[nruns] : 0u;
     if (total == 0 && (!fresh || dbase >= 0)) return;   // nothing to merge / no rows to emit
+    if (!SORT && dbase >= 0 && total <= (uint32_t)kSparseRows) {
+        agg_sparse<NVC>(p, gd, st, lds, r_start, r_pre, nruns, total, bucket, kk, slot, rel, dbase, pane_err, res);
+        return;
+    }
 
     uint32_t* lcnt = (uint32_t*)(lds + lay.off_cnt);
     for (int k = threadIdx.x; k < lay.bytes / 4; k += kAggBlock) ((uint32_t*)lds)[k] = 0;
