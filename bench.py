@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events", type=int, default=N_EVENTS)
-    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", 50_000_000)))
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", N_EVENTS)))
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
