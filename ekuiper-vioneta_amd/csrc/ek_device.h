@@ -146,44 +146,68 @@ __device__ inline Val simple_eval(Val l, Val r, int op) {
     }
 }
 
-// Postfix program over one row (aggs != nullptr for HAVING). Mirrors evalBinaryExpr's
-// short-circuit: a decided lhs of AND/OR wins over an error on the rhs.
-__device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, const DBatch* b, int64_t row,
-                                const Val* aggs) {
-    Val st[16];
-    int sp = 0;
-    for (int k = 0; k < n; ++k) {
-        const ek_instr in = prog[k];
-        if (in.op == EK_OP_COL) {
-            int c = in.arg;
-            Val v{V_NULL, 0, 0.0};
-            if (b && col_valid(*b, c, row)) {
-                if (p.col_type[c] == EK_COL_F64) v = Val{V_F64, 0, col_f64(*b, c, row)};
-                else v = Val{V_I64, col_i64(p, *b, c, row), 0.0};
-            }
-            st[sp++] = v;
-        } else if (in.op == EK_OP_AGG) {
-            st[sp++] = aggs ? aggs[in.arg] : Val{V_NULL, 0, 0.0};
-        } else if (in.op == EK_OP_CONST_I64) {
-            st[sp++] = Val{V_I64, in.i64, 0.0};
-        } else if (in.op == EK_OP_CONST_F64) {
-            st[sp++] = Val{V_F64, 0, in.f64};
-        } else {
-            Val r = st[--sp], l = st[--sp], res;
-            if (l.tag == V_ERR) res = l;
-            else if (in.op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mkb(false);
-            else if (in.op == EK_OP_OR && l.tag == V_BOOL && l.i) res = mkb(true);
-            else if (r.tag == V_ERR) res = r;
-            else res = simple_eval(l, r, in.op);
-            st[sp++] = res;
+// Register-resident evaluation stack: kEvalDepth slots addressed through switches, so the interpreter never
+// touches per-lane scratch memory (a dynamically indexed array would live there). ek_create rejects deeper
+// programs.
+constexpr int kEvalDepth = 8;
+struct EvalStack {
+    Val s0, s1, s2, s3, s4, s5, s6, s7;
+    __device__ __forceinline__ Val get(int i) const {
+        switch (i) {
+        case 0: return s0; case 1: return s1; case 2: return s2; case 3: return s3;
+        case 4: return s4; case 5: return s5; case 6: return s6; default: return s7;
         }
     }
-    return sp ? st[sp - 1] : Val{V_NULL, 0, 0.0};
+    __device__ __forceinline__ void set(int i, Val v) {
+        switch (i) {
+        case 0: s0 = v; break; case 1: s1 = v; break; case 2: s2 = v; break; case 3: s3 = v; break;
+        case 4: s4 = v; break; case 5: s5 = v; break; case 6: s6 = v; break; default: s7 = v; break;
+        }
+    }
+};
+
+// Postfix program over one row; aggf(k) yields aggregate slot k (HAVING). Mirrors evalBinaryExpr's
+// short-circuit: a decided lhs of AND/OR wins over an error on the rhs.
+template <typename AGGF>
+__device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, const DBatch* b, int64_t row, AGGF aggf) {
+    EvalStack st;
+    int sp = 0;
+    for (int k = 0; k < n; ++k) {
+        const int op = prog[k].op;
+        const int arg = prog[k].arg;
+        if (op == EK_OP_COL) {
+            Val v{V_NULL, 0, 0.0};
+            if (b && col_valid(*b, arg, row)) {
+                if (p.col_type[arg] == EK_COL_F64) v = Val{V_F64, 0, col_f64(*b, arg, row)};
+                else v = Val{V_I64, col_i64(p, *b, arg, row), 0.0};
+            }
+            st.set(sp++, v);
+        } else if (op == EK_OP_AGG) {
+            st.set(sp++, aggf(arg));
+        } else if (op == EK_OP_CONST_I64) {
+            st.set(sp++, Val{V_I64, prog[k].i64, 0.0});
+        } else if (op == EK_OP_CONST_F64) {
+            st.set(sp++, Val{V_F64, 0, prog[k].f64});
+        } else {
+            const Val r = st.get(--sp), l = st.get(--sp);
+            Val res;
+            if (l.tag == V_ERR) res = l;
+            else if (op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mkb(false);
+            else if (op == EK_OP_OR && l.tag == V_BOOL && l.i) res = mkb(true);
+            else if (r.tag == V_ERR) res = r;
+            else res = simple_eval(l, r, op);
+            st.set(sp++, res);
+        }
+    }
+    return sp ? st.get(sp - 1) : Val{V_NULL, 0, 0.0};
 }
+struct NoAggs {
+    __device__ __forceinline__ Val operator()(int) const { return Val{V_NULL, 0, 0.0}; }
+};
 
 // WHERE decision: 1 keep, 0 drop, -1 error (filter_operator.go:63-77: nil -> drop, non-bool -> error)
 __device__ inline int where_decide_slow(const DPlan& p, const DBatch& b, int64_t row) {
-    Val v = eval_prog(p.where_prog, p.n_where, p, &b, row, nullptr);
+    Val v = eval_prog(p.where_prog, p.n_where, p, &b, row, NoAggs{});
     if (v.tag == V_BOOL) return v.i ? 1 : 0;
     if (v.tag == V_NULL) return 0;
     return -1;

@@ -134,7 +134,7 @@ int prog_depth_ok(const ek_instr* prog, int n) {
         if (op == EK_OP_COL || op == EK_OP_AGG || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) sp++;
         else if (op >= EK_OP_EQ && op <= EK_OP_MOD) { if (sp < 2) return 0; sp--; }
         else return 0;
-        if (sp > 16) return 0;
+        if (sp > kEvalDepth) return 0;   // the device interpreter's register stack
     }
     return n == 0 || sp == 1;
 }

@@ -699,17 +699,12 @@ __device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int
     return Val{V_NULL, 0, 0.0};
 }
 
-__device__ __noinline__ Val having_eval(const DPlan& p, const Val* aggs) {
-    return eval_prog(p.having_prog, p.n_having, p, nullptr, 0, aggs);
-}
-
 // HAVING (having_operator.go:41-56): true keeps the group, false drops it, anything else is an error.
+// Aggregate slots are evaluated on demand from the group's partial (no per-lane array).
 template <int NVC>
 __device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, int32_t* win_err, const SortRes* sr = nullptr) {
     if (p.n_having <= 0) return true;
-    Val hv[EK_MAX_AGGS];
-    for (int k = 0; k < p.n_aggs; ++k) hv[k] = agg_value(p, s, k, sr);
-    Val h = having_eval(p, hv);
+    const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, [&](int k) { return agg_value(p, s, k, sr); });
     if (h.tag != V_BOOL) { atomicOr(win_err, EK_WIN_HAVING_ERROR); return false; }
     return h.i != 0;
 }

@@ -107,7 +107,7 @@ __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, in
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
         uint8_t f = 1;
         if (p.n_trigger > 0) {
-            Val v = eval_prog(p.trigger_prog, p.n_trigger, p, &b, i, nullptr);
+            Val v = eval_prog(p.trigger_prog, p.n_trigger, p, &b, i, NoAggs{});
             f = (v.tag == V_BOOL && v.i) ? 1 : 0;
         }
         flags[i - i0] = f;
