@@ -2052,6 +2052,265 @@ struct Engine {
         return hipStreamSynchronize(stream) == hipSuccess ? 0 : fail(EK_ERR_DEVICE, "reset sync failed");
     }
 
+    // ------------------------------------------------------------------ checkpoint (ek_export_state / ek_import_state)
+    // The state the reference checkpoints through ctx.PutState — WatermarkOp's lastWatermarkTs and buffered events
+    // (watermark_op.go:204-211), WindowOperator's inputs / triggerTime / msgCount (window_op.go:283-340,419-420,
+    // event_window_trigger.go:196) — in this engine's representation: watermark and window cursor, the accepted
+    // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
+    // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
+    static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
+    static constexpr int64_t kStateVersion = 1;
+
+    // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
+    uint64_t plan_hash() const {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](const void* p, size_t n) {
+            const uint8_t* b = (const uint8_t*)p;
+            for (size_t k = 0; k < n; ++k) { h ^= b[k]; h *= 1099511628211ull; }
+        };
+        auto i32 = [&](int32_t v) { mix(&v, 4); };
+        auto i64 = [&](int64_t v) { mix(&v, 8); };
+        i32(plan.window_type); i32(plan.time_unit); i32(plan.length); i32(plan.interval); i32(plan.delay);
+        i32(plan.is_event_time); i32(plan.tz_offset_s); i64(plan.late_tolerance_ms); i32(plan.n_columns);
+        for (int c = 0; c < plan.n_columns; ++c) i32(plan.column_type[c]);
+        i32(plan.ts_column); i32(plan.key_column); i32((int32_t)plan.num_keys); i32(plan.debug_membership);
+        i32((int32_t)plan.nullable_mask); i32(plan.n_aggs);
+        for (int k = 0; k < plan.n_aggs; ++k) {
+            i32(plan.aggs[k].fn); i32(plan.aggs[k].column);
+            if (plan.aggs[k].fn == EK_AGG_PERCENTILE_CONT || plan.aggs[k].fn == EK_AGG_PERCENTILE_DISC) mix(&plan.aggs[k].param, 8);
+        }
+        auto prog = [&](const ek_instr* p, int n) {
+            i32(n);
+            for (int k = 0; k < n; ++k) {
+                i32(p[k].op); i32(p[k].arg);
+                if (p[k].op == EK_OP_CONST_I64) i64(p[k].i64);
+                if (p[k].op == EK_OP_CONST_F64) mix(&p[k].f64, 8);
+            }
+        };
+        prog(plan.where_prog, plan.n_where);
+        prog(plan.having_prog, plan.n_having);
+        prog(plan.trigger_prog, plan.n_trigger);
+        i32(range_mode ? 1 : 0);
+        return h;
+    }
+
+    struct StateOut {
+        std::vector<uint8_t> b;
+        void put(const void* p, size_t n) {
+            if (n) b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+            while (b.size() & 7) b.push_back(0);
+        }
+        void i64(int64_t v) { put(&v, 8); }
+    };
+    struct StateIn {
+        const uint8_t* p;
+        int64_t n, o;
+        bool ok;
+        const uint8_t* take(int64_t k) {
+            if (!ok || k < 0 || k > n - o) { ok = false; return nullptr; }
+            const uint8_t* r = p + o;
+            o = std::min(n, o + ((k + 7) & ~(int64_t)7));
+            return r;
+        }
+        bool read(void* dst, int64_t k) {
+            const uint8_t* r = take(k);
+            if (r && k) memcpy(dst, r, (size_t)k);
+            return r != nullptr;
+        }
+        int64_t i64() { int64_t v = 0; read(&v, 8); return v; }
+    };
+    // device bytes -> blob (the stream was drained by the caller)
+    int dev_append(StateOut& s, const void* d, size_t n) {
+        const size_t o = s.b.size();
+        s.b.resize(o + ((n + 7) & ~(size_t)7), 0);
+        if (n && (hipMemcpyAsync(s.b.data() + o, d, n, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                  hipStreamSynchronize(stream) != hipSuccess))
+            return fail(EK_ERR_DEVICE, "state copy (device -> host) failed");
+        return 0;
+    }
+    // blob -> device
+    int dev_restore(StateIn& r, void* d, size_t n) {
+        const uint8_t* p = r.take((int64_t)n);
+        if (!p) return fail(EK_ERR_INVALID, "state blob truncated");
+        if (n && hipMemcpyAsync(d, p, n, hipMemcpyHostToDevice, stream) != hipSuccess)
+            return fail(EK_ERR_DEVICE, "state copy (host -> device) failed");
+        return 0;
+    }
+
+    int export_state(void* buf, int64_t cap, int64_t* size) {
+        if (!wins.empty()) return fail(EK_ERR_STATE, "poll and release the results before exporting the state");
+        if (!range_mode && reg_win != next_win) return fail(EK_ERR_STATE, "windows registered but not emitted");
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "sync failed");
+        StateOut s;
+        s.i64((int64_t)kStateMagic);
+        s.i64(kStateVersion);
+        s.i64((int64_t)plan_hash());
+        // watermark and window cursor (WatermarkKey, TriggerTimeKey, MsgCountKey)
+        for (int64_t v : {(int64_t)has_M, M, (int64_t)has_W, W, (int64_t)e1_known, E1, first_ts, next_win, reg_win,
+                          arrivals, grid.origin, grid.P, (int64_t)grid.tumbling})
+            s.i64(v);
+        s.put(&stats, sizeof stats);
+        // accepted events before the first release (EventInputKey)
+        s.i64(pend_n);
+        s.i64(pend_min);
+        s.i64(pend_max);
+        for (int c = 0; c < plan.n_columns; ++c) {
+            s.i64(pend_has_valid[c] ? 1 : 0);
+            s.put(pend_host[c].data(), pend_host[c].size());
+            if (pend_has_valid[c]) s.put(pend_vhost[c].data(), pend_vhost[c].size());
+        }
+        s.put(pend_arr.data(), pend_arr.size() * 8);
+        if (wtype != EK_WINDOW_NONE && !range_mode) {
+            // partials of every open pane: field-major SoA, field f of slot x at ((f * ring) + x) * Kpad
+            const int nf = n_state_fields();
+            const int64_t first_live = win_first_pane(next_win);
+            std::vector<int> live;
+            for (int x = 0; x < ring; ++x)
+                if (slot_pane[x] != INT64_MIN && slot_pane[x] >= first_live) live.push_back(x);
+            s.i64(Kpad);
+            s.i64(nf);
+            s.i64(ring);
+            s.i64((int64_t)live.size());
+            const size_t per = (size_t)Kpad * 8;
+            for (int x : live) {
+                s.i64(slot_pane[x]);
+                for (int f = 0; f < nf; ++f)
+                    if (int rc = dev_append(s, (char*)state_buf.p + ((size_t)f * ring + x) * per, per)) return rc;
+                if (int rc = dev_append(s, (char*)pane_err.p + (size_t)x * 4, 4)) return rc;
+                if (int rc = dev_append(s, (char*)pane_mcnt.p + (size_t)x * 8, 8)) return rc;
+                if (int rc = dev_append(s, (char*)pane_mhash.p + (size_t)x * 8, 8)) return rc;
+            }
+        }
+        if (range_mode) {
+            // event-buffer rows from the oldest row a future window can start at (WindowInputsKey)
+            const int64_t drop = std::max<int64_t>(0, std::min(eb_floor, eb.n));
+            const int64_t live = eb.n - drop;
+            uint32_t vmask = 0;
+            for (int c = 0; c < plan.n_columns; ++c) if (eb_valid_on[c]) vmask |= 1u << c;
+            for (int64_t v : {eb_base + drop, eb_rel - drop, eb_floor - drop, live, sW, range_wins, count_k, (int64_t)vmask,
+                              (int64_t)sess_last_ticked, (int64_t)sess_has_trigger, sess_trigger})
+                s.i64(v);
+            if (live) {
+                for (int c = 0; c < plan.n_columns; ++c) {
+                    if (int rc = dev_append(s, (char*)eb.col[c].p + drop * col_es(c), (size_t)live * col_es(c))) return rc;
+                    if (eb_valid_on[c])
+                        if (int rc = dev_append(s, (uint8_t*)eb.valid[c].p + drop, (size_t)live)) return rc;
+                }
+                if (int rc = dev_append(s, (int64_t*)eb.arr.p + drop, (size_t)live * 8)) return rc;
+                if (need_rel) if (int rc = dev_append(s, (int64_t*)eb.rel.p + drop, (size_t)live * 8)) return rc;
+            }
+            const int64_t nd = (int64_t)(delayq.size() - delayq_head);   // queued delayed sliding triggers
+            s.i64(nd);
+            s.put(delayq.data() + delayq_head, (size_t)nd * sizeof(DelayTrig));
+            s.i64(h_rts_base);                                                // session: released timestamps
+            s.i64((int64_t)h_rts.size());
+            s.put(h_rts.data(), h_rts.size() * 8);
+        }
+        *size = (int64_t)s.b.size();
+        if (!buf) return 0;
+        if (cap < *size) return fail(EK_ERR_INVALID, "state buffer too small (%lld < %lld bytes)", (long long)cap, (long long)*size);
+        memcpy(buf, s.b.data(), s.b.size());
+        return 0;
+    }
+
+    int import_state(const void* buf, int64_t size) {
+        if (!buf || size < 24) return fail(EK_ERR_INVALID, "state blob too short");
+        StateIn r{(const uint8_t*)buf, size, 0, true};
+        if ((uint64_t)r.i64() != kStateMagic || r.i64() != kStateVersion)
+            return fail(EK_ERR_INVALID, "not an ekgpu state blob of version %lld", (long long)kStateVersion);
+        if ((uint64_t)r.i64() != plan_hash()) return fail(EK_ERR_INVALID, "state blob was exported by a different plan");
+        if (int rc = reset()) return rc;
+        int rc = import_body(r, size);
+        if (rc == 0 && !r.ok) rc = fail(EK_ERR_INVALID, "state blob truncated");
+        if (rc == 0 && hipStreamSynchronize(stream) != hipSuccess) rc = fail(EK_ERR_DEVICE, "state restore sync failed");
+        if (rc) {
+            const std::string e = err;
+            reset();
+            err = e;
+        }
+        return rc;
+    }
+
+    int import_body(StateIn& r, int64_t size) {
+        has_M = r.i64() != 0; M = r.i64();
+        has_W = r.i64() != 0; W = r.i64();
+        e1_known = r.i64() != 0; E1 = r.i64(); first_ts = r.i64();
+        next_win = r.i64(); reg_win = r.i64(); arrivals = r.i64();
+        grid.origin = r.i64(); grid.P = r.i64(); grid.tumbling = (int32_t)r.i64();
+        r.read(&stats, sizeof stats);
+        pend_n = r.i64(); pend_min = r.i64(); pend_max = r.i64();
+        if (pend_n < 0 || pend_n > size) return fail(EK_ERR_INVALID, "bad pending-event count");
+        for (int c = 0; c < plan.n_columns; ++c) {
+            pend_has_valid[c] = r.i64() != 0;
+            pend_host[c].resize((size_t)pend_n * col_es(c));
+            r.read(pend_host[c].data(), (int64_t)pend_host[c].size());
+            if (pend_has_valid[c]) {
+                pend_vhost[c].resize((size_t)pend_n);
+                r.read(pend_vhost[c].data(), pend_n);
+            }
+        }
+        pend_arr.resize((size_t)pend_n);
+        r.read(pend_arr.data(), pend_n * 8);
+        if (!r.ok) return fail(EK_ERR_INVALID, "state blob truncated");
+        if (wtype != EK_WINDOW_NONE && !range_mode) {
+            const int64_t kp = r.i64(), nf = r.i64(), R = r.i64(), nl = r.i64();
+            if (kp != Kpad || nf != n_state_fields() || R < 1 || R > (1 << 24) || nl < 0 || nl > R)
+                return fail(EK_ERR_INVALID, "pane state does not match this plan");
+            if (int rc = ensure_ring(R)) return rc;
+            const size_t per = (size_t)Kpad * 8;
+            for (int64_t l = 0; l < nl; ++l) {
+                const int64_t q = r.i64();
+                const int x = (int)(q % ring);
+                if (!r.ok || q < 0 || slot_pane[x] != INT64_MIN) return fail(EK_ERR_INVALID, "bad pane in state blob");
+                slot_pane[x] = q;
+                for (int f = 0; f < nf; ++f)
+                    if (int rc = dev_restore(r, (char*)state_buf.p + ((size_t)f * ring + x) * per, per)) return rc;
+                if (int rc = dev_restore(r, (char*)pane_err.p + (size_t)x * 4, 4)) return rc;
+                if (int rc = dev_restore(r, (char*)pane_mcnt.p + (size_t)x * 8, 8)) return rc;
+                if (int rc = dev_restore(r, (char*)pane_mhash.p + (size_t)x * 8, 8)) return rc;
+            }
+        }
+        if (range_mode) {
+            const int64_t base = r.i64(), rel = r.i64(), floor = r.i64(), live = r.i64();
+            const int64_t sw = r.i64(), rw = r.i64(), ck = r.i64(), vmask = r.i64();
+            const int64_t slt = r.i64(), sht = r.i64(), strig = r.i64();
+            if (!r.ok || live < 0 || live > size) return fail(EK_ERR_INVALID, "bad event-buffer size in state blob");
+            eb.n = 0;
+            eb_floor = eb_rel = 0;
+            for (int c = 0; c < plan.n_columns; ++c)
+                if ((vmask >> c) & 1) if (int rc = eb_enable_valid(c)) return rc;
+            if (int rc = eb_reserve(live)) return rc;
+            for (int c = 0; c < plan.n_columns; ++c) {
+                if (int rc = dev_restore(r, eb.col[c].p, (size_t)live * col_es(c))) return rc;
+                if ((vmask >> c) & 1) { if (int rc = dev_restore(r, eb.valid[c].p, (size_t)live)) return rc; }
+                else if (eb_valid_on[c]) fill_valid_ones(c, 0, live);
+            }
+            if (int rc = dev_restore(r, eb.arr.p, (size_t)live * 8)) return rc;
+            if (need_rel) if (int rc = dev_restore(r, eb.rel.p, (size_t)live * 8)) return rc;
+            eb.n = live;
+            eb_base = base;
+            eb_rel = rel;
+            eb_floor = floor;
+            sW = sw;
+            range_wins = rw;
+            count_k = ck;
+            sess_last_ticked = slt != 0;
+            sess_has_trigger = sht != 0;
+            sess_trigger = strig;
+            const int64_t nd = r.i64();
+            if (!r.ok || nd < 0 || nd > size) return fail(EK_ERR_INVALID, "bad delay queue in state blob");
+            delayq.resize((size_t)nd);
+            r.read(delayq.data(), nd * (int64_t)sizeof(DelayTrig));
+            delayq_head = 0;
+            h_rts_base = r.i64();
+            const int64_t nr = r.i64();
+            if (!r.ok || nr < 0 || nr > size) return fail(EK_ERR_INVALID, "bad session mirror in state blob");
+            h_rts.resize((size_t)nr);
+            r.read(h_rts.data(), nr * 8);
+        }
+        return 0;
+    }
+
     ~Engine() {
         if (stream) hipStreamSynchronize(stream);
         release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash); release(bstats); release(bstats_part);
@@ -2168,6 +2427,16 @@ const char* ek_last_error(void* h) {
 int ek_destroy(void* h) {
     delete (Engine*)h;
     return 0;
+}
+
+int ek_export_state(void* h, void* buf, int64_t cap, int64_t* size) {
+    if (!h || !size) return EK_ERR_INVALID;
+    return ((Engine*)h)->export_state(buf, cap, size);
+}
+
+int ek_import_state(void* h, const void* buf, int64_t size) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->import_state(buf, size);
 }
 
 }  // extern "C"

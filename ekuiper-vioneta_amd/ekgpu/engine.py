@@ -65,6 +65,10 @@ def lib():
         L.ek_json_last_error.restype = C.c_char_p
         L.ek_json_destroy.argtypes = [C.c_void_p]
         L.ek_json_destroy.restype = C.c_int
+        L.ek_export_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.ek_export_state.restype = C.c_int
+        L.ek_import_state.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        L.ek_import_state.restype = C.c_int
         if L.ek_abi_version() != A.EKGPU_ABI_VERSION:
             raise EngineError(A.EK_ERR_INVALID, "libekgpu.so ABI version mismatch")
         _lib = L
@@ -74,7 +78,7 @@ def lib():
 EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_batch", "ek_poll_results",
                     "ek_release_results", "ek_reset", "ek_sync", "ek_set_stream", "ek_get_stats", "ek_last_error",
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
-                    "ek_json_last_error", "ek_json_destroy"]
+                    "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -157,6 +161,18 @@ class Engine:
         s = A.ek_stats()
         self._check(lib().ek_get_stats(self.h, C.byref(s)))
         return s
+
+    def export_state(self) -> bytes:
+        """Checkpoint of the stream state (results must have been polled): a host byte string."""
+        n = C.c_int64()
+        self._check(lib().ek_export_state(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(max(n.value, 1))
+        self._check(lib().ek_export_state(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[: n.value]
+
+    def import_state(self, blob: bytes):
+        """Restore a checkpoint taken by export_state on a handle of the same plan (replaces the stream state)."""
+        self._check(lib().ek_import_state(self.h, blob, len(blob)))
 
     def close(self):
         if self.h:

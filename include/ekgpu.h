@@ -217,6 +217,20 @@ int ek_get_stats(void* h, ek_stats* out);
 const char* ek_last_error(void* h);
 int ek_destroy(void* h);
 
+/* Checkpoint / restore of the stream state of a handle: what the reference's checkpoint coordinator
+ * saves through ctx.PutState and restores through ctx.GetState for this chain —
+ *   WatermarkOp: WatermarkKey / EventInputKey / StreamWMKey    (watermark_op.go:72-101,149,204-211)
+ *   WindowOperator: WindowInputsKey / TriggerTimeKey / MsgCountKey (window_op.go:83-85,131-168,283-340,
+ *                   event_window_trigger.go:196).
+ * The blob holds the watermark, the window cursor, the partial aggregates of every open pane (pane mode)
+ * or the buffered events a future window can still contain (range mode), and the counters. It is a
+ * host-side byte string bound to the plan: a hash of the ek_plan fields is checked on import.
+ * ek_export_state: results must have been polled and released first (EK_ERR_STATE otherwise).
+ *   *size = bytes of the blob; buf == NULL only queries the size; cap < *size -> EK_ERR_INVALID.
+ * ek_import_state: replaces the handle's stream state (ek_reset, then restore); unpolled results are dropped. */
+int ek_export_state(void* h, void* buf, int64_t cap, int64_t* size);
+int ek_import_state(void* h, const void* buf, int64_t size);
+
 /* ---------------------------------------------------------------- columnar JSON ingest
  * Replaces the per-message FastJsonConverter.Decode of a schema-typed stream
  * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) for flat JSON objects

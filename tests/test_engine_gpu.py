@@ -58,7 +58,8 @@ def test_window_rule_kat_engine(oracle, engine_mod, case):
     cols = [np.array(rows[:, 0], np.int64), np.array(rows[:, 1], np.int64), np.array(rows[:, 2], np.uint32),
             np.array(rows[:, 3], np.float64)]
     schema = {"ts": "bigint", "size": "bigint", "color": "key", "temp": "float"}
-    rule = compile_rule(case["sql"], schema, late_tolerance_ms=1000, num_keys=4, debug_membership=True)
+    rule = compile_rule(case["sql"], schema, late_tolerance_ms=1000, num_keys=4, debug_membership=True,
+                        is_event_time=case.get("event_time", True))
     got, exp, st = run_both(oracle, engine_mod, rule, cols)
     assert len(got) == case["windows_out"]
     assert st.records_late == case["late"]

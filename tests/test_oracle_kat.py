@@ -89,7 +89,7 @@ SCHEMA = {"ts": "bigint", "size": "bigint", "color": "key", "temp": "float"}
 def test_window_rule_kat(oracle, case):
     g = _load("kat_window_rules.json")
     cols = _stream_cols(g["streams"][case["stream"]])
-    rule = compile_rule(case["sql"], SCHEMA, is_event_time=True, late_tolerance_ms=1000, num_keys=4)
+    rule = compile_rule(case["sql"], SCHEMA, is_event_time=case.get("event_time", True), late_tolerance_ms=1000, num_keys=4)
     run = oracle.run(rule.plan, cols)
     assert len(run.windows) == case["windows_out"]
     assert run.records_late == case["late"]
@@ -102,5 +102,7 @@ def test_window_rule_kat(oracle, case):
             kept = [m for m in kept if where_sizes[m] > 2]
         assert sorted(kept) == sorted(exp["members"])
         assert w.value(0, 0) == len(exp["members"])  # count(*)
+        if "first_color" in exp:                     # collect(*)[0]->color
+            assert cols[2][kept[0]] == exp["first_color"]
         if "window_start" in exp:
             assert w.start == exp["window_start"] and w.end == exp["window_end"]

@@ -42,7 +42,8 @@ KAT_SCHEMA = {"ts": "bigint", "size": "bigint", "color": "key", "temp": "float"}
 def test_window_rule_kat_range(oracle, engine_mod, case, force_range):
     """Every reference window KAT (window_rule_test.go) through range mode, whole stream and one event per push."""
     cols = _kat_cols(case)
-    rule = compile_rule(case["sql"], KAT_SCHEMA, late_tolerance_ms=1000, num_keys=4, debug_membership=True)
+    rule = compile_rule(case["sql"], KAT_SCHEMA, late_tolerance_ms=1000, num_keys=4, debug_membership=True,
+                        is_event_time=case.get("event_time", True))
     got, exp, st = run_both(oracle, engine_mod, rule, cols)
     assert len(got) == case["windows_out"]
     assert st.records_late == case["late"]
