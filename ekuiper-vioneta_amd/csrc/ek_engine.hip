@@ -838,7 +838,7 @@ struct Engine {
                 if (hipHostMalloc((void**)&h_small, h_small_cap * 8) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
             }
             if (int rc = ensure(bounds_idx, (size_t)nb * 8)) return rc;
-            hipLaunchKernelGGL(k_pane_bounds, dim3((nb + 255) / 256), dim3(256), 0, stream,
+            hipLaunchKernelGGL(k_pane_bounds, dim3((nb + kBoundsBlock / 64 - 1) / (kBoundsBlock / 64)), dim3(kBoundsBlock), 0, stream,
                                (const int64_t*)db.col[dp.ts_col], start, n, grid, q_lo, nb, (int64_t*)bounds_idx.p);
             hipMemcpyAsync(h_small + nb, bounds_idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "bounds sync failed");
@@ -1082,20 +1082,22 @@ struct Engine {
         return 0;
     }
 
-    // most panes any chunk of the group overlaps (sorted groups)
-    // Largest number of panes one chunk of the aligned grid spans (sorted groups; cursors are monotone).
+    // Largest number of panes one chunk of the aligned grid spans (sorted groups): 1 + the most pane starts that
+    // fall strictly inside one chunk (the device's chunk_panes: pa = last pane with pbnd <= c0, pb = last < c1).
+    // O(panes), not O(chunks): the host computes this for every group of every push.
     int max_panes_in_chunk(const int64_t* pb, const GroupDesc& gd, int64_t chunk_sz) const {
         if (!pb) return gd.n_panes;
-        int best = 1, a = 0, b = 0;
-        for (int64_t a0 = gd.abase; a0 < gd.hi; a0 += chunk_sz) {
-            int64_t c0 = std::max(gd.lo, a0);
-            int64_t c1 = std::min(gd.hi, a0 + chunk_sz);
-            while (a + 1 < gd.n_panes && pb[a + 1] <= c0) a++;
-            b = std::max(a, b);
-            while (b + 1 < gd.n_panes && pb[b + 1] < c1) b++;
-            best = std::max(best, b - a + 1);
+        int best = 0, run = 0;
+        int64_t cur = -1;
+        for (int k = 1; k < gd.n_panes; ++k) {
+            const int64_t x = pb[k];
+            if (x >= gd.hi) break;
+            const int64_t c = (x - gd.abase) / chunk_sz;
+            if (x <= std::max(gd.lo, gd.abase + c * chunk_sz)) continue;
+            if (c != cur) { cur = c; run = 0; }
+            best = std::max(best, ++run);
         }
-        return best;
+        return best + 1;
     }
     // Largest number of chunks one pane spans (bounded by k_agg's per-partition run list).
     int max_chunks_in_pane(const int64_t* pb, const GroupDesc& gd, int64_t chunk_sz) const {
@@ -2034,12 +2036,9 @@ struct Engine {
     int release_results() {
         // windows handed out are dropped; device regions are recycled
         int64_t nw = (int64_t)wins.size();
-        if (nw && r_wcnt.p) {
-            hipMemsetAsync(r_wcnt.p, 0, nw * 8, stream);
-            hipMemsetAsync(r_werr.p, 0, nw * 4, stream);
-            hipMemsetAsync(r_wmc.p, 0, nw * 8, stream);
-            hipMemsetAsync(r_wmh.p, 0, nw * 8, stream);
-        }
+        if (nw && r_wcnt.p)
+            hipLaunchKernelGGL(k_zero_wins, dim3((unsigned)std::min<int64_t>(1024, (nw + 255) / 256)), dim3(256), 0, stream, nw,
+                               (int64_t*)r_wcnt.p, (int32_t*)r_werr.p, (int64_t*)r_wmc.p, (int64_t*)r_wmh.p);
         wins.clear();
         r_rows_used = 0;
         return 0;

@@ -197,19 +197,43 @@ __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ t
     }
 }
 
-// first index in [lo, hi) with ts >= start of pane q_lo + k (sorted batches; k = 0 -> lo for pane 0 of tumbling)
-__global__ void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, PaneGrid g, int64_t q_lo, int nb,
-                              int64_t* out) {
-    int k = blockIdx.x * blockDim.x + threadIdx.x;
+// first index in [lo, hi) with ts >= start of pane q_lo + k (sorted batches; k = 0 -> lo for pane 0 of tumbling).
+// One wave per pane, 64-ary search: each round the 64 lanes probe 64 evenly spaced rows of the bracket and a ballot
+// narrows it 65-fold, so a 1e8-row batch costs 5 dependent load rounds instead of 27.
+constexpr int kBoundsBlock = 256;
+__global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi,
+                                                              PaneGrid g, int64_t q_lo, int nb, int64_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int k = blockIdx.x * (kBoundsBlock / 64) + (threadIdx.x >> 6);
     if (k >= nb) return;
-    int64_t q = q_lo + k;
-    if (k == nb - 1) { out[k] = hi; return; }
+    if (k == nb - 1) { if (lane == 0) out[k] = hi; return; }
+    const int64_t q = q_lo + k;
     int64_t x;
     if (g.tumbling) x = q == 0 ? INT64_MIN : g.origin + (q - 1) * g.P;
     else x = g.origin + q * g.P;
-    int64_t a = lo, b = hi;
-    while (a < b) { int64_t m = (a + b) >> 1; if (ts[m] < x) a = m + 1; else b = m; }
-    out[k] = a;
+    int64_t a = lo, b = hi;   // the answer lies in [a, b]
+    while (b - a > 64) {
+        const int64_t m = a + ((b - a) * (lane + 1)) / 65;
+        const unsigned long long below = __ballot(ts[m] < x);
+        const int c = __popcll(below);   // probes 0 .. c-1 are below x (ts is non-decreasing)
+        const int64_t mlo = __shfl(m, c > 0 ? c - 1 : 0, 64);
+        const int64_t mhi = __shfl(m, c < 64 ? c : 63, 64);
+        if (c > 0) a = mlo + 1;
+        if (c < 64) b = mhi;
+    }
+    const int64_t m = a + lane;
+    const unsigned long long below = __ballot(m < b && ts[m] < x);
+    if (lane == 0) out[k] = a + __popcll(below);
+}
+
+// per-window result counters of the windows handed out by a poll: one launch instead of four fills
+__global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        wcnt[i] = 0;
+        werr[i] = 0;
+        wmc[i] = 0;
+        wmh[i] = 0;
+    }
 }
 
 // first index in [lo, hi) with ts >= bound[k] (sorted batches)
