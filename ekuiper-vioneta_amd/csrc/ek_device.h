@@ -44,6 +44,7 @@ struct DPlan {
     int32_t agg_sidx[EK_MAX_AGGS];  // sort slot of aggregate k (-1 otherwise)
     int32_t sagg_scol[kMaxSortAggs];
     int32_t sagg_agg[kMaxSortAggs];
+    int32_t inc;                  // incremental-window semantics (inc_sum / inc_avg float64, funcs_inc_agg.go:56-117)
 };
 
 // Columns of one micro-batch (device pointers).

@@ -316,8 +316,30 @@ struct Engine {
         } else if (wtype != EK_WINDOW_COUNT) {
             return fail(EK_ERR_UNSUPPORTED, "processing-time windows other than COUNTWINDOW are wall-clock driven (use event time)");
         }
+        // incremental-aggregation window (planOptimizeStrategy.enableIncrementalWindow): the planner rewrites the
+        // rule only when every aggregate is incremental and the window is COUNT (no interval) / SLIDING / HOPPING /
+        // TUMBLING (rewriteIfIncAggStmt + supportedWindowType, planner.go:910-1017); otherwise the regular chain runs
+        {
+            bool fns = plan.n_aggs > 0;
+            for (int k = 0; k < plan.n_aggs; ++k) fns &= plan.aggs[k].fn >= EK_AGG_COUNT_STAR && plan.aggs[k].fn <= EK_AGG_MAX;
+            const bool win = (wtype == EK_WINDOW_COUNT && plan.interval <= 0) || wtype == EK_WINDOW_SLIDING ||
+                             wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_TUMBLING;
+            inc = plan.incremental != 0 && fns && win;
+        }
+        if (inc) {
+            if (wtype == EK_WINDOW_SLIDING)
+                return fail(EK_ERR_UNSUPPORTED, "incremental sliding windows (window_inc_agg_event_op.go:148-296) are not built");
+            if (wtype == EK_WINDOW_COUNT && plan.is_event_time)
+                return fail(EK_ERR_UNSUPPORTED, "incremental event-time count windows (window_inc_agg_event_op.go:340-439) are not built");
+            if (plan.n_where > 0)
+                return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
+                                                "(FilterPlan above IncWindowPlan): not built");
+            for (int k = 0; k < plan.n_aggs; ++k)
+                if (plan.aggs[k].fn != EK_AGG_COUNT_STAR && ((plan.nullable_mask >> plan.aggs[k].column) & 1u))
+                    return fail(EK_ERR_UNSUPPORTED, "incremental aggregates over a nullable column (nil at a group's last row) are not built");
+        }
         range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT || sort_aggs ||
-                     env_int("EKGPU_FORCE_RANGE", 0) != 0;
+                     (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         need_rel = wtype == EK_WINDOW_SLIDING;
         if (plan.is_event_time) {
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
@@ -374,6 +396,7 @@ struct Engine {
         memcpy(dp.having_prog, plan.having_prog, sizeof plan.having_prog);
         memcpy(dp.trigger_prog, plan.trigger_prog, sizeof plan.trigger_prog);
         dp.n_aggs = plan.n_aggs;
+        dp.inc = inc ? 1 : 0;
         for (int k = 0; k < plan.n_aggs; ++k) {
             const ek_agg_spec& a = plan.aggs[k];
             dp.agg_fn[k] = a.fn;
@@ -398,8 +421,9 @@ struct Engine {
             int f = 0;
             switch (a.fn) {
             case EK_AGG_COUNT: f = NEED_CNT; break;
-            case EK_AGG_SUM: f = NEED_SUM; break;
-            case EK_AGG_AVG: f = NEED_SUM | NEED_CNT; break;
+            // inc_sum / inc_avg accumulate float64 even over a BIGINT column (funcs_inc_agg.go:56-75,102-117)
+            case EK_AGG_SUM: f = NEED_SUM | (inc && !fl ? NEED_FSUM : 0); break;
+            case EK_AGG_AVG: f = NEED_SUM | NEED_CNT | (inc && !fl ? NEED_FSUM : 0); break;
             case EK_AGG_MIN: f = NEED_MIN; break;
             case EK_AGG_MAX: f = NEED_MAX; break;
             case EK_AGG_MEDIAN: case EK_AGG_PERCENTILE_CONT: case EK_AGG_PERCENTILE_DISC: {
@@ -599,6 +623,9 @@ struct Engine {
         sess_last_ticked = sess_has_trigger = false;
         sess_trigger = 0;
         count_k = 1;
+        inc_has_T = false;
+        inc_T = 0;
+        inc_pend.clear();
         wins.clear();
         r_rows_used = 0;
         stats = ek_stats{};
@@ -1202,6 +1229,13 @@ struct Engine {
     bool sess_last_ticked = false, sess_has_trigger = false;
     int64_t sess_trigger = 0;
     int64_t count_k = 1;               // COUNTWINDOW: next window index
+    // incremental-aggregation windows (window_inc_agg_event_op.go:26-146): NextTriggerWindowTime and the
+    // windows opened by rows but not emitted yet (creation order == end order)
+    bool inc = false;
+    bool inc_has_T = false;
+    int64_t inc_T = 0;
+    struct IncWin { int64_t start, end, floor_abs; };
+    std::vector<IncWin> inc_pend;
     DevBuf rq_d, ab_d, slot_d, trig_d, flags_d, cnts_d, runmax_d, runcm_d, mrg_keys[2], mrg_src[2], mrg_tmp, mrg_tail,
         mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh, sort_pbase, sort_scr, chunk_pa;
     std::vector<int64_t> h_ab;
@@ -1414,10 +1448,13 @@ struct Engine {
         // register in trigger order; rows reserved = min(K, members)
         int64_t rows = 0;
         for (int w = 0; w < nq; ++w) rows += std::min<int64_t>(K, h_ab[2 * w + 1] - h_ab[2 * w]);
+        // incremental windows none of whose rows joined them (opened by a row outside their range) are not reported
+        const auto skip = [&](int w) { return inc && h_ab[2 * w + 1] == h_ab[2 * w]; };
         if (int rc = ensure_results(rows, nq)) return rc;
         std::vector<int32_t> slots(nq);
         std::vector<int64_t> obase(nq);
         for (int w = 0; w < nq; ++w) {
+            if (skip(w)) { slots[w] = -1; obase[w] = -1; continue; }
             WinInfo wi{};
             wi.j = range_wins++;
             wi.start = pw[w].start;
@@ -1430,7 +1467,7 @@ struct Engine {
             slots[w] = wi.slot;
             obase[w] = wi.out_base;
         }
-        stats.windows_out += nq;
+        for (int w = 0; w < nq; ++w) stats.windows_out += skip(w) ? 0 : 1;
         if (plan.debug_membership) {
             if (int rc = ensure(slot_d, (size_t)nq * 4)) return rc;
             hipMemcpyAsync(slot_d.p, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
@@ -1596,6 +1633,12 @@ struct Engine {
                     delayq_head = 0;
                 }
             }
+        } else if (inc) {
+            if (int rc = inc_triggers(rel_prev, pw)) return rc;
+            int rc = fire_windows(pw);
+            // rows a pending window will aggregate stay in the buffer (windows opened later start at >= eb_rel)
+            eb_floor = inc_pend.empty() ? eb_rel : std::min(eb_rel, inc_pend.front().floor_abs - eb_base);
+            return rc;
         } else if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_HOPPING) {
             if (!e1_known && eb_rel > 0) {
                 e1_known = true;
@@ -1619,6 +1662,109 @@ struct Engine {
             if (int rc = session_triggers(rel_prev, pw)) return rc;
         }
         return fire_windows(pw);
+    }
+
+    // ---- incremental-aggregation windows, event time (HoppingWindowIncAggEventOp, window_inc_agg_event_op.go:71-146;
+    // TUMBLING = the same op with Length = Interval, :298-307). Over the rows released in release order:
+    //   triggerWindow: a row with ts > T (NextTriggerWindowTime) sets T = getAlignedWindowEndTime(ts) and opens
+    //                  the window [T - Interval, T - Interval + Length);
+    //   calIncAggWindow: the row joins every open window whose range holds its ts;
+    //   at a watermark, windows with end <= watermark are emitted (emitWindow) and dropped (gcIncAggWindow).
+    // A window therefore holds the rows with ts in its range from the row that opened it on: an index range
+    // [first row >= max(opener, lb(start)), lb(end)) of the ts-sorted buffer -> RangeQ RB_LB with floor = opener.
+    // getAlignedWindowEndTime is monotone in ts and piecewise constant on "cells" [lo_k, lo_k+1) with end e_k; inside
+    // a cell only the first row with ts > T opens a window (T becomes e_k), except rows with ts > e_k (the second
+    // "second == interval" of window_op.go:194-227), each of which opens one. All the row indices the rule needs
+    // are lower bounds in the sorted buffer: one batched search per push, no per-row host work.
+    int64_t next_cell_lo(int64_t x) const {
+        const int64_t e = aligned_end(x, raw_interval, plan.time_unit, plan.tz_offset_s);
+        int64_t lo = x + 1, hi = std::max(x, e) + 2 * 86400000LL;   // aligned_end(hi) > e
+        while (lo < hi) {
+            const int64_t m = lo + ((hi - lo) >> 1);
+            if (aligned_end(m, raw_interval, plan.time_unit, plan.tz_offset_s) > e) hi = m; else lo = m + 1;
+        }
+        return lo;
+    }
+
+    int inc_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
+        const int64_t I = H;
+        if (eb_rel > rel_prev) {
+            const int64_t* bts = (const int64_t*)eb.col[dp.ts_col].p;
+            int64_t t01[2];
+            hipMemcpyAsync(&t01[0], bts + rel_prev, 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(&t01[1], bts + eb_rel - 1, 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "inc window ts fetch failed");
+            // cells covering [t0, t1]
+            std::vector<int64_t> clo, ce;
+            for (int64_t x = t01[0]; x <= t01[1];) {
+                clo.push_back(x);
+                ce.push_back(aligned_end(x, raw_interval, plan.time_unit, plan.tz_offset_s));
+                x = next_cell_lo(x);
+                if (clo.size() > ((size_t)1 << 22)) return fail(EK_ERR_UNSUPPORTED, "incremental window: too many window cells in one batch");
+            }
+            const int K = (int)clo.size();
+            // bounds: F_k = lb(lo_k), U_k = lb(e_k + 1) (first row with ts > e_k), Q = lb(T + 1)
+            std::vector<int64_t> q((size_t)2 * K + 1);
+            for (int k = 0; k < K; ++k) { q[k] = clo[k]; q[K + k] = ce[k] + 1; }
+            q[2 * K] = inc_has_T ? inc_T + 1 : INT64_MIN;
+            const int nq = 2 * K + 1;
+            if (int rc = ensure(bounds_val, (size_t)nq * 8)) return rc;
+            if (int rc = ensure(bounds_idx, (size_t)nq * 8)) return rc;
+            hipMemcpyAsync(bounds_val.p, q.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_lower_bound, dim3((nq + 255) / 256), dim3(256), 0, stream, bts, rel_prev, eb_rel,
+                               (const int64_t*)bounds_val.p, nq, (int64_t*)bounds_idx.p);
+            std::vector<int64_t> b((size_t)nq);
+            hipMemcpyAsync(b.data(), bounds_idx.p, (size_t)nq * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "inc window bounds failed");
+            int64_t T = inc_T, ubT = b[2 * K];
+            bool hasT = inc_has_T;
+            const int64_t dup_cap = env_int("EKGPU_INC_MAX_OPEN", 65536);
+            int64_t opened = 0;
+            auto open_win = [&](int64_t e, int64_t row) -> int {
+                if (++opened > dup_cap)
+                    return fail(EK_ERR_UNSUPPORTED, "incremental window: more than %lld windows opened in one batch (the reference "
+                                                    "opens one per row in the second where the alignment ends before the row)",
+                                (long long)dup_cap);
+                inc_pend.push_back(IncWin{e - I, e - I + L, eb_base + row});
+                return 0;
+            };
+            for (int k = 0; k < K; ++k) {
+                const int64_t s0 = k == 0 ? rel_prev : b[k];
+                const int64_t s1 = k + 1 < K ? b[k + 1] : eb_rel;
+                if (s0 >= s1) continue;
+                const int64_t Uk = b[K + k];
+                const int64_t nend = std::min(Uk, s1);        // rows with ts <= e_k
+                const int64_t r = hasT ? std::max(s0, ubT) : s0;
+                if (r < nend) {
+                    if (int rc = open_win(ce[k], r)) return rc;
+                    T = ce[k]; ubT = Uk; hasT = true;
+                }
+                const int64_t a0 = std::max(Uk, s0);          // rows with ts > e_k: each opens a window
+                if (a0 < s1) {
+                    T = ce[k]; ubT = Uk; hasT = true;
+                    // with Length == Interval those windows end at e_k, before their rows: nothing to report
+                    if (L > I)
+                        for (int64_t row = a0; row < s1; ++row) if (int rc = open_win(ce[k], row)) return rc;
+                }
+            }
+            inc_T = T;
+            inc_has_T = hasT;
+        }
+        // emitWindow at the watermark: every open window with end <= W, in opening order
+        size_t nf = 0;
+        while (has_W && nf < inc_pend.size() && inc_pend[nf].end <= W) {
+            const IncWin& iw = inc_pend[nf++];
+            PendWin p{};
+            p.q.kind = RB_LB;
+            p.q.lo_ts = iw.start;
+            p.q.hi_ts = iw.end;
+            p.q.floor = iw.floor_abs - eb_base;
+            p.start = iw.start;
+            p.end = iw.end;
+            pw.push_back(p);
+        }
+        inc_pend.erase(inc_pend.begin(), inc_pend.begin() + (int64_t)nf);
+        return 0;
     }
 
     // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
@@ -2204,6 +2350,10 @@ struct Engine {
             s.i64(h_rts_base);                                                // session: released timestamps
             s.i64((int64_t)h_rts.size());
             s.put(h_rts.data(), h_rts.size() * 8);
+            s.i64(inc_has_T ? 1 : 0);                                         // incremental windows: T + open windows
+            s.i64(inc_T);
+            s.i64((int64_t)inc_pend.size());
+            s.put(inc_pend.data(), inc_pend.size() * sizeof(IncWin));
         }
         *size = (int64_t)s.b.size();
         if (!buf) return 0;
@@ -2306,6 +2456,12 @@ struct Engine {
             if (!r.ok || nr < 0 || nr > size) return fail(EK_ERR_INVALID, "bad session mirror in state blob");
             h_rts.resize((size_t)nr);
             r.read(h_rts.data(), nr * 8);
+            inc_has_T = r.i64() != 0;
+            inc_T = r.i64();
+            const int64_t ni = r.i64();
+            if (!r.ok || ni < 0 || ni > size) return fail(EK_ERR_INVALID, "bad incremental windows in state blob");
+            inc_pend.resize((size_t)ni);
+            r.read(inc_pend.data(), ni * (int64_t)sizeof(IncWin));
         }
         return 0;
     }

@@ -707,9 +707,9 @@ __device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int
     if (n == 0) return Val{V_NULL, 0, 0.0};      // every value nil
     const bool fl = p.vc_is_float[v];
     switch (fn) {
-    case EK_AGG_SUM: return fl ? Val{V_F64, 0, sel(s.fsum, v)} : Val{V_I64, sel(s.isum, v), 0.0};
-    case EK_AGG_AVG: {   // funcs_agg.go:56-86: int -> truncating int64 division
-        if (fl) return Val{V_F64, 0, __ddiv_rn(sel(s.fsum, v), (double)n)};
+    case EK_AGG_SUM: return (fl || p.inc) ? Val{V_F64, 0, sel(s.fsum, v)} : Val{V_I64, sel(s.isum, v), 0.0};
+    case EK_AGG_AVG: {   // funcs_agg.go:56-86: int -> truncating int64 division; inc_avg: float64 (funcs_inc_agg.go:56-75)
+        if (fl || p.inc) return Val{V_F64, 0, __ddiv_rn(sel(s.fsum, v), (double)n)};
         int64_t t = sel(s.isum, v);
         return Val{V_I64, (t == INT64_MIN && n == -1) ? t : t / n, 0.0};
     }

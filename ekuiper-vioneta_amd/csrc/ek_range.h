@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_range_members(const int64_t* __restr
     __shared__ unsigned long long s[kBlock / 64];
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = h;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && slot[blockIdx.x] >= 0) {   // slot -1: window not reported
         wmc[slot[blockIdx.x]] = b - a;
         wmh[slot[blockIdx.x]] = s[0] + s[1] + s[2] + s[3];
     }

@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 1
+EKGPU_ABI_VERSION = 2
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -73,6 +73,7 @@ class ek_plan(C.Structure):
         ("having_prog", ek_instr * EK_MAX_PROG),
         ("n_trigger", C.c_int32),
         ("trigger_prog", ek_instr * EK_MAX_PROG),
+        ("incremental", C.c_int32),
     ]
 
 

@@ -226,7 +226,7 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
 
 def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True, late_tolerance_ms: int = 0,
                  timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
-                 debug_membership: bool = False, nullable=()) -> CompiledRule:
+                 debug_membership: bool = False, nullable=(), incremental: bool = False) -> CompiledRule:
     """schema: ordered {column: "bigint" | "float" | "key"}; the TIMESTAMP column must be bigint (epoch ms)."""
     if len(schema) > A.EK_MAX_COLUMNS:
         raise RuleError("too many columns")
@@ -245,6 +245,9 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     plan.key_column = -1
     plan.num_keys = int(num_keys)
     plan.debug_membership = 1 if debug_membership else 0
+    # def.RuleOption.PlanOptimizeStrategy.EnableIncrementalWindow (def/rule.go:55-61); the engine applies the
+    # planner's own eligibility test (planner.go:910-1017) and keeps the regular path when it fails
+    plan.incremental = 1 if incremental else 0
     plan.nullable_mask = 0
     for name in nullable:
         plan.nullable_mask |= 1 << p.col(name)
@@ -377,4 +380,5 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     if key_col >= 0 and num_keys <= 0:
         raise RuleError("num_keys (dictionary size of the GROUP BY key) is required")
     return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
-                        options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms))
+                        options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms,
+                                     planOptimizeStrategy=dict(enableIncrementalWindow=bool(incremental))))

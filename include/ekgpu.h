@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 1
+#define EKGPU_ABI_VERSION 2
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -118,6 +118,15 @@ typedef struct {
     ek_instr having_prog[EK_MAX_PROG];
     int32_t n_trigger;            /* SLIDINGWINDOW(...) OVER (WHEN <prog>)                       */
     ek_instr trigger_prog[EK_MAX_PROG];
+    /* def.RuleOption.PlanOptimizeStrategy.EnableIncrementalWindow (def/rule.go:55-61): the planner's
+     * incremental-aggregation window (planner.go:905-997 rewriteIfIncAggStmt -> IncWindowPlan ->
+     * node.NewWindowIncAggOp, window_inc_agg_op.go:59-101 / window_inc_agg_event_op.go). Honoured for
+     * event-time TUMBLING/HOPPING and processing-time COUNTWINDOW(n) when every aggregate is one of
+     * count/sum/avg/min/max (function.IsSupportedIncAgg, funcs_inc_agg.go:28-41); with another aggregate
+     * the reference planner keeps the regular path and so does the engine. Inc semantics: windows are
+     * created by the events themselves (HoppingWindowIncAggEventOp.triggerWindow), each group reports
+     * the inc_* values computed at its last row, inc_sum / inc_avg are float64 (funcs_inc_agg.go:56-117). */
+    int32_t incremental;
 } ek_plan;
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };

@@ -499,6 +499,173 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
     v_push(&ob->st, status);
 }
 
+/* ------------------------------------------------------------------ incremental-aggregation windows
+ * The planner's opt-in incremental path (planner.go:905-997 rewriteIfIncAggStmt: every aggregate call becomes
+ * a scalar inc_<fn> whose running state lives per (window, dimension); node.NewWindowIncAggOp,
+ * window_inc_agg_op.go:59-101). Per row of a window, incAggCal (window_inc_agg_op.go:792-809) evaluates every
+ * inc_<fn> and OVERWRITES the dimension's Fields with the result, and keeps the row as LastRow; the window
+ * emits one row per dimension = LastRow + the Fields of its last evaluation (emit, :768-781). So a group's
+ * value is the one computed at its LAST row: a nil argument there makes the field nil (the builtin's `check`
+ * returnNilIfHasAnyNil skips exec, function.go:155-170, static_executor.go:59-71), and a nil row never
+ * updates the state. State rules (funcs_inc_agg.go:266-325): inc_count +1 per non-nil row -> int64;
+ * inc_sum float64 (cast.ToFloat64 CONVERT_ALL, first value taken as is, then prev + arg); inc_avg =
+ * inc_sum / inc_count (float64); inc_min / inc_max = min/max over [arg, prev] (funcs_agg.go:96-113). */
+typedef struct { int has; int lastnil; int64_t cnt; double fsum; val_t mm; } incstate;
+
+static void inc_step(const dataset* d, int fn, int c, int64_t row, incstate* s) {
+    if (fn == EK_AGG_COUNT_STAR) { s->cnt++; s->lastnil = 0; s->has = 1; return; }
+    val_t v = col_val(d, c, row);
+    if (v.tag == V_NULL) { s->lastnil = 1; return; }
+    s->lastnil = 0;
+    const double x = v.tag == V_F64 ? v.f : (double)v.i;
+    switch (fn) {
+    case EK_AGG_COUNT: s->cnt++; break;
+    case EK_AGG_SUM: case EK_AGG_AVG:
+        s->fsum = s->has ? s->fsum + x : x;
+        s->cnt++;
+        break;
+    case EK_AGG_MIN: case EK_AGG_MAX:
+        if (!s->has) s->mm = v;
+        else {
+            /* min/max(args) with args = [arg, prev] (funcs_inc_agg.go:234-264) */
+            int64_t iv[2] = {v.i, s->mm.i};
+            double fv[2] = {v.f, s->mm.f};
+            uint8_t nul[2] = {0, 0};
+            agg_out ao;
+            agg_eval(fn, v.tag == V_F64, 2, iv, fv, nul, 0.0, &ao);
+            s->mm.tag = ao.tag == EK_TAG_F64 ? V_F64 : V_I64;
+            s->mm.i = ao.i; s->mm.f = ao.f;
+        }
+        break;
+    }
+    s->has = 1;
+}
+
+static val_t inc_value(int fn, const incstate* s) {
+    val_t r; r.tag = V_NULL; r.i = 0; r.f = 0;
+    if (s->lastnil || !s->has) return r;
+    switch (fn) {
+    case EK_AGG_COUNT_STAR: case EK_AGG_COUNT: r.tag = V_I64; r.i = s->cnt; break;
+    case EK_AGG_SUM: r.tag = V_F64; r.f = s->fsum; break;
+    case EK_AGG_AVG: r.tag = V_F64; r.f = s->fsum / (double)s->cnt; break;
+    default: r = s->mm; break;
+    }
+    return r;
+}
+
+static int inc_supported_fn(int fn) {
+    return fn == EK_AGG_COUNT_STAR || fn == EK_AGG_COUNT || fn == EK_AGG_SUM || fn == EK_AGG_AVG || fn == EK_AGG_MIN ||
+           fn == EK_AGG_MAX;
+}
+
+/* One incremental window: content = the rows incAggCal added, in processing order. A window none of whose
+ * rows was added (created by a row outside its own range) is not reported. */
+static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc) {
+    const ek_plan* p = d->p;
+    if (nc == 0) return;
+    int64_t w = ob->ws.n;
+    v_push(&ob->ws, wstart);
+    v_push(&ob->we, wend);
+    v_push(&ob->roff, ob->key.n);
+    v_push(&ob->moff, ob->mem.n);
+    uint64_t h = 0;
+    for (int64_t k = 0; k < nc; ++k) { v_push(&ob->mem, content[k]); h += ek_mix64((uint64_t)content[k]); }
+    v_push(&ob->mcnt, nc);
+    v_push(&ob->mhash, (int64_t)h);
+    if (ob->werr_cap <= w) { ob->werr_cap = (w + 1) * 2; ob->werr = (char*)realloc(ob->werr, (size_t)ob->werr_cap * 128); }
+    ob->werr[w * 128] = 0;
+    int status = EK_WIN_OK;
+    int64_t rows_before = ob->key.n;
+    /* dimensions in first-appearance order (the reference iterates a Go map: unspecified order) */
+    int64_t cap = 16; while (cap < nc * 2) cap <<= 1;
+    int64_t* slot = (int64_t*)malloc((size_t)cap * 8);
+    int64_t* gkey = (int64_t*)malloc((size_t)nc * 8);
+    int64_t* glast = (int64_t*)malloc((size_t)nc * 8);
+    incstate* st = (incstate*)calloc((size_t)nc * (p->n_aggs ? p->n_aggs : 1), sizeof(incstate));
+    for (int64_t k = 0; k < cap; ++k) slot[k] = -1;
+    int64_t ng = 0;
+    for (int64_t k = 0; k < nc; ++k) {
+        int64_t g = 0;
+        if (p->key_column >= 0) {
+            val_t kv = col_val(d, p->key_column, content[k]);
+            int64_t key = kv.tag == V_NULL ? -1 : kv.i;
+            uint64_t hh = ek_mix64((uint64_t)key) & (uint64_t)(cap - 1);
+            while (slot[hh] >= 0 && gkey[slot[hh]] != key) hh = (hh + 1) & (uint64_t)(cap - 1);
+            if (slot[hh] < 0) { slot[hh] = ng; gkey[ng] = key; ng++; }
+            g = slot[hh];
+        } else {
+            if (ng == 0) { gkey[0] = 0; ng = 1; }
+        }
+        glast[g] = content[k];
+        for (int a = 0; a < p->n_aggs; ++a) inc_step(d, p->aggs[a].fn, p->aggs[a].column, content[k], &st[g * p->n_aggs + a]);
+    }
+    val_t aggv[EK_MAX_AGGS];
+    for (int64_t g = 0; g < ng; ++g) {
+        for (int a = 0; a < p->n_aggs; ++a) aggv[a] = inc_value(p->aggs[a].fn, &st[g * p->n_aggs + a]);
+        if (p->n_having > 0) {
+            /* HavingOp IsIncAgg branch (having_operator.go:73-98): evaluated on each emitted row */
+            val_t r = eval_prog(p->having_prog, p->n_having, d, glast[g], aggv);
+            if (r.tag != V_BOOL) {
+                status = EK_WIN_HAVING_ERROR;
+                snprintf(ob->werr + w * 128, 128, r.tag == V_ERR ? "run Having error: evaluation error"
+                                                                  : "run Having error: invalid condition that returns non-bool value");
+                break;
+            }
+            if (!r.i) continue;
+        }
+        v_push(&ob->key, gkey[g]);
+        for (int a = 0; a < p->n_aggs; ++a) {
+            int64_t bits = aggv[a].i;
+            if (aggv[a].tag == V_F64) memcpy(&bits, &aggv[a].f, 8);
+            v_push(&ob->aval[a], aggv[a].tag == V_NULL ? 0 : bits);
+            v_push(&ob->atag[a], aggv[a].tag == V_NULL ? EK_TAG_NULL : (aggv[a].tag == V_F64 ? EK_TAG_F64 : EK_TAG_I64));
+        }
+    }
+    if (status != EK_WIN_OK) {
+        ob->key.n = rows_before;
+        for (int a = 0; a < p->n_aggs; ++a) { ob->aval[a].n = rows_before; ob->atag[a].n = rows_before; }
+    }
+    free(slot); free(gkey); free(glast); free(st);
+    v_push(&ob->rcnt, ob->key.n - rows_before);
+    v_push(&ob->st, status);
+}
+
+/* HoppingWindowIncAggEventOp (window_inc_agg_event_op.go:26-146), also TUMBLING (:298-307, Length = Interval) */
+typedef struct { int64_t start; vec64 mem; } incwin;
+typedef struct {
+    const dataset* d;
+    outbuf* ob;
+    int64_t L, I;
+    int32_t raw_interval, unit, tz;
+    int has_T; int64_t T;      /* NextTriggerWindowTime (zero time before the first row) */
+    incwin* w; int64_t nw, cap;
+    int64_t* ts;
+} incop;
+
+static void inc_on_event(incop* o, int64_t e) {
+    const int64_t t = o->ts[e];
+    /* triggerWindow (:130-137): a row later than NextTriggerWindowTime opens [next - Interval, +Length) */
+    if (!o->has_T || o->T < t) {
+        o->T = eko_aligned_window_end(t, o->raw_interval, o->unit, o->tz);
+        o->has_T = 1;
+        if (o->nw == o->cap) { o->cap = o->cap ? 2 * o->cap : 16; o->w = (incwin*)realloc(o->w, (size_t)o->cap * sizeof(incwin)); }
+        memset(&o->w[o->nw], 0, sizeof(incwin));
+        o->w[o->nw++].start = o->T - o->I;
+    }
+    /* calIncAggWindow (:104-111): every open window whose [start, start + Length) holds t */
+    for (int64_t k = 0; k < o->nw; ++k)
+        if (o->w[k].start <= t && t < o->w[k].start + o->L) v_push(&o->w[k].mem, e);
+}
+
+static void inc_on_watermark(incop* o, int64_t wm) {
+    /* emitWindow (:113-119) then gcIncAggWindow (window_inc_agg_op.go:843-857) */
+    for (int64_t k = 0; k < o->nw; ++k)
+        if (o->w[k].start + o->L <= wm) emit_inc_window(o->d, o->ob, o->w[k].start, o->w[k].start + o->L, o->w[k].mem.a, o->w[k].mem.n);
+    int64_t g = 0;
+    while (g < o->nw && wm - o->w[g].start >= o->L) { free(o->w[g].mem.a); g++; }
+    if (g > 0) { memmove(o->w, o->w + g, (size_t)(o->nw - g) * sizeof(incwin)); o->nw -= g; }
+}
+
 /* ------------------------------------------------------------------ window operator (event time) */
 typedef struct {
     const dataset* d;
@@ -687,6 +854,20 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     dataset d = { p, n, columns, validity };
     outbuf ob; memset(&ob, 0, sizeof ob);
 
+    /* rewriteIfIncAggStmt (planner.go:910-997): every aggregate must be incremental, and the window type one of
+     * COUNT (without interval) / SLIDING / HOPPING / TUMBLING; otherwise the regular operator chain is planned */
+    int inc_ok = p->incremental != 0 && p->n_aggs > 0;
+    for (int a = 0; a < p->n_aggs; ++a) inc_ok &= inc_supported_fn(p->aggs[a].fn);
+    if (p->window_type == EK_WINDOW_COUNT && p->interval > 0) inc_ok = 0;
+    if (p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_NONE) inc_ok = 0;
+    if (inc_ok && (p->window_type == EK_WINDOW_SLIDING || (p->window_type == EK_WINDOW_COUNT && p->is_event_time))) {
+        set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding / event-time count windows are not restated"); return out->status;
+    }
+    if (inc_ok && p->n_where > 0) {
+        /* FilterPlan stays above IncWindowPlan (IncWindowPlan.PushDownPredicate keeps it): WHERE would filter the
+         * emitted last rows; not restated */
+        set_status(out, EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates is not restated"); return out->status;
+    }
     if (p->is_event_time) {
         /* NewEventTimeTrigger (event_window_trigger.go:35-53) */
         if (p->window_type == EK_WINDOW_COUNT || p->window_type > EK_WINDOW_COUNT || p->window_type < 0) {
@@ -695,6 +876,16 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "event time requires a timestamp column"); return out->status; }
         int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
         for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
+        const int inc = p->incremental && (p->window_type == EK_WINDOW_TUMBLING || p->window_type == EK_WINDOW_HOPPING) && inc_ok;
+        incop io; memset(&io, 0, sizeof io);
+        io.d = &d; io.ob = &ob; io.ts = ts;
+        {
+            int64_t uu = unit_ms(p->time_unit);
+            io.L = (int64_t)p->length * uu;
+            io.I = (int64_t)(p->window_type == EK_WINDOW_HOPPING ? p->interval : p->length) * uu;
+            io.raw_interval = p->window_type == EK_WINDOW_HOPPING ? p->interval : p->length;
+            io.unit = p->time_unit; io.tz = p->tz_offset_s;
+        }
         winop o; memset(&o, 0, sizeof o);
         o.d = &d; o.ob = &ob; o.wtype = p->window_type; o.ts = ts;
         int64_t u = unit_ms(p->time_unit);
@@ -723,13 +914,15 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                 if (wm >= ts[buf.a[0]]) {
                     int64_t c = buf.n;
                     for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
-                    for (int64_t k = 0; k < c; ++k) win_on_event(&o, buf.a[k]);
+                    for (int64_t k = 0; k < c; ++k) { if (inc) inc_on_event(&io, buf.a[k]); else win_on_event(&o, buf.a[k]); }
                     v_erase_front(&buf, c);
                 }
-                win_on_watermark(&o, wm);
+                if (inc) inc_on_watermark(&io, wm); else win_on_watermark(&o, wm);
                 last_wm = wm;
             }
         }
+        for (int64_t k = 0; k < io.nw; ++k) free(io.w[k].mem.a);
+        free(io.w);
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
     } else {
@@ -775,7 +968,9 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
             if (msg % itv != 0) continue;
             msg = 0;
             if (inputs.n >= len) {
-                emit_window(&d, &ob, 0, 0, inputs.a + (inputs.n - len), len);  /* wall-clock range: not comparable */
+                /* CountWindowIncAggOp (window_inc_agg_op.go:239-314): the same consecutive blocks of len rows */
+                if (inc_ok) emit_inc_window(&d, &ob, 0, 0, inputs.a + (inputs.n - len), len);
+                else emit_window(&d, &ob, 0, 0, inputs.a + (inputs.n - len), len);  /* wall-clock range: not comparable */
                 v_erase_front(&inputs, inputs.n - len + 1);
             }
         }
