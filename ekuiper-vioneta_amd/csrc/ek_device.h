@@ -45,6 +45,9 @@ struct DPlan {
     int32_t sagg_scol[kMaxSortAggs];
     int32_t sagg_agg[kMaxSortAggs];
     int32_t inc;                  // incremental-window semantics (inc_sum / inc_avg float64, funcs_inc_agg.go:56-117)
+    int32_t n_begin, n_emit;      // STATEWINDOW(begin, emit) conditions (window_v2_op.go:111-148)
+    ek_instr begin_prog[EK_MAX_PROG];
+    ek_instr emit_prog[EK_MAX_PROG];
 };
 
 // Columns of one micro-batch (device pointers).

@@ -264,10 +264,12 @@ struct Engine {
         if (plan.n_columns <= 0 || plan.n_columns > EK_MAX_COLUMNS) return fail(EK_ERR_INVALID, "bad n_columns");
         if (plan.n_aggs < 0 || plan.n_aggs > EK_MAX_AGGS) return fail(EK_ERR_INVALID, "bad n_aggs");
         if (plan.n_where < 0 || plan.n_where > EK_MAX_PROG || plan.n_having < 0 || plan.n_having > EK_MAX_PROG ||
-            plan.n_trigger < 0 || plan.n_trigger > EK_MAX_PROG)
+            plan.n_trigger < 0 || plan.n_trigger > EK_MAX_PROG || plan.n_begin < 0 || plan.n_begin > EK_MAX_PROG ||
+            plan.n_emit < 0 || plan.n_emit > EK_MAX_PROG)
             return fail(EK_ERR_INVALID, "bad program length");
         if (!prog_depth_ok(plan.where_prog, plan.n_where) || !prog_depth_ok(plan.having_prog, plan.n_having) ||
-            !prog_depth_ok(plan.trigger_prog, plan.n_trigger))
+            !prog_depth_ok(plan.trigger_prog, plan.n_trigger) || !prog_depth_ok(plan.begin_prog, plan.n_begin) ||
+            !prog_depth_ok(plan.emit_prog, plan.n_emit))
             return fail(EK_ERR_INVALID, "malformed expression program");
         for (int c = 0; c < plan.n_columns; ++c)
             if (plan.column_type[c] < EK_COL_I64 || plan.column_type[c] > EK_COL_U32) return fail(EK_ERR_INVALID, "bad column type %d", c);
@@ -275,6 +277,15 @@ struct Engine {
         for (int k = 0; k < plan.n_where; ++k)
             if (plan.where_prog[k].op == EK_OP_COL && !col_ok(plan.where_prog[k].arg)) return fail(EK_ERR_INVALID, "WHERE column out of range");
             else if (plan.where_prog[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in WHERE");
+        for (const ek_instr* pr : {plan.trigger_prog, plan.begin_prog, plan.emit_prog})
+            for (int k = 0; k < EK_MAX_PROG; ++k) {
+                const int n = pr == plan.trigger_prog ? plan.n_trigger : pr == plan.begin_prog ? plan.n_begin : plan.n_emit;
+                if (k >= n) break;
+                if (pr[k].op == EK_OP_COL && !col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "condition column out of range");
+                if (pr[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in a window condition");
+            }
+        if (plan.window_version != 0 && plan.window_version != 1 && plan.window_type != EK_WINDOW_STATE)
+            return fail(EK_ERR_UNSUPPORTED, "window version %d (WindowV2Operator) is built for STATEWINDOW only", plan.window_version);
         for (int k = 0; k < plan.n_having; ++k) {
             if (plan.having_prog[k].op == EK_OP_COL) return fail(EK_ERR_UNSUPPORTED, "non-aggregate column in HAVING");
             if (plan.having_prog[k].op == EK_OP_AGG && (plan.having_prog[k].arg < 0 || plan.having_prog[k].arg >= plan.n_aggs))
@@ -310,7 +321,13 @@ struct Engine {
             reset_state();
             return 0;
         }
-        if (plan.is_event_time) {
+        if (wtype == EK_WINDOW_STATE) {
+            // WindowV2Operator / StateWindowOp (window_v2_op.go:39-58,94-148): rows in arrival order (processing
+            // time) or in WatermarkOp release order (event time); no time grid. WHERE is pushed below a
+            // processing-time window (windowPlan.go:82-99) and then decides which rows reach the conditions
+            if (!plan.is_event_time && plan.n_where > 0)
+                return fail(EK_ERR_UNSUPPORTED, "WHERE below a processing-time STATEWINDOW (pushed-down filter) is not built");
+        } else if (plan.is_event_time) {
             // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time
             if (wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
         } else if (wtype != EK_WINDOW_COUNT) {
@@ -338,7 +355,8 @@ struct Engine {
                 if (plan.aggs[k].fn != EK_AGG_COUNT_STAR && ((plan.nullable_mask >> plan.aggs[k].column) & 1u))
                     return fail(EK_ERR_UNSUPPORTED, "incremental aggregates over a nullable column (nil at a group's last row) are not built");
         }
-        range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT || sort_aggs ||
+        range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT ||
+                     wtype == EK_WINDOW_STATE || sort_aggs ||
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         need_rel = wtype == EK_WINDOW_SLIDING;
         if (plan.is_event_time) {
@@ -352,8 +370,10 @@ struct Engine {
             if (plan.num_keys == 0) return fail(EK_ERR_INVALID, "num_keys must be > 0");
             if (plan.nullable_mask & (1u << plan.key_column)) return fail(EK_ERR_UNSUPPORTED, "nullable GROUP BY key");
         }
-        if (plan.length <= 0) return fail(EK_ERR_INVALID, "Window size should not be less than zero.");
-        if (wtype == EK_WINDOW_COUNT) {
+        if (plan.length <= 0 && wtype != EK_WINDOW_STATE) return fail(EK_ERR_INVALID, "Window size should not be less than zero.");
+        if (wtype == EK_WINDOW_STATE) {
+            L = H = P = 1;   // no time grid
+        } else if (wtype == EK_WINDOW_COUNT) {
             // window_op.go:100-103: CountInterval defaults to CountLength
             if (plan.interval < 0) return fail(EK_ERR_INVALID, "count window interval must be >= 0");
             L = plan.length;
@@ -395,6 +415,12 @@ struct Engine {
         memcpy(dp.where_prog, plan.where_prog, sizeof plan.where_prog);
         memcpy(dp.having_prog, plan.having_prog, sizeof plan.having_prog);
         memcpy(dp.trigger_prog, plan.trigger_prog, sizeof plan.trigger_prog);
+        if (wtype == EK_WINDOW_STATE) {
+            dp.n_begin = plan.n_begin;
+            dp.n_emit = plan.n_emit;
+            memcpy(dp.begin_prog, plan.begin_prog, sizeof plan.begin_prog);
+            memcpy(dp.emit_prog, plan.emit_prog, sizeof plan.emit_prog);
+        }
         dp.n_aggs = plan.n_aggs;
         dp.inc = inc ? 1 : 0;
         for (int k = 0; k < plan.n_aggs; ++k) {
@@ -622,6 +648,8 @@ struct Engine {
         h_rts_base = 0;
         sess_last_ticked = sess_has_trigger = false;
         sess_trigger = 0;
+        st_on = false;
+        st_start_abs = 0;
         count_k = 1;
         inc_has_T = false;
         inc_T = 0;
@@ -1229,6 +1257,9 @@ struct Engine {
     bool sess_last_ticked = false, sess_has_trigger = false;
     int64_t sess_trigger = 0;
     int64_t count_k = 1;               // COUNTWINDOW: next window index
+    // STATEWINDOW (StateWindowOp.onBegin): a window is open from absolute stream position st_start_abs
+    bool st_on = false;
+    int64_t st_start_abs = 0;
     // incremental-aggregation windows (window_inc_agg_event_op.go:26-146): NextTriggerWindowTime and the
     // windows opened by rows but not emitted yet (creation order == end order)
     bool inc = false;
@@ -1660,8 +1691,71 @@ struct Engine {
             }
         } else if (wtype == EK_WINDOW_SESSION) {
             if (int rc = session_triggers(rel_prev, pw)) return rc;
+        } else if (wtype == EK_WINDOW_STATE) {
+            return state_scan(rel_prev, eb_rel);
         }
         return fire_windows(pw);
+    }
+
+    // ---- STATEWINDOW (StateWindowOp.exec, window_v2_op.go:111-148) over buffer rows [lo, hi), in order:
+    //   if no window is open, a row whose begin condition holds opens one (canBegin);
+    //   a row of an open window joins it; if its emit condition holds the window [start, row] is emitted and closed;
+    //   a row that opened AND closed a window re-opens one at once (`if canBegin && !s.onBegin`), starting at the next row.
+    // Only rows whose begin or emit condition holds can change the state: the device evaluates both conditions,
+    // compacts those rows, and the host walks them.
+    int state_scan(int64_t lo, int64_t hi) {
+        std::vector<PendWin> pw;
+        const int64_t n_new = hi - lo;
+        if (n_new > 0) {
+            if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
+            if (int rc = ensure(trig_d, (size_t)n_new * 8)) return rc;
+            const int nb = (int)((n_new + kCompactTile - 1) / kCompactTile);
+            if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+            const DBatch bv = buffer_view();
+            const int g = (int)std::min<int64_t>(4096, (n_new + 255) / 256);
+            hipLaunchKernelGGL(k_state_flags, dim3(g), dim3(256), 0, stream, d_plan, bv, lo, hi, (uint8_t*)flags_d.p);
+            hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new, (int64_t*)cnts_d.p);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+            hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new,
+                               (const int64_t*)cnts_d.p, lo, (int64_t*)trig_d.p);
+            const int64_t nt = fetch_i64((const int64_t*)cnts_d.p + nb);
+            if (nt > 0) {
+                std::vector<int64_t> pos(nt);
+                std::vector<uint8_t> fl(nt);
+                if (int rc = ensure(mrg_col, (size_t)nt)) return rc;
+                const int gg = (int)std::min<int64_t>(4096, (nt + 255) / 256);
+                hipLaunchKernelGGL(k_gather_flags, dim3(gg), dim3(256), 0, stream, (const int64_t*)trig_d.p, nt, lo,
+                                   (const uint8_t*)flags_d.p, (uint8_t*)mrg_col.p);
+                hipMemcpyAsync(pos.data(), trig_d.p, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                hipMemcpyAsync(fl.data(), mrg_col.p, (size_t)nt, hipMemcpyDeviceToHost, stream);
+                if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "state condition copy failed");
+                for (int64_t k = 0; k < nt; ++k) {
+                    const int64_t i = pos[k];
+                    bool can_begin = false;
+                    if (!st_on) {
+                        can_begin = (fl[k] & 1) != 0;
+                        if (!can_begin) continue;
+                        st_on = true;
+                        st_start_abs = eb_base + i;
+                    }
+                    if (fl[k] & 2) {
+                        PendWin p{};
+                        p.q.kind = RB_FIXED;
+                        p.q.pos = st_start_abs - eb_base;
+                        p.q.rstep = i + 1;
+                        p.start = EK_STATE_WINDOW_START_MS;
+                        p.end = EK_STATE_WINDOW_END_MS;
+                        pw.push_back(p);
+                        st_on = can_begin;   // opened and closed by this row: the next window starts at the next row
+                        st_start_abs = eb_base + i + 1;
+                    }
+                }
+            }
+        }
+        int rc = fire_windows(pw);
+        // rows before the open window (or every scanned row) are never needed again (scanner.gc(InfTime))
+        eb_floor = std::max(eb_floor, st_on ? st_start_abs - eb_base : hi);
+        return rc;
     }
 
     // ---- incremental-aggregation windows, event time (HoppingWindowIncAggEventOp, window_inc_agg_event_op.go:71-146;
@@ -1989,6 +2083,15 @@ struct Engine {
             const int rc = push_count(db);
             return rc ? rc : record_time();
         }
+        if (wtype == EK_WINDOW_STATE && !plan.is_event_time) {
+            // processing time: the rows reach StateWindowOp in arrival order
+            if (int rc = eb_append(db, 0, n, arrivals)) return rc;
+            arrivals += n;
+            const int64_t lo = eb_rel;
+            eb_rel = eb.n;
+            const int rc = state_scan(lo, eb_rel);
+            return rc ? rc : record_time();
+        }
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
 
         // ---- 1. batch statistics (one pass over ts)
@@ -2204,7 +2307,7 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 1;
+    static constexpr int64_t kStateVersion = 2;
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -2235,6 +2338,10 @@ struct Engine {
         prog(plan.where_prog, plan.n_where);
         prog(plan.having_prog, plan.n_having);
         prog(plan.trigger_prog, plan.n_trigger);
+        if (wtype == EK_WINDOW_STATE) {
+            prog(plan.begin_prog, plan.n_begin);
+            prog(plan.emit_prog, plan.n_emit);
+        }
         i32(range_mode ? 1 : 0);
         return h;
     }
@@ -2354,6 +2461,8 @@ struct Engine {
             s.i64(inc_T);
             s.i64((int64_t)inc_pend.size());
             s.put(inc_pend.data(), inc_pend.size() * sizeof(IncWin));
+            s.i64(st_on ? 1 : 0);                                             // state window: onBegin + its first row
+            s.i64(st_start_abs);
         }
         *size = (int64_t)s.b.size();
         if (!buf) return 0;
@@ -2462,6 +2571,8 @@ struct Engine {
             if (!r.ok || ni < 0 || ni > size) return fail(EK_ERR_INVALID, "bad incremental windows in state blob");
             inc_pend.resize((size_t)ni);
             r.read(inc_pend.data(), ni * (int64_t)sizeof(IncWin));
+            st_on = r.i64() != 0;
+            st_start_abs = r.i64();
         }
         return 0;
     }

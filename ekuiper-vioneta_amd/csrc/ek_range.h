@@ -114,6 +114,35 @@ __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, in
     }
 }
 
+// STATEWINDOW conditions of rows [i0, i1) of the buffer (isMatchCondition, window_v2_op.go:212-238: nil, an
+// error or a non-bool is false): bit 0 = begin condition true, bit 1 = emit condition true
+__global__ void k_state_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {
+    const DPlan& p = *pp;
+    for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
+        uint8_t f = 0;
+        if (p.n_begin > 0) {
+            const Val v = eval_prog(p.begin_prog, p.n_begin, p, &b, i, NoAggs{});
+            f |= (v.tag == V_BOOL && v.i) ? 1 : 0;
+        } else {
+            f |= 1;
+        }
+        if (p.n_emit > 0) {
+            const Val v = eval_prog(p.emit_prog, p.n_emit, p, &b, i, NoAggs{});
+            f |= (v.tag == V_BOOL && v.i) ? 2 : 0;
+        } else {
+            f |= 2;
+        }
+        flags[i - i0] = f;
+    }
+}
+
+// gather of the flag bytes at compacted positions (positions are absolute: base_idx + i)
+__global__ void k_gather_flags(const int64_t* __restrict__ pos, int64_t n, int64_t base_idx, const uint8_t* __restrict__ flags,
+                               uint8_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = flags[pos[k] - base_idx];
+}
+
 // FilterOp over a window-less batch (filter_operator.go:36-90): 1 keep; nil/false drop; error drop + count
 __global__ void k_filter_flags(DPlan* __restrict__ pp, DBatch b, uint8_t* __restrict__ flags, unsigned long long* n_err) {
     const DPlan& p = *pp;

@@ -5,13 +5,16 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 2
+EKGPU_ABI_VERSION = 3
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
 
 # window types == pkg/ast/statement.go:185-193
-EK_WINDOW_NONE, EK_WINDOW_TUMBLING, EK_WINDOW_HOPPING, EK_WINDOW_SLIDING, EK_WINDOW_SESSION, EK_WINDOW_COUNT = range(6)
+(EK_WINDOW_NONE, EK_WINDOW_TUMBLING, EK_WINDOW_HOPPING, EK_WINDOW_SLIDING, EK_WINDOW_SESSION, EK_WINDOW_COUNT,
+ EK_WINDOW_STATE) = range(7)
+# state windows: WindowRange [time.Time{}, InfTime] in ms (window_v2_op.go:30,111-148)
+EK_STATE_WINDOW_START_MS, EK_STATE_WINDOW_END_MS = -62135596800000, -62135596800001
 # time units (pkg/ast/token.go:117-121)
 EK_UNIT_DD, EK_UNIT_HH, EK_UNIT_MI, EK_UNIT_SS, EK_UNIT_MS = 1, 2, 3, 4, 5
 UNIT_BY_NAME = {"dd": EK_UNIT_DD, "hh": EK_UNIT_HH, "mi": EK_UNIT_MI, "ss": EK_UNIT_SS, "ms": EK_UNIT_MS}
@@ -74,6 +77,11 @@ class ek_plan(C.Structure):
         ("n_trigger", C.c_int32),
         ("trigger_prog", ek_instr * EK_MAX_PROG),
         ("incremental", C.c_int32),
+        ("window_version", C.c_int32),
+        ("n_begin", C.c_int32),
+        ("begin_prog", ek_instr * EK_MAX_PROG),
+        ("n_emit", C.c_int32),
+        ("emit_prog", ek_instr * EK_MAX_PROG),
     ]
 
 

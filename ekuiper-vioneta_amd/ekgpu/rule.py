@@ -29,6 +29,7 @@ WINDOW_TYPES = {
     "slidingwindow": A.EK_WINDOW_SLIDING,
     "sessionwindow": A.EK_WINDOW_SESSION,
     "countwindow": A.EK_WINDOW_COUNT,
+    "statewindow": A.EK_WINDOW_STATE,
 }
 _CMP = {"=": A.EK_OP_EQ, "!=": A.EK_OP_NEQ, "<>": A.EK_OP_NEQ, "<": A.EK_OP_LT, "<=": A.EK_OP_LTE,
         ">": A.EK_OP_GT, ">=": A.EK_OP_GTE}
@@ -226,7 +227,8 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
 
 def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True, late_tolerance_ms: int = 0,
                  timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
-                 debug_membership: bool = False, nullable=(), incremental: bool = False) -> CompiledRule:
+                 debug_membership: bool = False, nullable=(), incremental: bool = False,
+                 window_version: str = "") -> CompiledRule:
     """schema: ordered {column: "bigint" | "float" | "key"}; the TIMESTAMP column must be bigint (epoch ms)."""
     if len(schema) > A.EK_MAX_COLUMNS:
         raise RuleError("too many columns")
@@ -248,6 +250,8 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     # def.RuleOption.PlanOptimizeStrategy.EnableIncrementalWindow (def/rule.go:55-61); the engine applies the
     # planner's own eligibility test (planner.go:910-1017) and keeps the regular path when it fails
     plan.incremental = 1 if incremental else 0
+    # planOptimizeStrategy.windowOption.windowVersion (def/rule.go:68-76; planner.go:416-425)
+    plan.window_version = 2 if window_version == "v2" else 0
     plan.nullable_mask = 0
     for name in nullable:
         plan.nullable_mask |= 1 << p.col(name)
@@ -293,6 +297,7 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
         where = p.expr(False)
     key_col = -1
     trigger = []
+    begin, emit = [], []
     wtype = A.EK_WINDOW_NONE
     if p.kw("group"):
         p.expect("by")
@@ -303,6 +308,16 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                 p.i += 1
                 p.expect("(")
                 nums = []
+                if wtype == A.EK_WINDOW_STATE:
+                    # STATEWINDOW(<begin condition>, <emit condition>) (parser.go:1047-1053,1119-1124)
+                    begin = p.expr(False)
+                    p.expect(",")
+                    emit = p.expr(False)
+                    p.expect(")")
+                    if p.peek() == ",":
+                        p.i += 1
+                        continue
+                    break
                 if wtype != A.EK_WINDOW_COUNT:
                     unit = p.peek().lower()
                     if unit not in A.UNIT_BY_NAME:
@@ -377,8 +392,11 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     plan.n_where = _fill_prog(plan.where_prog, where)
     plan.n_having = _fill_prog(plan.having_prog, having)
     plan.n_trigger = _fill_prog(plan.trigger_prog, trigger)
+    plan.n_begin = _fill_prog(plan.begin_prog, begin)
+    plan.n_emit = _fill_prog(plan.emit_prog, emit)
     if key_col >= 0 and num_keys <= 0:
         raise RuleError("num_keys (dictionary size of the GROUP BY key) is required")
     return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
                         options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms,
-                                     planOptimizeStrategy=dict(enableIncrementalWindow=bool(incremental))))
+                                     planOptimizeStrategy=dict(enableIncrementalWindow=bool(incremental),
+                                                               windowOption=dict(windowVersion=window_version))))

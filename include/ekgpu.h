@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 2
+#define EKGPU_ABI_VERSION 3
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -38,8 +38,14 @@ enum {
     EK_WINDOW_HOPPING = 2,
     EK_WINDOW_SLIDING = 3,
     EK_WINDOW_SESSION = 4,
-    EK_WINDOW_COUNT = 5
+    EK_WINDOW_COUNT = 5,
+    EK_WINDOW_STATE = 6         /* STATEWINDOW(begin, emit): WindowV2Operator only (window_v2_op.go:94-148) */
 };
+
+/* WindowRange reported by a state window (window_v2_op.go:111-148 emitWindow(time.Time{}, InfTime)):
+ * time.Time{}.UnixMilli() and InfTime.UnixMilli() (window_v2_op.go:30, the int64 product wraps in Go). */
+#define EK_STATE_WINDOW_START_MS (-62135596800000LL)
+#define EK_STATE_WINDOW_END_MS (-62135596800001LL)
 
 /* Time units of the window literal (pkg/ast/token.go:117-121: DD, HH, MI, SS, MS). */
 enum { EK_UNIT_DD = 1, EK_UNIT_HH = 2, EK_UNIT_MI = 3, EK_UNIT_SS = 4, EK_UNIT_MS = 5 };
@@ -127,6 +133,21 @@ typedef struct {
      * created by the events themselves (HoppingWindowIncAggEventOp.triggerWindow), each group reports
      * the inc_* values computed at its last row, inc_sum / inc_avg are float64 (funcs_inc_agg.go:56-117). */
     int32_t incremental;
+    /* def.RuleOption.PlanOptimizeStrategy.WindowOption.WindowVersion (def/rule.go:68-76): 2 selects
+     * node.NewWindowV2Op (planner.go:416-425). EK_WINDOW_STATE exists only there and is accepted with any
+     * value; for the other window types only 0/1 (the regular WindowOperator) is built. */
+    int32_t window_version;
+    /* STATEWINDOW(<begin>, <emit>) (parser.go:1047-1053,1119-1124; StateWindowOp.exec, window_v2_op.go:111-148).
+     * Rows are taken in arrival order (processing time) or release order (event time: after WatermarkOp).
+     * While no window is open, a row whose begin condition is true opens one; every row of an open window
+     * joins it and a row whose emit condition is true closes it and emits the rows since the opening row
+     * (WindowRange = [time.Time{}, InfTime] in ms: -62135596800000, -62135596800001 after Go's int64 wrap).
+     * A row that both opens and closes a window opens the next one at the following row. A nil, non-bool
+     * or failing condition is false (isMatchCondition, window_v2_op.go:212-238). */
+    int32_t n_begin;
+    ek_instr begin_prog[EK_MAX_PROG];
+    int32_t n_emit;
+    ek_instr emit_prog[EK_MAX_PROG];
 } ek_plan;
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };

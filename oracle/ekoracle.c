@@ -839,6 +839,48 @@ static void win_on_watermark(winop* o, int64_t wm) {
     o->next_end = we;
 }
 
+/* ------------------------------------------------------------------ state window (WindowV2Operator) */
+/* StateWindowOp.exec (window_v2_op.go:111-148); rows arrive in arrival order (processing time) or in
+ * WatermarkOp release order (event time; watermark tuples are ignored by this op). */
+typedef struct {
+    const dataset* d;
+    outbuf* ob;
+    int on;                    /* onBegin */
+    vec64 rows;                /* WindowScanner.tuples */
+    const int64_t* ts;         /* event time: row timestamps; NULL in processing time */
+} stateop;
+
+/* isMatchCondition (window_v2_op.go:212-238): nil condition -> true; nil / error / non-bool result -> false */
+static int cond_true(const dataset* d, const ek_instr* prog, int n, int64_t e) {
+    if (n <= 0) return 1;
+    val_t r = eval_prog(prog, n, d, e, NULL);
+    return r.tag == V_BOOL && r.i;
+}
+
+static void state_on_row(stateop* o, int64_t e) {
+    const ek_plan* p = o->d->p;
+    int can_begin = 0, can_emit = 0;
+    if (!o->on) {
+        can_begin = cond_true(o->d, p->begin_prog, p->n_begin, e);
+        if (can_begin) o->on = 1;
+    }
+    if (o->on) {
+        v_push(&o->rows, e);
+        can_emit = cond_true(o->d, p->emit_prog, p->n_emit, e);
+    }
+    if (o->on && can_emit) {
+        /* emitWindow(time.Time{}, InfTime) -> scanWindow (window_v2_op.go:75-87,252-263): rows with a timestamp
+         * after time.Time{} (processing-time rows carry the ingest wall clock) */
+        int64_t nc = 0;
+        for (int64_t k = 0; k < o->rows.n; ++k)
+            if (!o->ts || o->ts[o->rows.a[k]] > ZERO_MS) o->rows.a[nc++] = o->rows.a[k];
+        emit_window(o->d, o->ob, EK_STATE_WINDOW_START_MS, EK_STATE_WINDOW_END_MS, o->rows.a, nc);
+        o->rows.n = 0;          /* scanner.gc(InfTime) */
+        o->on = 0;
+    }
+    if (can_begin && !o->on) o->on = 1;
+}
+
 /* ------------------------------------------------------------------ driver */
 static void set_status(eko_output* out, int st, const char* msg) {
     out->status = st;
@@ -859,7 +901,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     int inc_ok = p->incremental != 0 && p->n_aggs > 0;
     for (int a = 0; a < p->n_aggs; ++a) inc_ok &= inc_supported_fn(p->aggs[a].fn);
     if (p->window_type == EK_WINDOW_COUNT && p->interval > 0) inc_ok = 0;
-    if (p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_NONE) inc_ok = 0;
+    if (p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_NONE || p->window_type == EK_WINDOW_STATE) inc_ok = 0;
     if (inc_ok && (p->window_type == EK_WINDOW_SLIDING || (p->window_type == EK_WINDOW_COUNT && p->is_event_time))) {
         set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding / event-time count windows are not restated"); return out->status;
     }
@@ -868,9 +910,16 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
          * emitted last rows; not restated */
         set_status(out, EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates is not restated"); return out->status;
     }
+    if (p->window_type == EK_WINDOW_STATE && !p->is_event_time && p->n_where > 0) {
+        /* windowPlan.PushDownPredicate (windowPlan.go:82-99) moves WHERE below a processing-time window */
+        set_status(out, EK_ERR_UNSUPPORTED, "pushed-down WHERE below a processing-time state window is not restated"); return out->status;
+    }
+    stateop so; memset(&so, 0, sizeof so);
+    so.d = &d; so.ob = &ob;
     if (p->is_event_time) {
-        /* NewEventTimeTrigger (event_window_trigger.go:35-53) */
-        if (p->window_type == EK_WINDOW_COUNT || p->window_type > EK_WINDOW_COUNT || p->window_type < 0) {
+        /* NewEventTimeTrigger (event_window_trigger.go:35-53); STATEWINDOW runs in WindowV2Operator (window_v2_op.go:39-58) */
+        if ((p->window_type == EK_WINDOW_COUNT || p->window_type > EK_WINDOW_COUNT || p->window_type < 0) &&
+            p->window_type != EK_WINDOW_STATE) {
             set_status(out, EK_ERR_UNSUPPORTED, "unsupported window type"); return out->status;
         }
         if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "event time requires a timestamp column"); return out->status; }
@@ -888,6 +937,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         }
         winop o; memset(&o, 0, sizeof o);
         o.d = &d; o.ob = &ob; o.wtype = p->window_type; o.ts = ts;
+        so.ts = ts;
         int64_t u = unit_ms(p->time_unit);
         o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = (int64_t)p->delay * u;
         o.raw_interval = (p->window_type == EK_WINDOW_HOPPING) ? p->interval : p->length; /* planner.go:394-400 */
@@ -914,10 +964,15 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                 if (wm >= ts[buf.a[0]]) {
                     int64_t c = buf.n;
                     for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
-                    for (int64_t k = 0; k < c; ++k) { if (inc) inc_on_event(&io, buf.a[k]); else win_on_event(&o, buf.a[k]); }
+                    for (int64_t k = 0; k < c; ++k) {
+                        if (p->window_type == EK_WINDOW_STATE) state_on_row(&so, buf.a[k]);
+                        else if (inc) inc_on_event(&io, buf.a[k]);
+                        else win_on_event(&o, buf.a[k]);
+                    }
                     v_erase_front(&buf, c);
                 }
-                if (inc) inc_on_watermark(&io, wm); else win_on_watermark(&o, wm);
+                if (p->window_type == EK_WINDOW_STATE) { /* WatermarkTuple: no effect on StateWindowOp */ }
+                else if (inc) inc_on_watermark(&io, wm); else win_on_watermark(&o, wm);
                 last_wm = wm;
             }
         }
@@ -925,6 +980,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         free(io.w);
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
+    } else if (p->window_type == EK_WINDOW_STATE) {
+        for (int64_t i = 0; i < n; ++i) state_on_row(&so, i);
     } else {
         if (p->window_type == EK_WINDOW_NONE) {
             /* window-less rule: FilterOp.Apply per event (filter_operator.go:36-90) + SELECT * projection.
@@ -978,6 +1035,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         }
     }
 
+    free(so.rows.a);
     out->r.n_windows = ob.ws.n;
     out->r.n_rows = ob.key.n;
     out->r.n_aggs = p->window_type == EK_WINDOW_NONE ? p->n_columns : p->n_aggs;

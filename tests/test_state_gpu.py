@@ -71,6 +71,12 @@ CASES = [
      lambda: _with_trig(_iot(30_000, 30, seed=85, epm=3), 300), 0.5),
     ("count_window", "SELECT deviceId, avg(temperature), count(*) FROM demo GROUP BY deviceId, COUNTWINDOW(700, 300)",
      IOT_SCHEMA, dict(num_keys=60, is_event_time=False), lambda: _iot(20_000, 60, seed=86, epm=10), 0.43),
+    ("state_window_proc", "SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo "
+     "GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 99)", TRIG_SCHEMA,
+     dict(num_keys=100, is_event_time=False), lambda: _with_trig(_iot(40_000, 100, seed=88, epm=10), 300), 0.52),
+    ("state_window_event", "SELECT deviceId, count(*), min(temperature) FROM demo "
+     "GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 98)", TRIG_SCHEMA,
+     dict(num_keys=100, late_tolerance_ms=200), lambda: _with_trig(_iot(40_000, 100, seed=89, epm=5), 200), 0.47),
     ("median_range", "SELECT deviceId, median(temperature), percentile_disc(humidity, 0.5), count(*) FROM demo "
      "GROUP BY deviceId, TUMBLINGWINDOW(ss, 2)", IOT_SCHEMA, dict(num_keys=200),
      lambda: _iot(60_000, 200, seed=87, epm=5), 0.71),

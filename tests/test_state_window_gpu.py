@@ -1,0 +1,91 @@
+"""GPU parity of STATEWINDOW(begin, emit) (WindowV2Operator / StateWindowOp, window_v2_op.go:94-148) against the
+CPU oracle: the reference KAT (window_v2_op_test.go:40-91), the re-open chain, randomized processing-time and
+event-time streams (out of order, late tolerance, WHERE above the window, HAVING, order statistics), split batches."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ekgpu import abi as A
+from ekgpu.rule import compile_rule
+from parity import assert_windows_equal
+from test_engine_gpu import engine_mod, run_both  # noqa: F401  (fixture + helper)
+from test_range_gpu import TRIG_SCHEMA, _iot, _with_trig
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_state_window_kat_engine(oracle, engine_mod):
+    g = json.load(open(os.path.join(GOLD, "kat_state_window.json")))
+    for case in g["tests"]:
+        a = np.array([r["a"] for r in case["rows"]], np.int64)
+        rule = compile_rule(case["sql"].replace("stream", "demo"), {"a": "bigint"}, is_event_time=False,
+                            debug_membership=True)
+        for batches in (1, len(a)):
+            got, exp, _ = run_both(oracle, engine_mod, rule, [a], batches=batches)
+            assert len(got) == len(case["windows"])
+            assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+            assert got[0].value(0, 0) == len(case["windows"][0]["content"])
+
+
+def test_state_window_reopen_chain_engine(oracle, engine_mod):
+    a = np.array([0, 7, 3, 9, 2, 6, 1, 8, 8, 0, 2, 2, 7], np.int64)
+    rule = compile_rule("SELECT count(*), sum(a), min(a) FROM demo GROUP BY STATEWINDOW(a > 1, a > 5)", {"a": "bigint"},
+                        is_event_time=False, debug_membership=True)
+    for batches in (1, 4, len(a)):
+        got, exp, _ = run_both(oracle, engine_mod, rule, [a], batches=batches)
+        assert len(got) == len(exp.windows) == 6
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("batches", [1, 13])
+def test_state_window_processing_time(oracle, engine_mod, batches):
+    sql = ("SELECT deviceId, count(*), sum(temperature), min(humidity), max(temperature), stddev(temperature) FROM demo "
+           "GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 99)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=500, is_event_time=False, debug_membership=True)
+    cols = _with_trig(_iot(200_000, 500, seed=91, epm=10), 400)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert len(got) > 100
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_state_window_order_statistics(oracle, engine_mod):
+    sql = ("SELECT deviceId, median(temperature), percentile_disc(humidity, 0.25), count(*) FROM demo "
+           "GROUP BY deviceId, STATEWINDOW(trig = 1, temperature > 99.8)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=300, is_event_time=False, debug_membership=True)
+    cols = _with_trig(_iot(100_000, 300, seed=92, epm=10), 250)
+    for batches in (1, 7):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) > 20
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("batches", [1, 9])
+def test_state_window_event_time_out_of_order(oracle, engine_mod, batches):
+    """Event time: rows reach the state window in WatermarkOp release order; WHERE stays above the window
+    (windowPlan.go:82-99), HAVING after the aggregate."""
+    sql = ("SELECT deviceId, count(*), avg(temperature), max(humidity) FROM demo WHERE temperature > 5 "
+           "GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 98) HAVING count(*) > 1")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=200, late_tolerance_ms=300, debug_membership=True)
+    cols = _with_trig(_iot(60_000, 200, seed=93, epm=4), 200)
+    rng = np.random.default_rng(11)
+    cols[1] = (cols[1] + rng.integers(-500, 500, len(cols[1]))).astype(np.int64)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert exp.records_late > 0 and st.records_late == exp.records_late
+    assert len(got) > 20
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_state_window_rejections(engine_mod):
+    r1 = compile_rule("SELECT count(*) FROM demo WHERE trig > 0 GROUP BY STATEWINDOW(trig = 1, trig = 2)", TRIG_SCHEMA,
+                      is_event_time=False)
+    with pytest.raises(engine_mod.EngineError) as e:
+        engine_mod.Engine(r1.plan)
+    assert e.value.code == A.EK_ERR_UNSUPPORTED
+    r2 = compile_rule("SELECT deviceId, count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)", TRIG_SCHEMA,
+                      num_keys=10, window_version="v2")
+    with pytest.raises(engine_mod.EngineError) as e:
+        engine_mod.Engine(r2.plan)
+    assert e.value.code == A.EK_ERR_UNSUPPORTED
