@@ -284,8 +284,17 @@ struct Engine {
                 if (pr[k].op == EK_OP_COL && !col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "condition column out of range");
                 if (pr[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in a window condition");
             }
-        if (plan.window_version != 0 && plan.window_version != 1 && plan.window_type != EK_WINDOW_STATE)
-            return fail(EK_ERR_UNSUPPORTED, "window version %d (WindowV2Operator) is built for STATEWINDOW only", plan.window_version);
+        if (plan.window_version == 2 && plan.window_type == EK_WINDOW_SLIDING) {
+            // WindowV2Operator sliding windows (window_v2_op.go:39-58): the event-time op without delay is built
+            if (!plan.is_event_time)
+                return fail(EK_ERR_UNSUPPORTED, "processing-time v2 sliding windows are wall-clock driven (use event time)");
+            if (plan.delay != 0)
+                return fail(EK_ERR_UNSUPPORTED, "delayed v2 sliding windows re-emit every fired window at each later watermark "
+                                                "until a pending one is newer (window_v2_event_op.go:60-76): not built");
+        } else if (plan.window_version != 0 && plan.window_version != 1 && plan.window_type != EK_WINDOW_STATE) {
+            return fail(EK_ERR_UNSUPPORTED, "window version %d (WindowV2Operator) is built for STATEWINDOW and SLIDINGWINDOW only",
+                        plan.window_version);
+        }
         for (int k = 0; k < plan.n_having; ++k) {
             if (plan.having_prog[k].op == EK_OP_COL) return fail(EK_ERR_UNSUPPORTED, "non-aggregate column in HAVING");
             if (plan.having_prog[k].op == EK_OP_AGG && (plan.having_prog[k].arg < 0 || plan.having_prog[k].arg >= plan.n_aggs))
@@ -1627,7 +1636,18 @@ struct Engine {
                     if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
                     for (int64_t k = 0; k < nt; ++k) {
                         const int64_t i = pos[k], t = tts[k], r = trel[k];
-                        if (D == 0) {
+                        if (plan.window_version == 2) {
+                            // EventSlidingWindowOp (window_v2_event_op.go:78-96): scanWindow over the rows added so far,
+                            // left-open (t - L, t] (window_v2_op.go:252-263); WindowRange (t - L, t)
+                            PendWin p{};
+                            p.q.kind = RB_UPTO;
+                            p.q.lo_ts = t - L + 1;
+                            p.q.pos = i;
+                            p.q.floor = eb_floor;
+                            p.start = t - L;
+                            p.end = t;
+                            pw.push_back(p);
+                        } else if (D == 0) {
                             PendWin p{};
                             p.q.kind = RB_SLIDE;
                             p.q.lo_ts = t - L;

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict
 }
 
 // Window range descriptor (host -> device): content = [max(floor, lo(lo_ts)), hi(...)) of the buffer.
-enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2 };
+enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3 };
 struct RangeQ {
     int64_t lo_ts;      // lower bound ts: content starts at the first row with ts >= lo_ts (INT64_MIN: from floor)
     int64_t hi_ts;      // RB_LB: first row with ts >= hi_ts; RB_SLIDE: ts <= hi_ts and release step <= rstep
@@ -254,6 +254,8 @@ __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* 
         a = d.lo_ts == INT64_MIN ? d.floor : max(d.floor, lb_i64(bts, d.floor, n_rel, d.lo_ts));
         if (d.kind == RB_LB) {
             b = lb_i64(bts, a, n_rel, d.hi_ts);
+        } else if (d.kind == RB_UPTO) {
+            b = d.pos + 1;   // v2 sliding: the rows the scanner holds when the trigger row is added (window_v2_event_op.go:78-96)
         } else {
             // sliding (window_op.go:605-655 with ts <= t): rows after the trigger with the same ts that were
             // released at the same watermark step belong to the window; later ones do not

@@ -881,6 +881,26 @@ static void state_on_row(stateop* o, int64_t e) {
     if (can_begin && !o->on) o->on = 1;
 }
 
+/* EventSlidingWindowOp without delay (window_v2_event_op.go:78-96): each released row joins the scanner; a row
+ * matching the trigger condition emits scanWindow(ts - L, ts): the rows added so far with ts in (ts - L, ts]
+ * (window_v2_op.go:252-263). The scanner is in release order, so the scan stops at the first later row. */
+static void v2slide_on_row(winop* o, int64_t e) {
+    v_push(&o->inputs, e);
+    const ek_plan* p = o->d->p;
+    if (p->n_trigger > 0) {
+        val_t r = eval_prog(p->trigger_prog, p->n_trigger, o->d, e, NULL);
+        if (!(r.tag == V_BOOL && r.i)) return;
+    }
+    const int64_t t = ev_ts(o, e), ws = t - o->L;
+    o->content.n = 0;
+    for (int64_t i = 0; i < o->inputs.n; ++i) {
+        const int64_t x = ev_ts(o, o->inputs.a[i]);
+        if (x > ws && x <= t) v_push(&o->content, o->inputs.a[i]);
+        else if (x > t) break;
+    }
+    emit_window(o->d, o->ob, ws, t, o->content.a, o->content.n);
+}
+
 /* ------------------------------------------------------------------ driver */
 static void set_status(eko_output* out, int st, const char* msg) {
     out->status = st;
@@ -913,6 +933,10 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     if (p->window_type == EK_WINDOW_STATE && !p->is_event_time && p->n_where > 0) {
         /* windowPlan.PushDownPredicate (windowPlan.go:82-99) moves WHERE below a processing-time window */
         set_status(out, EK_ERR_UNSUPPORTED, "pushed-down WHERE below a processing-time state window is not restated"); return out->status;
+    }
+    const int v2slide = p->window_version == 2 && p->window_type == EK_WINDOW_SLIDING;
+    if (v2slide && (!p->is_event_time || p->delay != 0)) {
+        set_status(out, EK_ERR_UNSUPPORTED, "only the event-time v2 sliding window without delay is restated"); return out->status;
     }
     stateop so; memset(&so, 0, sizeof so);
     so.d = &d; so.ob = &ob;
@@ -966,12 +990,19 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                     for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
                     for (int64_t k = 0; k < c; ++k) {
                         if (p->window_type == EK_WINDOW_STATE) state_on_row(&so, buf.a[k]);
+                        else if (v2slide) v2slide_on_row(&o, buf.a[k]);
                         else if (inc) inc_on_event(&io, buf.a[k]);
                         else win_on_event(&o, buf.a[k]);
                     }
                     v_erase_front(&buf, c);
                 }
                 if (p->window_type == EK_WINDOW_STATE) { /* WatermarkTuple: no effect on StateWindowOp */ }
+                else if (v2slide) {
+                    /* scanner.gc(now - Length - Delay): rows a later window can no longer hold */
+                    int64_t g = 0;
+                    while (g < o.inputs.n && ts[o.inputs.a[g]] <= wm - o.L) g++;
+                    v_erase_front(&o.inputs, g);
+                }
                 else if (inc) inc_on_watermark(&io, wm); else win_on_watermark(&o, wm);
                 last_wm = wm;
             }

@@ -141,3 +141,35 @@ def test_state_window_processing_time_where_rejected(oracle):
                         is_event_time=False)
     with pytest.raises(RuntimeError):
         oracle.run(rule.plan, [np.arange(5, dtype=np.int64)])
+
+
+# ------------------------------------------------------------------ v2 event-time sliding windows
+def _v2_cols(case, t0=1541152480000):
+    a = np.array([r["a"] for r in case["rows"]], np.int64)
+    ts = np.array([t0 + r["dt_ms"] for r in case["rows"]], np.int64)
+    return a, ts
+
+
+@pytest.mark.parametrize("case", _load("kat_window_v2.json")["tests"], ids=lambda c: c["name"])
+def test_window_v2_sliding_kat(oracle, case):
+    """window_v2_event_op_test.go: the first emitted window holds exactly the reference's rows."""
+    a, ts = _v2_cols(case)
+    rule = compile_rule(case["sql"].replace("eventStream", "demo"), {"a": "bigint", "ts": "bigint"}, window_version="v2")
+    run = oracle.run(rule.plan, [a, ts])
+    assert len(run.windows) >= 1
+    assert [int(a[i]) for i in run.members[0]] == [r["a"] for r in case["content"]]
+    assert run.windows[0].value(0, 0) == len(case["content"])
+
+
+def test_window_v2_sliding_left_open_and_arrival_cut(oracle):
+    """v2 windows are (t - L, t] over the rows added so far: a row exactly L before the trigger is out, and so is a
+    row with the trigger's ts released in the same watermark step after it; v1 keeps both (window_op.go:605-655)."""
+    ts = np.array([0, 1000, 4000, 4000, 5000], np.int64) + 1541152480000
+    a = np.array([1, 2, 3, 4, 5], np.int64)
+    sql = "SELECT count(*), sum(a) FROM demo GROUP BY SLIDINGWINDOW(ss, 4) OVER (WHEN a = 3)"
+    sch = {"a": "bigint", "ts": "bigint"}
+    v2 = oracle.run(compile_rule(sql, sch, late_tolerance_ms=1000, window_version="v2").plan, [a, ts])
+    v1 = oracle.run(compile_rule(sql, sch, late_tolerance_ms=1000).plan, [a, ts])
+    assert [list(map(int, m)) for m in v2.members] == [[1, 2]]
+    assert v2.windows[0].value(1, 0) == 5 and (v2.windows[0].start, v2.windows[0].end) == (ts[2] - 4000, ts[2])
+    assert [list(map(int, m)) for m in v1.members] == [[0, 1, 2, 3]]

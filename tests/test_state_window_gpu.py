@@ -1,5 +1,6 @@
-"""GPU parity of STATEWINDOW(begin, emit) (WindowV2Operator / StateWindowOp, window_v2_op.go:94-148) against the
-CPU oracle: the reference KAT (window_v2_op_test.go:40-91), the re-open chain, randomized processing-time and
+"""GPU parity of the WindowV2Operator windows against the CPU oracle: STATEWINDOW(begin, emit) (StateWindowOp,
+window_v2_op.go:94-148) and the event-time v2 sliding window (EventSlidingWindowOp, window_v2_event_op.go:78-96).
+STATEWINDOW: the reference KAT (window_v2_op_test.go:40-91), the re-open chain, randomized processing-time and
 event-time streams (out of order, late tolerance, WHERE above the window, HAVING, order statistics), split batches."""
 import json
 import os
@@ -89,3 +90,50 @@ def test_state_window_rejections(engine_mod):
     with pytest.raises(engine_mod.EngineError) as e:
         engine_mod.Engine(r2.plan)
     assert e.value.code == A.EK_ERR_UNSUPPORTED
+
+
+# ------------------------------------------------------------------ v2 event-time sliding windows
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLD, "kat_window_v2.json")))["tests"], ids=lambda c: c["name"])
+def test_window_v2_sliding_kat_engine(oracle, engine_mod, case):
+    a = np.array([r["a"] for r in case["rows"]], np.int64)
+    ts = np.array([1541152480000 + r["dt_ms"] for r in case["rows"]], np.int64)
+    rule = compile_rule(case["sql"].replace("eventStream", "demo"), {"a": "bigint", "ts": "bigint"}, window_version="v2",
+                        debug_membership=True)
+    got, exp, _ = run_both(oracle, engine_mod, rule, [a, ts], batches=len(a))
+    assert got[0].value(0, 0) == len(case["content"])
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("batches", [1, 7])
+def test_window_v2_sliding_out_of_order(oracle, engine_mod, batches):
+    sql = ("SELECT deviceId, count(*), sum(temperature), min(humidity), stddev(temperature) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ms, 300) OVER (WHEN trig = 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=60, late_tolerance_ms=100, debug_membership=True, window_version="v2")
+    cols = _with_trig(_iot(40_000, 60, seed=94, epm=3), 80)
+    rng = np.random.default_rng(12)
+    cols[1] = (cols[1] + rng.integers(-150, 150, len(cols[1]))).astype(np.int64)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert exp.records_late > 0 and st.records_late == exp.records_late
+    assert len(got) > 100
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_window_v2_sliding_every_row_with_ties(oracle, engine_mod):
+    """No OVER: a window per released row; rows sharing a ts see only the tied rows released before them."""
+    sql = "SELECT deviceId, count(*), max(humidity) FROM demo GROUP BY deviceId, SLIDINGWINDOW(ms, 20)"
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=10, debug_membership=True, window_version="v2")
+    cols = _with_trig(_iot(4000, 10, seed=95, epm=4), 10)
+    for batches in (1, 5):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(got) == len(exp.windows) > 3900
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_window_v2_rejections(engine_mod):
+    for kw in (dict(is_event_time=False), dict()):
+        sql = "SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ms, 20, 10)" if kw == {} else \
+              "SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ms, 20)"
+        r = compile_rule(sql, TRIG_SCHEMA, window_version="v2", **kw)
+        with pytest.raises(engine_mod.EngineError) as e:
+            engine_mod.Engine(r.plan)
+        assert e.value.code == A.EK_ERR_UNSUPPORTED
