@@ -337,8 +337,11 @@ struct Engine {
             if (!plan.is_event_time && plan.n_where > 0)
                 return fail(EK_ERR_UNSUPPORTED, "WHERE below a processing-time STATEWINDOW (pushed-down filter) is not built");
         } else if (plan.is_event_time) {
-            // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time
-            if (wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
+            // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time, except on the
+            // incremental path (CountWindowIncAggEventOp, window_inc_agg_event_op.go:340-439), decided below
+            const bool inc_count = plan.incremental && wtype == EK_WINDOW_COUNT && plan.interval <= 0;
+            if ((wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) && !inc_count)
+                return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
         } else if (wtype != EK_WINDOW_COUNT) {
             return fail(EK_ERR_UNSUPPORTED, "processing-time windows other than COUNTWINDOW are wall-clock driven (use event time)");
         }
@@ -353,10 +356,11 @@ struct Engine {
             inc = plan.incremental != 0 && fns && win;
         }
         if (inc) {
-            if (wtype == EK_WINDOW_SLIDING)
-                return fail(EK_ERR_UNSUPPORTED, "incremental sliding windows (window_inc_agg_event_op.go:148-296) are not built");
-            if (wtype == EK_WINDOW_COUNT && plan.is_event_time)
-                return fail(EK_ERR_UNSUPPORTED, "incremental event-time count windows (window_inc_agg_event_op.go:340-439) are not built");
+            if (wtype == EK_WINDOW_SLIDING && !plan.is_event_time)
+                return fail(EK_ERR_UNSUPPORTED, "processing-time incremental sliding windows are wall-clock driven (use event time)");
+            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
+                return fail(EK_ERR_UNSUPPORTED, "delayed incremental sliding windows (appendDelayIncAggWindowInEvent, "
+                                                "window_inc_agg_event_op.go:275-296: a window per row) are not built");
             if (plan.n_where > 0)
                 return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
                                                 "(FilterPlan above IncWindowPlan): not built");
@@ -367,7 +371,9 @@ struct Engine {
         range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT ||
                      wtype == EK_WINDOW_STATE || sort_aggs ||
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
-        need_rel = wtype == EK_WINDOW_SLIDING;
+        if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
+            return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
+        need_rel = wtype == EK_WINDOW_SLIDING || (inc && wtype == EK_WINDOW_COUNT);
         if (plan.is_event_time) {
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
                 return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
@@ -1603,6 +1609,8 @@ struct Engine {
     int range_triggers(int64_t rel_prev) {
         std::vector<PendWin> pw;
         const int64_t n_new = eb_rel - rel_prev;
+        if (inc && wtype == EK_WINDOW_SLIDING) return inc_slide_triggers(rel_prev);
+        if (inc && wtype == EK_WINDOW_COUNT) return inc_count_triggers(rel_prev);
         if (wtype == EK_WINDOW_SLIDING) {
             const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
             if (n_new > 0) {
@@ -1881,8 +1889,129 @@ struct Engine {
         return 0;
     }
 
+    // Watermarks at / before the release steps of the listed buffer rows (k_step_wm); rows must be released in this batch
+    int step_watermarks(const int64_t* d_pos, int64_t nt, std::vector<int64_t>& w_step, std::vector<int64_t>& w_prev) {
+        if (int rc = ensure(mrg_col, (size_t)nt * 24)) return rc;
+        int64_t* g_rel = (int64_t*)mrg_col.p;
+        const int gg = (int)std::min<int64_t>(4096, (nt + 255) / 256);
+        hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, d_pos, nt, INT64_MAX, (const int64_t*)eb.rel.p,
+                           (const int64_t*)nullptr, (const int64_t*)nullptr, g_rel);
+        hipLaunchKernelGGL(k_step_wm, dim3(gg), dim3(256), 0, stream, (const int64_t*)g_rel, nt, (const int64_t*)runmax_d.p,
+                           cur_nb, cur_arr_base, cur_prevmax, plan.late_tolerance_ms, g_rel + nt, g_rel + 2 * nt);
+        w_step.resize(nt);
+        w_prev.resize(nt);
+        hipMemcpyAsync(w_step.data(), g_rel + nt, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+        hipMemcpyAsync(w_prev.data(), g_rel + 2 * nt, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "step watermark gather failed");
+        return 0;
+    }
+
+    // ---- incremental sliding window, event time, no delay (SlidingWindowIncAggEventOp.appendIncAggWindowInEvent +
+    // emitList + gcIncAggWindow, window_inc_agg_event_op.go:193-273). Per released row in release order: a trigger
+    // row opens a window starting at its ts; every row joins the open windows whose [start, start + L) holds its ts;
+    // a trigger row then queues a CLONE OF THE OLDEST OPEN WINDOW (CurrWindowList[0]) with StartTime = its ts, which
+    // the next WatermarkTuple emits with WindowRange (ts, watermark); at each watermark windows with
+    // watermark - start >= L are dropped. The oldest open window at trigger row j is the first trigger k whose
+    // window survived the watermark before j's release step, and its rows are [k, min(j + 1, lb(ts_k + L))) of the
+    // ts-sorted buffer. Open windows: inc_pend (start = ts, floor_abs = row).
+    int inc_slide_triggers(int64_t rel_prev) {
+        std::vector<PendWin> pw;
+        const int64_t n_new = eb_rel - rel_prev;
+        if (n_new > 0) {
+            if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
+            if (int rc = ensure(trig_d, (size_t)n_new * 8)) return rc;
+            const int nb = (int)((n_new + kCompactTile - 1) / kCompactTile);
+            if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+            const DBatch bv = buffer_view();
+            hipLaunchKernelGGL(k_trigger_flags, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
+                               d_plan, bv, rel_prev, eb_rel, (uint8_t*)flags_d.p);
+            hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new, (int64_t*)cnts_d.p);
+            hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+            hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new,
+                               (const int64_t*)cnts_d.p, rel_prev, (int64_t*)trig_d.p);
+            const int64_t nt = fetch_i64((const int64_t*)cnts_d.p + nb);
+            if (nt > 0) {
+                std::vector<int64_t> pos(nt), tts(nt), w_step, w_prev;
+                if (int rc = step_watermarks((const int64_t*)trig_d.p, nt, w_step, w_prev)) return rc;
+                if (int rc = ensure(bounds_val, (size_t)nt * 8)) return rc;
+                const int gg = (int)std::min<int64_t>(4096, (nt + 255) / 256);
+                hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, (const int64_t*)trig_d.p, nt, INT64_MAX,
+                                   (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)nullptr, (const int64_t*)nullptr,
+                                   (int64_t*)bounds_val.p);
+                hipMemcpyAsync(pos.data(), trig_d.p, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                hipMemcpyAsync(tts.data(), bounds_val.p, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+                if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+                size_t head = 0;
+                for (int64_t k = 0; k < nt; ++k) {
+                    const int64_t wp = w_prev[k];
+                    while (wp != INT64_MIN && head < inc_pend.size() && wp - inc_pend[head].start >= L) head++;
+                    inc_pend.push_back(IncWin{tts[k], 0, eb_base + pos[k]});
+                    const IncWin& f = inc_pend[head];
+                    PendWin p{};
+                    p.q.kind = RB_CAP;
+                    p.q.pos = f.floor_abs - eb_base;
+                    p.q.rstep = pos[k] + 1;
+                    p.q.hi_ts = f.start + L;
+                    p.start = tts[k];
+                    p.end = w_step[k];
+                    pw.push_back(p);
+                }
+                inc_pend.erase(inc_pend.begin(), inc_pend.begin() + (int64_t)head);
+            }
+        }
+        // the batch's last watermark: gcIncAggWindow
+        size_t head = 0;
+        while (has_W && head < inc_pend.size() && W - inc_pend[head].start >= L) head++;
+        inc_pend.erase(inc_pend.begin(), inc_pend.begin() + (int64_t)head);
+        const int rc = fire_windows(pw);
+        eb_floor = std::max(eb_floor, inc_pend.empty() ? eb_rel : inc_pend.front().floor_abs - eb_base);
+        return rc;
+    }
+
+    // ---- incremental count window, event time (CountWindowIncAggEventOp, window_inc_agg_event_op.go:351-408): the
+    // released rows form consecutive blocks of n; a block is emitted by the WatermarkTuple after its last row, with
+    // WindowRange (ts of its first row, watermark). inc_T = absolute buffer position of the open block's first row.
+    int inc_count_triggers(int64_t rel_prev) {
+        std::vector<PendWin> pw;
+        const int64_t n = plan.length;
+        if (!inc_has_T) { inc_has_T = true; inc_T = eb_base + rel_prev; }
+        std::vector<int64_t> firsts, lasts;
+        for (int64_t s = inc_T; s + n <= eb_base + eb_rel; s += n) {
+            firsts.push_back(s - eb_base);
+            lasts.push_back(s + n - 1 - eb_base);
+        }
+        const int64_t nw = (int64_t)firsts.size();
+        if (nw > 0) {
+            if (int rc = ensure(trig_d, (size_t)nw * 16)) return rc;
+            hipMemcpyAsync(trig_d.p, lasts.data(), (size_t)nw * 8, hipMemcpyHostToDevice, stream);
+            hipMemcpyAsync((int64_t*)trig_d.p + nw, firsts.data(), (size_t)nw * 8, hipMemcpyHostToDevice, stream);
+            std::vector<int64_t> w_step, w_prev, t0(nw);
+            if (int rc = step_watermarks((const int64_t*)trig_d.p, nw, w_step, w_prev)) return rc;
+            if (int rc = ensure(bounds_val, (size_t)nw * 8)) return rc;
+            const int gg = (int)std::min<int64_t>(4096, (nw + 255) / 256);
+            hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, (const int64_t*)trig_d.p + nw, nw, INT64_MAX,
+                               (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)nullptr, (const int64_t*)nullptr,
+                               (int64_t*)bounds_val.p);
+            hipMemcpyAsync(t0.data(), bounds_val.p, (size_t)nw * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "count window ts gather failed");
+            for (int64_t w = 0; w < nw; ++w) {
+                PendWin p{};
+                p.q.kind = RB_FIXED;
+                p.q.pos = firsts[w];
+                p.q.rstep = lasts[w] + 1;
+                p.start = t0[w];
+                p.end = w_step[w];
+                pw.push_back(p);
+            }
+            inc_T += nw * n;
+        }
+        const int rc = fire_windows(pw);
+        eb_floor = std::max(eb_floor, inc_T - eb_base);
+        return rc;
+    }
+
     // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
-    int64_t cur_arr_base = 0;
+    int64_t cur_arr_base = 0, cur_nb = 0, cur_prevmax = INT64_MIN;
     int64_t relstep_w(int64_t r) {
         const int64_t j = r - cur_arr_base;
         if (j < 0 || !runmax_d.p) return W;
@@ -1963,6 +2092,8 @@ struct Engine {
         const int64_t n = db.n;
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
         cur_arr_base = arrival_base;
+        cur_nb = n;
+        cur_prevmax = had_M ? M_prev : INT64_MIN;
         // running max of the batch: release steps (sliding) and the step at which W was reached
         if (int rc = batch_runmax(ts, n, had_M ? M_prev : INT64_MIN)) return rc;
         if (n_acc > 0) {
@@ -2099,7 +2230,7 @@ struct Engine {
             const int rc = push_filter(db);
             return rc ? rc : record_time();
         }
-        if (wtype == EK_WINDOW_COUNT) {
+        if (wtype == EK_WINDOW_COUNT && !plan.is_event_time) {
             const int rc = push_count(db);
             return rc ? rc : record_time();
         }

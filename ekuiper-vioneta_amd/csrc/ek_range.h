@@ -136,6 +136,20 @@ __global__ void k_state_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int6
     }
 }
 
+// Watermarks around the release step r of each listed row (incremental event-time windows): w_step = the
+// watermark whose WatermarkTuple follows the row (emission), w_prev = the one before its step (the last gc).
+// runmax[0..nb) = batch running max (arrival arr_base + j); prevmax = stream max before the batch.
+__global__ void k_step_wm(const int64_t* __restrict__ rel, int64_t n, const int64_t* __restrict__ runmax, int64_t nb,
+                          int64_t arr_base, int64_t prevmax, int64_t late_tol, int64_t* __restrict__ w_step,
+                          int64_t* __restrict__ w_prev) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = rel[k] - arr_base;
+        w_step[k] = (j >= 0 && j < nb) ? runmax[j] - late_tol : INT64_MIN;
+        const int64_t pm = (j - 1 >= 0 && j - 1 < nb) ? runmax[j - 1] : prevmax;
+        w_prev[k] = pm == INT64_MIN ? INT64_MIN : pm - late_tol;
+    }
+}
+
 // gather of the flag bytes at compacted positions (positions are absolute: base_idx + i)
 __global__ void k_gather_flags(const int64_t* __restrict__ pos, int64_t n, int64_t base_idx, const uint8_t* __restrict__ flags,
                                uint8_t* __restrict__ out) {
@@ -230,7 +244,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict
 }
 
 // Window range descriptor (host -> device): content = [max(floor, lo(lo_ts)), hi(...)) of the buffer.
-enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3 };
+enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3, RB_CAP = 4 };
 struct RangeQ {
     int64_t lo_ts;      // lower bound ts: content starts at the first row with ts >= lo_ts (INT64_MIN: from floor)
     int64_t hi_ts;      // RB_LB: first row with ts >= hi_ts; RB_SLIDE: ts <= hi_ts and release step <= rstep
@@ -250,6 +264,10 @@ __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* 
     if (d.kind == RB_FIXED) {
         a = d.pos;
         b = d.rstep;
+    } else if (d.kind == RB_CAP) {
+        // [pos, min(rstep, first row with ts >= hi_ts)): an incremental window's rows from its opening row
+        a = d.pos;
+        b = min(d.rstep, lb_i64(bts, a, max(a, d.rstep), d.hi_ts));
     } else {
         a = d.lo_ts == INT64_MIN ? d.floor : max(d.floor, lb_i64(bts, d.floor, n_rel, d.lo_ts));
         if (d.kind == RB_LB) {

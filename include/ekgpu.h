@@ -127,7 +127,7 @@ typedef struct {
     /* def.RuleOption.PlanOptimizeStrategy.EnableIncrementalWindow (def/rule.go:55-61): the planner's
      * incremental-aggregation window (planner.go:905-997 rewriteIfIncAggStmt -> IncWindowPlan ->
      * node.NewWindowIncAggOp, window_inc_agg_op.go:59-101 / window_inc_agg_event_op.go). Honoured for
-     * event-time TUMBLING/HOPPING and processing-time COUNTWINDOW(n) when every aggregate is one of
+     * event-time TUMBLING/HOPPING/SLIDING (no delay), COUNTWINDOW(n) in either time mode, when every aggregate is one of
      * count/sum/avg/min/max (function.IsSupportedIncAgg, funcs_inc_agg.go:28-41); with another aggregate
      * the reference planner keeps the regular path and so does the engine. Inc semantics: windows are
      * created by the events themselves (HoppingWindowIncAggEventOp.triggerWindow), each group reports

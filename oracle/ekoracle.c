@@ -666,6 +666,84 @@ static void inc_on_watermark(incop* o, int64_t wm) {
     if (g > 0) { memmove(o->w, o->w + g, (size_t)(o->nw - g) * sizeof(incwin)); o->nw -= g; }
 }
 
+/* SlidingWindowIncAggEventOp without delay (window_inc_agg_event_op.go:193-273): a trigger row opens a window at its
+ * ts (newIncAggWindow); every row joins the open windows with start <= ts < start + Length (incAggCal); a trigger row
+ * then queues a clone of the OLDEST open window (CurrWindowList[0].Clone) whose StartTime becomes the row's ts; the
+ * next WatermarkTuple emits every queued clone (zero EventTime + 0 <= watermark) with WindowRange (StartTime,
+ * watermark) and drops the open windows with watermark - start >= Length (gcIncAggWindow, window_inc_agg_op.go:843-857). */
+typedef struct {
+    const dataset* d;
+    outbuf* ob;
+    int64_t L;
+    incwin* w; int64_t nw, cap;    /* CurrWindowList */
+    incwin* e; int64_t ne, ecap;   /* EmitList (start = the trigger row's ts) */
+    const int64_t* ts;
+} incslide;
+
+static void incslide_on_event(incslide* o, int64_t e) {
+    const ek_plan* p = o->d->p;
+    const int64_t t = o->ts[e];
+    int trig = 1;
+    if (p->n_trigger > 0) { val_t r = eval_prog(p->trigger_prog, p->n_trigger, o->d, e, NULL); trig = r.tag == V_BOOL && r.i; }
+    if (trig) {
+        if (o->nw == o->cap) { o->cap = o->cap ? 2 * o->cap : 16; o->w = (incwin*)realloc(o->w, (size_t)o->cap * sizeof(incwin)); }
+        memset(&o->w[o->nw], 0, sizeof(incwin));
+        o->w[o->nw++].start = t;
+    }
+    for (int64_t k = 0; k < o->nw; ++k)
+        if (o->w[k].start <= t && t < o->w[k].start + o->L) v_push(&o->w[k].mem, e);
+    if (trig) {
+        if (o->ne == o->ecap) { o->ecap = o->ecap ? 2 * o->ecap : 16; o->e = (incwin*)realloc(o->e, (size_t)o->ecap * sizeof(incwin)); }
+        incwin* c = &o->e[o->ne++];
+        memset(c, 0, sizeof *c);
+        c->start = t;
+        for (int64_t k = 0; k < o->w[0].mem.n; ++k) v_push(&c->mem, o->w[0].mem.a[k]);
+    }
+}
+
+static void incslide_on_watermark(incslide* o, int64_t wm) {
+    for (int64_t k = 0; k < o->ne; ++k) {
+        emit_inc_window(o->d, o->ob, o->e[k].start, wm, o->e[k].mem.a, o->e[k].mem.n);
+        free(o->e[k].mem.a);
+    }
+    o->ne = 0;
+    int64_t g = 0;
+    while (g < o->nw && wm - o->w[g].start >= o->L) { free(o->w[g].mem.a); g++; }
+    if (g > 0) { memmove(o->w, o->w + g, (size_t)(o->nw - g) * sizeof(incwin)); o->nw -= g; }
+}
+
+/* CountWindowIncAggEventOp (window_inc_agg_event_op.go:351-408): consecutive blocks of CountLength released rows
+ * (StartTime = the first row's ts); the next WatermarkTuple emits the completed blocks, WindowRange (StartTime, wm). */
+typedef struct {
+    const dataset* d;
+    outbuf* ob;
+    int64_t n;
+    vec64 cur; int64_t cur_start;
+    incwin* e; int64_t ne, ecap;
+    const int64_t* ts;
+} inccount;
+
+static void inccount_on_event(inccount* o, int64_t e) {
+    if (o->cur.n == 0) o->cur_start = o->ts[e];
+    v_push(&o->cur, e);
+    if (o->cur.n >= o->n) {
+        if (o->ne == o->ecap) { o->ecap = o->ecap ? 2 * o->ecap : 16; o->e = (incwin*)realloc(o->e, (size_t)o->ecap * sizeof(incwin)); }
+        o->e[o->ne].start = o->cur_start;
+        o->e[o->ne].mem = o->cur;
+        o->ne++;
+        memset(&o->cur, 0, sizeof o->cur);
+    }
+}
+
+static void inccount_on_watermark(inccount* o, int64_t wm) {
+    /* every queued block started at or before the watermark (its rows were released by it) */
+    for (int64_t k = 0; k < o->ne; ++k) {
+        emit_inc_window(o->d, o->ob, o->e[k].start, wm, o->e[k].mem.a, o->e[k].mem.n);
+        free(o->e[k].mem.a);
+    }
+    o->ne = 0;
+}
+
 /* ------------------------------------------------------------------ window operator (event time) */
 typedef struct {
     const dataset* d;
@@ -922,8 +1000,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     for (int a = 0; a < p->n_aggs; ++a) inc_ok &= inc_supported_fn(p->aggs[a].fn);
     if (p->window_type == EK_WINDOW_COUNT && p->interval > 0) inc_ok = 0;
     if (p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_NONE || p->window_type == EK_WINDOW_STATE) inc_ok = 0;
-    if (inc_ok && (p->window_type == EK_WINDOW_SLIDING || (p->window_type == EK_WINDOW_COUNT && p->is_event_time))) {
-        set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding / event-time count windows are not restated"); return out->status;
+    if (inc_ok && p->window_type == EK_WINDOW_SLIDING && (!p->is_event_time || p->delay != 0)) {
+        set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding windows are restated in event time without delay only"); return out->status;
     }
     if (inc_ok && p->n_where > 0) {
         /* FilterPlan stays above IncWindowPlan (IncWindowPlan.PushDownPredicate keeps it): WHERE would filter the
@@ -943,13 +1021,19 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     if (p->is_event_time) {
         /* NewEventTimeTrigger (event_window_trigger.go:35-53); STATEWINDOW runs in WindowV2Operator (window_v2_op.go:39-58) */
         if ((p->window_type == EK_WINDOW_COUNT || p->window_type > EK_WINDOW_COUNT || p->window_type < 0) &&
-            p->window_type != EK_WINDOW_STATE) {
+            p->window_type != EK_WINDOW_STATE && !(inc_ok && p->window_type == EK_WINDOW_COUNT)) {
             set_status(out, EK_ERR_UNSUPPORTED, "unsupported window type"); return out->status;
         }
         if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "event time requires a timestamp column"); return out->status; }
         int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
         for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
         const int inc = p->incremental && (p->window_type == EK_WINDOW_TUMBLING || p->window_type == EK_WINDOW_HOPPING) && inc_ok;
+        const int inc_slide = inc_ok && p->window_type == EK_WINDOW_SLIDING;
+        const int inc_count = inc_ok && p->window_type == EK_WINDOW_COUNT;
+        incslide isl; memset(&isl, 0, sizeof isl);
+        isl.d = &d; isl.ob = &ob; isl.ts = ts; isl.L = (int64_t)p->length * unit_ms(p->time_unit);
+        inccount icn; memset(&icn, 0, sizeof icn);
+        icn.d = &d; icn.ob = &ob; icn.ts = ts; icn.n = p->length;
         incop io; memset(&io, 0, sizeof io);
         io.d = &d; io.ob = &ob; io.ts = ts;
         {
@@ -990,6 +1074,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                     for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
                     for (int64_t k = 0; k < c; ++k) {
                         if (p->window_type == EK_WINDOW_STATE) state_on_row(&so, buf.a[k]);
+                        else if (inc_slide) incslide_on_event(&isl, buf.a[k]);
+                        else if (inc_count) inccount_on_event(&icn, buf.a[k]);
                         else if (v2slide) v2slide_on_row(&o, buf.a[k]);
                         else if (inc) inc_on_event(&io, buf.a[k]);
                         else win_on_event(&o, buf.a[k]);
@@ -997,6 +1083,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                     v_erase_front(&buf, c);
                 }
                 if (p->window_type == EK_WINDOW_STATE) { /* WatermarkTuple: no effect on StateWindowOp */ }
+                else if (inc_slide) incslide_on_watermark(&isl, wm);
+                else if (inc_count) inccount_on_watermark(&icn, wm);
                 else if (v2slide) {
                     /* scanner.gc(now - Length - Delay): rows a later window can no longer hold */
                     int64_t g = 0;
@@ -1009,6 +1097,11 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         }
         for (int64_t k = 0; k < io.nw; ++k) free(io.w[k].mem.a);
         free(io.w);
+        for (int64_t k = 0; k < isl.nw; ++k) free(isl.w[k].mem.a);
+        for (int64_t k = 0; k < isl.ne; ++k) free(isl.e[k].mem.a);
+        free(isl.w); free(isl.e);
+        for (int64_t k = 0; k < icn.ne; ++k) free(icn.e[k].mem.a);
+        free(icn.e); free(icn.cur.a);
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
     } else if (p->window_type == EK_WINDOW_STATE) {
