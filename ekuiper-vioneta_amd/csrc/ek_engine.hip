@@ -536,6 +536,7 @@ struct Engine {
             lay.bytes = (int32_t)std::max<size_t>((size_t)((o + 15) & ~15), (sparse_lds_bytes(dp.n_vc) + 15) & ~(size_t)15);
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
+        small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
         // chunk-local partitions k_part can sort through LDS: 8 B each next to the 4096-row staging (~13 K)
@@ -1285,6 +1286,8 @@ struct Engine {
     DevBuf rq_d, ab_d, slot_d, trig_d, flags_d, cnts_d, runmax_d, runcm_d, mrg_keys[2], mrg_src[2], mrg_tmp, mrg_tail,
         mrg_bidx, mrg_col, vp_err, vp_mc, vp_mh, sort_pbase, sort_scr, chunk_pa;
     std::vector<int64_t> h_ab;
+    DevBuf sw_d;                        // small-window launch lists
+    bool small_win_on = true;           // EKGPU_SMALL_WIN=0: every range window through k_part + k_agg
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
 
@@ -1522,6 +1525,37 @@ struct Engine {
                                (unsigned long long*)r_wmh.p);
             hipStreamSynchronize(stream);   // slots/ab host vectors are reused
         }
+        // small windows: one workgroup each (k_small_win); no order statistics on that path
+        std::vector<uint8_t> small(nq, 0);
+        if (dp.n_sagg == 0 && small_win_on) {
+            std::vector<int32_t> wl;
+            for (int w = 0; w < nq; ++w) {
+                const int64_t sz = h_ab[2 * w + 1] - h_ab[2 * w];
+                if (slots[w] >= 0 && sz > 0 && sz <= kSmallWin) { small[w] = 1; wl.push_back(w); }
+            }
+            if (!wl.empty()) {
+                const int nw = (int)wl.size();
+                if (int rc = ensure(sw_d, (size_t)nw * 4 + (size_t)nq * 12 + 16)) return rc;
+                int32_t* d_wl = (int32_t*)sw_d.p;
+                int32_t* d_slot = d_wl + nw;
+                int64_t* d_ob = (int64_t*)(((uintptr_t)(d_slot + nq) + 7) & ~(uintptr_t)7);
+                hipMemcpyAsync(d_wl, wl.data(), (size_t)nw * 4, hipMemcpyHostToDevice, stream);
+                hipMemcpyAsync(d_slot, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
+                hipMemcpyAsync(d_ob, obase.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
+                const DBatch bv = buffer_view();
+                Results rv = results_view();
+                const int ph = phase_begin(EK_PHASE_AGGREGATE);
+                switch (std::max(1, dp.n_vc)) {
+                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
+                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
+                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
+                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
+                }
+                phase_end(ph);
+                // the host vectors above are reused by the next fire: keep them alive until the copies ran
+                hipStreamSynchronize(stream);
+            }
+        }
         // virtual-pane groups of consecutive non-empty windows
         const int64_t vcap = (int64_t)env_int("EKGPU_RANGE_GROUP_EVENTS", 1 << 26);
         int w = 0;
@@ -1530,7 +1564,7 @@ struct Engine {
             int64_t V = 0;
             while (w < nq && (int)members.size() < max_panes_group) {
                 const int64_t sz = h_ab[2 * w + 1] - h_ab[2 * w];
-                if (sz == 0) { w++; continue; }       // empty window: no output (aggregate_operator.go:66-75)
+                if (sz == 0 || small[w]) { w++; continue; }   // empty window: no output (aggregate_operator.go:66-75)
                 if (!members.empty() && V + sz > vcap) break;
                 members.push_back(w);
                 V += sz;
@@ -2751,7 +2785,7 @@ struct Engine {
             release(e->rel);
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
-                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa})
+                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d})
             release(*d);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
