@@ -1630,7 +1630,7 @@ struct Engine {
         gd.nch = (int32_t)((V + csz - 1) / csz);
         gd.np = npn * NB;
         gd.has_accept = 0;
-        gd.pad = 0;
+        gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
         if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
         if (int rc = ensure(vp_err, (size_t)npn * 4)) return rc;
         if (int rc = ensure(vp_mc, (size_t)npn * 8)) return rc;

@@ -28,8 +28,19 @@ def _stream(n, keys, epm, seed=91, t0=T0):
     return cols
 
 
-def _push_time(eng, n, cols):
+def _warm(eng, pushes):
+    """Run the same pushes once and reset: the timed run then finds its device buffers already sized
+    (a first push also pays hipMalloc of the staging / event-buffer / result stores)."""
+    for n, cols in pushes:
+        eng.push_device(n, [c.data_ptr() for c in cols])
+    eng.poll()
+    eng.reset()
+
+
+def _push_time(eng, n, cols, warm=True):
     import torch
+    if warm:
+        _warm(eng, [(n, cols)])
     torch.cuda.synchronize()
     t = time.perf_counter()
     eng.push_device(n, [c.data_ptr() for c in cols])
@@ -117,12 +128,13 @@ def test_c5_median_full_shard(engine_mod):
     rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys)
     cols = _stream(n, keys, 2084, seed=94, t0=t_min)   # 1.25e8 events inside [t_min, t_min + 60 s)
     eng = engine_mod.Engine(rule.plan)
-    dt = _push_time(eng, n, cols)
     sentinel = [torch.tensor([0], dtype=torch.int32, device="cuda:0"),
                 torch.tensor([t_min + 60_000], dtype=torch.int64, device="cuda:0"),
                 torch.tensor([50.0], dtype=torch.float64, device="cuda:0"),
                 torch.tensor([50.0], dtype=torch.float64, device="cuda:0")]
-    dt2 = _push_time(eng, 1, sentinel)
+    _warm(eng, [(n, cols), (1, sentinel)])
+    dt = _push_time(eng, n, cols, warm=False)
+    dt2 = _push_time(eng, 1, sentinel, warm=False)
     wins = eng.poll()
     eng.close()
     print(f"\nC5 shard: {n} events, {len(wins[0].keys) if wins else 0} groups, ingest {dt * 1e3:.1f} ms + "
