@@ -537,6 +537,7 @@ struct Engine {
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
+        stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
         // chunk-local partitions k_part can sort through LDS: 8 B each next to the 4096-row staging (~13 K)
@@ -1288,6 +1289,7 @@ struct Engine {
     std::vector<int64_t> h_ab;
     DevBuf sw_d;                        // small-window launch lists
     bool small_win_on = true;           // EKGPU_SMALL_WIN=0: every range window through k_part + k_agg
+    int stats_blocks = 1024;            // k_stats grid (EKGPU_STATS_BLOCKS)
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
 
@@ -2280,7 +2282,7 @@ struct Engine {
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
 
         // ---- 1. batch statistics (one pass over ts)
-        int sblocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
+        int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
         if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
         const int ph_s = phase_begin(EK_PHASE_STATS);
         hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats_part.p);
