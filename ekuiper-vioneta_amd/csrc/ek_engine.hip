@@ -2133,7 +2133,7 @@ struct Engine {
         // running max of the batch: release steps (sliding) and the step at which W was reached
         if (int rc = batch_runmax(ts, n, had_M ? M_prev : INT64_MIN)) return rc;
         if (n_acc > 0) {
-            if (sorted && (eb.n == 0 || !had_M || min_acc >= M_prev)) {
+            if (sorted && !d_acc && (eb.n == 0 || !had_M || min_acc >= M_prev)) {
                 if (int rc = eb_append(db, start, n_acc, arrival_base)) return rc;
             } else {
                 int64_t max_acc = max_ts;
@@ -2285,7 +2285,8 @@ struct Engine {
         int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
         if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
         const int ph_s = phase_begin(EK_PHASE_STATS);
-        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, (BatchStats*)bstats_part.p);
+        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, has_M ? M : INT64_MIN,
+                           (BatchStats*)bstats_part.p);
         hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
                            (BatchStats*)bstats.p);
         phase_end(ph_s);
@@ -2342,6 +2343,27 @@ struct Engine {
             has_M = true;
             W = M - T;
             has_W = true;
+        }
+        // ---- 3b. hopping empty-window discard (window_op.go:605-655, lateTolerance 0): only a batch with an
+        // arrival gap wider than the window can trigger an empty window, so the mask pass runs only then
+        if (wtype == EK_WINDOW_HOPPING && T == 0 && n_acc > 0 && s.max_gap > L) {
+            // the first window end: E1 = aligned end of the first released event (= min accepted ts when T = 0)
+            const int64_t e1 = e1_known ? E1 : aligned_end(min_acc, raw_interval, plan.time_unit, plan.tz_offset_s);
+            const int nch = (int)((n + kAccChunk - 1) / kAccChunk);
+            if (int rc = ensure(cmax, (size_t)nch * 8)) return rc;
+            if (int rc = ensure(acc, (size_t)n)) return rc;
+            hipLaunchKernelGGL(k_chunk_max, dim3(nch), dim3(kBlock), 0, stream, ts, n, (int64_t*)cmax.p);
+            hipLaunchKernelGGL(k_scan_max, dim3(1), dim3(1024), 0, stream, (int64_t*)cmax.p, nch, had_M ? M_prev : INT64_MIN);
+            hipLaunchKernelGGL(k_hop_drop, dim3(nch), dim3(kBlock), 0, stream, ts, n, (const int64_t*)cmax.p, start, d_acc,
+                               e1, H, L, (uint8_t*)acc.p, (BatchStats*)bstats.p);
+            int64_t dropped = 0;
+            hipMemcpyAsync(&dropped, &((BatchStats*)bstats.p)->n_dropped, 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "hopping discard kernel failed");
+            if (dropped) {
+                d_acc = (const uint8_t*)acc.p;
+                n_acc -= dropped;
+                stats.records_discarded += dropped;
+            }
         }
         if (range_mode) {
             const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M);

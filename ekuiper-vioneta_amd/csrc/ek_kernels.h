@@ -25,6 +25,8 @@ struct BatchStats {
     int64_t min_accepted;
     int32_t unsorted;
     int32_t pad;
+    int64_t max_gap;    // max over arrival-adjacent pairs of ts[i] - ts[i-1] (ts[0] - seed when seeded)
+    int64_t n_dropped;  // events removed by the hopping empty-window discard (k_hop_drop)
 };
 
 struct PaneGrid {
@@ -50,8 +52,8 @@ __device__ __forceinline__ int64_t wave_max64(int64_t v) {
 
 // ---------------------------------------------------------------- k_stats
 // One streaming pass over ts (16 B per lane per load): min, max and "arrival order is non-decreasing".
-__global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts, int64_t n, BatchStats* part) {
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
+__global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts, int64_t n, int64_t seed, BatchStats* part) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN, mg = INT64_MIN;
     int uns = 0;
     const int64_t npair = n >> 1;
     const longlong2* t2 = (const longlong2*)ts;
@@ -75,6 +77,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
             if (lane == 0) prev = pi > 0 ? lp[u] : v[u].x;
             if (pi < npair) {
                 uns |= (v[u].x < prev) | (v[u].y < v[u].x);
+                mg = max(mg, max(v[u].x - prev, v[u].y - v[u].x));
                 mn = min(mn, min(v[u].x, v[u].y));
                 mx = max(mx, max(v[u].x, v[u].y));
             }
@@ -84,37 +87,46 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
         int64_t last = ts[n - 1];
         mn = min(mn, last);
         mx = max(mx, last);
-        if (n > 1) uns |= last < ts[n - 2];
+        if (n > 1) { uns |= last < ts[n - 2]; mg = max(mg, last - ts[n - 2]); }
     }
+    // the gap between the carried stream max and the first event (hopping empty-window check)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0 && seed != INT64_MIN) mg = max(mg, ts[0] - seed);
     mn = wave_min64(mn);
     mx = wave_max64(mx);
+    mg = wave_max64(mg);
     uns = __any(uns);
     // one partial per block (same-address atomics from every wave would serialise at the memory side)
     __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];
+    __shared__ int64_t smg[kBlock / 64];
     __shared__ int suns[kBlock / 64];
-    if (lane == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; suns[threadIdx.x >> 6] = uns; }
+    if (lane == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; smg[threadIdx.x >> 6] = mg; suns[threadIdx.x >> 6] = uns; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / 64; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); uns |= suns[w]; }
-        part[blockIdx.x] = BatchStats{mn, mx, 0, INT64_MAX, uns, 0};
+        for (int w = 1; w < kBlock / 64; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); mg = max(mg, smg[w]); uns |= suns[w]; }
+        part[blockIdx.x] = BatchStats{mn, mx, 0, INT64_MAX, uns, 0, mg, 0};
     }
 }
 
 __global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
-    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    int64_t mn = INT64_MAX, mx = INT64_MIN, mg = INT64_MIN;
     int uns = 0;
-    for (int k = threadIdx.x; k < nb; k += 1024) { mn = min(mn, part[k].min_ts); mx = max(mx, part[k].max_ts); uns |= part[k].unsorted; }
+    for (int k = threadIdx.x; k < nb; k += 1024) {
+        mn = min(mn, part[k].min_ts); mx = max(mx, part[k].max_ts); mg = max(mg, part[k].max_gap); uns |= part[k].unsorted;
+    }
     mn = wave_min64(mn);
     mx = wave_max64(mx);
+    mg = wave_max64(mg);
     uns = __any(uns);
-    __shared__ int64_t smn[16], smx[16];
+    __shared__ int64_t smn[16], smx[16], smg[16];
     __shared__ int su[16];
-    if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; su[threadIdx.x >> 6] = uns; }
+    if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; smg[threadIdx.x >> 6] = mg; su[threadIdx.x >> 6] = uns; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); uns |= su[w]; }
+        for (int w = 1; w < 16; ++w) { mn = min(mn, smn[w]); mx = max(mx, smx[w]); mg = max(mg, smg[w]); uns |= su[w]; }
         st->min_ts = mn;
         st->max_ts = mx;
+        st->max_gap = mg;
+        st->n_dropped = 0;
         st->unsorted = uns;
         st->n_accepted = 0;
         st->min_accepted = INT64_MAX;
@@ -195,6 +207,55 @@ __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ t
         atomicAdd((unsigned long long*)&st->n_accepted, (unsigned long long)cnt);
         atomicMin((long long*)&st->min_accepted, (long long)mn);
     }
+}
+
+// Hopping windows with lateTolerance 0: the empty-window discard of window_op.go:605-655 (handleInputs). When the
+// watermark step of event i triggers a hopping window [e - L, e) that holds no released event, handleInputs finds
+// no member (nextleft < 0) and returns inputs[:0]: every buffered input is dropped. With lateTolerance 0 the only
+// buffered input that is not expired at that step is event i itself (events released earlier are <= the previous
+// watermark < e - L, and the watermark rises to ts_i exactly at i), so event i reaches no window. Window ends lie on
+// the grid E1 + k H; the largest one <= ts_i is e_max, and some triggered window is empty iff
+// e_max - L > W_{i-1} (the watermark before i, the exclusive running max of ts seeded with the carried stream max).
+// acc_out[i] = accepted(i) && !dropped(i); accepted = acc_in[i] (out-of-order batches) or i >= start (sorted).
+__global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+                                                     int64_t start, const uint8_t* acc_in, int64_t E1, int64_t H,
+                                                     int64_t L, uint8_t* acc_out, BatchStats* st) {
+    __shared__ int64_t tmax[kBlock];
+    const int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
+    int64_t v[kAccPerThread];
+    int64_t lm = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < kAccPerThread; ++k) {
+        const int64_t i = base + k;
+        v[k] = i < n ? ts[i] : INT64_MIN;
+        lm = max(lm, v[k]);
+    }
+    tmax[threadIdx.x] = lm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t run = excl[blockIdx.x];
+        for (int t = 0; t < kBlock; ++t) { int64_t x = tmax[t]; tmax[t] = run; run = max(run, x); }
+    }
+    __syncthreads();
+    int64_t run = tmax[threadIdx.x];
+    int64_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kAccPerThread; ++k) {
+        const int64_t i = base + k;
+        if (i < n) {
+            const bool a = acc_in ? acc_in[i] != 0 : i >= start;
+            bool drop = false;
+            if (a && run != INT64_MIN && v[k] > run && v[k] >= E1) {
+                const int64_t e_max = E1 + ((v[k] - E1) / H) * H;
+                drop = e_max - L > run;
+            }
+            acc_out[i] = (a && !drop) ? 1 : 0;
+            cnt += drop;
+            run = max(run, v[k]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd((unsigned long long*)&st->n_dropped, (unsigned long long)cnt);
 }
 
 // first index in [lo, hi) with ts >= start of pane q_lo + k (sorted batches; k = 0 -> lo for pane 0 of tumbling).
@@ -329,6 +390,8 @@ __device__ __forceinline__ int local_part(const DPlan& p, const DBatch& b, const
         int64_t r = q - gd.q_lo;
         if (q < 0 || r < 0 || r >= gd.n_panes) return -1;
         rel = (int)r;
+    } else if (MODE == 1) {
+        if (gd.has_accept && !acc[i]) return -1;   // hopping empty-window discard (k_hop_drop)
     }
     if (gd.key_col >= 0 && key >= gd.num_keys) return -1;
     if (WHERE) {

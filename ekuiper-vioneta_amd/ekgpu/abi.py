@@ -124,6 +124,7 @@ class ek_stats(C.Structure):
         ("phase_ms", C.c_double * 4),
         ("phase_launches", C.c_int64 * 4),
         ("records_filter_error", C.c_int64),
+        ("records_discarded", C.c_int64),
     ]
 
 

@@ -200,6 +200,8 @@ typedef struct {
     double phase_ms[4];
     int64_t phase_launches[4];
     int64_t records_filter_error; /* window-less rules: events whose WHERE evaluation errored      */
+    int64_t records_discarded;    /* hopping windows: inputs dropped when a triggered window is empty
+                                   * (handleInputs returns inputs[:0], window_op.go:605-655)          */
 } ek_stats;
 
 enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };
