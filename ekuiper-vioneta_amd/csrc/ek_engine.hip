@@ -2285,8 +2285,12 @@ struct Engine {
         int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
         if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
         const int ph_s = phase_begin(EK_PHASE_STATS);
-        hipLaunchKernelGGL(k_stats, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, has_M ? M : INT64_MIN,
-                           (BatchStats*)bstats_part.p);
+        if (wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms == 0)
+            hipLaunchKernelGGL(k_stats<true>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, has_M ? M : INT64_MIN,
+                               (BatchStats*)bstats_part.p);
+        else
+            hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN,
+                               (BatchStats*)bstats_part.p);
         hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
                            (BatchStats*)bstats.p);
         phase_end(ph_s);

@@ -52,6 +52,8 @@ __device__ __forceinline__ int64_t wave_max64(int64_t v) {
 
 // ---------------------------------------------------------------- k_stats
 // One streaming pass over ts (16 B per lane per load): min, max and "arrival order is non-decreasing".
+// GAP (hopping, lateTolerance 0 only): also the widest arrival gap, for the empty-window discard check.
+template <bool GAP>
 __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts, int64_t n, int64_t seed, BatchStats* part) {
     int64_t mn = INT64_MAX, mx = INT64_MIN, mg = INT64_MIN;
     int uns = 0;
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
             if (lane == 0) prev = pi > 0 ? lp[u] : v[u].x;
             if (pi < npair) {
                 uns |= (v[u].x < prev) | (v[u].y < v[u].x);
-                mg = max(mg, max(v[u].x - prev, v[u].y - v[u].x));
+                if (GAP) mg = max(mg, max(v[u].x - prev, v[u].y - v[u].x));
                 mn = min(mn, min(v[u].x, v[u].y));
                 mx = max(mx, max(v[u].x, v[u].y));
             }
@@ -87,13 +89,13 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
         int64_t last = ts[n - 1];
         mn = min(mn, last);
         mx = max(mx, last);
-        if (n > 1) { uns |= last < ts[n - 2]; mg = max(mg, last - ts[n - 2]); }
+        if (n > 1) { uns |= last < ts[n - 2]; if (GAP) mg = max(mg, last - ts[n - 2]); }
     }
     // the gap between the carried stream max and the first event (hopping empty-window check)
-    if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0 && seed != INT64_MIN) mg = max(mg, ts[0] - seed);
+    if (GAP && blockIdx.x == 0 && threadIdx.x == 0 && n > 0 && seed != INT64_MIN) mg = max(mg, ts[0] - seed);
     mn = wave_min64(mn);
     mx = wave_max64(mx);
-    mg = wave_max64(mg);
+    if (GAP) mg = wave_max64(mg);
     uns = __any(uns);
     // one partial per block (same-address atomics from every wave would serialise at the memory side)
     __shared__ int64_t smn[kBlock / 64], smx[kBlock / 64];

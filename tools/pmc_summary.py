@@ -14,7 +14,7 @@ import re
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_part": r"ek::k_part<", "k_agg": r"ek::k_agg<", "k_stats": r"ek::k_stats\(",
+KERNELS = {"k_part": r"ek::k_part<", "k_agg": r"ek::k_agg<", "k_stats": r"ek::k_stats[<(]",
            "k_finalize": r"ek::k_finalize<"}
 
 

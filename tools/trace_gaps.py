@@ -5,7 +5,7 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_stats(" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if "k_stats<" in r["Kernel_Name"] or "k_stats(" in r["Kernel_Name"]]
 seg = rows[idx[-2]:idx[-1] + 1]
 t0 = int(seg[0]["Start_Timestamp"])
 prev = None
