@@ -98,3 +98,17 @@ def test_hopping_gap_engine_range_mode(oracle, engine_mod, batches):
     got, st = _run(engine_mod, rule, cols, batches)
     assert st.records_discarded > 0
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("median", [False, True], ids=["pane", "range"])
+def test_hopping_gap_checkpoint(oracle, engine_mod, median):
+    # the discard check reads the carried stream max and E1: both must survive ek_export_state / ek_import_state
+    from test_state_gpu import run_split
+    sql = SQL if not median else ("SELECT deviceId, count(*), median(temperature) FROM demo "
+                                  "GROUP BY deviceId, HOPPINGWINDOW(ss, 10, 5)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=16, debug_membership=True)
+    cols = _gap_stream(20_000, 16, seed=97)
+    for cut in (5_000, 13_333):
+        got, exp, st, _ = run_split(oracle, engine_mod, rule, cols, cut, batches=(3, 5), twice=True)
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
