@@ -2348,6 +2348,7 @@ struct Engine {
             W = M - T;
             has_W = true;
         }
+        bool hop_dropped = false;
         // ---- 3b. hopping empty-window discard (window_op.go:605-655, lateTolerance 0): only a batch with an
         // arrival gap wider than the window can trigger an empty window, so the mask pass runs only then
         if (wtype == EK_WINDOW_HOPPING && T == 0 && n_acc > 0 && s.max_gap > L) {
@@ -2367,13 +2368,15 @@ struct Engine {
                 d_acc = (const uint8_t*)acc.p;
                 n_acc -= dropped;
                 stats.records_discarded += dropped;
+                hop_dropped = true;
             }
         }
         if (range_mode) {
             const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M);
             return rc ? rc : record_time();
         }
-        if (n_acc == 0) return record_time();
+        // a batch whose every accepted event was discarded still advanced the watermark: its windows close below
+        if (n_acc == 0 && !(hop_dropped && e1_known)) return record_time();
 
         // ---- 4. first window alignment once the first event is released
         if (!e1_known) {

@@ -112,3 +112,19 @@ def test_hopping_gap_checkpoint(oracle, engine_mod, median):
     for cut in (5_000, 13_333):
         got, exp, st, _ = run_split(oracle, engine_mod, rule, cols, cut, batches=(3, 5), twice=True)
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("median", [False, True], ids=["pane", "range"])
+def test_hopping_gap_one_event_per_push(oracle, engine_mod, median):
+    # a push whose only event is discarded still advances the watermark and closes the windows below it
+    sql = SQL if not median else ("SELECT deviceId, count(*), median(temperature) FROM demo "
+                                  "GROUP BY deviceId, HOPPINGWINDOW(ss, 10, 5)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=4, debug_membership=True)
+    ts = np.array([1000, 2000, 60000, 61000, 80000, 80500, 200000, 200001, 260000], np.int64)
+    n = len(ts)
+    cols = [(np.arange(n) % 4).astype(np.uint32), ts, np.arange(n, dtype=np.float64) * 1.5, np.ones(n)]
+    exp = oracle.run(rule.plan, cols)
+    got, st = _run(engine_mod, rule, cols, n)
+    assert st.records_discarded == 4
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
