@@ -34,6 +34,7 @@ using namespace ek;
 namespace {
 
 constexpr int64_t kMinTs = INT64_MIN;
+constexpr int64_t kYear1Ms = -62135596800000LL;   // Go's time.Time{} (0001-01-01T00:00:00Z) in Unix ms
 
 struct DevBuf {
     void* p = nullptr;
@@ -1815,6 +1816,18 @@ struct Engine {
                     }
                 }
             }
+        }
+        if (!pw.empty() && plan.is_event_time && eb.n > 0) {
+            // emitWindow(time.Time{}, InfTime) -> scanWindow keeps rows whose timestamp is After(time.Time{})
+            // (window_v2_op.go:77-87,254-263): in the ts-ordered buffer those are the rows from lb(year 1 + 1 ms) on
+            const int64_t bound = kYear1Ms + 1;
+            if (int rc = ensure(bounds_val, 8)) return rc;
+            if (int rc = ensure(bounds_idx, 8)) return rc;
+            hipMemcpyAsync(bounds_val.p, &bound, 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p, (int64_t)0,
+                               eb.n, (const int64_t*)bounds_val.p, 1, (int64_t*)bounds_idx.p);
+            const int64_t y1 = fetch_i64(bounds_idx.p);
+            for (PendWin& p : pw) p.q.pos = std::max(p.q.pos, std::min(y1, p.q.rstep));
         }
         int rc = fire_windows(pw);
         // rows before the open window (or every scanned row) are never needed again (scanner.gc(InfTime))

@@ -137,3 +137,19 @@ def test_window_v2_rejections(engine_mod):
         with pytest.raises(engine_mod.EngineError) as e:
             engine_mod.Engine(r.plan)
         assert e.value.code == A.EK_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("batches", [1, 5])
+def test_state_window_event_time_year1_rows(oracle, engine_mod, batches):
+    """scanWindow keeps rows whose timestamp is After(time.Time{}) (window_v2_op.go:254-263): rows stamped exactly
+    0001-01-01T00:00:00Z (the earliest the watermark accepts) join the state machine but no window's content."""
+    sql = "SELECT deviceId, count(*), sum(temperature) FROM demo GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 97)"
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=50, debug_membership=True)
+    cols = _with_trig(_iot(20_000, 50, seed=95, epm=4), 40)
+    cols[1] = cols[1].astype(np.int64).copy()
+    cols[1][:300] = -62135596800000   # Go's time.Time{} in Unix ms
+    cols[-1][:300] = 1                # the first window opens on a year-1 row
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert st.records_late == exp.records_late
+    assert len(got) > 5
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
