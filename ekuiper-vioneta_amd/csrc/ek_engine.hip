@@ -28,6 +28,7 @@
 #include "ek_kernels.h"
 #include "ek_lib.h"
 #include "ek_range.h"
+#include "ek_global.h"
 
 using namespace ek;
 
@@ -672,6 +673,11 @@ struct Engine {
         inc_has_T = false;
         inc_T = 0;
         inc_pend.clear();
+        gmode = 0;
+        g_row_arr = nullptr;
+        g_wm_arr.clear();
+        g_wm_ts.clear();
+        g_trig.clear();
         wins.clear();
         r_rows_used = 0;
         stats = ek_stats{};
@@ -1204,6 +1210,11 @@ struct Engine {
                 hipMemcpyAsync(valh[c].data(), db.valid[c], n, hipMemcpyDeviceToHost, stream);
             }
         }
+        std::vector<int64_t> garr;
+        if (g_row_arr) {   // shard mode: global arrivals
+            garr.resize(n);
+            hipMemcpyAsync(garr.data(), g_row_arr, n * 8, hipMemcpyDeviceToHost, stream);
+        }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "pending copy failed");
         const int64_t* ts = (const int64_t*)colh[dp.ts_col].data();
         for (int64_t i = 0; i < n; ++i) {
@@ -1214,7 +1225,7 @@ struct Engine {
                 if (db.valid[c] && !pend_has_valid[c]) { pend_vhost[c].assign(pend_n, 1); pend_has_valid[c] = true; }
                 if (pend_has_valid[c]) pend_vhost[c].push_back(db.valid[c] ? valh[c][i] : 1);
             }
-            pend_arr.push_back(arrival_base + i);
+            pend_arr.push_back(g_row_arr ? garr[i] : arrival_base + i);
             pend_min = std::min(pend_min, ts[i]);
             pend_max = std::max(pend_max, ts[i]);
             pend_n++;
@@ -1363,8 +1374,12 @@ struct Engine {
                 else fill_valid_ones(c, eb.n, cnt);
             }
         }
-        const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
-        hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
+        if (g_row_arr) {   // shard mode: the rows' global arrival indices
+            if (cnt > 0) hipMemcpyAsync((int64_t*)eb.arr.p + eb.n, g_row_arr + start, (size_t)cnt * 8, hipMemcpyDeviceToDevice, stream);
+        } else {
+            const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
+            hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
+        }
         if (need_rel) hipMemsetAsync((int64_t*)eb.rel.p + eb.n, 0x7f, (size_t)cnt * 8, stream);   // "not released"
         eb.n += cnt;
         return 0;
@@ -1447,8 +1462,11 @@ struct Engine {
         }
         // arrivals of the batch rows: arr_base + row
         if (int rc = ensure(mrg_col, (size_t)std::max<int64_t>(n, 1) * 8)) return rc;
-        hipLaunchKernelGGL(k_iota64, dim3((int)std::min<int64_t>(4096, (n + 255) / 256)), dim3(256), 0, stream,
-                           (int64_t*)mrg_col.p, arr_base, n);
+        if (g_row_arr)
+            hipMemcpyAsync(mrg_col.p, g_row_arr, (size_t)n * 8, hipMemcpyDeviceToDevice, stream);
+        else
+            hipLaunchKernelGGL(k_iota64, dim3((int)std::min<int64_t>(4096, (n + 255) / 256)), dim3(256), 0, stream,
+                               (int64_t*)mrg_col.p, arr_base, n);
         hipLaunchKernelGGL(k_gather8, dim3(g), dim3(256), 0, stream, perm, nm, ntail, (const int64_t*)tail_slot(plan.n_columns),
                            (const int64_t*)mrg_col.p, (const int64_t*)bidx, (int64_t*)eb.arr.p + p);
         if (need_rel) {
@@ -1493,7 +1511,8 @@ struct Engine {
         for (int w = 0; w < nq; ++w) hq[w] = pw[w].q;
         hipMemcpyAsync(rq_d.p, hq.data(), (size_t)nq * sizeof(RangeQ), hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(k_window_ranges, dim3((nq + 255) / 256), dim3(256), 0, stream, (const int64_t*)eb.col[std::max(0, dp.ts_col)].p,
-                           need_rel ? (const int64_t*)eb.rel.p : nullptr, eb_rel, (const RangeQ*)rq_d.p, nq, (int64_t*)ab_d.p);
+                           need_rel ? (const int64_t*)eb.rel.p : nullptr, (const int64_t*)eb.arr.p, eb_rel, (const RangeQ*)rq_d.p, nq,
+                           (int64_t*)ab_d.p);
         h_ab.resize((size_t)nq * 2);
         hipMemcpyAsync(h_ab.data(), ab_d.p, (size_t)nq * 16, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window range kernel failed");
@@ -1648,7 +1667,9 @@ struct Engine {
         const int64_t n_new = eb_rel - rel_prev;
         if (inc && wtype == EK_WINDOW_SLIDING) return inc_slide_triggers(rel_prev);
         if (inc && wtype == EK_WINDOW_COUNT) return inc_count_triggers(rel_prev);
-        if (wtype == EK_WINDOW_SLIDING) {
+        if (wtype == EK_WINDOW_SLIDING && gmode) {
+            if (int rc = global_slide_triggers(pw)) return rc;
+        } else if (wtype == EK_WINDOW_SLIDING) {
             const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
             if (n_new > 0) {
                 // trigger events among the newly released rows (OVER (WHEN ...)), in release order
@@ -1736,7 +1757,7 @@ struct Engine {
             eb_floor = inc_pend.empty() ? eb_rel : std::min(eb_rel, inc_pend.front().floor_abs - eb_base);
             return rc;
         } else if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_HOPPING) {
-            if (!e1_known && eb_rel > 0) {
+            if (!e1_known && eb_rel > 0 && !gmode) {
                 e1_known = true;
                 first_ts = fetch_i64(eb.col[dp.ts_col].p);
                 E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
@@ -2245,19 +2266,9 @@ struct Engine {
         return rc;
     }
 
-    int push(const ek_batch* b) {
-        if (!b) return fail(EK_ERR_INVALID, "null batch");
-        int64_t n = b->n_rows;
-        if (n < 0) return fail(EK_ERR_INVALID, "negative row count");
-        if (n == 0) return 0;
-        if (n > ((int64_t)1 << 31) - 1) return fail(EK_ERR_UNSUPPORTED, "batch larger than 2^31-1 rows");
-        for (int c = 0; c < plan.n_columns; ++c) {
-            if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
-            if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
-        }
-        phase_used = 0;
-        hipEventRecord(ev0, stream);
-        DBatch db{};
+    // the batch's columns on the device (host batches are copied to the handle's staging buffers)
+    int stage_batch(const ek_batch* b, DBatch& db) {
+        const int64_t n = b->n_rows;
         db.n = n;
         if (b->memory == EK_MEM_HOST) {
             for (int c = 0; c < plan.n_columns; ++c) {
@@ -2274,6 +2285,24 @@ struct Engine {
         } else {
             for (int c = 0; c < plan.n_columns; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
         }
+        return 0;
+    }
+
+    int push(const ek_batch* b) {
+        if (!b) return fail(EK_ERR_INVALID, "null batch");
+        int64_t n = b->n_rows;
+        if (n < 0) return fail(EK_ERR_INVALID, "negative row count");
+        if (n == 0) return 0;
+        if (n > ((int64_t)1 << 31) - 1) return fail(EK_ERR_UNSUPPORTED, "batch larger than 2^31-1 rows");
+        for (int c = 0; c < plan.n_columns; ++c) {
+            if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
+            if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
+        }
+        if (gmode) return fail(EK_ERR_STATE, "the handle takes its watermark from ek_push_batch_global (shard mode)");
+        phase_used = 0;
+        hipEventRecord(ev0, stream);
+        DBatch db{};
+        if (int rc = stage_batch(b, db)) return rc;
         stats.records_in += n;
         if (wtype == EK_WINDOW_NONE) {
             const int rc = push_filter(db);
@@ -2434,6 +2463,337 @@ struct Engine {
             }
         }
         phase_used = 0;
+        return 0;
+    }
+
+
+    // ================================================================== SHARD mode (global watermark)
+    // One key-hash shard of a rule (include/ekgpu.h, ek_push_batch_global): the rows of this handle carry their
+    // global arrival index; the WatermarkTuples of the whole stream come from the host that assigns the arrival
+    // order (ekgpu/shard.py GlobalWatermark, watermark_op.go:144-225). Acceptance, release steps and window closing
+    // follow those tuples instead of the handle's own rows. Rows are otherwise processed exactly as in the local
+    // modes (pane partials for tumbling / hopping, the ts-ordered event buffer for sliding windows, the arrival
+    // ordered buffer for processing-time count windows).
+    int gmode = 0;                      // 1: shard mode (entered by the first global push, left by ek_reset)
+    const int64_t* g_row_arr = nullptr; // device: global arrival of the current batch's rows
+    std::vector<int64_t> g_wm_arr, g_wm_ts;   // the current push's WatermarkTuples (host copy)
+    DevBuf g_wm_d, g_arr_d, g_acc_d;
+    struct GTrig { int64_t a, t; };
+    std::vector<GTrig> g_trig;          // accepted global sliding triggers not released yet (arrival order)
+
+    int global_check() {
+        if (plan.is_event_time) {
+            if (inc || plan.window_version == 2 || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_STATE)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: session, state, v2 and incremental windows depend on every row "
+                                                "of the stream (not shardable by key)");
+            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: delayed sliding windows are not built");
+            if (wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms != 0)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: the hopping empty-window discard is built for lateTolerance 0");
+        } else if (wtype != EK_WINDOW_COUNT || inc) {
+            return fail(EK_ERR_UNSUPPORTED, "shard mode: processing time is built for COUNTWINDOW");
+        }
+        return 0;
+    }
+
+    WmList wm_list() const {
+        WmList w{};
+        w.arr = (const int64_t*)g_wm_d.p;
+        w.ts = w.arr ? w.arr + g_wm_arr.size() : nullptr;
+        w.n = (int64_t)g_wm_arr.size();
+        w.carry = has_W ? W : INT64_MIN;
+        return w;
+    }
+
+    // host copies + one device upload of the tuple list; the rows' arrivals on the device
+    int global_stage(const ek_global_ctx* g, int64_t n) {
+        if (g->n_wm < 0 || g->n_trig < 0) return fail(EK_ERR_INVALID, "negative list length");
+        if ((g->n_wm > 0 && (!g->wm_arrival || !g->wm_ts)) || (g->n_trig > 0 && (!g->trig_arrival || !g->trig_ts)))
+            return fail(EK_ERR_INVALID, "missing watermark / trigger list");
+        if (n > 0 && !g->row_arrival) return fail(EK_ERR_INVALID, "missing row arrivals");
+        g_wm_arr.assign(g->wm_arrival, g->wm_arrival + g->n_wm);
+        g_wm_ts.assign(g->wm_ts, g->wm_ts + g->n_wm);
+        for (int64_t k = 0; k < g->n_wm; ++k) {
+            if ((k > 0 && (g_wm_arr[k] <= g_wm_arr[k - 1] || g_wm_ts[k] <= g_wm_ts[k - 1])) || (has_W && g_wm_ts[k] <= W))
+                return fail(EK_ERR_INVALID, "WatermarkTuples must advance (tuple %lld)", (long long)k);
+        }
+        if (g->n_wm > 0) {
+            if (int rc = ensure(g_wm_d, (size_t)g->n_wm * 16)) return rc;
+            // one upload from a pinned staging block
+            int64_t* h = desc_alloc((size_t)g->n_wm * 2);
+            if (!h) return fail(EK_ERR_NOMEM, "pinned");
+            memcpy(h, g_wm_arr.data(), (size_t)g->n_wm * 8);
+            memcpy(h + g->n_wm, g_wm_ts.data(), (size_t)g->n_wm * 8);
+            hipMemcpyAsync(g_wm_d.p, h, (size_t)g->n_wm * 16, hipMemcpyHostToDevice, stream);
+        }
+        g_row_arr = nullptr;
+        if (n > 0) {
+            if (g->memory == EK_MEM_HOST) {
+                if (int rc = ensure(g_arr_d, (size_t)n * 8)) return rc;
+                hipMemcpyAsync(g_arr_d.p, g->row_arrival, (size_t)n * 8, hipMemcpyHostToDevice, stream);
+                g_row_arr = (const int64_t*)g_arr_d.p;
+            } else {
+                g_row_arr = g->row_arrival;
+            }
+        }
+        return 0;
+    }
+
+    // accept mask of the staged batch (nullptr: every row accepted); n_acc / min_acc / dropped out
+    int global_accept(const DBatch& db, int64_t min_ts, bool hop, int64_t e1, const uint8_t** d_acc, int64_t* n_acc,
+                      int64_t* min_acc, int64_t* dropped) {
+        const int64_t n = db.n;
+        const WmList w = wm_list();
+        int64_t wmax = w.carry;
+        if (w.n > 0) wmax = std::max(wmax, g_wm_ts.back());
+        *d_acc = nullptr; *n_acc = n; *min_acc = min_ts; *dropped = 0;
+        if (!hop && (wmax == INT64_MIN || min_ts >= wmax)) return 0;   // no row can be late
+        if (int rc = ensure(g_acc_d, (size_t)n)) return rc;
+        hipMemsetAsync(&((BatchStats*)bstats.p)->n_accepted, 0, 8, stream);
+        hipMemsetAsync(&((BatchStats*)bstats.p)->n_dropped, 0, 8, stream);
+        const int64_t big = INT64_MAX;
+        hipMemcpyAsync(&((BatchStats*)bstats.p)->min_accepted, &big, 8, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_accept_global, dim3((int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                           (const int64_t*)db.col[dp.ts_col], g_row_arr, n, w, hop ? 1 : 0, e1, H, L, (uint8_t*)g_acc_d.p,
+                           (BatchStats*)bstats.p);
+        hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "global accept kernel failed");
+        *n_acc = h_stats->n_accepted;
+        *min_acc = h_stats->min_accepted;
+        *dropped = h_stats->n_dropped;
+        if (*n_acc < n) *d_acc = (const uint8_t*)g_acc_d.p;
+        return 0;
+    }
+
+    int push_global(const ek_batch* b, const ek_global_ctx* g) {
+        if (!g) return fail(EK_ERR_INVALID, "null global context");
+        const int64_t n = b ? b->n_rows : 0;
+        if (n < 0) return fail(EK_ERR_INVALID, "negative row count");
+        if (n > ((int64_t)1 << 31) - 1) return fail(EK_ERR_UNSUPPORTED, "batch larger than 2^31-1 rows");
+        if (wtype == EK_WINDOW_NONE) return fail(EK_ERR_UNSUPPORTED, "shard mode needs a window");
+        if (!gmode) {
+            if (stats.records_in > 0 || has_W) return fail(EK_ERR_STATE, "the handle already runs on its own watermark (ek_push_batch)");
+            if (int rc = global_check()) return rc;
+            gmode = 1;
+        }
+        if (g->arrivals_end < arrivals) return fail(EK_ERR_INVALID, "arrivals_end went backwards");
+        if (n > 0) {
+            for (int c = 0; c < plan.n_columns; ++c) {
+                if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
+                if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
+            }
+        }
+        phase_used = 0;
+        hipEventRecord(ev0, stream);
+        h_wdesc_used = 0;
+        h_desc_used = 0;
+        aux_used = 0;
+        hipStreamSynchronize(stream);   // the pinned descriptor blocks are reused below
+        if (int rc = global_stage(g, n)) return rc;
+        DBatch db{};
+        if (n > 0) {
+            if (int rc = stage_batch(b, db)) return rc;
+        }
+        stats.records_in += n;
+        int rc = 0;
+        if (!plan.is_event_time) rc = push_count_global(db, g);
+        else rc = push_global_event(db, g);
+        g_row_arr = nullptr;
+        if (rc) return rc;
+        arrivals = g->arrivals_end;
+        return record_time();
+    }
+
+    int push_global_event(const DBatch& db, const ek_global_ctx* g) {
+        const int64_t n = db.n;
+        const int64_t T = plan.late_tolerance_ms;
+        BatchStats s{};
+        s.min_ts = INT64_MAX;
+        s.max_ts = INT64_MIN;
+        if (n > 0) {
+            const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+            const int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
+            if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
+            const int ph_s = phase_begin(EK_PHASE_STATS);
+            hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN, (BatchStats*)bstats_part.p);
+            hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
+                               (BatchStats*)bstats.p);
+            phase_end(ph_s);
+            hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
+            s = *h_stats;
+        }
+        // the first window's anchor: the global earliest released event (getEarliestEventTs at that tuple)
+        const bool origin_now = !e1_known && g->origin_known;
+        const int64_t e1_anchor = g->origin_known ? aligned_end(g->origin_ts, raw_interval, plan.time_unit, plan.tz_offset_s) : 0;
+        const bool hop = wtype == EK_WINDOW_HOPPING && T == 0 && (e1_known || g->origin_known);
+        const uint8_t* d_acc = nullptr;
+        int64_t n_acc = 0, min_acc = s.min_ts, dropped = 0;
+        if (n > 0) {
+            if (int rc = global_accept(db, s.min_ts, hop, e1_known ? E1 : e1_anchor, &d_acc, &n_acc, &min_acc, &dropped)) return rc;
+        }
+        stats.records_late += n - n_acc - dropped;
+        stats.records_discarded += dropped;
+        // the shard's own max ts (buffer order bookkeeping only: it does not move the watermark)
+        const int64_t M_prev = M;
+        const bool had_M = has_M;
+        if (n > 0 && (!has_M || s.max_ts > M)) { M = s.max_ts; has_M = true; }
+        if (!g_wm_ts.empty()) {
+            W = g_wm_ts.back();
+            has_W = true;
+            sW = g_wm_arr.back();
+        }
+        if (origin_now) {
+            e1_known = true;
+            first_ts = g->origin_ts;
+            E1 = e1_anchor;
+            grid.tumbling = wtype == EK_WINDOW_TUMBLING;
+            grid.origin = grid.tumbling ? E1 : E1 - L;
+            grid.P = P;
+        }
+        const int64_t arrival_base = arrivals;
+        if (range_mode) {
+            if (n_acc > 0) {
+                if (!s.unsorted && !d_acc && (eb.n == 0 || !had_M || min_acc >= M_prev)) {
+                    if (int rc = eb_append(db, 0, n_acc, arrival_base)) return rc;
+                } else {
+                    if (int rc = eb_merge(db, 0, d_acc, n_acc, min_acc, s.max_ts, arrival_base)) return rc;
+                }
+            }
+            const int64_t rel_prev = eb_rel;
+            if (has_W && eb.n > 0) {
+                if (int rc = ensure(bounds_idx, 8)) return rc;
+                hipLaunchKernelGGL(k_rel_end, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
+                                   (const int64_t*)eb.arr.p, eb.n, W, sW, (int64_t*)bounds_idx.p);
+                eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
+            }
+            if (need_rel && eb_rel > rel_prev) {
+                const int gg = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
+                hipLaunchKernelGGL(k_release_step_global, dim3(gg), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
+                                   (const int64_t*)eb.arr.p, rel_prev, eb_rel, wm_list(), (int64_t*)eb.rel.p);
+            }
+            for (int64_t k = 0; k < g->n_trig; ++k) g_trig.push_back(GTrig{g->trig_arrival[k], g->trig_ts[k]});
+            return range_triggers(rel_prev);
+        }
+        // pane mode: rows before the anchor wait (host side) until the first release is known
+        if (!e1_known) {
+            if (n_acc > 0) return append_pending(db, d_acc, arrival_base);
+            return 0;
+        }
+        if (origin_now && pend_n) {
+            if (int rc = flush_pending()) return rc;
+        }
+        if (n_acc > 0) {
+            const int64_t save = arrivals;
+            arrivals = arrival_base;
+            int rc = process(db, !s.unsorted, 0, d_acc, min_acc, s.max_ts, g_row_arr);
+            arrivals = save;
+            if (rc) return rc;
+        }
+        // windows the global watermark closed beyond this shard's rows
+        return finalize_ready(INT64_MAX / 4);
+    }
+
+    // SLIDINGWINDOW triggers of the whole stream (shard mode): a trigger fires at the tuple that releases it
+    // (ts < W, or ts == W and it arrived no later than that tuple's event), over the rows released so far with
+    // t - L <= ts <= t and release step <= the trigger's (window_op.go:605-655, event_window_trigger.go:147-166).
+    int global_slide_triggers(std::vector<PendWin>& pw) {
+        if (!has_W || g_trig.empty()) return 0;
+        std::vector<GTrig> rel, keep;
+        for (const GTrig& x : g_trig) {
+            if (x.t < W || (x.t == W && x.a <= sW)) rel.push_back(x);
+            else keep.push_back(x);
+        }
+        g_trig.swap(keep);
+        std::stable_sort(rel.begin(), rel.end(), [](const GTrig& x, const GTrig& y) { return x.t < y.t || (x.t == y.t && x.a < y.a); });
+        for (const GTrig& x : rel) {
+            // the releasing tuple: the first one at or after its arrival whose watermark reaches its ts
+            const size_t k0 = std::lower_bound(g_wm_arr.begin(), g_wm_arr.end(), x.a) - g_wm_arr.begin();
+            const size_t k1 = std::lower_bound(g_wm_ts.begin(), g_wm_ts.end(), x.t) - g_wm_ts.begin();
+            const size_t k = std::max(k0, k1);
+            if (k >= g_wm_arr.size()) return fail(EK_ERR_INVALID, "trigger at arrival %lld is not released by this batch's tuples", (long long)x.a);
+            PendWin p{};
+            p.q.kind = RB_SLIDE;
+            p.q.lo_ts = x.t - L;
+            p.q.hi_ts = x.t;
+            p.q.pos = eb_floor - 1;      // the search starts at the floor: every row before the trigger's run is a member candidate
+            p.q.rstep = g_wm_arr[k];
+            p.q.floor = eb_floor;
+            p.start = x.t - L;
+            p.end = x.t;
+            pw.push_back(p);
+        }
+        return 0;
+    }
+
+    // COUNTWINDOW(n[, m]) of a shard: blocks of the GLOBAL arrival order (window_op.go:390-418)
+    int push_count_global(const DBatch& db, const ek_global_ctx* g) {
+        const int64_t n = db.n;
+        if (n > 0) {
+            if (int rc = eb_append(db, 0, n, 0)) return rc;
+        }
+        eb_rel = eb.n;
+        const int64_t len = plan.length, itv = plan.interval > 0 ? plan.interval : plan.length;
+        std::vector<PendWin> pw;
+        for (; count_k * itv <= g->arrivals_end; ++count_k) {
+            const int64_t e = count_k * itv;
+            if (e < len) continue;
+            PendWin p{};
+            p.q.kind = RB_ARR;
+            p.q.lo_ts = e - len;
+            p.q.hi_ts = e;
+            p.q.floor = eb_floor;
+            pw.push_back(p);
+        }
+        return fire_windows(pw);
+    }
+
+    // ek_shard_triggers: accepted rows of the batch that match OVER (WHEN ...)
+    int shard_triggers(const ek_batch* b, const ek_global_ctx* g, int64_t* out_a, int64_t* out_t, int64_t cap, int64_t* n_out) {
+        if (!b || !g || !n_out) return fail(EK_ERR_INVALID, "null argument");
+        if (wtype != EK_WINDOW_SLIDING || !plan.is_event_time) return fail(EK_ERR_UNSUPPORTED, "triggers belong to event-time sliding windows");
+        if (!gmode) {
+            if (stats.records_in > 0 || has_W) return fail(EK_ERR_STATE, "the handle already runs on its own watermark (ek_push_batch)");
+            if (int rc = global_check()) return rc;
+        }
+        const int64_t n = b->n_rows;
+        *n_out = 0;
+        if (n <= 0) return 0;
+        hipStreamSynchronize(stream);
+        h_desc_used = 0;
+        if (int rc = global_stage(g, n)) return rc;
+        DBatch db{};
+        if (int rc = stage_batch(b, db)) return rc;
+        const uint8_t* d_acc = nullptr;
+        int64_t n_acc = 0, min_acc = 0, dropped = 0;
+        if (int rc = global_accept(db, INT64_MIN, false, 0, &d_acc, &n_acc, &min_acc, &dropped)) return rc;
+        if (int rc = ensure(flags_d, (size_t)n)) return rc;
+        if (int rc = ensure(trig_d, (size_t)n * 8)) return rc;
+        const int nb = (int)((n + kCompactTile - 1) / kCompactTile);
+        if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+        const int gg = (int)std::min<int64_t>(4096, (n + 255) / 256);
+        hipLaunchKernelGGL(k_trigger_flags, dim3(gg), dim3(256), 0, stream, d_plan, db, (int64_t)0, n, (uint8_t*)flags_d.p);
+        if (d_acc) hipLaunchKernelGGL(k_and_flags, dim3(gg), dim3(256), 0, stream, (uint8_t*)flags_d.p, d_acc, n);
+        hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (int64_t*)cnts_d.p);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+        hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (const int64_t*)cnts_d.p,
+                           (int64_t)0, (int64_t*)trig_d.p);
+        const int64_t nt = fetch_i64((const int64_t*)cnts_d.p + nb);
+        *n_out = nt;
+        const int64_t nc = std::min(nt, cap);
+        if (nc > 0 && out_a && out_t) {
+            if (int rc = ensure(mrg_col, (size_t)nc * 16)) return rc;
+            int64_t* gbuf = (int64_t*)mrg_col.p;
+            const int g2 = (int)std::min<int64_t>(4096, (nc + 255) / 256);
+            hipLaunchKernelGGL(k_gather8, dim3(g2), dim3(256), 0, stream, (const int64_t*)trig_d.p, nc, INT64_MAX, g_row_arr,
+                               (const int64_t*)nullptr, (const int64_t*)nullptr, gbuf);
+            hipLaunchKernelGGL(k_gather8, dim3(g2), dim3(256), 0, stream, (const int64_t*)trig_d.p, nc, INT64_MAX,
+                               (const int64_t*)db.col[dp.ts_col], (const int64_t*)nullptr, (const int64_t*)nullptr, gbuf + nc);
+            hipMemcpyAsync(out_a, gbuf, (size_t)nc * 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(out_t, gbuf + nc, (size_t)nc * 8, hipMemcpyDeviceToHost, stream);
+        }
+        g_row_arr = nullptr;
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger evaluation failed");
         return 0;
     }
 
@@ -2922,6 +3282,30 @@ const char* ek_last_error(void* h) {
 int ek_destroy(void* h) {
     delete (Engine*)h;
     return 0;
+}
+
+int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->push_global(batch, g);
+}
+
+int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end) {
+    if (!h) return EK_ERR_INVALID;
+    Engine* e = (Engine*)h;
+    const int64_t a = std::max<int64_t>(0, arrivals_end - 1);
+    ek_global_ctx g{};
+    g.arrivals_end = arrivals_end;
+    g.wm_arrival = &a;
+    g.wm_ts = &wm_ms;
+    g.n_wm = 1;
+    g.memory = EK_MEM_HOST;
+    return e->push_global(nullptr, &g);
+}
+
+int ek_shard_triggers(void* h, const ek_batch* batch, const ek_global_ctx* g, int64_t* out_arrival, int64_t* out_ts,
+                      int64_t cap, int64_t* n_out) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->shard_triggers(batch, g, out_arrival, out_ts, cap, n_out);
 }
 
 int ek_export_state(void* h, void* buf, int64_t cap, int64_t* size) {

@@ -244,10 +244,11 @@ __global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict
 }
 
 // Window range descriptor (host -> device): content = [max(floor, lo(lo_ts)), hi(...)) of the buffer.
-enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3, RB_CAP = 4 };
+enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3, RB_CAP = 4, RB_ARR = 5 };
 struct RangeQ {
     int64_t lo_ts;      // lower bound ts: content starts at the first row with ts >= lo_ts (INT64_MIN: from floor)
     int64_t hi_ts;      // RB_LB: first row with ts >= hi_ts; RB_SLIDE: ts <= hi_ts and release step <= rstep
+                        // RB_ARR (shard count windows): rows with global arrival in [lo_ts, hi_ts)
     int64_t pos;        // RB_SLIDE: buffer index of the trigger event; RB_FIXED: a (index)
     int64_t rstep;      // RB_SLIDE: release step of the trigger event; RB_FIXED: b (index)
     int64_t floor;      // smallest buffer index a window may start at
@@ -255,13 +256,17 @@ struct RangeQ {
     int32_t pad;
 };
 
-__global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* __restrict__ brel, int64_t n_rel,
-                                const RangeQ* __restrict__ q, int nq, int64_t* __restrict__ ab) {
+__global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* __restrict__ brel,
+                                const int64_t* __restrict__ barr, int64_t n_rel, const RangeQ* __restrict__ q, int nq,
+                                int64_t* __restrict__ ab) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nq) return;
     const RangeQ d = q[w];
     int64_t a, b;
-    if (d.kind == RB_FIXED) {
+    if (d.kind == RB_ARR) {
+        a = max(d.floor, lb_i64(barr, d.floor, n_rel, d.lo_ts));
+        b = lb_i64(barr, a, n_rel, d.hi_ts);
+    } else if (d.kind == RB_FIXED) {
         a = d.pos;
         b = d.rstep;
     } else if (d.kind == RB_CAP) {

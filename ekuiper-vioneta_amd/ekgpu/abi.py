@@ -131,6 +131,26 @@ class ek_stats(C.Structure):
 EK_PHASE_STATS, EK_PHASE_PARTITION, EK_PHASE_AGGREGATE, EK_PHASE_FINALIZE = 0, 1, 2, 3
 
 
+class ek_global_ctx(C.Structure):
+    """Global context of one shard's micro-batch (ekgpu.h, ek_push_batch_global)."""
+    _fields_ = [
+        ("row_arrival", C.c_void_p),
+        ("arrivals_end", C.c_int64),
+        ("wm_arrival", C.c_void_p),
+        ("wm_ts", C.c_void_p),
+        ("n_wm", C.c_int64),
+        ("origin_known", C.c_int32),
+        ("pad", C.c_int32),
+        ("origin_ts", C.c_int64),
+        ("origin_arrival", C.c_int64),
+        ("trig_arrival", C.c_void_p),
+        ("trig_ts", C.c_void_p),
+        ("n_trig", C.c_int64),
+        ("memory", C.c_int32),
+        ("pad2", C.c_int32),
+    ]
+
+
 def mix64(x: int) -> int:
     """ek_mix64 from the header (splitmix64 finaliser), on python ints."""
     m = (1 << 64) - 1

@@ -125,6 +125,26 @@ def all_gather_partials(local: np.ndarray, group=None) -> List[np.ndarray]:
     return [o[:c].cpu().numpy() for o, c in zip(outs, counts)]
 
 
+def exchange_triggers(trig_arrival: np.ndarray, trig_ts: np.ndarray, group=None) -> Tuple[np.ndarray, np.ndarray]:
+    """The sliding-window trigger exchange of a key-hash-sharded rule: every rank's accepted OVER (WHEN ...) rows
+    (global arrival, ts) of the micro-batch (ek_shard_triggers) go to every rank with one all_gather (RCCL over
+    xGMI with backend "nccl"); the merged list, in global arrival order, is the ek_global_ctx trigger list every
+    shard fires its windows for (event_window_trigger.go:190-192: a trigger opens a window over ALL keys)."""
+    from .shard import merge_triggers
+    local = np.stack([np.asarray(trig_arrival, np.int64), np.asarray(trig_ts, np.int64)], axis=1) \
+        if len(trig_arrival) else np.zeros((0, 2), np.int64)
+    parts = all_gather_partials(local, group)
+    return merge_triggers([(p[:, 0], p[:, 1]) for p in parts])
+
+
+def all_gather_objects(obj, group=None) -> list:
+    """Picklable per-rank results to every rank (result gather of the tests / tools; not on the data path)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
 # ------------------------------------------------------------------ merge
 def _val(bits: int, tag: int):
     if tag == A.EK_TAG_NULL:

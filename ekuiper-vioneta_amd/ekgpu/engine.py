@@ -52,6 +52,13 @@ def lib():
         L.ek_last_error.restype = C.c_char_p
         L.ek_destroy.argtypes = [C.c_void_p]
         L.ek_destroy.restype = C.c_int
+        L.ek_push_batch_global.argtypes = [C.c_void_p, C.POINTER(A.ek_batch), C.POINTER(A.ek_global_ctx)]
+        L.ek_push_batch_global.restype = C.c_int
+        L.ek_advance_watermark.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+        L.ek_advance_watermark.restype = C.c_int
+        L.ek_shard_triggers.argtypes = [C.c_void_p, C.POINTER(A.ek_batch), C.POINTER(A.ek_global_ctx), C.c_void_p,
+                                        C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.ek_shard_triggers.restype = C.c_int
         L.ek_json_create.argtypes = [C.POINTER(A.ek_json_schema), C.c_int, C.POINTER(C.c_void_p)]
         L.ek_json_create.restype = C.c_int
         L.ek_json_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int32,
@@ -78,7 +85,8 @@ def lib():
 EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_batch", "ek_poll_results",
                     "ek_release_results", "ek_reset", "ek_sync", "ek_set_stream", "ek_get_stats", "ek_last_error",
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
-                    "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state"]
+                    "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
+                    "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -131,6 +139,47 @@ class Engine:
     def push_batch(self, batch: A.ek_batch):
         """Push an ek_batch as is (e.g. the device columns returned by JsonDecoder.decode)."""
         self._check(lib().ek_push_batch(self.h, C.byref(batch)))
+
+    def _host_batch(self, columns, validity=None):
+        cols = [np.ascontiguousarray(columns[k], dtype=_NP[self.plan.column_type[k]]) for k in range(self.plan.n_columns)]
+        b = A.ek_batch()
+        b.n_rows = len(cols[0]) if cols else 0
+        b.memory = A.EK_MEM_HOST
+        keep = list(cols)
+        for k, c in enumerate(cols):
+            b.columns[k] = c.ctypes.data
+            if validity is not None and validity[k] is not None:
+                v = np.ascontiguousarray(validity[k], dtype=np.uint8)
+                keep.append(v)
+                b.validity[k] = v.ctypes.data
+        return b, keep
+
+    def push_global(self, columns, ctx: A.ek_global_ctx, validity=None):
+        """Shard mode (ek_push_batch_global): this handle's rows (host arrays) + the global context."""
+        b, _keep = self._host_batch(columns, validity)
+        self._check(lib().ek_push_batch_global(self.h, C.byref(b), C.byref(ctx)))
+
+    def push_global_device(self, n_rows: int, col_ptrs, ctx: A.ek_global_ctx):
+        b = A.ek_batch()
+        b.n_rows = n_rows
+        b.memory = A.EK_MEM_DEVICE
+        for k, ptr in enumerate(col_ptrs):
+            b.columns[k] = ptr
+        self._check(lib().ek_push_batch_global(self.h, C.byref(b), C.byref(ctx)))
+
+    def advance_watermark(self, wm_ms: int, arrivals_end: int):
+        self._check(lib().ek_advance_watermark(self.h, int(wm_ms), int(arrivals_end)))
+
+    def shard_triggers(self, columns, ctx: A.ek_global_ctx, validity=None):
+        """(global arrival, ts) of this handle's accepted trigger rows of the batch (ek_shard_triggers)."""
+        b, _keep = self._host_batch(columns, validity)
+        n = int(b.n_rows)
+        oa = np.zeros(max(n, 1), np.int64)
+        ot = np.zeros(max(n, 1), np.int64)
+        cnt = C.c_int64(0)
+        self._check(lib().ek_shard_triggers(self.h, C.byref(b), C.byref(ctx), oa.ctypes.data, ot.ctypes.data, n, C.byref(cnt)))
+        k = int(cnt.value)
+        return oa[:k].copy(), ot[:k].copy()
 
     def poll(self):
         r = A.ek_result()

@@ -263,6 +263,53 @@ int ek_destroy(void* h);
 int ek_export_state(void* h, void* buf, int64_t cap, int64_t* size);
 int ek_import_state(void* h, const void* buf, int64_t size);
 
+/* ---------------------------------------------------------------- external / global watermark (sharding)
+ * The reference splits the chain into WatermarkOp -> WindowOperator: WatermarkOp tracks the stream, drops
+ * late events and emits a WatermarkTuple at every advance (watermark_op.go:144-225); the WindowOperator closes
+ * windows on those tuples (event_window_trigger.go:126-180). A key-hash shard of a rule (one handle per GPU)
+ * keeps that split: the host that assigns the global arrival order runs the WatermarkOp tracking over the
+ * WHOLE stream and broadcasts its WatermarkTuples; every shard receives only its own rows, each with its
+ * global arrival index. A handle enters this mode at its first ek_push_batch_global / ek_advance_watermark
+ * (before any ek_push_batch) and stays in it until ek_reset; its own rows no longer move its watermark.
+ * Built for event-time TUMBLING / HOPPING / SLIDING (no delay) and processing-time COUNTWINDOW (global
+ * arrival blocks); other windows -> EK_ERR_UNSUPPORTED (session gaps and state windows depend on every row
+ * of the stream). Global un-grouped aggregates are merged across shards by the caller (ekgpu/dist.py). */
+typedef struct {
+    const int64_t* row_arrival;   /* per row of the batch: global arrival index, strictly increasing       */
+    int64_t arrivals_end;         /* global arrivals after this batch (>= last row_arrival + 1)           */
+    /* WatermarkTuples emitted while the batch's global arrivals were tracked, in order: the tuple k follows
+     * the event of global arrival wm_arrival[k] and carries watermark wm_ts[k] (strictly increasing)       */
+    const int64_t* wm_arrival;
+    const int64_t* wm_ts;
+    int64_t n_wm;
+    /* event time: the first window's alignment anchor (getEarliestEventTs at the first WatermarkTuple that
+     * released an event, event_window_trigger.go:57-75,211-219): valid when origin_known != 0; the tuple
+     * that released it is the last one with wm_arrival <= origin_arrival */
+    int32_t origin_known;
+    int32_t pad;
+    int64_t origin_ts;
+    int64_t origin_arrival;
+    /* SLIDINGWINDOW: the accepted trigger events of the WHOLE stream in this batch (every shard's, from
+     * ek_shard_triggers + an all-gather), in arrival order: (global arrival, ts) */
+    const int64_t* trig_arrival;
+    const int64_t* trig_ts;
+    int64_t n_trig;
+    int32_t memory;               /* EK_MEM_HOST or EK_MEM_DEVICE: where row_arrival lives (the other arrays
+                                   * are always host memory) */
+    int32_t pad2;
+} ek_global_ctx;
+
+/* One micro-batch of a shard: the rows owned by this handle plus the global context above. */
+int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g);
+/* A WatermarkTuple with no new rows (event_window_trigger.go:126-146): the global watermark reached wm_ms after
+ * `arrivals_end` global arrivals. Equivalent to ek_push_batch_global with an empty batch and one tuple. */
+int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end);
+/* The rows of `batch` (global arrivals g->row_arrival) that are accepted by the global watermark and match
+ * SLIDINGWINDOW ... OVER (WHEN ...) (every accepted row when there is no OVER): their global arrival and ts,
+ * in arrival order, up to cap (n_out = the total). g->trig_* are ignored. */
+int ek_shard_triggers(void* h, const ek_batch* batch, const ek_global_ctx* g, int64_t* out_arrival, int64_t* out_ts,
+                      int64_t cap, int64_t* n_out);
+
 /* ---------------------------------------------------------------- columnar JSON ingest
  * Replaces the per-message FastJsonConverter.Decode of a schema-typed stream
  * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) for flat JSON objects

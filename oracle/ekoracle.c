@@ -103,7 +103,10 @@ typedef struct {
     int64_t n;
     const void* const* cols;
     const uint8_t* const* valid;
+    const int64_t* arrival;    /* shard model: global arrival index of each row (NULL: row index = arrival) */
 } dataset;
+
+static int64_t row_arrival(const dataset* d, int64_t e) { return d->arrival ? d->arrival[e] : e; }
 
 static val_t col_val(const dataset* d, int c, int64_t row) {
     val_t v; v.tag = V_NULL; v.i = 0; v.f = 0;
@@ -390,7 +393,11 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
     v_push(&ob->roff, ob->key.n);
     v_push(&ob->moff, ob->mem.n);
     uint64_t h = 0;
-    for (int64_t k = 0; k < nc; ++k) { v_push(&ob->mem, content[k]); h += ek_mix64((uint64_t)content[k]); }
+    for (int64_t k = 0; k < nc; ++k) {
+        const int64_t a = row_arrival(d, content[k]);
+        v_push(&ob->mem, a);
+        h += ek_mix64((uint64_t)a);
+    }
     v_push(&ob->mcnt, nc);
     v_push(&ob->mhash, (int64_t)h);
     if (ob->werr_cap <= w) { ob->werr_cap = (w + 1) * 2; ob->werr = (char*)realloc(ob->werr, (size_t)ob->werr_cap * 128); }
@@ -569,7 +576,11 @@ static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_
     v_push(&ob->roff, ob->key.n);
     v_push(&ob->moff, ob->mem.n);
     uint64_t h = 0;
-    for (int64_t k = 0; k < nc; ++k) { v_push(&ob->mem, content[k]); h += ek_mix64((uint64_t)content[k]); }
+    for (int64_t k = 0; k < nc; ++k) {
+        const int64_t a = row_arrival(d, content[k]);
+        v_push(&ob->mem, a);
+        h += ek_mix64((uint64_t)a);
+    }
     v_push(&ob->mcnt, nc);
     v_push(&ob->mhash, (int64_t)h);
     if (ob->werr_cap <= w) { ob->werr_cap = (w + 1) * 2; ob->werr = (char*)realloc(ob->werr, (size_t)ob->werr_cap * 128); }
@@ -758,6 +769,10 @@ typedef struct {
     int last_ticked;
     int64_t* ts;
     vec64 content;
+    /* shard model (eko_run_shard): the window op of one key-hash shard fed the global WatermarkTuples */
+    int shard;
+    int origin_known;
+    int64_t origin_ts, origin_arrival, cur_wm_arrival;
 } winop;
 
 static int64_t ev_ts(const winop* o, int64_t e) { return o->ts[e]; }
@@ -794,6 +809,12 @@ static void handle_inputs(winop* o, int64_t right, int64_t* keep_from) {
         } else {
             if (nextleft < 0 && !ov) nextleft = i;
         }
+    }
+    if (nextleft < 0 && ov && o->shard) {
+        /* shard model: an empty LOCAL window is not an empty global one (the global discard quirk is decided per
+         * event at acceptance, hop_discard below); only the expired rows go */
+        nextleft = 0;
+        while (nextleft < o->inputs.n && ev_ts(o, o->inputs.a[nextleft]) < left) nextleft++;
     }
     *keep_from = nextleft < 0 ? o->inputs.n : nextleft;
 }
@@ -833,6 +854,11 @@ static int64_t next_window(const winop* o, int64_t current, int64_t wm) {
     case EK_WINDOW_TUMBLING: case EK_WINDOW_HOPPING: {
         int64_t interval = o->wtype == EK_WINDOW_TUMBLING ? o->L : o->I;
         if (current != ZERO_MS) return current + interval;
+        if (o->shard) {
+            /* the first end is anchored on the GLOBAL earliest released event, known from the tuple that released it */
+            if (!o->origin_known || o->cur_wm_arrival < o->origin_arrival) return MAXT_MS;
+            return eko_aligned_window_end(o->origin_ts, o->raw_interval, o->unit, o->tz);
+        }
         int64_t nt = earliest(o, ZERO_MS, wm);
         if (nt == MAXT_MS) return nt;
         return eko_aligned_window_end(nt, o->raw_interval, o->unit, o->tz);
@@ -877,8 +903,8 @@ static int match_trigger(const winop* o, int64_t e) {
 
 /* event_window_trigger.go:182-196 (EventRow branch) */
 static void win_on_event(winop* o, int64_t e) {
-    if (!o->has_trigger) { o->has_trigger = 1; o->trigger_time = ev_ts(o, e); }
-    if (o->wtype == EK_WINDOW_SLIDING && match_trigger(o, e)) v_push(&o->trigger_ts, ev_ts(o, e));
+    if (!o->has_trigger) { o->has_trigger = 1; o->trigger_time = o->shard ? o->origin_ts : ev_ts(o, e); }
+    if (o->wtype == EK_WINDOW_SLIDING && !o->shard && match_trigger(o, e)) v_push(&o->trigger_ts, ev_ts(o, e));
     v_push(&o->inputs, e);
 }
 
@@ -895,6 +921,14 @@ static void win_on_watermark(winop* o, int64_t wm) {
     if (we == MAXT_MS || o->wtype == EK_WINDOW_SESSION || o->wtype == EK_WINDOW_SLIDING) {
         if (o->wtype == EK_WINDOW_SESSION) we = next_session(o, wm, &ticked);
         else we = next_window(o, o->prev_end, wm);
+    }
+    if (o->shard && o->wtype == EK_WINDOW_SLIDING) {
+        /* shard model: every trigger fires at the tuple that released it (its window = the rows released so far) */
+        while (o->trigger_ts.n > 0 && o->trigger_ts.a[0] <= wm) {
+            scan(o, o->trigger_ts.a[0], o->L, 1);
+            v_erase_front(&o->trigger_ts, 1);
+        }
+        return;
     }
     while (we != ZERO_MS && we <= wm) {
         if (o->wtype == EK_WINDOW_SESSION && !o->last_ticked && o->inputs.n > 0) {
@@ -987,11 +1021,48 @@ static void set_status(eko_output* out, int st, const char* msg) {
 
 static int64_t* take(vec64* v) { int64_t* a = v->a; v->a = NULL; v->n = v->cap = 0; return a ? a : (int64_t*)calloc(1, 8); }
 
+/* the outbuf of a run -> the eko_output arrays */
+static void finish_output(const ek_plan* p, outbuf* ob, eko_output* out) {
+    out->r.n_windows = ob->ws.n;
+    out->r.n_rows = ob->key.n;
+    out->r.n_aggs = p->window_type == EK_WINDOW_NONE ? p->n_columns : p->n_aggs;
+    out->r.memory = EK_MEM_HOST;
+    v_push(&ob->moff, ob->mem.n);
+    out->r.win_start = take(&ob->ws);
+    out->r.win_end = take(&ob->we);
+    out->r.win_row_offset = take(&ob->roff);
+    out->r.win_row_count = take(&ob->rcnt);
+    out->r.win_member_count = take(&ob->mcnt);
+    out->r.win_member_hash = (uint64_t*)take(&ob->mhash);
+    {
+        int64_t* st = take(&ob->st);
+        out->r.win_status = (int32_t*)calloc((size_t)(out->r.n_windows ? out->r.n_windows : 1), 4);
+        for (int64_t w = 0; w < out->r.n_windows; ++w) out->r.win_status[w] = (int32_t)st[w];
+        free(st);
+    }
+    {
+        int64_t* k = take(&ob->key);
+        out->r.key = (uint32_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 4);
+        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.key[r] = (uint32_t)k[r];
+        free(k);
+    }
+    for (int a = 0; a < out->r.n_aggs; ++a) {
+        out->r.agg_value[a] = take(&ob->aval[a]);
+        int64_t* t = take(&ob->atag[a]);
+        out->r.agg_tag[a] = (uint8_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 1);
+        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.agg_tag[a][r] = (uint8_t)t[r];
+        free(t);
+    }
+    out->member_offset = take(&ob->moff);
+    out->members = take(&ob->mem);
+    out->win_error = ob->werr ? ob->werr : (char*)calloc(1, 128);
+}
+
 int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity, eko_output* out) {
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
     if (p->n_aggs < 0 || p->n_aggs > EK_MAX_AGGS) { set_status(out, EK_ERR_INVALID, "bad n_aggs"); return out->status; }
-    dataset d = { p, n, columns, validity };
+    dataset d = { p, n, columns, validity, NULL };
     outbuf ob; memset(&ob, 0, sizeof ob);
 
     /* rewriteIfIncAggStmt (planner.go:910-997): every aggregate must be incremental, and the window type one of
@@ -1160,40 +1231,141 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     }
 
     free(so.rows.a);
-    out->r.n_windows = ob.ws.n;
-    out->r.n_rows = ob.key.n;
-    out->r.n_aggs = p->window_type == EK_WINDOW_NONE ? p->n_columns : p->n_aggs;
-    out->r.memory = EK_MEM_HOST;
-    v_push(&ob.moff, ob.mem.n);
-    out->r.win_start = take(&ob.ws);
-    out->r.win_end = take(&ob.we);
-    out->r.win_row_offset = take(&ob.roff);
-    out->r.win_row_count = take(&ob.rcnt);
-    out->r.win_member_count = take(&ob.mcnt);
-    out->r.win_member_hash = (uint64_t*)take(&ob.mhash);
-    {
-        int64_t* st = take(&ob.st);
-        out->r.win_status = (int32_t*)calloc((size_t)(out->r.n_windows ? out->r.n_windows : 1), 4);
-        for (int64_t w = 0; w < out->r.n_windows; ++w) out->r.win_status[w] = (int32_t)st[w];
-        free(st);
-    }
-    {
-        int64_t* k = take(&ob.key);
-        out->r.key = (uint32_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 4);
-        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.key[r] = (uint32_t)k[r];
-        free(k);
-    }
-    for (int a = 0; a < out->r.n_aggs; ++a) {
-        out->r.agg_value[a] = take(&ob.aval[a]);
-        int64_t* t = take(&ob.atag[a]);
-        out->r.agg_tag[a] = (uint8_t*)calloc((size_t)(out->r.n_rows ? out->r.n_rows : 1), 1);
-        for (int64_t r = 0; r < out->r.n_rows; ++r) out->r.agg_tag[a][r] = (uint8_t)t[r];
-        free(t);
-    }
-    out->member_offset = take(&ob.moff);
-    out->members = take(&ob.mem);
-    out->win_error = ob.werr ? ob.werr : (char*)calloc(1, 128);
+    finish_output(p, &ob, out);
     return 0;
+}
+
+/* ------------------------------------------------------------------ shard model (multi-GPU protocol)
+ * One key-hash shard of a rule: the shard's own rows (global arrival indices g->row_arrival) plus the global
+ * WatermarkTuples (wm list), the global window anchor (origin) and the global sliding triggers — exactly what
+ * ek_push_batch_global hands one engine handle. The WatermarkOp tracking runs over the WHOLE stream on the host
+ * (ekgpu/shard.py GlobalWatermark, watermark_op.go:144-225); here, per shard:
+ *   track:    a row is accepted iff ts >= the last watermark emitted before its arrival (watermark_op.go:144-155)
+ *   release:  at each WatermarkTuple, the buffered rows / trigger ghosts with ts <= watermark, in (ts, arrival)
+ *             order (watermark_op.go:157-204), then the window op's WatermarkTuple branch
+ *   hopping:  the "empty window discards every input" quirk (window_op.go:605-655) for lateTolerance 0, decided
+ *             per event: event i reaches no window iff ts_i > W_{i-1} and e_max(ts_i) - L > W_{i-1}
+ *   count:    processing-time COUNTWINDOW blocks over the GLOBAL arrival order (window_op.go:390-418)
+ * The union of the shards' rows (and the sum of their membership fingerprints) is compared with eko_run on the
+ * whole stream by the tests. */
+int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
+                  const ek_global_ctx* g, eko_output* out) {
+    memset(out, 0, sizeof *out);
+    if (!p || p->abi_version != EKGPU_ABI_VERSION || !g) { set_status(out, EK_ERR_INVALID, "bad plan / context"); return out->status; }
+    if (p->incremental || p->window_version == 2 || p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_STATE ||
+        p->window_type == EK_WINDOW_NONE || (p->window_type == EK_WINDOW_SLIDING && p->delay != 0) ||
+        (p->window_type == EK_WINDOW_HOPPING && p->late_tolerance_ms != 0) ||
+        (p->window_type == EK_WINDOW_COUNT && p->is_event_time)) {
+        set_status(out, EK_ERR_UNSUPPORTED, "window not shardable"); return out->status;
+    }
+    dataset d = { p, n, columns, validity, g->row_arrival };
+    outbuf ob; memset(&ob, 0, sizeof ob);
+    if (!p->is_event_time) {
+        /* COUNTWINDOW(len, itv) over the global arrival order: window k = arrivals [k*itv - len, k*itv) */
+        const int64_t len = p->length, itv = p->interval > 0 ? p->interval : p->length;
+        int64_t lo = 0;
+        for (int64_t e = itv; e <= g->arrivals_end; e += itv) {
+            if (e < len) continue;
+            while (lo < n && g->row_arrival[lo] < e - len) lo++;
+            int64_t hi = lo;
+            while (hi < n && g->row_arrival[hi] < e) hi++;
+            vec64 c; memset(&c, 0, sizeof c);
+            for (int64_t k = lo; k < hi; ++k) v_push(&c, k);
+            emit_window(&d, &ob, 0, 0, c.a, c.n);
+            free(c.a);
+        }
+        finish_output(p, &ob, out);
+        return 0;
+    }
+    if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "event time requires a timestamp column"); return out->status; }
+    /* ts of own rows [0, n) and of the trigger ghosts [n, n + n_trig) */
+    const int64_t nt = p->window_type == EK_WINDOW_SLIDING ? g->n_trig : 0;
+    int64_t* ts = (int64_t*)malloc((size_t)(n + nt + 1) * 8);
+    for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.i; }
+    for (int64_t k = 0; k < nt; ++k) ts[n + k] = g->trig_ts[k];
+    winop o; memset(&o, 0, sizeof o);
+    o.d = &d; o.ob = &ob; o.wtype = p->window_type; o.ts = ts;
+    const int64_t u = unit_ms(p->time_unit);
+    o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = 0;
+    o.raw_interval = (p->window_type == EK_WINDOW_HOPPING) ? p->interval : p->length;
+    o.unit = p->time_unit; o.tz = p->tz_offset_s;
+    o.next_end = MAXT_MS; o.prev_end = ZERO_MS;
+    o.shard = 1;
+    o.origin_known = g->origin_known; o.origin_ts = g->origin_ts; o.origin_arrival = g->origin_arrival;
+    const int64_t H = p->window_type == EK_WINDOW_HOPPING ? o.I : o.L;
+    int64_t last_wm = ZERO_MS;
+    vec64 buf; memset(&buf, 0, sizeof buf);   /* own rows (< n) and trigger ghosts (>= n), release order */
+    int64_t ir = 0, iw = 0, itr = 0;
+    for (;;) {
+        int64_t a = INT64_MAX;
+        if (ir < n) a = g->row_arrival[ir];
+        if (itr < nt && g->trig_arrival[itr] < a) a = g->trig_arrival[itr];
+        if (iw < g->n_wm && g->wm_arrival[iw] < a) a = g->wm_arrival[iw];
+        if (a == INT64_MAX) break;
+        int64_t add[2]; int na = 0;
+        if (ir < n && g->row_arrival[ir] == a) {
+            const int64_t t = ts[ir];
+            int ok = t >= last_wm;
+            if (!ok) out->records_late++;
+            if (ok && p->window_type == EK_WINDOW_HOPPING && o.origin_known && t > last_wm) {
+                const int64_t e1 = eko_aligned_window_end(o.origin_ts, o.raw_interval, o.unit, o.tz);
+                if (t >= e1) {
+                    const int64_t emax = e1 + floordiv(t - e1, H) * H;
+                    if (emax - o.L > last_wm) ok = 0;   /* reaches no window: discarded with the empty window */
+                }
+            }
+            if (ok) add[na++] = ir;
+            ir++;
+        }
+        if (itr < nt && g->trig_arrival[itr] == a) add[na++] = n + itr++;
+        for (int k = 0; k < na; ++k) {
+            const int64_t e = add[k], t = ts[e];
+            int64_t lo = 0, hi = buf.n;
+            while (lo < hi) { int64_t mid = (lo + hi) / 2; if (ts[buf.a[mid]] > t) hi = mid; else lo = mid + 1; }
+            v_push(&buf, 0);
+            memmove(buf.a + lo + 1, buf.a + lo, (size_t)(buf.n - 1 - lo) * 8);
+            buf.a[lo] = e;
+        }
+        if (iw < g->n_wm && g->wm_arrival[iw] == a) {
+            const int64_t wm = g->wm_ts[iw++];
+            o.cur_wm_arrival = a;
+            int64_t c = 0;
+            while (c < buf.n && ts[buf.a[c]] <= wm) c++;
+            for (int64_t k = 0; k < c; ++k) {
+                const int64_t e = buf.a[k];
+                if (e < n) win_on_event(&o, e);
+                else v_push(&o.trigger_ts, ts[e]);
+            }
+            v_erase_front(&buf, c);
+            win_on_watermark(&o, wm);
+            last_wm = wm;
+        }
+    }
+    free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a); free(ts);
+    finish_output(p, &ob, out);
+    return 0;
+}
+
+/* The shard's accepted trigger rows (ek_shard_triggers): OVER (WHEN ...) true (every row without OVER) and
+ * ts >= the last global watermark before the row's arrival. out_* sized n. Returns the count. */
+int64_t eko_shard_triggers(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
+                           const ek_global_ctx* g, int64_t* out_arrival, int64_t* out_ts) {
+    dataset d = { p, n, columns, validity, g->row_arrival };
+    int64_t k = 0, iw = 0, last_wm = ZERO_MS;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t a = g->row_arrival[i];
+        while (iw < g->n_wm && g->wm_arrival[iw] < a) last_wm = g->wm_ts[iw++];
+        const int64_t t = col_val(&d, p->ts_column, i).i;
+        if (t < last_wm) continue;
+        if (p->n_trigger > 0) {
+            val_t r = eval_prog(p->trigger_prog, p->n_trigger, &d, i, NULL);
+            if (!(r.tag == V_BOOL && r.i)) continue;
+        }
+        out_arrival[k] = a;
+        out_ts[k] = t;
+        k++;
+    }
+    return k;
 }
 
 void eko_free(eko_output* o) {

@@ -38,6 +38,14 @@ int eko_run(const ek_plan* plan, int64_t n_rows, const void* const* columns,
             const uint8_t* const* validity, eko_output* out);
 void eko_free(eko_output* out);
 
+/* Shard model of the multi-GPU protocol: one key-hash shard's rows (global arrivals g->row_arrival) with the
+ * global WatermarkTuples / window anchor / sliding triggers of the whole stream (g: host memory). */
+int eko_run_shard(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,
+                  const ek_global_ctx* g, eko_output* out);
+/* The shard's accepted trigger rows (arrival, ts) in arrival order; returns their number (out_* sized n_rows). */
+int64_t eko_shard_triggers(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,
+                           const ek_global_ctx* g, int64_t* out_arrival, int64_t* out_ts);
+
 /* window_op.go:194-227 getAlignedWindowEndTime, with time.Local = UTC + tz_offset_s. */
 int64_t eko_aligned_window_end(int64_t ts_ms, int32_t interval, int32_t unit, int32_t tz_offset_s);
 

@@ -53,6 +53,12 @@ def lib():
         _lib.eko_agg_exec.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_double,
                                       C.POINTER(C.c_int64), C.POINTER(C.c_uint8), C.c_char_p, C.c_int32]
         _lib.eko_agg_exec.restype = C.c_int
+        _lib.eko_run_shard.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                       C.POINTER(A.ek_global_ctx), C.POINTER(eko_output)]
+        _lib.eko_run_shard.restype = C.c_int
+        _lib.eko_shard_triggers.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                            C.POINTER(A.ek_global_ctx), C.c_void_p, C.c_void_p]
+        _lib.eko_shard_triggers.restype = C.c_int64
     return _lib
 
 
@@ -72,24 +78,22 @@ def _col_arrays(plan: A.ek_plan, columns: List[np.ndarray]):
     return keep
 
 
-def run(plan: A.ek_plan, columns: List[np.ndarray], validity: Optional[List[Optional[np.ndarray]]] = None) -> OracleRun:
-    L = lib()
+def _ptrs(plan, columns, validity):
     cols = _col_arrays(plan, columns)
     n = len(cols[0]) if cols else 0
     cptr = (C.c_void_p * A.EK_MAX_COLUMNS)()
     vptr = (C.c_void_p * A.EK_MAX_COLUMNS)()
-    vkeep = []
+    keep = list(cols)
     for k, a in enumerate(cols):
         cptr[k] = a.ctypes.data
         if validity is not None and validity[k] is not None:
             v = np.ascontiguousarray(validity[k], dtype=np.uint8)
-            vkeep.append(v)
+            keep.append(v)
             vptr[k] = v.ctypes.data
-    out = eko_output()
-    rc = L.eko_run(C.byref(plan), n, cptr, vptr, C.byref(out))
-    if rc != 0:
-        msg = out.error.decode()
-        raise RuntimeError(f"oracle error {rc}: {msg}")
+    return n, cptr, vptr, keep
+
+
+def _collect(L, out) -> OracleRun:
     try:
         wins = result_to_python(out.r)
         nw = int(out.r.n_windows)
@@ -101,6 +105,40 @@ def run(plan: A.ek_plan, columns: List[np.ndarray], validity: Optional[List[Opti
         return OracleRun(wins, members, int(out.records_late), errors)
     finally:
         L.eko_free(C.byref(out))
+
+
+def run(plan: A.ek_plan, columns: List[np.ndarray], validity: Optional[List[Optional[np.ndarray]]] = None) -> OracleRun:
+    L = lib()
+    n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
+    out = eko_output()
+    rc = L.eko_run(C.byref(plan), n, cptr, vptr, C.byref(out))
+    if rc != 0:
+        msg = out.error.decode()
+        raise RuntimeError(f"oracle error {rc}: {msg}")
+    return _collect(L, out)
+
+
+def run_shard(plan: A.ek_plan, columns: List[np.ndarray], ctx: A.ek_global_ctx,
+              validity: Optional[List[Optional[np.ndarray]]] = None) -> OracleRun:
+    """Shard model of the multi-GPU protocol (eko_run_shard): one shard's rows + the whole stream's context."""
+    L = lib()
+    n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
+    out = eko_output()
+    rc = L.eko_run_shard(C.byref(plan), n, cptr, vptr, C.byref(ctx), C.byref(out))
+    if rc != 0:
+        msg = out.error.decode()
+        raise RuntimeError(f"oracle error {rc}: {msg}")
+    return _collect(L, out)
+
+
+def shard_triggers(plan: A.ek_plan, columns: List[np.ndarray], ctx: A.ek_global_ctx,
+                   validity: Optional[List[Optional[np.ndarray]]] = None):
+    L = lib()
+    n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
+    oa = np.zeros(max(n, 1), np.int64)
+    ot = np.zeros(max(n, 1), np.int64)
+    k = int(L.eko_shard_triggers(C.byref(plan), n, cptr, vptr, C.byref(ctx), oa.ctypes.data, ot.ctypes.data))
+    return oa[:k], ot[:k]
 
 
 def aligned_window_end(ts_ms: int, interval: int, unit: int, tz_offset_s: int = 0) -> int:

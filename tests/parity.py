@@ -49,3 +49,48 @@ def assert_windows_equal(plan, got, exp, check_members=False, max_report=5):
                 elif not (x == y or (isinstance(x, float) and math.isnan(x) and math.isnan(y))):
                     bad.append((key, a, x, y, "exact"))
         assert not bad, f"window {w} (end {e.end}): {len(bad)} mismatches, e.g. {bad[:max_report]}"
+
+
+def assert_windows_equal_np(plan, got, exp, check_members=False):
+    """assert_windows_equal for full-size runs (millions of rows): the same rule, vectorised per window.
+    Rows are matched by key after sorting both sides; tags (Go dynamic types) must match exactly, values
+    bit-exactly (NaN == NaN) except the FP_TOL_FNS over float results (relative <= REL_TOL)."""
+    import numpy as np
+    assert len(got) == len(exp), f"window count {len(got)} != {len(exp)}"
+    tol_aggs = set()
+    for a in range(plan.n_aggs):
+        fn, c = plan.aggs[a].fn, plan.aggs[a].column
+        is_float_col = c >= 0 and plan.column_type[c] == A.EK_COL_F64
+        if fn in FP_TOL_FNS and (is_float_col or fn != A.EK_AGG_SUM):
+            tol_aggs.add(a)
+    for w, (g, e) in enumerate(zip(got, exp)):
+        assert (g.start, g.end, g.status) == (e.start, e.end, e.status), \
+            f"window {w}: got {(g.start, g.end, g.status)} expected {(e.start, e.end, e.status)}"
+        if check_members:
+            assert (g.member_count, g.member_hash) == (e.member_count, e.member_hash), \
+                f"window {w} membership: got {(g.member_count, g.member_hash)} expected {(e.member_count, e.member_hash)}"
+        go, eo = np.argsort(g.keys, kind="stable"), np.argsort(e.keys, kind="stable")
+        gk, ek = g.keys[go], e.keys[eo]
+        assert len(gk) == len(ek) and np.array_equal(gk, ek), \
+            f"window {w} (end {e.end}): key sets differ ({len(gk)} vs {len(ek)} rows; " \
+            f"missing {np.setdiff1d(ek, gk)[:5]}, extra {np.setdiff1d(gk, ek)[:5]})"
+        assert len(np.unique(gk)) == len(gk), f"window {w}: duplicate keys"
+        for a in range(plan.n_aggs):
+            gt, et = g.tags[a][go], e.tags[a][eo]
+            bad = np.nonzero(gt != et)[0]
+            assert len(bad) == 0, f"window {w} agg {a}: {len(bad)} type mismatches, e.g. key {gk[bad[0]]}: {gt[bad[0]]} vs {et[bad[0]]}"
+            gv, ev = g.values[a][go], e.values[a][eo]
+            isf = et == A.EK_TAG_F64
+            gf, ef = gv.view(np.float64), ev.view(np.float64)
+            nan_both = isf & np.isnan(gf) & np.isnan(ef)
+            if a in tol_aggs:
+                with np.errstate(invalid="ignore", over="ignore"):
+                    scale = np.maximum(np.maximum(np.abs(gf), np.abs(ef)), 1e-300)
+                    ok_f = (np.abs(gf - ef) <= REL_TOL * scale) | (gf == ef) | nan_both
+                ok = np.where(isf, ok_f, gv == ev)
+            else:
+                ok = (gv == ev) | nan_both
+            ok |= et == A.EK_TAG_NULL
+            bad = np.nonzero(~ok)[0]
+            assert len(bad) == 0, f"window {w} (end {e.end}) agg {a}: {len(bad)} value mismatches, e.g. key {gk[bad[0]]}: " \
+                                  f"{gv[bad[0]]} vs {ev[bad[0]]}"

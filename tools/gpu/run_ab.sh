@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two engine builds in one box (EKGPU_LIB = the alternative .so): C2 bench, alternating, per-phase times.
-cd "$(dirname "$0")"
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 for i in 1 2 3; do
   for v in prev new; do

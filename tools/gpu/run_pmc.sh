@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter passes (separate runs; no tracing domains combined with --pmc)
-cd "$(dirname "$0")"; mkdir -p gpurun_out/pmc
+cd "$(dirname "$0")/../.."; mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 i=0

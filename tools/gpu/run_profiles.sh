@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary + PMC traffic passes of the C2 bench (each pass its own run)
-cd "$(dirname "$0")"; mkdir -p gpurun_out/prof gpurun_out/pmc
+cd "$(dirname "$0")/../.."; mkdir -p gpurun_out/prof gpurun_out/pmc
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/prof.log 2>&1 || exit $?
 echo "kernel-trace ok"
