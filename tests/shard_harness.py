@@ -29,7 +29,7 @@ CASES = {
 
 
 def global_stream(kind, n=40_000, keys=300, seed=7):
-    """key, ts, temperature, humidity, trig. 'ooo': ~20 events/ms with jitter (ties, out of order, late
+    """key, ts, temperature, humidity, trig. 'ooo': 2 events/ms with jitter (ties, out of order, late
     events); 'gaps': bursts separated by gaps wider than the hopping window; 'sorted': in order."""
     rng = np.random.default_rng(seed)
     i = np.arange(n, dtype=np.int64)
@@ -37,7 +37,7 @@ def global_stream(kind, n=40_000, keys=300, seed=7):
         burst = i // 5000
         ts = T0 + burst * 9000 + (i % 5000) // 5
     else:
-        ts = T0 + i // 20
+        ts = T0 + i // 2
     if kind == "ooo":
         # 5 % of events up to 600 ms behind (late when lateTolerance is smaller), 0.2 % up to 5 ms ahead
         u = rng.random(n)
