@@ -1,13 +1,23 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X window/aggregate hot path (BASELINE.json metric, configs[1] = C2):
+"""Benchmark of the MI355X window/aggregate hot path (BASELINE.json metric; default config = configs[1] = C2):
 
-  SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo
-  GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)       -- 1e8 synthetic events, 64 Ki keys, 1 MI355X
+  C2  SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo
+      GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)           -- 1e8 synthetic events, 64 Ki keys per GPU
 
-A step = one pass of the hot path over one batch: ek_reset + ek_push_batch of the 1e8-event batch
-(inputs already resident in HBM) through the C ABI, which triggers 99 tumbling windows and writes their
-GROUP BY result rows to HBM. Multi-GPU (torch.distributed.run): each rank owns a disjoint key-hash shard
-of its own 1e8-event stream (weak scaling, no data-path collective); rank 0 prints one JSON line.
+A step = one pass of the hot path over one batch (ek_reset + the batch's ek_push_batch through the C ABI, inputs
+already resident in HBM); it triggers the batch's windows and writes their GROUP BY rows to HBM.
+`--config C3|C4a|C4b|C5` runs the other BASELINE configs at their per-GPU sizes.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): ONE global stream of N x the per-GPU events
+over N x the keys, key-hash sharded (mix64(key) % N, dense local ids per rank). Every rank runs its handle in
+shard mode (ek_push_batch_global): the global WatermarkTuples of the (sorted) stream and the rows' global arrival
+indices come from the router; sliding triggers (C4a) are exchanged with one all_gather over RCCL per step; C5's
+un-grouped count(*) is merged with one all_gather. value = all ranks' events / the slowest rank's time (weak
+scaling: per-GPU work fixed).
+
+roofline: whole-step algorithmic bytes (one read of every referenced input column + one write of
+the result rows) / ms_per_step against the 8 TB/s HBM peak; `kernels` splits the step per engine phase with the
+HIP-event time of its launches on the engine stream and the algorithmic bytes that kernel itself must move.
 """
 import argparse
 import json
@@ -18,17 +28,42 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ekuiper-vioneta_amd"))
 
-C2_SQL = ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo "
-          "GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)")
-N_EVENTS = 100_000_000
-N_KEYS = 65536
-EVENTS_PER_MS = 100
-BYTES_IN_PER_EVENT = 4 + 8 + 8 + 8      # key u32, ts i64, temperature f64, humidity f64
-BYTES_OUT_PER_ROW = 4 + 8 + 8 + 8       # key, avg, max, count
 HBM_PEAK_GBS = 8000.0                   # MI355X_MICROARCH.md: 8.0 TB/s spec
 PHASES = ("stats", "partition", "aggregate", "finalize")
-KERNEL_OF_PHASE = {"stats": "k_stats", "partition": "k_part", "aggregate": "k_agg", "finalize": "k_finalize"}
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+KERNEL_OF_PHASE = {"stats": "k_stats (+k_pane_bounds)", "partition": "k_part", "aggregate": "k_agg / k_small_win",
+                   "finalize": "k_finalize"}
+T0 = 1541152480000
+
+CONFIGS = {
+    "C2": dict(sql="SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo "
+                   "GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)",
+               n=100_000_000, keys=65536, epm=100, seed=44, t0=T0, in_cols=("key", "ts", "temperature", "humidity"),
+               out_bytes=4 + 8 + 8 + 8),
+    "C3": dict(sql="SELECT deviceId, sum(temperature), min(temperature), max(temperature) FROM demo "
+                   "GROUP BY deviceId, HOPPINGWINDOW(ss, 60, 5)",
+               n=25_000_000, keys=131072, epm=42, seed=91, t0=T0, in_cols=("key", "ts", "temperature"),
+               out_bytes=4 + 3 * 8),
+    "C4a": dict(sql="SELECT deviceId, stddev(temperature), var(temperature) FROM demo "
+                    "GROUP BY deviceId, SLIDINGWINDOW(ss, 30) OVER (WHEN trig = 1) HAVING count(*) > 1",
+                n=10_000_000, keys=1_000_000, epm=10, seed=92, t0=T0, in_cols=("key", "ts", "temperature", "trig"),
+                out_bytes=4 + 8 + 8, trig=True),
+    "C4b": dict(sql="SELECT deviceId, stddev(temperature), var(temperature) FROM demo "
+                    "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1",
+                n=100_000_000, keys=1_000_000, epm=100, seed=93, t0=T0, in_cols=("key", "temperature"),
+                out_bytes=4 + 8 + 8, processing_time=True),
+    "C5": dict(sql="SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
+                   "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)",
+               n=125_000_000, keys=12_500_000, epm=2084, seed=94, t0=1541152440000, in_cols=("key", "ts", "temperature"),
+               out_bytes=4 + 8 + 8, sentinel=True, global_count="SELECT count(*) FROM demo GROUP BY TUMBLINGWINDOW(ss, 60)"),
+}
+COL_BYTES = {"key": 4, "ts": 8, "temperature": 8, "humidity": 8, "trig": 8}
+# bytes each phase must move at least (per event / per result row)
+PHASE_IN = {"stats": ("ts",), "partition": ("key", "temperature", "humidity", "trig")}
+
+N_EVENTS = CONFIGS["C2"]["n"]
+N_KEYS = CONFIGS["C2"]["keys"]
+EVENTS_PER_MS = CONFIGS["C2"]["epm"]
+C2_SQL = CONFIGS["C2"]["sql"]
 
 
 def _tmix(x):
@@ -42,33 +77,90 @@ def _tmix(x):
     return x
 
 
-def make_device_stream(n, keys, dev, seed=44, key_offset=0, events_per_ms=EVENTS_PER_MS, t0=1541152480000):
-    """ekgpu.synth.iot_stream generated directly in HBM (bit-identical counter-based splitmix64)."""
+def make_device_stream(n, keys, dev, seed=44, key_offset=0, events_per_ms=EVENTS_PER_MS, t0=T0, lo=0, hi=None):
+    """ekgpu.synth.iot_stream generated directly in HBM (bit-identical counter-based splitmix64); rows [lo, hi)."""
     import torch
-    key = torch.empty(n, dtype=torch.int32, device=dev)
-    ts = torch.empty(n, dtype=torch.int64, device=dev)
-    temp = torch.empty(n, dtype=torch.float64, device=dev)
-    hum = torch.empty(n, dtype=torch.float64, device=dev)
+    hi = n if hi is None else hi
+    m = hi - lo
+    key = torch.empty(m, dtype=torch.int32, device=dev)
+    ts = torch.empty(m, dtype=torch.int64, device=dev)
+    temp = torch.empty(m, dtype=torch.float64, device=dev)
+    hum = torch.empty(m, dtype=torch.float64, device=dev)
     base = seed << 40
     step = 1 << 24
-    for lo in range(0, n, step):
-        hi = min(n, lo + step)
-        i = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+    for a in range(lo, hi, step):
+        b = min(hi, a + step)
+        i = torch.arange(a, b, dtype=torch.int64, device=dev)
         r0 = _tmix(base ^ (i * 8 + 0))
         hi1 = (r0 >> 1) & ((1 << 63) - 1)
-        key[lo:hi] = (((hi1 % keys) * 2 + (r0 & 1)) % keys + key_offset).to(torch.int32)
-        ts[lo:hi] = t0 + i // events_per_ms
+        key[a - lo:b - lo] = (((hi1 % keys) * 2 + (r0 & 1)) % keys + key_offset).to(torch.int32)
+        ts[a - lo:b - lo] = t0 + i // events_per_ms
         scale = 100.0 / 9007199254740992.0
-        temp[lo:hi] = ((_tmix(base ^ (i * 8 + 1)) >> 11) & ((1 << 53) - 1)).to(torch.float64) * scale
-        hum[lo:hi] = ((_tmix(base ^ (i * 8 + 2)) >> 11) & ((1 << 53) - 1)).to(torch.float64) * scale
+        temp[a - lo:b - lo] = ((_tmix(base ^ (i * 8 + 1)) >> 11) & ((1 << 53) - 1)).to(torch.float64) * scale
+        hum[a - lo:b - lo] = ((_tmix(base ^ (i * 8 + 2)) >> 11) & ((1 << 53) - 1)).to(torch.float64) * scale
     return [key, ts, temp, hum]
 
 
+def trig_column(i):
+    """C4a trigger flag of global event i: 1 in 1e4 events (tests/test_fullsize_parity_gpu.py)."""
+    import torch
+    return ((((i * 0x9E3779B1) >> 7) % 10_000) == 0).to(torch.int64)
+
+
+def config_columns(cfg, cols, i=None):
+    """The engine's columns for a config from the synthetic [key, ts, temperature, humidity] stream."""
+    import torch
+    key, ts, temp, hum = cols
+    if cfg.get("trig"):
+        return [key, ts, temp, hum, trig_column(i if i is not None else torch.arange(len(ts), device=ts.device))]
+    return [key, ts, temp, hum]
+
+
+def schema_of(cfg):
+    from ekgpu.synth import IOT_SCHEMA
+    return dict(IOT_SCHEMA, trig="bigint") if cfg.get("trig") else IOT_SCHEMA
+
+
+def shard_stream(cfg, world, rank, dev):
+    """Rank `rank`'s rows of the global stream (world x events, world x keys, world x rate): local columns with
+    dense key ids, their global arrival indices, and the number of global events."""
+    import torch
+    n_glob, k_glob, epm = cfg["n"] * world, cfg["keys"] * world, cfg["epm"] * world
+    parts, arrs = [], []
+    step = 1 << 25
+    for lo in range(0, n_glob, step):
+        hi = min(n_glob, lo + step)
+        c = make_device_stream(n_glob, k_glob, dev, seed=cfg["seed"], events_per_ms=epm, t0=cfg["t0"], lo=lo, hi=hi)
+        i = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+        c = config_columns(cfg, c, i)
+        own = (_tmix(c[0].to(torch.int64)) & ((1 << 62) - 1)) % world == rank
+        parts.append([x[own] for x in c])
+        arrs.append(i[own])
+        del c, i, own
+    cols = [torch.cat([p[k] for p in parts]) for k in range(len(parts[0]))]
+    arr = torch.cat(arrs)
+    del parts, arrs
+    uniq, inv = torch.unique(cols[0], return_inverse=True)
+    cols[0] = inv.to(torch.int32)
+    return cols, arr, n_glob, int(uniq.numel())
+
+
+def global_tuples(cfg, world, n_glob):
+    """WatermarkTuples of the sorted synthetic global stream (lateTolerance 0): the stream max advances at every
+    first event of a millisecond (ts = t0 + i // (epm * world))."""
+    import numpy as np
+    epm = cfg["epm"] * world
+    wa = np.arange(0, n_glob, epm, dtype=np.int64)
+    wt = cfg["t0"] + np.arange(len(wa), dtype=np.int64)
+    return {"wm_arrival": wa, "wm_ts": wt, "arrivals_end": n_glob, "all_accepted": True, "max_wm_step": 1,
+            "origin_known": True, "origin_ts": cfg["t0"], "origin_arrival": 0}
+
+
 def cpu_baseline(sample_events):
-    """The CPU oracle (C restatement of the reference per-tuple path, oracle/ekoracle.c) on the
-    first `sample_events` events of the same stream: single thread (the reference runs a rule's window ->
-    aggregate chain in one goroutine, operations.go:63-74), and as P key-hash shards on P host threads
-    (reference semantics on all of this job's host cores)."""
+    """The CPU oracle (C restatement of the reference per-tuple path, oracle/ekoracle.c) on the first
+    `sample_events` events of the C2 stream: single thread (the reference runs a rule's window -> aggregate chain
+    in one goroutine, operations.go:63-74), and as P key-hash shards on P host threads (reference semantics on all
+    of this job's host cores)."""
     import threading
     import numpy as np
     from oracle import ekoracle
@@ -83,7 +175,6 @@ def cpu_baseline(sample_events):
     out = {"value": sample_events / dt, "unit": "events/s", "cores": 1, "kind": "port",
            "sample": f"first {sample_events} events of the C2 stream ({len(run.windows)} windows closed), "
                      f"oracle/ekoracle.c single-threaded, {dt:.1f} s"}
-    # P key-hash shards (each a dense key space, like the GPU ranks), one thread each (ctypes drops the GIL)
     P = max(1, int(os.environ.get("EKGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", "8"))))
     shard = (key % P).astype(np.int64)
     parts = []
@@ -113,16 +204,44 @@ def cpu_baseline(sample_events):
     return out
 
 
+def ingest_inclusive(eng, cols, n, steps=2):
+    """C2 from host memory: pinned host columns copied by ek_push_batch (EK_MEM_HOST) + ek_poll_results to host.
+    Reported beside `value` (never as it): the PCIe-inclusive rate of a host-fed deployment."""
+    import torch
+    host = [c.cpu().pin_memory() for c in cols]
+    arrs = [h.numpy() for h in host]
+    eng.reset()
+    eng.push_host(arrs)
+    eng.poll()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    rows = 0
+    for _ in range(steps):
+        eng.reset()
+        eng.push_host(arrs)
+        rows += sum(len(w.keys) for w in eng.poll())
+    dt = (time.perf_counter() - t) / steps
+    in_bytes = sum(a.nbytes for a in arrs)
+    return {"events_per_s": n / dt, "ms_per_step": dt * 1e3, "h2d_bytes": in_bytes, "rows_to_host": rows // steps,
+            "what": "pinned host columns -> H2D inside ek_push_batch, then ek_poll_results into host memory"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events", type=int, default=N_EVENTS)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--events", type=int, default=0, help="override the per-GPU event count")
     ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", N_EVENTS)))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="one process plays rank 0 of an N-GPU run in shard mode (no collective; a single-GPU check of "
+                         "the shard path: C4a then sees only its own triggers)")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -134,23 +253,82 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.sim_world > 1 and world == 1:
+        world = args.sim_world
 
     from ekgpu.engine import Engine
     from ekgpu.rule import compile_rule
-    from ekgpu.synth import IOT_SCHEMA
+    from ekgpu.shard import make_ctx
 
-    n = args.events
-    # key-hash sharding: rank r owns a disjoint shard of the key space; the ingest side dictionary-encodes
-    # the shard's keys densely (0..K-1), so every rank runs the same plan on its own stream
-    rule = compile_rule(C2_SQL, IOT_SCHEMA, num_keys=N_KEYS)
-    cols = make_device_stream(n, N_KEYS, dev, seed=44 + rank)
+    cfg = dict(CONFIGS[args.config])
+    if args.events:
+        cfg["n"] = args.events
+    iet = not cfg.get("processing_time")
+    if world == 1:
+        c = make_device_stream(cfg["n"], cfg["keys"], dev, seed=cfg["seed"], events_per_ms=cfg["epm"], t0=cfg["t0"])
+        cols = config_columns(cfg, c)
+        del c
+        arr, n_glob, k_local = None, cfg["n"], cfg["keys"]
+    else:
+        cols, arr, n_glob, k_local = shard_stream(cfg, world, rank, dev)
+    n = int(cols[0].numel())
+    rule = compile_rule(cfg["sql"], schema_of(cfg), num_keys=max(1, k_local), is_event_time=iet)
     torch.cuda.synchronize()
     eng = Engine(rule.plan, device=local)
-    ptrs = [c.data_ptr() for c in cols]
+    ptrs = [x.data_ptr() for x in cols]
+    sent_ptrs, cnt_eng = None, None
+    if cfg.get("sentinel"):
+        # one event at the window end closes C5's single window (its key is outside the compared groups)
+        end = cfg["t0"] + 60_000
+        sent = [torch.tensor([0], dtype=torch.int32, device=dev), torch.tensor([end], dtype=torch.int64, device=dev),
+                torch.tensor([50.0], dtype=torch.float64, device=dev), torch.tensor([50.0], dtype=torch.float64, device=dev)]
+        sent_ptrs = [x.data_ptr() for x in sent]
+    if cfg.get("global_count"):
+        crule = compile_rule(cfg["global_count"], schema_of(cfg), num_keys=1, is_event_time=iet)
+        cnt_eng = Engine(crule.plan, device=local)
+    ctx = None
+    if world > 1:
+        tup = global_tuples(cfg, world, n_glob) if iet else {
+            "wm_arrival": np.zeros(0, np.int64), "wm_ts": np.zeros(0, np.int64), "arrivals_end": n_glob,
+            "origin_known": False, "origin_ts": 0, "origin_arrival": 0}
+        ctx_rows = make_ctx(tup, np.zeros(0, np.int64))
+        ctx_rows.row_arrival = arr.data_ptr()
+        ctx_rows.memory = 1   # EK_MEM_DEVICE: the rows' arrivals live in HBM
+        ctx = ctx_rows
+        if cfg.get("sentinel"):
+            sent_tup = {"wm_arrival": np.array([n_glob], np.int64), "wm_ts": np.array([cfg["t0"] + 60_000], np.int64),
+                        "arrivals_end": n_glob + 1, "all_accepted": True, "max_wm_step": 0, "origin_known": True,
+                        "origin_ts": cfg["t0"], "origin_arrival": 0}
+            sent_ctx = make_ctx(sent_tup, np.zeros(0, np.int64))
 
     def step():
         eng.reset()
-        eng.push_device(n, ptrs)
+        if world == 1:
+            eng.push_device(n, ptrs)
+            if sent_ptrs:
+                eng.push_device(1, sent_ptrs)
+        else:
+            g = ctx
+            if cfg.get("trig"):
+                from ekgpu.dist import exchange_triggers
+                ta, tt = eng.shard_triggers_device(n, ptrs, g)
+                ga, gt = exchange_triggers(ta, tt) if dist else (ta, tt)
+                g = make_ctx(tup, np.zeros(0, np.int64), ga, gt)
+                g.row_arrival = arr.data_ptr()
+                g.memory = 1
+            eng.push_global_device(n, ptrs, g)
+            if sent_ptrs:
+                eng.push_global(None, sent_ctx)
+        if cnt_eng is not None:
+            cnt_eng.reset()
+            if world == 1:
+                cnt_eng.push_device(n, ptrs)
+                if sent_ptrs:
+                    cnt_eng.push_device(1, sent_ptrs)
+            else:
+                cnt_eng.push_global_device(n, ptrs, ctx)
+                if sent_ptrs:
+                    cnt_eng.push_global(None, sent_ctx)
 
     for _ in range(args.warmup):
         step()
@@ -159,6 +337,15 @@ def main():
     n_windows = int(r.n_windows)
     rows = sum(int(r.win_row_count[w]) for w in range(n_windows))
     eng.release(r)
+    global_count = None
+    if cnt_eng is not None:
+        from ekgpu.dist import global_windows, make_partial_plan
+        cw = cnt_eng.poll()
+        if dist:
+            gw = global_windows(make_partial_plan(crule), cw)
+            global_count = [w.values for w in gw]
+        else:
+            global_count = [int(w.values[0][0]) for w in cw if len(w.keys)]
 
     if dist:
         dist.barrier()
@@ -185,23 +372,34 @@ def main():
         ph_ms = [float(x) for x in t[2:]]
 
     ms_per_step = dt * 1000.0 / args.steps
-    value = n * world * args.steps / dt
-    dev_ms_step = dev_ms / args.steps
-    alg_bytes = n * BYTES_IN_PER_EVENT + rows * BYTES_OUT_PER_ROW
-    path_gbs = alg_bytes / (dev_ms_step * 1e-3) / 1e9
-    # dominant kernel: k_part (one launch per push here); its algorithmic bytes are the input columns
-    # it must read once (28 B/event); staging writes are implementation traffic
-    part_launch_ms = ph_ms[1] / max(1, ph_n[1])
-    part_launches_per_step = ph_n[1] / args.steps
-    part_alg = n * BYTES_IN_PER_EVENT / max(1.0, part_launches_per_step)
-    achieved = part_alg / (part_launch_ms * 1e-3) / 1e9 if part_launch_ms > 0 else 0.0
+    value = n_glob * args.steps / dt
+    in_bytes_per_event = sum(COL_BYTES[c] for c in cfg["in_cols"])
+    alg_bytes = n * in_bytes_per_event + rows * cfg["out_bytes"]
+    achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
+    kernels = {}
+    for k, ph in enumerate(PHASES):
+        if ph_n[k] == 0:
+            continue
+        launch_ms = ph_ms[k] / ph_n[k]
+        per_step = ph_n[k] / args.steps
+        if ph == "stats":
+            kb = n * 8 if iet else 0
+        elif ph == "partition":
+            kb = n * sum(COL_BYTES[c] for c in cfg["in_cols"] if c != "ts")
+        else:
+            kb = rows * cfg["out_bytes"]
+        kb_launch = kb / per_step
+        kernels[KERNEL_OF_PHASE[ph]] = {"launch_ms": launch_ms, "launches_per_step": per_step,
+                                        "algorithmic_bytes_per_launch": kb_launch,
+                                        "achieved_gbs": kb_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None}
+    dominant = max(kernels.items(), key=lambda kv: kv[1]["launch_ms"] * kv[1]["launches_per_step"])[0] if kernels else None
     traffic, traffic_src = None, None
-    if os.path.exists(PMC_SUMMARY):
-        pm = json.load(open(PMC_SUMMARY))
-        k = pm.get("kernels", {}).get("k_part")
-        if k and k.get("events_per_launch") == n:
-            traffic = k["hbm_bytes_per_launch"]
-            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
+    pmc = os.path.join(ROOT, "profiles", f"r02_pmc_{args.config}.json")
+    if os.path.exists(pmc):
+        pm = json.load(open(pmc))
+        if pm.get("events_per_gpu") == n and world == 1:
+            traffic = pm.get("hbm_bytes_per_step")
+            traffic_src = os.path.relpath(pmc, ROOT)
     out = {
         "metric": "events/sec (whole node) for windowed GROUP BY at 1/2/4/8 GPUs; % HBM peak",
         "value": value,
@@ -214,25 +412,32 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (counter-based splitmix64 stream generated in HBM, SURVEY.md §8(d) C2 shape)",
-        "config": {"workload": "C2: " + C2_SQL, "events_per_gpu": n, "keys_per_gpu": N_KEYS,
-                   "event_rate": "100k ev/s event time (100 events per ms)", "windows_emitted": n_windows,
-                   "rows_per_step": rows, "parallelism": f"key-hash shards x{world}"},
+        "data": "synthetic (counter-based splitmix64 stream generated in HBM, SURVEY.md §8(d) shape)",
+        "config": {"workload": f"{args.config}: {cfg['sql']}", "events_per_gpu": cfg["n"], "keys_per_gpu": cfg["keys"],
+                   "events_total": n_glob, "events_rank0": n, "windows_emitted": n_windows, "rows_per_step_rank0": rows,
+                   "event_rate": f"{cfg['epm'] * world} events per ms of event time" if iet else "processing time",
+                   "parallelism": f"key-hash shards x{world}" + (" (shard mode: global WatermarkTuples, global arrivals"
+                                                                  + (", trigger all_gather" if cfg.get("trig") else "")
+                                                                  + (", count(*) all_gather" if cfg.get("global_count") else "")
+                                                                  + ")" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_part (dominant kernel; HIP events around each launch on the engine stream)",
-                     "algorithmic_bytes_per_launch": part_alg, "launch_ms": part_launch_ms,
-                     "traffic_source": traffic_src,
-                     "phase_ms_per_step": {PHASES[k]: ph_ms[k] / args.steps for k in range(4)},
-                     "path": {"achieved": path_gbs, "frac": path_gbs / HBM_PEAK_GBS, "device_ms": dev_ms_step,
-                              "algorithmic_bytes": alg_bytes,
-                              "what": "whole ek_push_batch: 28 B/event in + 28 B/result row out over its device time"}},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "what": f"whole step: {in_bytes_per_event} B/event in + {cfg['out_bytes']} B/result row out "
+                             f"(SURVEY.md §8(d)) over ms_per_step (driver clock)",
+                     "algorithmic_bytes_per_step": alg_bytes, "device_ms_per_step": dev_ms / args.steps,
+                     "dominant_kernel": dominant, "kernels": kernels},
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if global_count is not None:
+        out["config"]["global_count"] = str(global_count)[:200]
+    if rank == 0 and world == 1 and args.config == "C2" and not args.no_ingest:
+        out["ingest_inclusive"] = ingest_inclusive(eng, cols, n)
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == "C2":
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
+    if cnt_eng is not None:
+        cnt_eng.close()
     if dist:
         dist.destroy_process_group()
 

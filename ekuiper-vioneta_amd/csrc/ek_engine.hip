@@ -676,8 +676,8 @@ struct Engine {
         inc_pend.clear();
         gmode = 0;
         g_row_arr = nullptr;
-        g_wm_arr.clear();
-        g_wm_ts.clear();
+        g_wa = g_wt = nullptr;
+        g_nwm = 0;
         g_trig.clear();
         wins.clear();
         r_rows_used = 0;
@@ -2727,7 +2727,13 @@ struct Engine {
     // ordered buffer for processing-time count windows).
     int gmode = 0;                      // 1: shard mode (entered by the first global push, left by ek_reset)
     const int64_t* g_row_arr = nullptr; // device: global arrival of the current batch's rows
-    std::vector<int64_t> g_wm_arr, g_wm_ts;   // the current push's WatermarkTuples (host copy)
+    // the current push's WatermarkTuples: the caller's host arrays (valid for the duration of the call)
+    const int64_t* g_wa = nullptr;
+    const int64_t* g_wt = nullptr;
+    int64_t g_nwm = 0;
+    bool g_wm_on_dev = false;           // uploaded to g_wm_d (only when a kernel needs the list)
+    bool g_all_accepted = false;
+    int64_t g_max_step = 0;
     DevBuf g_wm_d, g_arr_d, g_acc_d;
     struct GTrig { int64_t a, t; };
     std::vector<GTrig> g_trig;          // accepted global sliding triggers not released yet (arrival order)
@@ -2747,12 +2753,25 @@ struct Engine {
         return 0;
     }
 
-    WmList wm_list() const {
+    // the tuple list on the device (one upload per push, from a pinned staging block)
+    int wm_to_device() {
+        if (g_wm_on_dev || g_nwm == 0) return 0;
+        if (int rc = ensure(g_wm_d, (size_t)g_nwm * 16)) return rc;
+        int64_t* h = desc_alloc((size_t)g_nwm * 2);
+        if (!h) return fail(EK_ERR_NOMEM, "pinned");
+        memcpy(h, g_wa, (size_t)g_nwm * 8);
+        memcpy(h + g_nwm, g_wt, (size_t)g_nwm * 8);
+        hipMemcpyAsync(g_wm_d.p, h, (size_t)g_nwm * 16, hipMemcpyHostToDevice, stream);
+        g_wm_on_dev = true;
+        return 0;
+    }
+    // W before this push's tuples (carry) and the list on the device (call wm_to_device first)
+    WmList wm_list(int64_t carry) const {
         WmList w{};
-        w.arr = (const int64_t*)g_wm_d.p;
-        w.ts = w.arr ? w.arr + g_wm_arr.size() : nullptr;
-        w.n = (int64_t)g_wm_arr.size();
-        w.carry = has_W ? W : INT64_MIN;
+        w.arr = g_nwm ? (const int64_t*)g_wm_d.p : nullptr;
+        w.ts = w.arr ? w.arr + g_nwm : nullptr;
+        w.n = g_nwm;
+        w.carry = carry;
         return w;
     }
 
@@ -2762,21 +2781,15 @@ struct Engine {
         if ((g->n_wm > 0 && (!g->wm_arrival || !g->wm_ts)) || (g->n_trig > 0 && (!g->trig_arrival || !g->trig_ts)))
             return fail(EK_ERR_INVALID, "missing watermark / trigger list");
         if (n > 0 && !g->row_arrival) return fail(EK_ERR_INVALID, "missing row arrivals");
-        g_wm_arr.assign(g->wm_arrival, g->wm_arrival + g->n_wm);
-        g_wm_ts.assign(g->wm_ts, g->wm_ts + g->n_wm);
-        for (int64_t k = 0; k < g->n_wm; ++k) {
-            if ((k > 0 && (g_wm_arr[k] <= g_wm_arr[k - 1] || g_wm_ts[k] <= g_wm_ts[k - 1])) || (has_W && g_wm_ts[k] <= W))
-                return fail(EK_ERR_INVALID, "WatermarkTuples must advance (tuple %lld)", (long long)k);
-        }
-        if (g->n_wm > 0) {
-            if (int rc = ensure(g_wm_d, (size_t)g->n_wm * 16)) return rc;
-            // one upload from a pinned staging block
-            int64_t* h = desc_alloc((size_t)g->n_wm * 2);
-            if (!h) return fail(EK_ERR_NOMEM, "pinned");
-            memcpy(h, g_wm_arr.data(), (size_t)g->n_wm * 8);
-            memcpy(h + g->n_wm, g_wm_ts.data(), (size_t)g->n_wm * 8);
-            hipMemcpyAsync(g_wm_d.p, h, (size_t)g->n_wm * 16, hipMemcpyHostToDevice, stream);
-        }
+        g_wa = g->wm_arrival;
+        g_wt = g->wm_ts;
+        g_nwm = g->n_wm;
+        g_wm_on_dev = false;
+        g_all_accepted = g->all_accepted != 0;
+        g_max_step = g->max_wm_step;
+        // the tuples advance (the whole list is checked when a kernel uploads it; here its ends)
+        if (g_nwm > 0 && ((has_W && g_wt[0] <= W) || g_wt[g_nwm - 1] < g_wt[0] || g_wa[g_nwm - 1] < g_wa[0]))
+            return fail(EK_ERR_INVALID, "WatermarkTuples must advance");
         g_row_arr = nullptr;
         if (n > 0) {
             if (g->memory == EK_MEM_HOST) {
@@ -2794,11 +2807,15 @@ struct Engine {
     int global_accept(const DBatch& db, int64_t min_ts, bool hop, int64_t e1, const uint8_t** d_acc, int64_t* n_acc,
                       int64_t* min_acc, int64_t* dropped) {
         const int64_t n = db.n;
-        const WmList w = wm_list();
-        int64_t wmax = w.carry;
-        if (w.n > 0) wmax = std::max(wmax, g_wm_ts.back());
+        const int64_t carry = has_W ? W : INT64_MIN;
+        int64_t wmax = carry;
+        if (g_nwm > 0) wmax = std::max(wmax, g_wt[g_nwm - 1]);
         *d_acc = nullptr; *n_acc = n; *min_acc = min_ts; *dropped = 0;
         if (!hop && (wmax == INT64_MIN || min_ts >= wmax)) return 0;   // no row can be late
+        // the host's WatermarkOp accepted every event and no tuple advanced by more than a hopping window
+        if (g_all_accepted && (!hop || (g_max_step > 0 && g_max_step <= L))) return 0;
+        if (int rc = wm_to_device()) return rc;
+        const WmList w = wm_list(carry);
         if (int rc = ensure(g_acc_d, (size_t)n)) return rc;
         hipMemsetAsync(&((BatchStats*)bstats.p)->n_accepted, 0, 8, stream);
         hipMemsetAsync(&((BatchStats*)bstats.p)->n_dropped, 0, 8, stream);
@@ -2850,6 +2867,8 @@ struct Engine {
         if (!plan.is_event_time) rc = push_count_global(db, g);
         else rc = push_global_event(db, g);
         g_row_arr = nullptr;
+        g_wa = g_wt = nullptr;
+        g_nwm = 0;
         if (rc) return rc;
         arrivals = g->arrivals_end;
         return record_time();
@@ -2889,10 +2908,11 @@ struct Engine {
         const int64_t M_prev = M;
         const bool had_M = has_M;
         if (n > 0 && (!has_M || s.max_ts > M)) { M = s.max_ts; has_M = true; }
-        if (!g_wm_ts.empty()) {
-            W = g_wm_ts.back();
+        const int64_t W_carry = has_W ? W : INT64_MIN;
+        if (g_nwm > 0) {
+            W = g_wt[g_nwm - 1];
             has_W = true;
-            sW = g_wm_arr.back();
+            sW = g_wa[g_nwm - 1];
         }
         if (origin_now) {
             e1_known = true;
@@ -2919,9 +2939,10 @@ struct Engine {
                 eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
             }
             if (need_rel && eb_rel > rel_prev) {
+                if (int rc = wm_to_device()) return rc;
                 const int gg = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
                 hipLaunchKernelGGL(k_release_step_global, dim3(gg), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                                   (const int64_t*)eb.arr.p, rel_prev, eb_rel, wm_list(), (int64_t*)eb.rel.p);
+                                   (const int64_t*)eb.arr.p, rel_prev, eb_rel, wm_list(W_carry), (int64_t*)eb.rel.p);
             }
             for (int64_t k = 0; k < g->n_trig; ++k) g_trig.push_back(GTrig{g->trig_arrival[k], g->trig_ts[k]});
             return range_triggers(rel_prev);
@@ -2959,16 +2980,16 @@ struct Engine {
         std::stable_sort(rel.begin(), rel.end(), [](const GTrig& x, const GTrig& y) { return x.t < y.t || (x.t == y.t && x.a < y.a); });
         for (const GTrig& x : rel) {
             // the releasing tuple: the first one at or after its arrival whose watermark reaches its ts
-            const size_t k0 = std::lower_bound(g_wm_arr.begin(), g_wm_arr.end(), x.a) - g_wm_arr.begin();
-            const size_t k1 = std::lower_bound(g_wm_ts.begin(), g_wm_ts.end(), x.t) - g_wm_ts.begin();
-            const size_t k = std::max(k0, k1);
-            if (k >= g_wm_arr.size()) return fail(EK_ERR_INVALID, "trigger at arrival %lld is not released by this batch's tuples", (long long)x.a);
+            const int64_t k0 = std::lower_bound(g_wa, g_wa + g_nwm, x.a) - g_wa;
+            const int64_t k1 = std::lower_bound(g_wt, g_wt + g_nwm, x.t) - g_wt;
+            const int64_t k = std::max(k0, k1);
+            if (k >= g_nwm) return fail(EK_ERR_INVALID, "trigger at arrival %lld is not released by this batch's tuples", (long long)x.a);
             PendWin p{};
             p.q.kind = RB_SLIDE;
             p.q.lo_ts = x.t - L;
             p.q.hi_ts = x.t;
             p.q.pos = eb_floor - 1;      // the search starts at the floor: every row before the trigger's run is a member candidate
-            p.q.rstep = g_wm_arr[k];
+            p.q.rstep = g_wa[k];
             p.q.floor = eb_floor;
             p.start = x.t - L;
             p.end = x.t;

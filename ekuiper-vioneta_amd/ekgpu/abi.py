@@ -140,7 +140,8 @@ class ek_global_ctx(C.Structure):
         ("wm_ts", C.c_void_p),
         ("n_wm", C.c_int64),
         ("origin_known", C.c_int32),
-        ("pad", C.c_int32),
+        ("all_accepted", C.c_int32),
+        ("max_wm_step", C.c_int64),
         ("origin_ts", C.c_int64),
         ("origin_arrival", C.c_int64),
         ("trig_arrival", C.c_void_p),

@@ -155,7 +155,10 @@ class Engine:
         return b, keep
 
     def push_global(self, columns, ctx: A.ek_global_ctx, validity=None):
-        """Shard mode (ek_push_batch_global): this handle's rows (host arrays) + the global context."""
+        """Shard mode (ek_push_batch_global): this handle's rows (host arrays; None = no rows) + the global context."""
+        if columns is None:
+            self._check(lib().ek_push_batch_global(self.h, None, C.byref(ctx)))
+            return
         b, _keep = self._host_batch(columns, validity)
         self._check(lib().ek_push_batch_global(self.h, C.byref(b), C.byref(ctx)))
 
@@ -166,6 +169,25 @@ class Engine:
         for k, ptr in enumerate(col_ptrs):
             b.columns[k] = ptr
         self._check(lib().ek_push_batch_global(self.h, C.byref(b), C.byref(ctx)))
+
+    def shard_triggers_device(self, n_rows: int, col_ptrs, ctx: A.ek_global_ctx):
+        """ek_shard_triggers over a device batch: (global arrival, ts) of the accepted trigger rows."""
+        b = A.ek_batch()
+        b.n_rows = n_rows
+        b.memory = A.EK_MEM_DEVICE
+        for k, ptr in enumerate(col_ptrs):
+            b.columns[k] = ptr
+        cap = max(1, n_rows // 1000 + 1024)
+        while True:
+            oa = np.zeros(cap, np.int64)
+            ot = np.zeros(cap, np.int64)
+            cnt = C.c_int64(0)
+            self._check(lib().ek_shard_triggers(self.h, C.byref(b), C.byref(ctx), oa.ctypes.data, ot.ctypes.data, cap,
+                                                C.byref(cnt)))
+            k = int(cnt.value)
+            if k <= cap:
+                return oa[:k], ot[:k]
+            cap = k
 
     def advance_watermark(self, wm_ms: int, arrivals_end: int):
         self._check(lib().ek_advance_watermark(self.h, int(wm_ms), int(arrivals_end)))

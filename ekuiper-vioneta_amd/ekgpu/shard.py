@@ -107,9 +107,12 @@ class GlobalWatermark:
             if len(acc_ts):
                 mn = int(acc_ts.min())
                 self._acc_min = mn if self._acc_min is None else min(self._acc_min, mn)
+        prev_w = self.mark - self.T
+        steps = np.diff(np.concatenate([[prev_w], wm_ts])) if len(wm_ts) else np.zeros(0, np.int64)
         self.mark = int(m[-1])
         self.arrivals += n
         return {"wm_arrival": wm_arrival, "wm_ts": wm_ts, "arrivals_end": self.arrivals, "accepted": accepted,
+                "all_accepted": bool(accepted.all()), "max_wm_step": int(steps.max()) if len(steps) else 0,
                 "origin_known": self.origin_known, "origin_ts": self.origin_ts, "origin_arrival": self.origin_arrival}
 
 
@@ -128,6 +131,8 @@ def make_ctx(wm: dict, row_arrival: np.ndarray, trig_arrival=None, trig_ts=None)
     g.wm_ts = wt.ctypes.data if len(wt) else None
     g.n_wm = len(wa)
     g.origin_known = 1 if wm["origin_known"] else 0
+    g.all_accepted = 1 if wm.get("all_accepted") else 0
+    g.max_wm_step = int(wm.get("max_wm_step", 0))
     g.origin_ts = int(wm["origin_ts"])
     g.origin_arrival = int(wm["origin_arrival"])
     g.trig_arrival = ta.ctypes.data if len(ta) else None

@@ -286,7 +286,12 @@ typedef struct {
      * released an event, event_window_trigger.go:57-75,211-219): valid when origin_known != 0; the tuple
      * that released it is the last one with wm_arrival <= origin_arrival */
     int32_t origin_known;
-    int32_t pad;
+    /* hints from the host's WatermarkOp (0 = unknown): all_accepted = no event of this batch was late;
+     * max_wm_step = the largest advance between consecutive WatermarkTuples (from the previous batch's last one).
+     * With all_accepted and (no hopping window with lateTolerance 0, or max_wm_step <= its length) a pane-mode
+     * shard needs only the batch's last tuple: no per-row watermark search. */
+    int32_t all_accepted;
+    int64_t max_wm_step;
     int64_t origin_ts;
     int64_t origin_arrival;
     /* SLIDINGWINDOW: the accepted trigger events of the WHOLE stream in this batch (every shard's, from
