@@ -13,6 +13,7 @@ namespace ek {
 
 constexpr int kBlock = 256;       // 4 wave64s per workgroup
 constexpr int kMaxVC = 4;         // value columns referenced by aggregates
+constexpr uint32_t kPseudoKeys = 65536;   // partial slots of an un-grouped pane-mode rule
 
 // fields kept per (pane, key) in the pane-partial state and per key in LDS tables
 enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32, NEED_SORT = 64 };
@@ -46,6 +47,8 @@ struct DPlan {
     int32_t sagg_agg[kMaxSortAggs];
     int32_t inc;                  // incremental-window semantics (inc_sum / inc_avg float64, funcs_inc_agg.go:56-117)
     int32_t n_begin, n_emit;      // STATEWINDOW(begin, emit) conditions (window_v2_op.go:111-148)
+    int32_t pseudo_keys;          // no GROUP BY in pane mode: rows spread over kPseudoKeys partial slots by row index
+                                  // (merged per window by k_finalize_merge) instead of one partition
     ek_instr begin_prog[EK_MAX_PROG];
     ek_instr emit_prog[EK_MAX_PROG];
 };

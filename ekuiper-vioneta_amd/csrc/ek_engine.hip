@@ -64,8 +64,10 @@ void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLa
                            pbase, scratch, scr_stride);
 }
 template <int N>
-void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res) {
-    hipLaunchKernelGGL(k_finalize<N>, g, dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
+void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res,
+                bool merge) {
+    if (merge) hipLaunchKernelGGL(k_finalize_merge<N>, dim3(g.y), dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
+    else hipLaunchKernelGGL(k_finalize<N>, g, dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
 }
 
 int64_t floordiv_h(int64_t a, int64_t b) {
@@ -427,6 +429,12 @@ struct Engine {
         dp.ts_col = plan.ts_column;
         dp.key_col = plan.key_column;
         dp.num_keys = plan.key_column >= 0 ? plan.num_keys : 1u;
+        // un-grouped pane-mode rule: spread the rows over kPseudoKeys partial slots (row index) so a pane is aggregated
+        // by many workgroups; k_finalize_merge folds the slots of a window into its one group
+        if (plan.key_column < 0 && !range_mode && env_int("EKGPU_PSEUDO_KEYS", 1)) {
+            dp.pseudo_keys = 1;
+            dp.num_keys = kPseudoKeys;
+        }
         dp.n_where = plan.n_where;
         dp.n_having = plan.n_having;
         dp.n_trigger = plan.n_trigger;
@@ -809,7 +817,7 @@ struct Engine {
     int64_t reg_win = 0;               // next window index to register
     int register_until(int64_t j) {
         while (reg_win <= j) {
-            if (int rc = ensure_results((int64_t)K, 1)) return rc;
+            if (int rc = ensure_results(Krows(), 1)) return rc;
             WinInfo wi{};
             wi.j = reg_win;
             wi.end = win_end(reg_win);
@@ -817,13 +825,14 @@ struct Engine {
             wi.out_base = r_rows_used;
             wi.slot = (int32_t)wins.size();
             wi.direct = false;
-            r_rows_used += K;
+            r_rows_used += Krows();
             wins.push_back(wi);
             reg_win++;
         }
         return 0;
     }
     WinInfo& win_info(int64_t j) { return wins[(size_t)(j - wins.front().j)]; }
+    int64_t Krows() const { return dp.pseudo_keys ? 1 : (int64_t)K; }   // result rows a window can hold
 
     // Emit every window j >= next_win with E_j <= W whose panes are complete (last pane <= q_done).
     int finalize_ready(int64_t q_done) {
@@ -873,10 +882,10 @@ struct Engine {
             const WinDesc* wd = (const WinDesc*)wdesc.p;
             const int ph = phase_begin(EK_PHASE_FINALIZE);
             switch (nvc) {
-            case 1: launch_fin<1>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
-            case 2: launch_fin<2>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
-            case 3: launch_fin<3>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
-            default: launch_fin<4>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv); break;
+            case 1: launch_fin<1>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
+            case 2: launch_fin<2>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
+            case 3: launch_fin<3>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
+            default: launch_fin<4>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
             }
             phase_end(ph);
         }
@@ -897,7 +906,7 @@ struct Engine {
         // size the result store once for every window this batch will close
         if (W >= win_end(next_win)) {
             int64_t nclose = (W - win_end(next_win)) / H + 1;
-            if (int rc = ensure_results(nclose * (int64_t)K, nclose)) return rc;
+            if (int rc = ensure_results(nclose * Krows(), nclose)) return rc;
         }
         int64_t q_lo = std::max<int64_t>(0, pane_host(min_acc));
         int64_t q_hi = pane_host(max_ts);
@@ -1058,7 +1067,7 @@ struct Engine {
         for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
         // direct emission: a fresh tumbling pane whose whole content is in this group and whose window
         // closes at this batch's watermark is finalised by k_agg itself (no pane-state round trip)
-        if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes) {
+        if (wtype == EK_WINDOW_TUMBLING && has_W && whole_panes && !dp.pseudo_keys) {
             for (int r = 0; r < npn; ++r) {
                 int64_t q = qa + r;
                 if (!h_fresh[r] || win_end(q) > W || q < next_win) continue;
@@ -2543,7 +2552,7 @@ struct Engine {
     // `owners` workgroups on each of the 8 XCDs (the kernel checks it before any side effect).
     int stream_setup() {
         stream_state = -1;
-        if (env_int("EKGPU_STREAM", 0) == 0 || range_mode || dp.n_sagg > 0 || dp.n_vc < 1 || dp.n_vc > 4) return 0;
+        if (env_int("EKGPU_STREAM", 0) == 0 || range_mode || dp.pseudo_keys || dp.n_sagg > 0 || dp.n_vc < 1 || dp.n_vc > 4) return 0;
         for (int v = 0; v < dp.n_vc; ++v)
             if (dp.vc_flags[v] & (NEED_CNT | NEED_M2 | NEED_FSUM | NEED_SORT)) return 0;
         int cus = 0;

@@ -500,7 +500,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
         for (int64_t v = c0 + threadIdx.x; v < c1; v += kPartBlock) {
             const int rel = chunk_rel(lb, nlb, pa, v);
             const int64_t i = v + loff[rel - pa];
-            const uint32_t key = kcol ? kcol[i] : 0u;
+            const uint32_t key = kcol ? kcol[i] : (p.pseudo_keys ? (uint32_t)(i & (kPseudoKeys - 1)) : 0u);
             const int lp = local_part<MODE, WHERE>(p, b, g, gd, rel, acc, i, pa, key, pane_err, true);
             if (lp >= 0) atomicAdd(&tcnt[lp], 1u);
         }
@@ -521,11 +521,12 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
             }
 #pragma unroll
             for (int u = 0; u < V; ++u) {
-                const uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
+                uint32_t kk[4] = {kv[u].x, kv[u].y, kv[u].z, kv[u].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int64_t i = base + (int64_t)u * kPartBlock * 4 + e;
                     if (i < c0 || i >= c1) continue;
+                    if (p.pseudo_keys) kk[e] = (uint32_t)(i & (kPseudoKeys - 1));
                     const int rel = MODE == 1 ? chunk_rel(lb, nlb, pa, i) : 0;
                     const int lp = local_part<MODE, WHERE>(p, b, g, gd, rel, acc, i, pa, kk[e], pane_err, true);
                     if (lp >= 0) atomicAdd(&tcnt[lp], 1u);
@@ -559,7 +560,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
                     rel[j] = chunk_rel(lb, nlb, pa, v);
                     phys[j] = v + loff[rel[j] - pa];
                 }
-                key[j] = (kcol && phys[j] >= 0) ? kcol[phys[j]] : 0u;
+                key[j] = (kcol && phys[j] >= 0) ? kcol[phys[j]] : (p.pseudo_keys && phys[j] >= 0 ? (uint32_t)(phys[j] & (kPseudoKeys - 1)) : 0u);
 #pragma unroll
                 for (int c = 0; c < NVC; ++c)
                     val[c][j] = (c < p.n_vc && phys[j] >= 0) ? ((const int64_t*)b.col[p.vc_col[c]])[phys[j]] : 0;
@@ -576,6 +577,10 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
                 } else {
                     key[2 * m] = (kcol && i < gd.nbatch) ? kcol[i] : 0u;
                     key[2 * m + 1] = 0u;
+                }
+                if (p.pseudo_keys) {   // un-grouped rule: partial slot from the row index
+                    key[2 * m] = (uint32_t)(i & (kPseudoKeys - 1));
+                    key[2 * m + 1] = (uint32_t)((i + 1) & (kPseudoKeys - 1));
                 }
 #pragma unroll
                 for (int v = 0; v < NVC; ++v) {
@@ -1434,6 +1439,75 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
     }
     __shared__ uint32_t esh[20];
     emit_rows(p, present, s, key, w.out_base, w.idx, res, esh);
+}
+
+// Un-grouped rule (pseudo keys): one workgroup per window merges every (pane, partial slot) entry of the window into
+// ONE group (Chan merge for M2, a fixed tree order for the sums), then HAVING and the single row (key 0).
+template <int NVC>
+__global__ __launch_bounds__(kBlock) void k_finalize_merge(DPlan* __restrict__ pp, const WinDesc* __restrict__ wins,
+                                                           DState ds, int32_t ring, const int32_t* __restrict__ pane_err,
+                                                           Results res) {
+    const DPlan& p = *pp;
+    const WinDesc w = wins[blockIdx.x];
+    int32_t werr = 0;
+    for (int64_t q = w.q_first; q <= w.q_last; ++q) werr |= pane_err[q % ring];
+    if (werr) {
+        if (threadIdx.x == 0) atomicOr(&res.win_err[w.idx], werr);
+        return;
+    }
+    Part<NVC> s{};
+    for (int64_t q = w.q_first; q <= w.q_last; ++q) {
+        for (int64_t key = threadIdx.x; key < (int64_t)kPseudoKeys; key += kBlock) {
+            const int64_t e = (q % ring) * ds.K + key;
+            const int64_t c = ds.cnt[e];
+            if (c == 0) continue;
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                const int f = p.vc_flags[v];
+                vc[v] = (f & NEED_CNT) ? ds.vcnt[v][e] : c;
+                is[v] = (!p.vc_is_float[v] && (f & NEED_SUM)) ? ds.sum[v][e] : 0;
+                fs[v] = p.vc_is_float[v] ? ((f & NEED_SUM) ? __longlong_as_double(ds.sum[v][e]) : 0.0)
+                                         : ((f & NEED_FSUM) ? ds.fsum[v][e] : 0.0);
+                m2[v] = (f & NEED_M2) ? ds.m2[v][e] : 0.0;
+                mn[v] = (f & NEED_MIN) ? (uint64_t)ds.mn[v][e] : 0ull;
+                mx[v] = (f & NEED_MAX) ? (uint64_t)ds.mx[v][e] : 0ull;
+            }
+            part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+        }
+    }
+    // block tree merge of the per-thread partials through LDS
+    __shared__ int64_t t_cnt[kBlock], t_vc[NVC][kBlock], t_is[NVC][kBlock];
+    __shared__ double t_fs[NVC][kBlock], t_m2[NVC][kBlock];
+    __shared__ uint64_t t_mn[NVC][kBlock], t_mx[NVC][kBlock];
+    const int t = threadIdx.x;
+    for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
+        if (t >= stride && t < 2 * stride) {
+            t_cnt[t] = s.cnt;
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                t_vc[v][t] = s.vcnt[v]; t_is[v][t] = s.isum[v]; t_fs[v][t] = s.fsum[v]; t_m2[v][t] = s.m2[v];
+                t_mn[v][t] = s.omn[v]; t_mx[v][t] = s.omx[v];
+            }
+        }
+        __syncthreads();
+        if (t < stride && t_cnt[t + stride] > 0) {
+            const int o = t + stride;
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) { vc[v] = t_vc[v][o]; is[v] = t_is[v][o]; fs[v] = t_fs[v][o]; m2[v] = t_m2[v][o]; mn[v] = t_mn[v][o]; mx[v] = t_mx[v][o]; }
+            part_merge(p, s, t_cnt[o], vc, is, fs, m2, mn, mx);
+        }
+        __syncthreads();
+    }
+    bool present = false;
+    if (t == 0) present = s.cnt > 0 && having_keep(p, s, &res.win_err[w.idx]);
+    __shared__ uint32_t esh[20];
+    emit_rows(p, present, s, 0, w.out_base, w.idx, res, esh);
 }
 
 // ---------------------------------------------------------------- debug: window membership fingerprint
