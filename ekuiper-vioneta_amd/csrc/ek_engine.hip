@@ -373,12 +373,16 @@ struct Engine {
                 if (plan.aggs[k].fn != EK_AGG_COUNT_STAR && ((plan.nullable_mask >> plan.aggs[k].column) & 1u))
                     return fail(EK_ERR_UNSUPPORTED, "incremental aggregates over a nullable column (nil at a group's last row) are not built");
         }
+        // hopping with lateTolerance > 0: the empty-window discard (window_op.go:605-655) can drop inputs released by
+        // earlier pushes, so the events are kept (range mode) instead of being folded into pane partials
         range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT ||
+                     (wtype == EK_WINDOW_HOPPING && plan.is_event_time && plan.late_tolerance_ms > 0) ||
                      wtype == EK_WINDOW_STATE || sort_aggs ||
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
             return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
-        need_rel = wtype == EK_WINDOW_SLIDING || (inc && wtype == EK_WINDOW_COUNT);
+        need_rel = wtype == EK_WINDOW_SLIDING || (inc && wtype == EK_WINDOW_COUNT) ||
+                   (wtype == EK_WINDOW_SESSION && plan.late_tolerance_ms > 0);
         if (plan.is_event_time) {
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
                 return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
@@ -673,6 +677,7 @@ struct Engine {
         delayq.clear();
         delayq_head = 0;
         h_rts.clear();
+        h_rwp.clear();
         h_rts_base = 0;
         sess_last_ticked = sess_has_trigger = false;
         sess_trigger = 0;
@@ -1309,6 +1314,7 @@ struct Engine {
     size_t delayq_head = 0;
     // session windows: host mirror of the released timestamps [h_rts_base, h_rts_base + size)
     std::vector<int64_t> h_rts;
+    std::vector<int64_t> h_rwp;        // lateTolerance > 0: watermark just before each mirrored row's release step
     int64_t h_rts_base = 0;
     bool sess_last_ticked = false, sess_has_trigger = false;
     int64_t sess_trigger = 0;
@@ -1527,11 +1533,12 @@ struct Engine {
 
     // A triggered window before its range is resolved
     struct PendWin { RangeQ q; int64_t start, end; };
+    bool hop_discard_pending = false;   // fire_windows applies the hopping empty-window discard to this set
 
     // Resolve the ranges of `pw` on the device, register the windows, launch their aggregation.
     int fire_windows(std::vector<PendWin>& pw) {
         const int nq = (int)pw.size();
-        if (nq == 0) return 0;
+        if (nq == 0) { hop_discard_pending = false; return 0; }
         if (int rc = ensure(rq_d, (size_t)nq * sizeof(RangeQ))) return rc;
         if (int rc = ensure(ab_d, (size_t)nq * 16)) return rc;
         std::vector<RangeQ> hq(nq);
@@ -1543,6 +1550,10 @@ struct Engine {
         h_ab.resize((size_t)nq * 2);
         hipMemcpyAsync(h_ab.data(), ab_d.p, (size_t)nq * 16, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window range kernel failed");
+        if (hop_discard_pending) {
+            hop_discard_pending = false;
+            if (int rc = hopping_discard(pw)) return rc;
+        }
         // register in trigger order; rows reserved = min(K, members)
         int64_t rows = 0;
         for (int w = 0; w < nq; ++w) rows += std::min<int64_t>(K, h_ab[2 * w + 1] - h_ab[2 * w]);
@@ -1625,8 +1636,44 @@ struct Engine {
         // windows never start below the last fired one's start (overlapping) or end (disjoint)
         const bool overlap = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_COUNT;
         eb_floor = std::max(eb_floor, overlap ? h_ab[2 * (nq - 1)] : h_ab[2 * (nq - 1) + 1]);
+        if (hop_floor >= 0) { eb_floor = std::max(eb_floor, hop_floor); hop_floor = -1; }
         return 0;
     }
+
+    // Hopping windows fired by this push, in order (handleInputs, window_op.go:605-655): a window's content starts at
+    // the inputs the previous window kept (nextleft = its first member); a window with no member drops EVERY input
+    // present at the WatermarkTuple that fired it, so the next windows start past the rows released by then.
+    int hopping_discard(const std::vector<PendWin>& pw) {
+        const int nq = (int)pw.size();
+        std::vector<int64_t> ends(nq), pre(nq);
+        for (int w = 0; w < nq; ++w) ends[w] = pw[w].end;
+        if (int rc = ensure(mrg_col, (size_t)nq * 16)) return rc;
+        int64_t* d_ends = (int64_t*)mrg_col.p;
+        hipMemcpyAsync(d_ends, ends.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_fire_prefix, dim3((nq + 255) / 256), dim3(256), 0, stream, (const int64_t*)runmax_d.p, cur_nb,
+                           cur_arr_base, plan.late_tolerance_ms, (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)eb.arr.p,
+                           eb.n, d_ends, nq, d_ends + nq);
+        hipMemcpyAsync(pre.data(), d_ends + nq, (size_t)nq * 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "fire prefix kernel failed");
+        int64_t floor = eb_floor;
+        for (int w = 0; w < nq; ++w) {
+            const int64_t a = std::max(h_ab[2 * w], floor), b = h_ab[2 * w + 1];
+            if (a >= b) {
+                // inputs released by the firing tuple beyond this window are dropped with it
+                stats.records_discarded += std::max<int64_t>(0, pre[w] - std::max(a, b));
+                h_ab[2 * w] = h_ab[2 * w + 1] = a;
+                floor = std::max(floor, pre[w]);
+            } else {
+                h_ab[2 * w] = a;
+                floor = a;
+            }
+        }
+        hop_floor = floor;
+        hipMemcpyAsync(ab_d.p, h_ab.data(), (size_t)nq * 16, hipMemcpyHostToDevice, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window range upload failed");
+        return 0;
+    }
+    int64_t hop_floor = -1;
 
     int run_vgroup(const std::vector<int>& members, int64_t V, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots) {
         const int npn = (int)members.size();
@@ -1790,6 +1837,7 @@ struct Engine {
                 E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
             }
             if (e1_known && has_W) {
+                hop_discard_pending = wtype == EK_WINDOW_HOPPING && !gmode;
                 while (win_end(next_win) <= W) {
                     const int64_t j = next_win++;
                     PendWin p{};
@@ -2125,6 +2173,17 @@ struct Engine {
             const size_t o = h_rts.size();
             h_rts.resize(o + n_new);
             hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            if (need_rel) {
+                // the watermark before each new row's release step (k_step_wm over the batch's running max)
+                if (int rc = ensure(mrg_col, (size_t)n_new * 16)) return rc;
+                int64_t* g = (int64_t*)mrg_col.p;
+                hipLaunchKernelGGL(k_step_wm, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
+                                   (const int64_t*)eb.rel.p + rel_prev, n_new, (const int64_t*)runmax_d.p, cur_nb, cur_arr_base,
+                                   cur_prevmax, plan.late_tolerance_ms, g, g + n_new);
+                if (h_rwp.size() != o) h_rwp.assign(o, INT64_MIN);   // rows mirrored before (e.g. restored): unknown
+                h_rwp.resize(o + n_new);
+                hipMemcpyAsync(h_rwp.data() + o, g + n_new, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            }
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "session mirror copy failed");
         }
         const int64_t timeout = H, duration = L;
@@ -2138,6 +2197,10 @@ struct Engine {
             int64_t p = INT64_MIN;
             for (int64_t i = i0; i < i1; ++i) {
                 const int64_t t = h_rts[i];
+                // lateTolerance > 0: a WatermarkTuple before this row's release already saw p as the last input and
+                // closed the session by the trailing check (now - p > timeout), before any tick at this row
+                if (need_rel && p != INT64_MIN && i < (int64_t)h_rwp.size() && h_rwp[i] != INT64_MIN && h_rwp[i] - p > timeout)
+                    return p + timeout;
                 int64_t r = INT64_MAX;
                 if (p != INT64_MIN && t - p > timeout) r = p + timeout;
                 if (t > tick) {
@@ -2178,6 +2241,7 @@ struct Engine {
         const int64_t drop = floor_abs - h_rts_base;
         if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
             h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+            if (!h_rwp.empty()) h_rwp.erase(h_rwp.begin(), h_rwp.begin() + drop);
             h_rts_base = floor_abs;
         }
         return 0;

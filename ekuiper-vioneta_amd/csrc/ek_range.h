@@ -100,6 +100,22 @@ __global__ void k_first_ge(const int64_t* __restrict__ a, int64_t n, int64_t x, 
     out[0] = lb_i64(a, 0, n, x);
 }
 
+// Released prefix of the buffer at the WatermarkTuple that fires each window end (hopping windows): the first step j
+// of the batch whose watermark runmax[j] - late_tol reaches the end, then the k_rel_end bound at (W_j, arrival j).
+// handleInputs (window_op.go:605-655) drops every input present at that tuple when the window finds no member.
+__global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base, int64_t late_tol,
+                              const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n,
+                              const int64_t* __restrict__ ends, int nq, int64_t* __restrict__ out) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nq) return;
+    const int64_t j = lb_i64(runmax, 0, nb, ends[w] + late_tol);
+    if (j >= nb) { out[w] = n; return; }   // not reached inside this batch (cannot happen for a fired window)
+    const int64_t W = runmax[j] - late_tol;
+    const int64_t p = lb_i64(bts, 0, n, W);
+    const int64_t q = ub_i64(bts, p, n, W);
+    out[w] = ub_i64(barr, p, q, arr_base + j);
+}
+
 // SLIDINGWINDOW trigger flags over buffer rows [i0, i1): 1 when OVER (WHEN cond) holds
 // (window_op.go:741-768: nil, error or non-bool -> no trigger); every row triggers without OVER.
 __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {
