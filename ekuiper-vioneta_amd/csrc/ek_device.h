@@ -47,6 +47,9 @@ struct DPlan {
     int32_t sagg_agg[kMaxSortAggs];
     int32_t inc;                  // incremental-window semantics (inc_sum / inc_avg float64, funcs_inc_agg.go:56-117)
     int32_t n_begin, n_emit;      // STATEWINDOW(begin, emit) conditions (window_v2_op.go:111-148)
+    int32_t n_user_cols;          // columns of the caller's batch; [n_user_cols, n_columns) are derived (aggregate args)
+    int32_t n_derived_prog[EK_MAX_DERIVED];
+    ek_instr derived_prog[EK_MAX_DERIVED][EK_MAX_PROG];
     int32_t pseudo_keys;          // no GROUP BY in pane mode: rows spread over kPseudoKeys partial slots by row index
                                   // (merged per window by k_finalize_merge) instead of one partition
     ek_instr begin_prog[EK_MAX_PROG];

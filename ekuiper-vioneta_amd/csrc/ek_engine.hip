@@ -148,6 +148,8 @@ int prog_depth_ok(const ek_instr* prog, int n) {
 
 struct Engine {
     ek_plan plan{};
+    int user_cols = 0;                  // columns of the caller's batches (plan.n_columns also counts the derived ones)
+    DevBuf der_val[EK_MAX_DERIVED], der_valid[EK_MAX_DERIVED];
     DPlan dp{};
     DPlan* d_plan = nullptr;
     int device = 0;
@@ -289,6 +291,37 @@ struct Engine {
                 if (pr[k].op == EK_OP_COL && !col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "condition column out of range");
                 if (pr[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in a window condition");
             }
+        // derived columns (expression arguments of aggregates): validated here, then appended to the engine's copy of
+        // the plan as ordinary columns [user_cols, user_cols + n_derived) computed per batch by k_derive
+        user_cols = plan.n_columns;
+        if (plan.n_derived < 0 || plan.n_derived > EK_MAX_DERIVED || plan.n_columns + plan.n_derived > EK_MAX_COLUMNS)
+            return fail(EK_ERR_INVALID, "bad n_derived");
+        if (plan.n_derived > 0 && plan.window_type == EK_WINDOW_NONE) return fail(EK_ERR_INVALID, "derived columns need aggregates");
+        for (int d = 0; d < plan.n_derived; ++d) {
+            const ek_instr* pr = plan.derived_prog[d];
+            const int np = plan.n_derived_prog[d];
+            if (np <= 0 || np > EK_MAX_PROG || !prog_depth_ok(pr, np)) return fail(EK_ERR_INVALID, "malformed derived column program %d", d);
+            if (plan.derived_type[d] != EK_COL_I64 && plan.derived_type[d] != EK_COL_F64) return fail(EK_ERR_INVALID, "bad derived column type");
+            bool nullable = false;
+            for (int k = 0; k < np; ++k) {
+                const int op = pr[k].op;
+                if (op == EK_OP_COL) {
+                    if (!col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "derived column reference out of range");
+                    nullable |= (plan.nullable_mask >> pr[k].arg) & 1u;
+                } else if (op == EK_OP_AGG || (op >= EK_OP_EQ && op <= EK_OP_OR)) {
+                    return fail(EK_ERR_UNSUPPORTED, "derived columns are arithmetic over columns and constants");
+                } else if (op == EK_OP_DIV || op == EK_OP_MOD) {
+                    const ek_instr& r = pr[k - 1];   // postfix: the divisor is the instruction before the operator
+                    const bool cz = (r.op == EK_OP_CONST_I64 && r.i64 != 0) || (r.op == EK_OP_CONST_F64 && r.f64 != 0.0);
+                    if (!cz) return fail(EK_ERR_UNSUPPORTED, "derived columns divide only by a non-zero constant "
+                                                             "(a zero divisor is a per-row evaluation error)");
+                }
+            }
+            const int c = plan.n_columns + d;
+            plan.column_type[c] = plan.derived_type[d];
+            if (nullable) plan.nullable_mask |= 1u << c;
+        }
+        plan.n_columns += plan.n_derived;
         if (plan.window_version == 2 && plan.window_type == EK_WINDOW_SLIDING) {
             // WindowV2Operator sliding windows (window_v2_op.go:39-58): the event-time op without delay is built
             if (!plan.is_event_time)
@@ -430,6 +463,11 @@ struct Engine {
         dp = DPlan{};
         dp.n_columns = plan.n_columns;
         for (int c = 0; c < plan.n_columns; ++c) dp.col_type[c] = plan.column_type[c];
+        dp.n_user_cols = user_cols;
+        for (int d = 0; d < plan.n_derived; ++d) {
+            dp.n_derived_prog[d] = plan.n_derived_prog[d];
+            memcpy(dp.derived_prog[d], plan.derived_prog[d], sizeof plan.derived_prog[d]);
+        }
         dp.ts_col = plan.ts_column;
         dp.key_col = plan.key_column;
         dp.num_keys = plan.key_column >= 0 ? plan.num_keys : 1u;
@@ -2362,7 +2400,7 @@ struct Engine {
         const int64_t n = b->n_rows;
         db.n = n;
         if (b->memory == EK_MEM_HOST) {
-            for (int c = 0; c < plan.n_columns; ++c) {
+            for (int c = 0; c < user_cols; ++c) {
                 size_t es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
                 if (int rc = ensure(in_cols[c], (size_t)n * es)) return rc;
                 hipMemcpyAsync(in_cols[c].p, b->columns[c], (size_t)n * es, hipMemcpyHostToDevice, stream);
@@ -2374,8 +2412,31 @@ struct Engine {
                 }
             }
         } else {
-            for (int c = 0; c < plan.n_columns; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
+            for (int c = 0; c < user_cols; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
         }
+        return derive(db);
+    }
+
+    // the derived columns of a staged batch (k_derive): engine-owned buffers appended to the batch's columns
+    int derive(DBatch& db) {
+        const int nd = plan.n_columns - user_cols;
+        if (nd <= 0 || db.n <= 0) return 0;
+        int64_t* o[4] = {nullptr, nullptr, nullptr, nullptr};
+        uint8_t* v[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int d = 0; d < nd; ++d) {
+            const int c = user_cols + d;
+            if (int rc = ensure(der_val[d], (size_t)db.n * 8)) return rc;
+            o[d] = (int64_t*)der_val[d].p;
+            db.col[c] = o[d];
+            db.valid[c] = nullptr;
+            if ((plan.nullable_mask >> c) & 1u) {
+                if (int rc = ensure(der_valid[d], (size_t)db.n)) return rc;
+                v[d] = (uint8_t*)der_valid[d].p;
+                db.valid[c] = v[d];
+            }
+        }
+        hipLaunchKernelGGL(k_derive, dim3((int)std::min<int64_t>(8192, (db.n + 255) / 256)), dim3(256), 0, stream, d_plan, db, db.n,
+                           o[0], o[1], o[2], o[3], v[0], v[1], v[2], v[3]);
         return 0;
     }
 
@@ -2385,7 +2446,7 @@ struct Engine {
         if (n < 0) return fail(EK_ERR_INVALID, "negative row count");
         if (n == 0) return 0;
         if (n > ((int64_t)1 << 31) - 1) return fail(EK_ERR_UNSUPPORTED, "batch larger than 2^31-1 rows");
-        for (int c = 0; c < plan.n_columns; ++c) {
+        for (int c = 0; c < user_cols; ++c) {
             if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
             if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
         }
@@ -2919,7 +2980,7 @@ struct Engine {
         }
         if (g->arrivals_end < arrivals) return fail(EK_ERR_INVALID, "arrivals_end went backwards");
         if (n > 0) {
-            for (int c = 0; c < plan.n_columns; ++c) {
+            for (int c = 0; c < user_cols; ++c) {
                 if (!b->columns[c]) return fail(EK_ERR_INVALID, "column %d missing", c);
                 if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
             }

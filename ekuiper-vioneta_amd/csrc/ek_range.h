@@ -116,6 +116,28 @@ __global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, in
     out[w] = ub_i64(barr, p, q, arr_base + j);
 }
 
+// Derived columns (expression arguments of aggregates, GroupedTuples.AggregateEval row.go:712-718): per row the
+// valuer's arithmetic over the batch's own columns (eval_prog); nil -> validity 0. The programs cannot error (host
+// lowering: / and % only by non-zero constants).
+__global__ void k_derive(DPlan* __restrict__ pp, DBatch b, int64_t n, int64_t* __restrict__ out0, int64_t* __restrict__ out1,
+                         int64_t* __restrict__ out2, int64_t* __restrict__ out3, uint8_t* __restrict__ v0, uint8_t* __restrict__ v1,
+                         uint8_t* __restrict__ v2, uint8_t* __restrict__ v3) {
+    const DPlan& p = *pp;
+    int64_t* outs[4] = {out0, out1, out2, out3};
+    uint8_t* vals[4] = {v0, v1, v2, v3};
+    const int nd = p.n_columns - p.n_user_cols;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int d = 0; d < EK_MAX_DERIVED; ++d) {
+            if (d >= nd) break;
+            const Val v = eval_prog(p.derived_prog[d], p.n_derived_prog[d], p, &b, i, NoAggs{});
+            const bool ok = v.tag == V_I64 || v.tag == V_F64;
+            outs[d][i] = !ok ? 0 : (v.tag == V_F64 ? __double_as_longlong(v.f) : v.i);
+            if (vals[d]) vals[d][i] = ok ? 1 : 0;
+        }
+    }
+}
+
 // SLIDINGWINDOW trigger flags over buffer rows [i0, i1): 1 when OVER (WHEN cond) holds
 // (window_op.go:741-768: nil, error or non-bool -> no trigger); every row triggers without OVER.
 __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {

@@ -5,10 +5,11 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 3
+EKGPU_ABI_VERSION = 4
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
+EK_MAX_DERIVED = 4
 
 # window types == pkg/ast/statement.go:185-193
 (EK_WINDOW_NONE, EK_WINDOW_TUMBLING, EK_WINDOW_HOPPING, EK_WINDOW_SLIDING, EK_WINDOW_SESSION, EK_WINDOW_COUNT,
@@ -82,6 +83,10 @@ class ek_plan(C.Structure):
         ("begin_prog", ek_instr * EK_MAX_PROG),
         ("n_emit", C.c_int32),
         ("emit_prog", ek_instr * EK_MAX_PROG),
+        ("n_derived", C.c_int32),
+        ("derived_type", C.c_int32 * EK_MAX_DERIVED),
+        ("n_derived_prog", C.c_int32 * EK_MAX_DERIVED),
+        ("derived_prog", (ek_instr * EK_MAX_PROG) * EK_MAX_DERIVED),
     ]
 
 

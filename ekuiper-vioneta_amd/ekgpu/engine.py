@@ -261,6 +261,14 @@ class JsonDecoder:
     """Columnar JSON ingest on the GPU (include/ekgpu.h ek_json_*): a micro-batch of JSON messages ->
     device columns of an ek_batch, ready for Engine.push_batch."""
 
+    @classmethod
+    def schemaless(cls, fields, device: int = 0) -> "JsonDecoder":
+        """A schemaless stream (CREATE STREAM demo () ...): FastJsonConverter without a schema decodes every JSON number
+        as float64 (converter/json/converter.go:507-520, useInt64ForWholeNumber off), so each field the rule reads
+        becomes a FLOAT column. A non-number value (the reference keeps it as a string / bool / map, which the rule's
+        numeric expressions then reject) drops the message with EK_JSON_ERR_TYPE."""
+        return cls({f: "float" for f in fields}, device)
+
     def __init__(self, schema: dict, device: int = 0):
         """schema: ordered {field: "bigint" | "float" | "key"} (same column order as the rule's schema)."""
         from .rule import COLTYPES

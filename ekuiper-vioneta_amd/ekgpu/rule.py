@@ -7,7 +7,7 @@ Host-side mirror of the pieces of the reference front-end that feed the hot path
   * rule options isEventTime / lateTolerance   internal/pkg/def/rule.go:27-66
 
 Supported subset (everything the BASELINE configs and the reference's window tests use):
-  SELECT <key | agg(col) | count(*) | window_start() | window_end()> [AS alias], ...
+  SELECT <key | agg(col | arithmetic over columns) | count(*) | window_start() | window_end()> [AS alias], ...
   FROM <stream> [WHERE <expr>]
   GROUP BY [<key>,] TUMBLINGWINDOW|HOPPINGWINDOW|SLIDINGWINDOW|SESSIONWINDOW|COUNTWINDOW(...)
            [OVER (WHEN <expr>)]
@@ -83,6 +83,7 @@ class _Parser:
         self.schema = {k.lower(): (k, v) for k, v in schema.items()}
         self.columns = list(schema.keys())
         self.aggs: List[Tuple[int, int, float]] = []
+        self.derived: List[Tuple[Tuple, str]] = []
 
     # token helpers
     def peek(self, k: int = 0) -> Optional[str]:
@@ -124,18 +125,47 @@ class _Parser:
             self.i += 1
             self.expect(")")
             return self.agg_slot(A.EK_AGG_COUNT_STAR, -1, 0.0)
-        arg = self.peek()
-        self.i += 1
-        c = self.col(arg)
+        prog = self.add(False)   # the argument: a column or an arithmetic expression over columns
+        c = prog[0][1] if len(prog) == 1 and prog[0][0] == A.EK_OP_COL else self.derived_col(prog)
         p = 0.0
         if self.peek() == ",":
             self.i += 1
             p = float(self.peek())
             self.i += 1
         self.expect(")")
-        if name in ("percentile_cont", "percentile_disc") and p == 0.0 and name:
-            pass
         return self.agg_slot(A.AGG_BY_NAME[name], c, p)
+
+    # aggregate argument expressions -> derived columns (GroupedTuples.AggregateEval, row.go:712-718)
+    def derived_col(self, prog: List[Tuple]) -> int:
+        types = []
+        for k, ins in enumerate(prog):
+            op = ins[0]
+            if op == A.EK_OP_COL:
+                t = self.schema[self.columns[ins[1]].lower()][1]
+                types.append("float" if t == "float" else "int")
+            elif op == A.EK_OP_CONST_I64:
+                types.append("int")
+            elif op == A.EK_OP_CONST_F64:
+                types.append("float")
+            elif op in (A.EK_OP_ADD, A.EK_OP_SUB, A.EK_OP_MUL, A.EK_OP_DIV, A.EK_OP_MOD):
+                if op in (A.EK_OP_DIV, A.EK_OP_MOD):
+                    r = prog[k - 1]
+                    if r[0] not in (A.EK_OP_CONST_I64, A.EK_OP_CONST_F64) or r[1] == 0:
+                        raise RuleError("an aggregate argument may divide only by a non-zero constant "
+                                        "(a zero divisor is a per-row evaluation error)")
+                b, a = types.pop(), types.pop()
+                # valuer.go:861-1000: int64 op int64 stays int64 (integer division), a float64 operand promotes
+                types.append("float" if "float" in (a, b) else "int")
+            else:
+                raise RuleError("aggregate arguments are arithmetic over columns and constants")
+        key = (tuple(prog), types[-1])
+        if key not in self.derived:
+            if len(self.derived) >= A.EK_MAX_DERIVED:
+                raise RuleError("too many expression arguments")
+            if len(self.columns) + len(self.derived) >= A.EK_MAX_COLUMNS:
+                raise RuleError("too many columns")
+            self.derived.append(key)
+        return len(self.columns) + self.derived.index(key)
 
     # expressions -> postfix program
     def expr(self, allow_agg: bool) -> List[Tuple]:
@@ -389,6 +419,10 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
         plan.aggs[k].fn = fn
         plan.aggs[k].column = c
         plan.aggs[k].param = prm if fn in (A.EK_AGG_PERCENTILE_CONT, A.EK_AGG_PERCENTILE_DISC) else 0.0
+    plan.n_derived = len(p.derived)
+    for d, (prog, t) in enumerate(p.derived):
+        plan.derived_type[d] = A.EK_COL_F64 if t == "float" else A.EK_COL_I64
+        plan.n_derived_prog[d] = _fill_prog(plan.derived_prog[d], list(prog))
     plan.n_where = _fill_prog(plan.where_prog, where)
     plan.n_having = _fill_prog(plan.having_prog, having)
     plan.n_trigger = _fill_prog(plan.trigger_prog, trigger)

@@ -26,10 +26,11 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 3
+#define EKGPU_ABI_VERSION 4
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
+#define EK_MAX_DERIVED 4
 
 /* Window types: identical values to pkg/ast/statement.go:185-193 (ast.WindowType). */
 enum {
@@ -148,6 +149,17 @@ typedef struct {
     ek_instr begin_prog[EK_MAX_PROG];
     int32_t n_emit;
     ek_instr emit_prog[EK_MAX_PROG];
+    /* Aggregate arguments that are expressions: GroupedTuples.AggregateEval evaluates the argument on every row of the
+     * group (internal/xsql/row.go:712-718). Derived column d is column index n_columns + d (an aggregate's `column`
+     * may name it); its value per row is derived_prog[d] over the stream's columns and constants with the valuer's
+     * arithmetic (valuer.go:861-1000: int64 op int64 stays int64 - integer division truncates -, any float64
+     * operand promotes, % on floats is math.Mod, a nil operand gives nil). Built for + - * and / % by a non-zero
+     * constant (a zero divisor is an evaluation error the aggregate functions would have to see per row);
+     * derived_type[d] is the expression's result type (EK_COL_I64 / EK_COL_F64). */
+    int32_t n_derived;
+    int32_t derived_type[EK_MAX_DERIVED];
+    int32_t n_derived_prog[EK_MAX_DERIVED];
+    ek_instr derived_prog[EK_MAX_DERIVED][EK_MAX_PROG];
 } ek_plan;
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };

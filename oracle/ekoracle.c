@@ -108,8 +108,18 @@ typedef struct {
 
 static int64_t row_arrival(const dataset* d, int64_t e) { return d->arrival ? d->arrival[e] : e; }
 
+static val_t eval_prog(const ek_instr* prog, int n, const dataset* d, int64_t row, const val_t* aggs);
+
+/* column c of a row; c in [n_columns, n_columns + n_derived) is an aggregate argument expression, evaluated on the
+ * row like GroupedTuples.AggregateEval (internal/xsql/row.go:712-718) */
 static val_t col_val(const dataset* d, int c, int64_t row) {
     val_t v; v.tag = V_NULL; v.i = 0; v.f = 0;
+    if (c >= d->p->n_columns && c < d->p->n_columns + d->p->n_derived) {
+        const int k = c - d->p->n_columns;
+        v = eval_prog(d->p->derived_prog[k], d->p->n_derived_prog[k], d, row, NULL);
+        if (v.tag != V_I64 && v.tag != V_F64) { v.tag = V_NULL; v.i = 0; v.f = 0; }
+        return v;
+    }
     if (c < 0 || c >= d->p->n_columns || !d->cols[c]) return v;
     if (d->valid && d->valid[c] && !d->valid[c][row]) return v;
     switch (d->p->column_type[c]) {
@@ -458,7 +468,8 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
             for (int a = 0; a < p->n_aggs; ++a) {
                 const ek_agg_spec* as = &p->aggs[a];
                 int c = as->column;
-                int is_float = (c >= 0 && c < p->n_columns) ? (p->column_type[c] == EK_COL_F64) : 0;
+                int is_float = (c >= 0 && c < p->n_columns) ? (p->column_type[c] == EK_COL_F64)
+                             : (c >= p->n_columns && c < p->n_columns + p->n_derived) ? (p->derived_type[c - p->n_columns] == EK_COL_F64) : 0;
                 for (int64_t k = 0; k < gn; ++k) {
                     if (as->fn == EK_AGG_COUNT_STAR) { nul[k] = 0; iv[k] = 0; continue; }
                     val_t v = col_val(d, c, rows[k]);

@@ -1,3 +1,4 @@
+import numpy as np
 """CPU-side checks of the boundary: the C-ABI library loads and exports every declared symbol; the
 ctypes mirror matches the header; the rule compiler builds the plans the configs need."""
 import ctypes as C
@@ -96,3 +97,35 @@ def test_engine_without_gpu_fails_loudly():
                      IOT_SCHEMA, num_keys=16)
     with pytest.raises(EngineError):
         Engine(r.plan)
+
+
+def test_expression_argument_lowering():
+    """agg(<arithmetic over columns>) lowers to derived columns (row.go:712-718); identical arguments share one;
+    int op int stays int, a float operand promotes; division only by a non-zero constant."""
+    r = compile_rule("SELECT deviceId, avg(temperature * 1.8 + 32), max(temperature * 1.8 + 32), sum(humidity), "
+                     "count(temperature - humidity) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)",
+                     IOT_SCHEMA, num_keys=16)
+    p = r.plan
+    assert p.n_derived == 2 and p.n_columns == 4
+    assert [p.aggs[k].column for k in range(4)] == [4, 4, 3, 5]
+    assert [p.derived_type[d] for d in range(2)] == [A.EK_COL_F64, A.EK_COL_F64]
+    schema = {"k": "key", "ts": "bigint", "a": "bigint", "x": "float"}
+    r = compile_rule("SELECT k, sum(a * 3 / 2), sum(a % 5 + x) FROM s GROUP BY k, TUMBLINGWINDOW(ss,1)", schema,
+                     num_keys=4)
+    assert [r.plan.derived_type[d] for d in range(2)] == [A.EK_COL_I64, A.EK_COL_F64]
+    for bad in ("sum(a / x)", "sum(a % 0)", "sum(a / 0.0)"):
+        with pytest.raises(RuleError):
+            compile_rule(f"SELECT k, {bad} FROM s GROUP BY k, TUMBLINGWINDOW(ss,1)", schema, num_keys=4)
+
+
+def test_oracle_expression_argument_is_per_row(oracle):
+    """The oracle's derived column equals the per-row formula: avg(t*1.8+32) == avg(t)*1.8+32 per window (CPU,
+    no engine)."""
+    from ekgpu.synth import iot_stream
+    cols = list(iot_stream(20_000, 8, events_per_ms=5))
+    sql = "SELECT deviceId, avg(temperature * 1.8 + 32), avg(temperature) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)"
+    exp = oracle.run(compile_rule(sql, IOT_SCHEMA, num_keys=8).plan, cols, None)
+    assert len(exp.windows) >= 3
+    for w in exp.windows:
+        a, b = (np.ascontiguousarray(w.values[k]).view(np.float64) for k in (0, 1))   # f64 bit patterns
+        assert np.allclose(a, b * 1.8 + 32, rtol=1e-12, atol=1e-9)

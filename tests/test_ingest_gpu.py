@@ -17,7 +17,7 @@ import pytest
 from ekgpu import abi as A
 from ekgpu.rule import compile_rule
 from ekgpu.synth import IOT_SCHEMA, iot_stream
-from parity import assert_windows_equal
+from parity import assert_windows_equal, assert_windows_equal_np
 from test_engine_gpu import engine_mod  # noqa: F401  (fixture)
 
 pytestmark = pytest.mark.gpu
@@ -178,3 +178,27 @@ def test_json_to_tumbling_group_by(oracle, engine_mod):
     exp = oracle.run(rule.plan, [key, ts, temp, hum]).windows
     assert len(got) >= 1
     assert_windows_equal(rule.plan, got, exp, check_members=True)
+
+
+def test_c1_schemaless_json_filter(oracle, engine_mod):
+    """C1 as SURVEY.md §8(d) states it: a schemaless stream, 1e6 payloads {"temperature":T,"humidity":H} with integer
+    T, H in [0, 100]: every number decodes as float64 (converter.go:507-520), SELECT * ... WHERE temperature > 50."""
+    n = 1_000_000
+    rng = np.random.default_rng(12)
+    t = rng.integers(0, 101, n)
+    h = rng.integers(0, 101, n)
+    msgs = [f'{{"temperature":{a},"humidity":{b}}}'.encode() for a, b in zip(t.tolist(), h.tolist())]
+    dec = engine_mod.JsonDecoder.schemaless(["temperature", "humidity"])
+    batch = dec.decode(msgs)
+    assert batch.n_rows == n
+    schema = {"temperature": "float", "humidity": "float"}
+    rule = compile_rule("SELECT * FROM demo WHERE temperature > 50", schema, is_event_time=False)
+    exp = oracle.run(rule.plan, [t.astype(np.float64), h.astype(np.float64)])
+    eng = engine_mod.Engine(rule.plan)
+    eng.push_batch(batch)
+    got = eng.poll()
+    eng.close()
+    dec.close()
+    assert_windows_equal_np(rule.plan, got, exp.windows)
+    w = got[0]
+    assert len(w.keys) == int((t > 50).sum()) and set(np.unique(w.tags[1])) == {A.EK_TAG_F64}
