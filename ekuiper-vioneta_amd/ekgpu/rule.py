@@ -221,6 +221,9 @@ class _Parser:
             v = self.peek()
             self.i += 1
             return [self._num("-" + v)]
+        if t == "-":        # unary minus on a column or sub-expression: x * -1 (keeps int64 int64, flips a float's sign)
+            self.i += 1
+            return self.prim(aa) + [(A.EK_OP_CONST_I64, -1), (A.EK_OP_MUL,)]
         if re.match(r"[\d.]", t):
             self.i += 1
             return [self._num(t)]

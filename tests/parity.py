@@ -14,6 +14,11 @@ FP_TOL_FNS = {A.EK_AGG_SUM, A.EK_AGG_AVG, A.EK_AGG_STDDEV, A.EK_AGG_STDDEVS, A.E
 REL_TOL = 1e-6
 
 
+def col_type(plan, c):
+    """Column type of an aggregate's argument; c >= n_columns names a derived (expression) column."""
+    return plan.column_type[c] if c < plan.n_columns else plan.derived_type[c - plan.n_columns]
+
+
 def _close(a, b, rel):
     if a is None or b is None:
         return a is b
@@ -39,7 +44,7 @@ def assert_windows_equal(plan, got, exp, check_members=False, max_report=5):
             for a in range(plan.n_aggs):
                 fn = plan.aggs[a].fn
                 c = plan.aggs[a].column
-                is_float_col = c >= 0 and plan.column_type[c] == A.EK_COL_F64
+                is_float_col = c >= 0 and col_type(plan, c) == A.EK_COL_F64
                 x, y = gv[a], ev[a]
                 if type(x) is not type(y):
                     bad.append((key, a, x, y, "type"))
@@ -60,7 +65,7 @@ def assert_windows_equal_np(plan, got, exp, check_members=False):
     tol_aggs = set()
     for a in range(plan.n_aggs):
         fn, c = plan.aggs[a].fn, plan.aggs[a].column
-        is_float_col = c >= 0 and plan.column_type[c] == A.EK_COL_F64
+        is_float_col = c >= 0 and col_type(plan, c) == A.EK_COL_F64
         if fn in FP_TOL_FNS and (is_float_col or fn != A.EK_AGG_SUM):
             tol_aggs.add(a)
     for w, (g, e) in enumerate(zip(got, exp)):

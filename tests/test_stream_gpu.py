@@ -22,9 +22,9 @@ def stream_on():
 
 @pytest.mark.parametrize("sql,n,keys,epm,batches", [
     ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)",
-     400_000, 65536, 100, 1),
+     4_000_000, 65536, 100, 1),
     ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)",
-     400_000, 1000, 20, 5),
+     800_000, 1000, 20, 5),
     ("SELECT deviceId, sum(temperature), min(temperature), max(humidity), count(*) FROM demo "
      "GROUP BY deviceId, HOPPINGWINDOW(ss, 6, 2)", 300_000, 5000, 20, 3),
     ("SELECT deviceId, avg(temperature), count(*) FROM demo WHERE humidity > 30 GROUP BY deviceId, TUMBLINGWINDOW(ss, 2)",
