@@ -30,6 +30,7 @@
 #include "ek_range.h"
 #include "ek_global.h"
 #include "ek_stream.h"
+#include "ek_keymajor.h"
 
 using namespace ek;
 
@@ -590,6 +591,7 @@ struct Engine {
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
+        km_mode = env_int("EKGPU_KEYMAJOR", 2);
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
@@ -1633,6 +1635,9 @@ struct Engine {
             }
             if (!wl.empty()) {
                 const int nw = (int)wl.size();
+                int max_n = 1;
+                for (int w : wl) max_n = std::max<int>(max_n, (int)(h_ab[2 * w + 1] - h_ab[2 * w]));
+                const size_t swl = sw_lds_bytes(max_n);
                 if (int rc = ensure(sw_d, (size_t)nw * 4 + (size_t)nq * 12 + 16)) return rc;
                 int32_t* d_wl = (int32_t*)sw_d.p;
                 int32_t* d_slot = d_wl + nw;
@@ -1644,15 +1649,23 @@ struct Engine {
                 Results rv = results_view();
                 const int ph = phase_begin(EK_PHASE_AGGREGATE);
                 switch (std::max(1, dp.n_vc)) {
-                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
-                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
-                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
-                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), 0, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv); break;
+                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
+                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
+                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
+                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
                 }
                 phase_end(ph);
                 // the host vectors above are reused by the next fire: keep them alive until the copies ran
                 hipStreamSynchronize(stream);
             }
+        }
+        // key-major aggregation of the other windows when the cost rule picks it (ek_keymajor.h)
+        {
+            std::vector<int> rest;
+            for (int w = 0; w < nq; ++w)
+                if (!small[w] && slots[w] >= 0 && h_ab[2 * w + 1] > h_ab[2 * w]) rest.push_back(w);
+            if (!rest.empty())
+                if (int rc = km_try(rest, obase, slots, small)) return rc;   // marks the windows it aggregated
         }
         // virtual-pane groups of consecutive non-empty windows
         const int64_t vcap = (int64_t)env_int("EKGPU_RANGE_GROUP_EVENTS", 1 << 26);
@@ -1712,6 +1725,163 @@ struct Engine {
         return 0;
     }
     int64_t hop_floor = -1;
+
+    // ---- key-major aggregation (ek_keymajor.h): the span of a run of fired windows is sorted once by key and one
+    // thread per key walks the windows. Picked (EKGPU_KEYMAJOR=2, default) for big key spaces when the windows overlap
+    // heavily (each event re-aggregated >= 4 times by the window-major path) or need order statistics over short
+    // per-key runs; 1 = whenever eligible, 0 = never. Ineligible: no GROUP BY, non-monotone window ranges, WHERE
+    // errors in the span (attributed per window by the window-major path), order statistics over a (key, window)
+    // run longer than kKmSelMax. The windows it aggregates are marked in `done`.
+    int km_mode = 2;
+    DevBuf km_k[2], km_p[2], km_tmp, km_start, km_val[kMaxVC], km_ok[kMaxVC], km_ab, km_bcnt, km_flag;
+    unsigned int* h_kmf = nullptr;     // pinned: WHERE errors, longest key run, long order-statistic run, scratch
+    std::vector<int64_t> km_hab;
+
+    int km_try(const std::vector<int>& rest, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots,
+               std::vector<uint8_t>& done) {
+        if (km_mode == 0 || dp.key_col < 0 || dp.pseudo_keys || K < 2) return 0;
+        for (size_t i = 1; i < rest.size(); ++i)
+            if (h_ab[2 * rest[i]] < h_ab[2 * rest[i - 1]] || h_ab[2 * rest[i] + 1] < h_ab[2 * rest[i - 1] + 1]) return 0;
+        for (size_t c0 = 0; c0 < rest.size(); c0 += kKmMaxWin) {
+            const size_t c1 = std::min(rest.size(), c0 + (size_t)kKmMaxWin);
+            std::vector<int> wl(rest.begin() + c0, rest.begin() + c1);
+            bool ok = false;
+            if (int rc = km_run(wl, obase, slots, &ok)) return rc;
+            if (ok) for (int w : wl) done[w] = 1;
+        }
+        return 0;
+    }
+
+    template <int N>
+    void km_walk(bool sort, bool write, int nblk, size_t lds, const KmDesc& d, const Results& rv) {
+        if (sort) {
+            if (write) hipLaunchKernelGGL((k_km_walk<N, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+            else hipLaunchKernelGGL((k_km_walk<N, true, false>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+        } else {
+            if (write) hipLaunchKernelGGL((k_km_walk<N, false, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+            else hipLaunchKernelGGL((k_km_walk<N, false, false>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+        }
+    }
+
+    int km_run(const std::vector<int>& wl, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots,
+               bool* handled) {
+        *handled = false;
+        const int nw = (int)wl.size();
+        const int64_t lo = h_ab[2 * wl[0]], hi = h_ab[2 * wl.back() + 1];
+        const int64_t n = hi - lo;
+        if (n <= 0 || n >= (1LL << 31)) return 0;
+        int64_t V = 0;
+        for (int w : wl) V += h_ab[2 * w + 1] - h_ab[2 * w];
+        const bool sort = dp.n_sagg > 0;
+        const double overlap = (double)V / (double)n, rows_kw = (double)V / nw / (double)K;
+        if (km_mode == 2 && !(K >= 16384 && (sort ? rows_kw <= 16.0 : overlap >= 4.0))) return 0;
+        int end_bit = 1;
+        while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)K) end_bit++;
+        size_t tb = 0;
+        ekl_sort_pairs_u32(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
+        for (int i = 0; i < 2; ++i) {
+            if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
+            if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
+        }
+        if (int rc = ensure(km_tmp, tb)) return rc;
+        if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
+        if (int rc = ensure(km_flag, 16)) return rc;
+        if (!h_kmf && hipHostMalloc((void**)&h_kmf, 16) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
+        unsigned int* d_flag = (unsigned int*)km_flag.p;
+        hipMemsetAsync(d_flag, 0, 16, stream);
+        const DBatch bv = buffer_view();
+        const int ph = phase_begin(EK_PHASE_PARTITION);
+        hipLaunchKernelGGL(k_km_keys, dim3((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                           d_plan, bv, lo, n, (uint32_t*)km_k[0].p, (uint32_t*)km_p[0].p, d_flag);
+        if (ekl_sort_pairs_u32(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p, (const uint32_t*)km_p[0].p,
+                               (uint32_t*)km_p[1].p, n, end_bit, stream))
+            return fail(EK_ERR_DEVICE, "key sort failed");
+        const uint32_t* sk = (const uint32_t*)km_k[1].p;
+        const uint32_t* spos = (const uint32_t*)km_p[1].p;
+        uint32_t* kstart = (uint32_t*)km_start.p;
+        hipLaunchKernelGGL(k_km_starts, dim3((unsigned)std::min<int64_t>(8192, (n + 1 + 255) / 256)), dim3(256), 0, stream, sk, n,
+                           K, kstart);
+        hipLaunchKernelGGL(k_km_maxrun, dim3((unsigned)std::min<int64_t>(4096, ((int64_t)K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           stream, (const uint32_t*)kstart, K, d_flag + 1);
+        phase_end(ph);
+        hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major sort failed");
+        if (h_kmf[0] > 0) return 0;                                                       // WHERE errors
+        if (km_mode == 2 && !sort && (double)h_kmf[1] * overlap > (double)(1 << 22)) return 0;   // one key dominates
+        // value columns in key order
+        KmCols cols{};
+        for (int v = 0; v < dp.n_vc; ++v) {
+            if (int rc = ensure(km_val[v], (size_t)n * 8)) return rc;
+            cols.val[v] = (int64_t*)km_val[v].p;
+            if (bv.valid[dp.vc_col[v]]) {
+                if (int rc = ensure(km_ok[v], (size_t)n)) return rc;
+                cols.ok[v] = (uint8_t*)km_ok[v].p;
+            }
+        }
+        const int nvc = std::max(1, dp.n_vc);
+        const int nblk = (int)(((int64_t)K + kKmBlock - 1) / kKmBlock);
+        if (int rc = ensure(km_ab, (size_t)nw * 28)) return rc;
+        if (int rc = ensure(km_bcnt, (size_t)nw * nblk * 4)) return rc;
+        km_hab.resize((size_t)nw * 3);
+        int64_t* h_rab = km_hab.data();
+        int64_t* h_rob = h_rab + 2 * nw;
+        for (int i = 0; i < nw; ++i) {
+            h_rab[2 * i] = h_ab[2 * wl[i]] - lo;
+            h_rab[2 * i + 1] = h_ab[2 * wl[i] + 1] - lo;
+            h_rob[i] = obase[wl[i]];
+        }
+        std::vector<int32_t> h_wi(nw);
+        for (int i = 0; i < nw; ++i) h_wi[i] = slots[wl[i]];
+        int64_t* d_ab = (int64_t*)km_ab.p;
+        int32_t* d_wi = (int32_t*)(d_ab + 3 * nw);
+        hipMemcpyAsync(d_ab, h_rab, (size_t)nw * 24, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(d_wi, h_wi.data(), (size_t)nw * 4, hipMemcpyHostToDevice, stream);
+        KmDesc d{};
+        d.n = n;
+        d.nw = nw;
+        d.nblk = nblk;
+        d.nkeys = K;
+        d.ab = d_ab;
+        d.obase = d_ab + 2 * nw;
+        d.widx = d_wi;
+        d.kstart = kstart;
+        d.spos = spos;
+        for (int v = 0; v < kMaxVC; ++v) { d.sval[v] = cols.val[v]; d.sok[v] = cols.ok[v]; }
+        d.bcnt = (uint32_t*)km_bcnt.p;
+        d.flags = (int32_t*)(d_flag + 2);
+        const Results rv = results_view();
+        // kept-row counters + window starts / ends (+ the order-statistic lanes)
+        const size_t lds = (size_t)((3 * nw + 1) & ~1) * 4 + (sort ? (size_t)kKmSegMax * kKmBlock * 8 : 0);
+        const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
+        const dim3 gg((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
+        switch (nvc) {
+        case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        }
+        auto walk = [&](bool write) {
+            switch (nvc) {
+            case 1: km_walk<1>(sort, write, nblk, lds, d, rv); break;
+            case 2: km_walk<2>(sort, write, nblk, lds, d, rv); break;
+            case 3: km_walk<3>(sort, write, nblk, lds, d, rv); break;
+            default: km_walk<4>(sort, write, nblk, lds, d, rv); break;
+            }
+        };
+        walk(false);
+        if (sort) {
+            hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major count pass failed");
+            if (h_kmf[2]) { phase_end(ph2); return 0; }   // a (key, window) run too long for one thread: window-major path
+        }
+        hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);
+        walk(true);
+        phase_end(ph2);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major aggregation failed");
+        stats.windows_keymajor += nw;
+        *handled = true;
+        return 0;
+    }
 
     int run_vgroup(const std::vector<int>& members, int64_t V, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots) {
         const int npn = (int)members.size();
@@ -3595,8 +3765,11 @@ struct Engine {
             release(e->rel);
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
-                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d})
+                          &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d,
+                          &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag})
             release(*d);
+        for (int v = 0; v < kMaxVC; ++v) { release(km_val[v]); release(km_ok[v]); }
+        if (h_kmf) hipHostFree(h_kmf);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
         for (auto& e : phase_ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }

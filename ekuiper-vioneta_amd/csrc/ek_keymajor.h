@@ -1,0 +1,331 @@
+// ek_keymajor.h — key-major aggregation of range windows (ek_engine.hip: Engine::km_run).
+//
+// A range window is an index range [a_k, b_k) of the event buffer (release order). The window-major path
+// (k_part MODE 2 + k_agg) partitions every window's members by (window, key bucket), so a sliding window that
+// overlaps its neighbours re-partitions each event once per window it belongs to, and a window over a huge key
+// space (C5: 12.5 M keys) spreads a handful of rows over thousands of partitions. Here the span of the fired
+// windows is sorted ONCE by key (stable, so each key's rows keep their buffer order), and one thread per key walks
+// the windows that hold any of its rows with two cursors over its sorted positions: window k's members of key g are
+// the contiguous sub-run of g's rows with a_k <= pos < b_k (aggregate_operator.go:34-82 groups a window's rows by
+// key; window_op.go:576-739 decides the members). The windows must be monotone (a_k and b_k non-decreasing in
+// trigger order), which holds for every window type the engine fires in order.
+//
+// Per (key, window) the thread folds the sub-run (count, sum, min, max, centred two-pass M2; median /
+// percentile_* by rank counting over at most kKmSelMax values), finalises (funcs_agg.go), applies HAVING and
+// emits. Result rows of window k land in its region [obase_k, obase_k + kept_k): a counting pass keeps a
+// per-(window, block) histogram in LDS, one workgroup per window scans it over the blocks, and the write pass
+// recomputes and stores at the block's offset + an LDS cursor (groups come in unspecified order, like the
+// reference's Go map iteration).
+#pragma once
+#include "ek_kernels.h"
+
+namespace ek {
+
+constexpr int kKmBlock = 256;
+constexpr int kKmMaxWin = 4096;    // windows per launch: the per-block LDS histogram
+constexpr int kKmSelMax = 256;     // order statistics: longest (key, window) sub-run selected by one thread
+constexpr int kKmSegMax = 32;      // ... sorted in the thread's LDS lane (longer ones: rank counting in memory)
+
+struct KmDesc {
+    int64_t n;                     // rows of the span (relative positions [0, n))
+    int32_t nw, nblk;
+    uint32_t nkeys;                // dense key ids < nkeys
+    int32_t pad;
+    const int64_t* ab;             // [2 * nw] window ranges relative to the span start
+    const int64_t* obase;          // [nw] first result row of each window's region
+    const int32_t* widx;           // [nw] result window slot
+    const uint32_t* kstart;        // [nkeys + 1] first sorted row of each key
+    const uint32_t* spos;          // relative positions in key order
+    const int64_t* sval[kMaxVC];   // value columns gathered in key order
+    const uint8_t* sok[kMaxVC];    // their validity (nullptr: all valid)
+    uint32_t* bcnt;                // [nw][nblk] kept rows per (window, block) -> exclusive offsets after k_km_scan
+    int32_t* flags;                // [0] a (key, window) sub-run longer than kKmSelMax (order statistics), [1] scratch
+};
+
+// (key, relative position) of every row of the span; rows that fail WHERE (or carry an out-of-range key) get the
+// sentinel key nkeys and sort last. WHERE errors are counted: the caller falls back to the window-major path,
+// which attributes them per window (filter_operator.go:63-77).
+__global__ __launch_bounds__(kBlock) void k_km_keys(DPlan* __restrict__ pp, DBatch b, int64_t lo, int64_t n,
+                                                    uint32_t* __restrict__ kout, uint32_t* __restrict__ pout,
+                                                    unsigned int* __restrict__ nerr) {
+    const DPlan& p = *pp;
+    const uint32_t* kcol = (const uint32_t*)b.col[p.key_col];
+    const uint32_t K = p.num_keys;
+    unsigned int e = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = lo + i;
+        const int wd = p.n_where > 0 ? where_decide_slow(p, b, r) : 1;
+        uint32_t k = kcol[r];
+        if (wd <= 0 || k >= K) k = K;
+        e += wd < 0;
+        kout[i] = k;
+        pout[i] = (uint32_t)i;
+    }
+    if (e) atomicAdd(nerr, e);
+}
+
+// kstart[g] = first sorted row with key >= g, for g in [0, K] (kstart[K] = rows that passed WHERE).
+__global__ void k_km_starts(const uint32_t* __restrict__ sk, int64_t n, uint32_t K, uint32_t* __restrict__ kstart) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+        // row i starts every key in (sk[i - 1], sk[i]] (keys <= K; the span's end closes (sk[n - 1], K])
+        const uint32_t g0 = i == 0 ? 0u : sk[i - 1] + 1u;
+        const uint32_t g1 = i == n ? K : min(sk[i], K);
+        for (uint32_t g = g0; g <= g1; ++g) kstart[g] = (uint32_t)i;
+    }
+}
+
+// longest key run (rows of one key over the whole span) -> atomicMax(*out)
+__global__ __launch_bounds__(kBlock) void k_km_maxrun(const uint32_t* __restrict__ kstart, uint32_t K, unsigned int* out) {
+    unsigned int m = 0;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < K; g += (int64_t)gridDim.x * kBlock)
+        m = max(m, kstart[g + 1] - kstart[g]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+struct KmCols {
+    int64_t* val[kMaxVC];
+    uint8_t* ok[kMaxVC];
+};
+
+// value columns (and validity) of the rows that passed WHERE, in key order
+template <int NVC>
+__global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DBatch b, int64_t lo,
+                                                      const uint32_t* __restrict__ spos, const uint32_t* __restrict__ kstart,
+                                                      KmCols out) {
+    const DPlan& p = *pp;
+    const int64_t m = kstart[p.num_keys];
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = lo + spos[i];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) {
+            if (v >= p.n_vc) break;
+            const int c = p.vc_col[v];
+            out.val[v][i] = ((const int64_t*)b.col[c])[r];
+            if (out.ok[v]) out.ok[v][i] = b.valid[c] ? b.valid[c][r] : (uint8_t)1;
+        }
+    }
+}
+
+// first window k in [k0, nw) with e[k] > x (e non-decreasing: window starts or ends in LDS), nw if none
+__device__ __forceinline__ int km_first_gt(const int32_t* e, int k0, int nw, int64_t x) {
+    int lo = k0, hi = nw;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)e[mid] > x) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+// rank-r value (ordered bits) among the valid values of sub-run [j0, j1) of column v: O(n^2) counting
+__device__ __forceinline__ uint64_t km_select(const int64_t* __restrict__ val, const uint8_t* __restrict__ ok, bool isf,
+                                              int64_t j0, int64_t j1, int64_t r) {
+    for (int64_t i = j0; i < j1; ++i) {
+        if (ok && !ok[i]) continue;
+        const uint64_t x = isf ? f64_to_ord(__longlong_as_double(val[i])) : i64_to_ord(val[i]);
+        int64_t less = 0, eq = 0;
+        for (int64_t j = j0; j < j1; ++j) {
+            if (ok && !ok[j]) continue;
+            const uint64_t y = isf ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
+            less += y < x;
+            eq += y == x;
+        }
+        if (less <= r && r < less + eq) return x;
+    }
+    return 0;
+}
+
+// HAVING (having_operator.go:41-56): 1 keeps the group, 0 drops it, -1 = a non-bool result (window error)
+template <int NVC>
+__device__ __forceinline__ int km_having(const DPlan& p, const Part<NVC>& s, const SortRes* sr) {
+    if (p.n_having <= 0) return 1;
+    const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, [&](int k) { return agg_value(p, s, k, sr); });
+    if (h.tag != V_BOOL) return -1;
+    return h.i != 0 ? 1 : 0;
+}
+
+// WRITE = false: count the rows each (window, block) keeps; true: emit them (and raise window errors).
+// A key's membership [j0, j1) of its sorted rows only changes where a window start passes row j0 or a window end
+// passes row j1, so the thread folds, finalises and tests HAVING once per membership state and emits that row into
+// every window of the state's run [k, kend) — about two states per row instead of one fold per (key, window).
+template <int NVC, bool SORT, bool WRITE>
+__global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, KmDesc d, Results res) {
+    extern __shared__ uint32_t s_dyn[];
+    const int nw = d.nw;
+    uint32_t* s_h = s_dyn;                          // [nw] kept rows (count pass) / cursors (write pass)
+    int32_t* s_a = (int32_t*)(s_dyn + nw);          // [nw] window starts (relative rows)
+    int32_t* s_b = s_a + nw;                        // [nw] window ends
+    uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
+    const DPlan& p = *pp;
+    for (int k = threadIdx.x; k < nw; k += kKmBlock) {
+        s_h[k] = 0;
+        s_a[k] = (int32_t)d.ab[2 * k];
+        s_b[k] = (int32_t)d.ab[2 * k + 1];
+    }
+    __syncthreads();
+    const int64_t g = (int64_t)blockIdx.x * kKmBlock + threadIdx.x;
+    if (g < d.nkeys) {
+        const int64_t s = d.kstart[g], e = d.kstart[g + 1];
+        int fl[NVC];
+        bool isf[NVC];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
+        int64_t j0 = s, j1 = s;
+        int k = s < e ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : nw;
+        while (k < nw) {
+            const int64_t wa = s_a[k], wb = s_b[k];
+            while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
+            if (j0 == e) break;
+            if (j1 < j0) j1 = j0;
+            while (j1 < e && (int64_t)d.spos[j1] < wb) ++j1;
+            const int64_t p0 = d.spos[j0];
+            if (j1 == j0) { k = km_first_gt(s_b, k + 1, nw, p0); continue; }
+            // windows [k, kend) hold exactly rows [j0, j1) of this key
+            int kend = km_first_gt(s_a, k + 1, nw, p0);
+            if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
+            // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull;
+                if (!fl[v]) continue;
+                const int64_t* __restrict__ val = d.sval[v];
+                const uint8_t* __restrict__ ok = d.sok[v];
+                for (int64_t j = j0; j < j1; ++j) {
+                    if (ok && !ok[j]) continue;
+                    const int64_t raw = val[j];
+                    const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
+                    vc[v]++;
+                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+                    fs[v] = __dadd_rn(fs[v], x);
+                    mn[v] = o < mn[v] ? o : mn[v];
+                    mx[v] = o > mx[v] ? o : mx[v];
+                }
+                if ((fl[v] & NEED_M2) && vc[v] > 0) {   // stats._variance shape
+                    const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+                    for (int64_t j = j0; j < j1; ++j) {
+                        if (ok && !ok[j]) continue;
+                        const int64_t raw = val[j];
+                        const double dd = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                        m2[v] = __dadd_rn(m2[v], __dmul_rn(dd, dd));
+                    }
+                }
+            }
+            Part<NVC> part{};
+            part_merge(p, part, j1 - j0, vc, is, fs, m2, mn, mx);
+            uint64_t sres[kMaxSortAggs];
+            uint8_t stag[kMaxSortAggs];
+            bool agg_err = false;
+#pragma unroll
+            for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
+            if constexpr (SORT) {
+                // per sort column: the sub-run's valid values (ordered bits), insertion-sorted in this thread's LDS
+                // lane (interleaved, conflict-free) when at most kKmSegMax, else ranked by counting in memory
+                for (int sc = 0; sc < p.n_scol; ++sc) {
+                    const int v = p.scol_vc[sc];
+                    const int64_t* __restrict__ val = d.sval[v];
+                    const uint8_t* __restrict__ ok = d.sok[v];
+                    const bool fv = p.vc_is_float[v] != 0;
+                    int64_t n = 0;
+                    for (int64_t j = j0; j < j1; ++j) n += (!ok || ok[j]) ? 1 : 0;
+                    if (n > kKmSelMax) { d.flags[0] = 1; agg_err = true; continue; }
+                    const bool inl = n <= kKmSegMax;
+                    if (inl) {
+                        int m = 0;
+                        for (int64_t j = j0; j < j1; ++j) {
+                            if (ok && !ok[j]) continue;
+                            const uint64_t x = fv ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
+                            int q = m;
+                            while (q > 0 && s_seg[(q - 1) * kKmBlock + threadIdx.x] > x) {
+                                s_seg[q * kKmBlock + threadIdx.x] = s_seg[(q - 1) * kKmBlock + threadIdx.x];
+                                --q;
+                            }
+                            s_seg[q * kKmBlock + threadIdx.x] = x;
+                            ++m;
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < kMaxSortAggs; ++a) {
+                        if (a >= p.n_sagg || p.sagg_scol[a] != sc) continue;
+                        const int ka = p.sagg_agg[a];
+                        order_stat(p.agg_fn[ka], fv, p.agg_p[ka], n,
+                                   [&](int64_t r) { return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r); },
+                                   &sres[a], &stag[a]);
+                        agg_err |= stag[a] == kTagErr;
+                    }
+                }
+            }
+            const SortRes sr{sres, stag, 0, 1};
+            if (agg_err) {   // "run Select error" replaces each of these windows' output
+                if (WRITE) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_AGG_ERROR);
+            } else {
+                const int hv = km_having(p, part, SORT ? &sr : nullptr);
+                if (WRITE && hv < 0) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
+                if (hv > 0) {
+                    if constexpr (!WRITE) {
+                        for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
+                    } else {
+                        int64_t ov[EK_MAX_AGGS];
+                        uint8_t ot[EK_MAX_AGGS];
+#pragma unroll
+                        for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                            ov[q] = 0;
+                            ot[q] = EK_TAG_NULL;
+                            if (q >= p.n_aggs) continue;
+                            const Val av = agg_value(p, part, q, SORT ? &sr : nullptr);
+                            ot[q] = av.tag == V_NULL ? EK_TAG_NULL : (av.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+                            ov[q] = av.tag == V_F64 ? __double_as_longlong(av.f) : av.i;
+                        }
+                        for (int kk = k; kk < kend; ++kk) {
+                            const int64_t pos = d.obase[kk] + (int64_t)d.bcnt[(int64_t)kk * d.nblk + blockIdx.x] + atomicAdd(&s_h[kk], 1u);
+                            res.key[pos] = (uint32_t)g;
+#pragma unroll
+                            for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                                if (q >= p.n_aggs) break;
+                                res.tag[q][pos] = ot[q];
+                                res.val[q][pos] = ov[q];
+                            }
+                        }
+                    }
+                }
+            }
+            k = kend;
+        }
+    }
+    if constexpr (!WRITE) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < nw; k += kKmBlock) d.bcnt[(int64_t)k * d.nblk + blockIdx.x] = s_h[k];
+    }
+}
+
+// one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count
+__global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
+    const int k = blockIdx.x;
+    uint32_t* c = d.bcnt + (int64_t)k * d.nblk;
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int base = 0; base < d.nblk; base += 1024) {
+        const int i = base + threadIdx.x;
+        const uint32_t x0 = i < d.nblk ? c[i] : 0u;
+        uint32_t x = x0;
+        for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        uint32_t wb = 0;
+        for (int w = 0; w < wv; ++w) wb += s_w[w];
+        const uint32_t carry = s_carry;
+        if (i < d.nblk) c[i] = carry + wb + x - x0;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = carry + wb + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && s_carry) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
+}
+
+}  // namespace ek

@@ -13,3 +13,10 @@ int ekl_sort_pairs_u64(void* tmp, size_t* tmp_bytes, const uint64_t* kin, uint64
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s);
     return e == hipSuccess ? 0 : -1;
 }
+
+int ekl_sort_pairs_u32(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                       uint32_t* vout, int64_t n, int end_bit, hipStream_t s) {
+    // stable: each key's rows keep their buffer order
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}

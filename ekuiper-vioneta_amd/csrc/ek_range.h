@@ -393,110 +393,143 @@ __global__ void k_arrivals_of(const int64_t* __restrict__ bidx, int64_t nb, int6
 // For a window of at most kSmallWin rows (COUNTWINDOW(1000), state windows, short sliding windows) the pane/bucket
 // partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here one
 // workgroup owns the whole window: it loads the window's rows [a, b) of the event buffer, applies WHERE (an error
-// replaces the window's output, filter_operator.go:63-77), sorts (key, row) in LDS (bitonic), and the first thread of
-// every key run aggregates that run in row order — the reference's per-group order (aggregate_operator.go:34-82) —
-// then HAVING and block-compacted emission. No staging, no dense key table.
+// replaces the window's output, filter_operator.go:63-77), groups the rows by key through an LDS hash table (linear
+// probing, 2n..4n slots) and a counting sort of the rows by slot, then the first thread of every group folds the
+// group's rows (aggregate_operator.go:34-82; exact two-pass M2), applies HAVING and emits (block-compacted).
+// A handful of barriers per window instead of the log^2 stages of a sorting network.
 constexpr int kSmallWin = 2048;
+__host__ __device__ inline int sw_slots(int n) { int h = 256; while (h < 2 * n) h <<= 1; return h; }
+inline size_t sw_lds_bytes(int max_n) { return (size_t)sw_slots(max_n) * 8 + (size_t)max_n * 6 + 16; }
+
+__device__ __forceinline__ uint32_t sw_hash(uint32_t k) {
+    k ^= k >> 16; k *= 0x7feb352du; k ^= k >> 15; k *= 0x846ca68bu; k ^= k >> 16;
+    return k;
+}
 
 template <int NVC>
 __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
                                                      const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
-                                                     const int64_t* __restrict__ obase, Results res) {
+                                                     const int64_t* __restrict__ obase, Results res, int max_n) {
+    constexpr int R = kSmallWin / kBlock;      // rows per thread
     const DPlan& p = *pp;
     const int w = wlist[blockIdx.x];
     const int64_t a = ab[2 * w];
     const int n = (int)(ab[2 * w + 1] - a);   // 1 <= n <= kSmallWin (host-checked)
     const int32_t widx = slots[w];
     const int64_t out = obase[w];
-    __shared__ uint64_t s_ent[kSmallWin];      // (key << 32 | row in window); UINT64_MAX = dropped / padding
-    __shared__ int s_err, s_m;
+    // dynamic LDS sized by the launch's largest window (sw_lds_bytes): slots = the power of two >= 2 max_n
+    extern __shared__ uint32_t s_dyn[];
+    const int Hmax = sw_slots(max_n);
+    uint32_t* s_key = s_dyn;                   // [Hmax] slot -> key (~0u: free)
+    uint32_t* s_off = s_key + Hmax;            // [Hmax] slot -> rows, then exclusive offset, then scatter cursor
+    uint32_t* s_grp = s_off + Hmax;            // [max_n] occupied slots: (first row in s_row) << 16 | rows
+    uint16_t* s_row = (uint16_t*)(s_grp + max_n);   // [max_n] window rows grouped by slot
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    __shared__ int s_err, s_ng;
     __shared__ uint32_t esh[20];
-    const int t = threadIdx.x;
-    if (t == 0) { s_err = 0; s_m = 0; }
-    int np = 64;
-    while (np < n) np <<= 1;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int H = 256;
+    while (H < 2 * n) H <<= 1;
+    for (int k = t; k < H; k += kBlock) { s_key[k] = ~0u; s_off[k] = 0; }
+    if (t == 0) { s_err = 0; s_ng = 0; }
     __syncthreads();
     const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
-    for (int k = t; k < np; k += kBlock) {
-        uint64_t e = ~0ull;
-        if (k < n) {
-            const int64_t i = a + k;
-            const int wd = p.n_where > 0 ? where_decide_slow(p, b, i) : 1;
-            if (wd < 0) s_err = 1;
-            if (wd > 0) e = ((uint64_t)(kcol ? kcol[i] : 0u) << 32) | (uint32_t)k;
+    int my[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int k = t + j * kBlock;
+        my[j] = -1;
+        if (k >= n) continue;
+        const int64_t i = a + k;
+        const int wd = p.n_where > 0 ? where_decide_slow(p, b, i) : 1;
+        if (wd < 0) s_err = 1;
+        if (wd <= 0) continue;
+        const uint32_t key = kcol ? kcol[i] : 0u;
+        uint32_t h = sw_hash(key) & (uint32_t)(H - 1);
+        while (true) {
+            const uint32_t old = atomicCAS(&s_key[h], ~0u, key);
+            if (old == ~0u || old == key) break;
+            h = (h + 1) & (uint32_t)(H - 1);
         }
-        s_ent[k] = e;
+        my[j] = (int)h;
+        atomicAdd(&s_off[h], 1u);
     }
     __syncthreads();
     if (s_err) {
         if (t == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
         return;
     }
-    for (int kk = 2; kk <= np; kk <<= 1) {
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < np; i += kBlock) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t x = s_ent[i], y = s_ent[ixj];
-                    if ((x > y) == ((i & kk) == 0)) { s_ent[i] = y; s_ent[ixj] = x; }
-                }
-            }
-            __syncthreads();
+    // exclusive scan of the slot counts (each thread H / kBlock consecutive slots); occupied slots -> group list
+    {
+        const int per = H / kBlock, s0 = t * per;
+        uint32_t sm = 0;
+        for (int k = s0; k < s0 + per; ++k) sm += s_off[k];
+        uint32_t x = sm;
+        for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+        if (lane == 63) s_wsum[wv] = x;
+        __syncthreads();
+        uint32_t run = x - sm;
+        for (int q = 0; q < wv; ++q) run += s_wsum[q];
+        for (int k = s0; k < s0 + per; ++k) {
+            const uint32_t c = s_off[k];
+            if (c) s_grp[atomicAdd(&s_ng, 1)] = (run << 16) | c;
+            s_off[k] = run;
+            run += c;
         }
     }
-    for (int i = t; i < np; i += kBlock)
-        if (s_ent[i] != ~0ull && (i + 1 == np || s_ent[i + 1] == ~0ull)) s_m = i + 1;
     __syncthreads();
-    const int m = s_m;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (my[j] >= 0) s_row[atomicAdd(&s_off[my[j]], 1u)] = (uint16_t)(t + j * kBlock);
+    __syncthreads();
+    const int ng = s_ng;
     int fl[NVC], col[NVC];
     bool isf[NVC];
 #pragma unroll
     for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; col[v] = v < p.n_vc ? p.vc_col[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
-    for (int base = 0; base < m; base += kBlock) {
-        const int i = base + t;
+    for (int base = 0; base < ng; base += kBlock) {
+        const int gi = base + t;
         Part<NVC> s{};
         bool present = false;
         uint32_t key = 0;
-        if (i < m) {
-            key = (uint32_t)(s_ent[i] >> 32);
-            if (i == 0 || (uint32_t)(s_ent[i - 1] >> 32) != key) {
-                int e = i + 1;
-                while (e < m && (uint32_t)(s_ent[e] >> 32) == key) ++e;
-                int64_t c = e - i, vc[NVC], is[NVC];
-                double fs[NVC], m2[NVC];
-                uint64_t mn[NVC], mx[NVC];
+        if (gi < ng) {
+            const uint32_t gw = s_grp[gi];
+            const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu), g1 = g0 + c;
+            key = kcol ? kcol[a + s_row[g0]] : 0u;
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
 #pragma unroll
-                for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
-                for (int u = i; u < e; ++u) {
-                    const int64_t r = a + (int64_t)(uint32_t)s_ent[u];
+            for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
+            for (int u = g0; u < g1; ++u) {
+                const int64_t r = a + s_row[u];
 #pragma unroll
-                    for (int v = 0; v < NVC; ++v) {
-                        if (!fl[v] || !col_valid(b, col[v], r)) continue;
-                        const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
-                        const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
-                        const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
-                        vc[v]++;
-                        is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
-                        fs[v] = __dadd_rn(fs[v], x);
-                        mn[v] = o < mn[v] ? o : mn[v];
-                        mx[v] = o > mx[v] ? o : mx[v];
-                    }
+                for (int v = 0; v < NVC; ++v) {
+                    if (!fl[v] || !col_valid(b, col[v], r)) continue;
+                    const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
+                    const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
+                    vc[v]++;
+                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+                    fs[v] = __dadd_rn(fs[v], x);
+                    mn[v] = o < mn[v] ? o : mn[v];
+                    mx[v] = o > mx[v] ? o : mx[v];
                 }
-#pragma unroll
-                for (int v = 0; v < NVC; ++v) {   // centred second pass (stats._variance shape)
-                    if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;
-                    const double mean = __ddiv_rn(fs[v], (double)vc[v]);
-                    for (int u = i; u < e; ++u) {
-                        const int64_t r = a + (int64_t)(uint32_t)s_ent[u];
-                        if (!col_valid(b, col[v], r)) continue;
-                        const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
-                        const double d = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
-                        m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
-                    }
-                }
-                part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-                present = having_keep(p, s, &res.win_err[widx]);
             }
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {   // centred second pass (stats._variance shape)
+                if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;
+                const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+                for (int u = g0; u < g1; ++u) {
+                    const int64_t r = a + s_row[u];
+                    if (!col_valid(b, col[v], r)) continue;
+                    const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
+                    const double d = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                    m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
+                }
+            }
+            part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+            present = having_keep(p, s, &res.win_err[widx]);
         }
         emit_rows(p, present, s, (int64_t)key, out, widx, res, esh);
     }

@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 4
+EKGPU_ABI_VERSION = 5
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -130,6 +130,7 @@ class ek_stats(C.Structure):
         ("phase_launches", C.c_int64 * 4),
         ("records_filter_error", C.c_int64),
         ("records_discarded", C.c_int64),
+        ("windows_keymajor", C.c_int64),
     ]
 
 

@@ -1,0 +1,169 @@
+"""Host dictionaries of GROUP BY keys: multi-dimension and string GROUP BY on top of the engine's dense u32 key.
+
+The reference groups a window's rows by a STRING key built from every dimension
+(internal/topo/operator/aggregate_operator.go:49-56):
+
+    for _, d := range dimensions { name += fmt.Sprintf("%v,", ve.Eval(d.Expr)) }
+
+so two rows share a group iff their concatenations are equal — including the quirk that dimensions whose values
+contain commas can collide ("a,b" + "c" and "a" + "b,c" both give "a,b,c,"), and that nil prints as "<nil>".
+`GroupKeyDict` assigns each distinct key string a dense id in first-seen order (the engine's u32 key column) and
+keeps the first row's dimension values per id, which is what a SELECT of a dimension shows
+(internal/xsql/row.go:720-726: non-aggregate fields come from the group's first row). Without a string dimension
+the %v strings are injective on the values (numbers never print a comma), so the dictionary keys on the value
+tuples directly (vectorised) instead of formatting strings.
+
+`StringDict` gives a string column dense u32 codes so it can travel to the device as a key-typed column.
+"""
+import math
+from decimal import Decimal
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+
+def go_v_float(x: float) -> str:
+    """fmt.Sprintf("%v", float64): strconv.FormatFloat(x, 'g', -1, 64) — shortest digits; exponent form when the
+    decimal exponent is < -4 or >= 6 (strconv/ftoa.go: shortest %g uses eprec 6), at least two exponent digits."""
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "+Inf" if x > 0 else "-Inf"
+    if x == 0:
+        return "-0" if math.copysign(1.0, x) < 0 else "0"
+    t = Decimal(repr(abs(x))).normalize().as_tuple()   # shortest round-trip digits, as strconv's shortest
+    digits = "".join(map(str, t.digits))
+    nd = len(digits)
+    dp = nd + t.exponent                  # decimal point position after the first dp digits
+    exp = dp - 1
+    sign = "-" if x < 0 else ""
+    if exp < -4 or exp >= 6:
+        m = digits[0] + ("." + digits[1:] if nd > 1 else "")
+        es = "-" if exp < 0 else "+"
+        return f"{sign}{m}e{es}{abs(exp):02d}"
+    if dp <= 0:
+        return f"{sign}0.{'0' * (-dp)}{digits}"
+    if dp >= nd:
+        return f"{sign}{digits}{'0' * (dp - nd)}"
+    return f"{sign}{digits[:dp]}.{digits[dp:]}"
+
+
+def go_v(v) -> str:
+    """fmt.Sprintf("%v", v) of a decoded column value (nil, bool, int64, float64 or string)."""
+    if v is None:
+        return "<nil>"
+    if isinstance(v, (bool, np.bool_)):
+        return "true" if v else "false"
+    if isinstance(v, (int, np.integer)):
+        return str(int(v))
+    if isinstance(v, (float, np.floating)):
+        return go_v_float(float(v))
+    return str(v)
+
+
+def group_key_string(values: Sequence) -> str:
+    """aggregate_operator.go:49-56: the key of one row."""
+    return "".join(go_v(v) + "," for v in values)
+
+
+class StringDict:
+    """Dense u32 codes of a string column (first-seen order)."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+        self.values: List[str] = []
+
+    def encode(self, col) -> np.ndarray:
+        out = np.empty(len(col), np.uint32)
+        ids = self.ids
+        for i, s in enumerate(col):
+            c = ids.get(s)
+            if c is None:
+                c = ids[s] = len(self.values)
+                self.values.append(s)
+            out[i] = c
+        return out
+
+
+def _canon_bits(col: np.ndarray) -> np.ndarray:
+    """Value identity of a numeric column as int64: floats by bit pattern (so -0 and 0 stay apart, as "%v" prints
+    them apart) with every NaN folded into one pattern ("NaN")."""
+    if col.dtype.kind == "f":
+        c = np.array(col, np.float64)
+        b = c.view(np.int64).copy()
+        b[np.isnan(c)] = 0x7FF8000000000000
+        return b
+    return np.asarray(col).astype(np.int64)
+
+
+class GroupKeyDict:
+    """Dense ids of GROUP BY keys over `dims` (names, in GROUP BY order) with their schema types
+    ("bigint" | "float" | "key" | "string"). `capacity` bounds the ids (the plan's num_keys)."""
+
+    def __init__(self, dims: Sequence[str], types: Sequence[str], capacity: int):
+        self.dims = list(dims)
+        self.types = list(types)
+        self.capacity = int(capacity)
+        self.by_string = any(t == "string" for t in self.types)
+        self.ids: Dict[object, int] = {}
+        self.first: List[tuple] = []      # id -> first row's dimension values
+
+    def __len__(self):
+        return len(self.first)
+
+    def _new(self, k, vals) -> int:
+        i = len(self.first)
+        if i >= self.capacity:
+            raise OverflowError(f"GROUP BY dictionary full ({self.capacity} keys): raise num_keys")
+        self.ids[k] = i
+        self.first.append(tuple(vals))
+        return i
+
+    def encode(self, cols: Sequence, valids: Optional[Sequence] = None) -> np.ndarray:
+        """cols: one array per dimension (numbers, or python strings for string dims); valids: optional u8 masks
+        (0 = nil). Returns the u32 key column."""
+        n = len(cols[0]) if cols else 0
+        valids = list(valids) if valids is not None else [None] * len(cols)
+        vals = []
+        for c, v, t in zip(cols, valids, self.types):
+            if t == "string":
+                a = np.asarray(c, dtype=object)
+            elif t == "float":
+                a = np.asarray(c, np.float64)
+            else:
+                a = np.asarray(c).astype(np.int64)
+            vals.append((a, None if v is None else np.asarray(v, np.uint8)))
+        out = np.empty(n, np.uint32)
+        if self.by_string:
+            for i in range(n):
+                row = tuple(None if (m is not None and not m[i]) else (a[i].item() if hasattr(a[i], "item") else a[i])
+                            for a, m in vals)
+                k = group_key_string(row)
+                j = self.ids.get(k)
+                out[i] = self._new(k, row) if j is None else j
+            return out
+        # numeric dimensions: key on the value tuples (nil -> its own value)
+        fields = []
+        for a, m in vals:
+            b = _canon_bits(a)
+            nil = np.zeros(n, np.int64) if m is None else (m == 0).astype(np.int64)
+            if m is not None:
+                b = np.where(m == 0, 0, b)
+            fields += [nil, b]
+        rec = np.rec.fromarrays(fields) if fields else np.zeros(n)
+        uniq, first_idx, inv = np.unique(rec, return_index=True, return_inverse=True)
+        order = np.argsort(first_idx, kind="stable")          # first-seen order inside the batch
+        uid = np.empty(len(uniq), np.uint32)
+        for u in order:
+            key = tuple(int(x) for x in uniq[u])
+            j = self.ids.get(key)
+            if j is None:
+                i0 = first_idx[u]
+                row = tuple(None if (m is not None and not m[i0]) else a[i0].item() for a, m in vals)
+                j = self._new(key, row)
+            uid[u] = j
+        out[:] = uid[inv.reshape(-1)]
+        return out
+
+    def decode(self, ids) -> List[tuple]:
+        return [self.first[int(i)] for i in ids]

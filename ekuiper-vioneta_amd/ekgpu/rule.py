@@ -13,13 +13,18 @@ Supported subset (everything the BASELINE configs and the reference's window tes
            [OVER (WHEN <expr>)]
   [HAVING <expr>]
 Expressions: comparisons, AND/OR, + - * / %, numeric literals, column refs, aggregate calls (HAVING).
-The GROUP BY dimension must be a dictionary-encoded key column (type "key" in the schema).
+GROUP BY dimensions: one dictionary-encoded key column (type "key") goes to the engine as is; any other set of
+dimensions (several columns, bigint / float / string columns) is grouped through a host dictionary of the
+reference's %v-concatenated key (ekgpu/keys.py, aggregate_operator.go:49-56) that fills a synthetic key column
+`__group_key` (CompiledRule.device_columns / decode_keys). String columns travel as dense u32 codes and may only be
+GROUP BY dimensions.
 """
 import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 from . import abi as A
+from .keys import GroupKeyDict, StringDict
 
 _TOKEN = re.compile(r"\s*(?:(\d+\.\d*|\.\d+|\d+(?:[eE][-+]?\d+)?)|([A-Za-z_][A-Za-z0-9_.]*)|(<=|>=|!=|<>|[=<>(),*+\-/%])|(\"[^\"]*\"|'[^']*'))")
 
@@ -35,7 +40,8 @@ _CMP = {"=": A.EK_OP_EQ, "!=": A.EK_OP_NEQ, "<>": A.EK_OP_NEQ, "<": A.EK_OP_LT, 
         ">": A.EK_OP_GT, ">=": A.EK_OP_GTE}
 _ADD = {"+": A.EK_OP_ADD, "-": A.EK_OP_SUB}
 _MUL = {"*": A.EK_OP_MUL, "/": A.EK_OP_DIV, "%": A.EK_OP_MOD}
-COLTYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32}
+COLTYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32, "string": A.EK_COL_U32}
+GROUP_KEY = "__group_key"
 
 
 class RuleError(ValueError):
@@ -57,8 +63,37 @@ class CompiledRule:
     sql: str
     options: Dict = field(default_factory=dict)
 
+    group_dims: List[str] = field(default_factory=list)       # composite GROUP BY dimensions (host dictionary)
+    key_dict: Optional[GroupKeyDict] = None
+    string_dicts: Dict[str, StringDict] = field(default_factory=dict)
+    schema: Dict[str, str] = field(default_factory=dict)
+
     def column_index(self, name: str) -> int:
         return self.columns.index(name)
+
+    def device_columns(self, cols, validity=None):
+        """Columns in the caller's schema order (string columns as python strings) -> the plan's columns: string
+        columns as their dictionary codes, plus `__group_key` from the GROUP BY dimensions when composite.
+        Returns (cols, validity)."""
+        user = [c for c in self.columns if c != GROUP_KEY]
+        if len(cols) != len(user):
+            raise ValueError(f"expected {len(user)} columns ({user}), got {len(cols)}")
+        validity = list(validity) if validity is not None else [None] * len(cols)
+        out = []
+        for name, c in zip(user, cols):
+            out.append(self.string_dicts[name].encode(c) if name in self.string_dicts else c)
+        vout = list(validity)
+        if self.key_dict is not None:
+            idx = [user.index(d) for d in self.group_dims]
+            out.append(self.key_dict.encode([cols[i] for i in idx], [validity[i] for i in idx]))
+            vout.append(None)
+        return out, (vout if any(v is not None for v in vout) else None)
+
+    def decode_keys(self, keys) -> list:
+        """Result key ids -> the GROUP BY dimension values (the group's first row), as tuples."""
+        if self.key_dict is not None:
+            return self.key_dict.decode(keys)
+        return [(int(k),) for k in keys]
 
 
 def _tokenize(sql: str) -> List[str]:
@@ -262,7 +297,29 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                  timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
                  debug_membership: bool = False, nullable=(), incremental: bool = False,
                  window_version: str = "") -> CompiledRule:
-    """schema: ordered {column: "bigint" | "float" | "key"}; the TIMESTAMP column must be bigint (epoch ms)."""
+    """schema: ordered {column: "bigint" | "float" | "key" | "string"}; the TIMESTAMP column must be bigint (epoch
+    ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring)."""
+    kw = dict(is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms, timestamp=timestamp,
+              num_keys=num_keys, tz_offset_s=tz_offset_s, debug_membership=debug_membership, nullable=nullable,
+              incremental=incremental, window_version=window_version)
+    try:
+        return _compile(sql, dict(schema), **kw)
+    except _Composite as c:
+        if GROUP_KEY in schema:
+            raise RuleError(f"column name {GROUP_KEY} is reserved")
+        rule = _compile(sql, dict(schema, **{GROUP_KEY: "key"}), group_dims=c.dims, **kw)
+        rule.key_dict = GroupKeyDict(c.dims, [schema[d] for d in c.dims], num_keys)
+        return rule
+
+
+class _Composite(Exception):
+    def __init__(self, dims):
+        self.dims = dims
+
+
+def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tolerance_ms: int,
+             timestamp: Optional[str], num_keys: int, tz_offset_s: int, debug_membership: bool, nullable,
+             incremental: bool, window_version: str, group_dims: Optional[List[str]] = None) -> CompiledRule:
     if len(schema) > A.EK_MAX_COLUMNS:
         raise RuleError("too many columns")
     p = _Parser(sql, schema)
@@ -329,6 +386,7 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     if p.kw("where"):
         where = p.expr(False)
     key_col = -1
+    dims: List[str] = []
     trigger = []
     begin, emit = [], []
     wtype = A.EK_WINDOW_NONE
@@ -380,17 +438,18 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                     trigger = p.expr(False)
                     p.expect(")")
             else:
-                c = p.col(t)
-                if schema[p.columns[c]] != "key":
-                    raise RuleError("GROUP BY dimension must be a dictionary-encoded key column")
-                if key_col >= 0:
-                    raise RuleError("only one GROUP BY dimension is supported")
-                key_col = c
+                dims.append(p.columns[p.col(t)])
                 p.i += 1
             if p.peek() == ",":
                 p.i += 1
                 continue
             break
+    if group_dims is not None:
+        key_col = p.columns.index(GROUP_KEY)
+    elif len(dims) == 1 and schema[dims[0]] == "key":
+        key_col = p.columns.index(dims[0])
+    elif dims:
+        raise _Composite(dims)
     having = []
     if p.kw("having"):
         having = p.expr(True)
@@ -412,11 +471,22 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                             options=dict(isEventTime=False, lateTolerance=0))
     for f in raw_select:
         if f.kind == "column":
+            cname = p.columns[f.slot]
+            if group_dims is not None and cname in group_dims:
+                fields.append(OutputField(f.name, "dim", group_dims.index(cname)))
+                continue
             if f.slot != key_col:
-                raise RuleError(f"non-aggregate field {f.name} must be the GROUP BY key")
+                raise RuleError(f"non-aggregate field {f.name} must be a GROUP BY dimension")
             fields.append(OutputField(f.name, "key"))
         else:
             fields.append(f)
+    strings = {c for c, t in schema.items() if t == "string"}
+    if strings:
+        used = {p.columns[c] for (_, c, _) in p.aggs if c >= 0 and c < len(p.columns)}
+        for prog in [where, having, trigger, begin, emit] + [list(pr) for pr, _ in p.derived]:
+            used |= {p.columns[ins[1]] for ins in prog if ins[0] == A.EK_OP_COL and ins[1] < len(p.columns)}
+        if used & strings:
+            raise RuleError(f"string column(s) {sorted(used & strings)} may only be GROUP BY dimensions")
     plan.n_aggs = len(p.aggs)
     for k, (fn, c, prm) in enumerate(p.aggs):
         plan.aggs[k].fn = fn
@@ -434,6 +504,8 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     if key_col >= 0 and num_keys <= 0:
         raise RuleError("num_keys (dictionary size of the GROUP BY key) is required")
     return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
+                        group_dims=list(group_dims or []), schema=dict(schema),
+                        string_dicts={c: StringDict() for c in strings},
                         options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms,
                                      planOptimizeStrategy=dict(enableIncrementalWindow=bool(incremental),
                                                                windowOption=dict(windowVersion=window_version))))

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 4
+#define EKGPU_ABI_VERSION 5
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -214,6 +214,8 @@ typedef struct {
     int64_t records_filter_error; /* window-less rules: events whose WHERE evaluation errored      */
     int64_t records_discarded;    /* hopping windows: inputs dropped when a triggered window is empty
                                    * (handleInputs returns inputs[:0], window_op.go:605-655)          */
+    int64_t windows_keymajor;     /* range windows aggregated key-major (sorted once by key, one thread
+                                   * per key walks the windows)                        */
 } ek_stats;
 
 enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };

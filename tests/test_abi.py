@@ -49,6 +49,7 @@ def test_plan_struct_layout():
 size_t off_aggs(void){return offsetof(ek_plan,aggs);} size_t off_having(void){return offsetof(ek_plan,having_prog);}
 size_t size_plan(void){return sizeof(ek_plan);} size_t size_result(void){return sizeof(ek_result);}
 size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){return sizeof(ek_batch);}
+size_t size_stats(void){return sizeof(ek_stats);} size_t off_kmaj(void){return offsetof(ek_stats,windows_keymajor);}
 '''
     d = tempfile.mkdtemp()
     with open(os.path.join(d, "p.c"), "w") as f:
@@ -56,7 +57,7 @@ size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){r
     so = os.path.join(d, "p.so")
     subprocess.check_call(["gcc", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(d, "p.c")])
     P = C.CDLL(so)
-    for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch"):
+    for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch", "size_stats", "off_kmaj"):
         getattr(P, fn).restype = C.c_size_t
     assert P.off_aggs() == A.ek_plan.aggs.offset
     assert P.off_having() == A.ek_plan.having_prog.offset
@@ -64,6 +65,8 @@ size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){r
     assert P.size_result() == C.sizeof(A.ek_result)
     assert P.off_rkey() == A.ek_result.key.offset
     assert P.size_batch() == C.sizeof(A.ek_batch)
+    assert P.size_stats() == C.sizeof(A.ek_stats)
+    assert P.off_kmaj() == A.ek_stats.windows_keymajor.offset
 
 
 def test_compile_baseline_configs():

@@ -1,0 +1,149 @@
+"""GPU parity of the key-major range path (ek_keymajor.h): the fired windows' span sorted once by key, one thread per
+key walking the windows. EKGPU_KEYMAJOR=1 takes it whenever the windows are eligible (the default cost rule takes it
+only for big key spaces), so the range-mode cases of test_range_gpu.py run through it here against the oracle; the
+cases it must decline (WHERE errors in the span, order statistics over long per-key runs) fall back to the
+window-major path and stay green."""
+import os
+
+import numpy as np
+import pytest
+
+import test_range_gpu as R
+from ekgpu.rule import compile_rule
+from ekgpu.synth import IOT_SCHEMA, iot_stream
+from parity import assert_windows_equal
+from test_engine_gpu import engine_mod, run_both  # noqa: F401  (fixture + helper)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def keymajor_forced():
+    os.environ["EKGPU_KEYMAJOR"] = "1"
+    yield
+    del os.environ["EKGPU_KEYMAJOR"]
+
+
+def _force_range():
+    os.environ["EKGPU_FORCE_RANGE"] = "1"
+
+
+def _unforce_range():
+    os.environ.pop("EKGPU_FORCE_RANGE", None)
+
+
+@pytest.mark.parametrize("batches", [1, 5])
+def test_km_sliding_over_when_c4a_shape(oracle, engine_mod, batches):
+    sql = ("SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, R.TRIG_SCHEMA, num_keys=3000, debug_membership=True)
+    cols = R._with_trig(R._iot(200_000, 3000, seed=61, epm=10), 500)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert len(got) > 100
+    assert st.windows_keymajor > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_sliding_every_event(oracle, engine_mod):
+    R.test_sliding_every_event(oracle, engine_mod)
+
+
+def test_km_sliding_late_tolerance_out_of_order(oracle, engine_mod):
+    R.test_sliding_late_tolerance_out_of_order(oracle, engine_mod)
+
+
+def test_km_sliding_with_delay(oracle, engine_mod):
+    R.test_sliding_with_delay(oracle, engine_mod)
+
+
+@pytest.mark.parametrize("n,m", [(1000, 0), (500, 200), (300, 700)])
+def test_km_count_window(oracle, engine_mod, n, m):
+    os.environ["EKGPU_SMALL_WIN"] = "0"   # the 1000-row windows would otherwise take k_small_win
+    try:
+        R.test_count_window(oracle, engine_mod, n, m)
+    finally:
+        del os.environ["EKGPU_SMALL_WIN"]
+
+
+def test_km_session_window(oracle, engine_mod):
+    R.test_session_window(oracle, engine_mod)
+
+
+def test_km_tumbling_hopping_range(oracle, engine_mod):
+    _force_range()
+    try:
+        R.test_tumbling_hopping_through_range_mode(oracle, engine_mod, None)
+        R.test_range_out_of_order_tumbling(oracle, engine_mod, None)
+    finally:
+        _unforce_range()
+
+
+@pytest.mark.parametrize("keys", [4000, 100, 3])
+def test_km_median_percentile(oracle, engine_mod, keys):
+    """4000 keys: short per-key runs, sorted in the thread's LDS lane; 100 keys: ~50 values per (key, window), ranked
+    by counting in memory; 3 keys: runs longer than kKmSelMax, so the count pass flags them and the window-major
+    path takes over."""
+    rule = compile_rule(R.MED_SQL, IOT_SCHEMA, num_keys=keys, debug_membership=True)
+    cols = R._iot(300_000, keys, seed=71, epm=5)
+    if keys > 3:   # 1 s windows
+        rule = compile_rule(R.MED_SQL.replace("TUMBLINGWINDOW(ss, 10)", "TUMBLINGWINDOW(ss, 1)"), IOT_SCHEMA,
+                            num_keys=keys, debug_membership=True)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=2)
+    assert len(got) >= 4
+    assert (st.windows_keymajor > 0) == (keys > 3)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_median_int_nulls(oracle, engine_mod):
+    R.test_median_percentile_int_columns_nulls(oracle, engine_mod)
+
+
+def test_km_percentile_window_error(oracle, engine_mod):
+    R.test_percentile_out_of_range_is_window_error(oracle, engine_mod)
+
+
+def test_km_c5_shape(oracle, engine_mod):
+    R.test_c5_shape_high_cardinality_median(oracle, engine_mod)
+
+
+def test_km_sliding_median(oracle, engine_mod):
+    R.test_sliding_median(oracle, engine_mod)
+
+
+def test_km_where_having_errors(oracle, engine_mod):
+    """A WHERE that errors on some rows (int / 0) makes its span ineligible (window-major fallback attributes the error
+    per window); HAVING errors (int / 0 on aggregates) are raised by the key-major write pass. Some windows of each
+    stream error, the others keep their rows."""
+    schema = {"k": "key", "ts": "bigint", "a": "bigint", "b": "bigint", "trig": "bigint"}
+    n = 30_000
+    rng = np.random.default_rng(12)
+    ts = (1541152480000 + np.arange(n) // 3).astype(np.int64)
+    a = rng.integers(-20, 20, n).astype(np.int64)
+    b = rng.integers(0, 5000, n).astype(np.int64)
+    trig = (rng.integers(0, 300, n) == 0).astype(np.int64)
+    for sql, keys in (
+            ("SELECT k, count(*), sum(a) FROM s WHERE a / b >= 0 GROUP BY k, SLIDINGWINDOW(ms, 800) OVER (WHEN trig = 1)", 40),
+            ("SELECT k, count(*), sum(a) FROM s WHERE a > 0 GROUP BY k, SLIDINGWINDOW(ms, 800) OVER (WHEN trig = 1) "
+             "HAVING sum(a) / (count(*) - 300) > 1", 4)):
+        k = np.random.default_rng(13).integers(0, keys, n).astype(np.uint32)
+        rule = compile_rule(sql, schema, num_keys=keys, debug_membership=True)
+        got, exp, _ = run_both(oracle, engine_mod, rule, [k, ts, a, b, trig], batches=3)
+        st = [w.status for w in exp.windows]
+        assert len(got) > 10 and 0 < sum(s != 0 for s in st) < len(st)
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_auto_rule_picks_big_key_spaces(oracle, engine_mod):
+    """Default cost rule (EKGPU_KEYMAJOR unset): a heavily overlapping sliding window over 100 k keys goes key-major."""
+    del os.environ["EKGPU_KEYMAJOR"]
+    try:
+        sql = ("SELECT deviceId, stddev(temperature), var(temperature) FROM demo "
+               "GROUP BY deviceId, SLIDINGWINDOW(ss, 5) OVER (WHEN trig = 1) HAVING count(*) > 1")
+        rule = compile_rule(sql, R.TRIG_SCHEMA, num_keys=100_000)
+        key, ts, temp, hum = iot_stream(1_000_000, 100_000, seed=81, events_per_ms=20)
+        cols = R._with_trig([key, ts, temp, hum], 2000)
+        got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=2)
+        assert len(got) > 100 and st.windows_keymajor > 0
+        assert_windows_equal(rule.plan, got, exp.windows)
+    finally:
+        os.environ["EKGPU_KEYMAJOR"] = "1"
