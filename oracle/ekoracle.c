@@ -395,6 +395,7 @@ typedef struct {
 /* Evaluate WHERE -> GROUP BY -> aggregates -> HAVING over one emitted window
  * (filter_operator.go:36-90, aggregate_operator.go:34-82, having_operator.go:32-104,
  *  project_operator.go:79-207 for the aggregate fields). */
+#define EKO_MEMBER_CAP ((int64_t)1 << 24)
 static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc) {
     const ek_plan* p = d->p;
     int64_t w = ob->ws.n;
@@ -403,9 +404,12 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
     v_push(&ob->roff, ob->key.n);
     v_push(&ob->moff, ob->mem.n);
     uint64_t h = 0;
+    /* the member lists themselves are kept only while they stay small (KAT-sized runs inspect them); full-size
+     * runs compare membership through (count, Σ mix64(arrival)) and would otherwise hold GBs of lists */
+    const int keep = ob->mem.n + nc <= EKO_MEMBER_CAP;
     for (int64_t k = 0; k < nc; ++k) {
         const int64_t a = row_arrival(d, content[k]);
-        v_push(&ob->mem, a);
+        if (keep) v_push(&ob->mem, a);
         h += ek_mix64((uint64_t)a);
     }
     v_push(&ob->mcnt, nc);
@@ -774,6 +778,7 @@ typedef struct {
     int64_t L, I, D;           /* ms */
     int32_t raw_interval, unit, tz;
     vec64 inputs;              /* event indices, release order */
+    int unsorted;              /* an input was released out of ts order (never in event time; kept as a guard) */
     int has_trigger; int64_t trigger_time;
     int64_t next_end, prev_end; /* prev_end ZERO_MS = IsZero */
     vec64 trigger_ts, delay_ts;
@@ -852,6 +857,17 @@ static void scan(winop* o, int64_t t, int64_t length, int is_first_part) {
 /* event_window_trigger.go:211-219 */
 static int64_t earliest(const winop* o, int64_t start, int64_t end) {
     int64_t m = MAXT_MS;
+    if (!o->unsorted) {
+        /* inputs hold released events in release order, i.e. non-decreasing ts: the minimum of the ts in
+         * (start, end] is the first ts > start (same result as the scan below, without its O(n) per watermark) */
+        int64_t lo = 0, hi = o->inputs.n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (ev_ts(o, o->inputs.a[mid]) > start) hi = mid; else lo = mid + 1;
+        }
+        if (lo < o->inputs.n && ev_ts(o, o->inputs.a[lo]) <= end) m = ev_ts(o, o->inputs.a[lo]);
+        return m;
+    }
     for (int64_t i = 0; i < o->inputs.n; ++i) {
         int64_t t = ev_ts(o, o->inputs.a[i]);
         if (t > start && t <= end && t < m) m = t;
@@ -916,6 +932,7 @@ static int match_trigger(const winop* o, int64_t e) {
 static void win_on_event(winop* o, int64_t e) {
     if (!o->has_trigger) { o->has_trigger = 1; o->trigger_time = o->shard ? o->origin_ts : ev_ts(o, e); }
     if (o->wtype == EK_WINDOW_SLIDING && !o->shard && match_trigger(o, e)) v_push(&o->trigger_ts, ev_ts(o, e));
+    if (o->inputs.n > 0 && ev_ts(o, e) < ev_ts(o, o->inputs.a[o->inputs.n - 1])) o->unsorted = 1;
     v_push(&o->inputs, e);
 }
 
