@@ -592,6 +592,8 @@ struct Engine {
         chunk = env_int("EKGPU_CHUNK", 8192);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
+        ung_mode = env_int("EKGPU_UNG", 1);
+        km_one = env_int("EKGPU_KM_ONE", 1);
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
@@ -1158,6 +1160,7 @@ struct Engine {
     // k_part (MODE 0 unsorted / 1 sorted / 2 virtual panes) + k_agg for one group
     int launch_part_agg(const DBatch& db, GroupDesc gd, int mode, const uint8_t* d_acc, int32_t* perr,
                         int64_t* pmc, unsigned long long* pmh, int lp_stride, bool any_fresh) {
+        if (dp.pseudo_keys && mode == 1 && dp.n_sagg == 0 && ung_mode) return launch_ung(db, gd, d_acc, perr, pmc, pmh, any_fresh);
         const int64_t rs = gd.chunk;                                // staging region per chunk
         int64_t ne = (int64_t)gd.nch * rs + 64;
         if (ne > st_cap) {
@@ -1229,6 +1232,32 @@ struct Engine {
             }
             phase_end(ph);
         }
+        if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
+        return 0;
+    }
+
+    // Un-grouped rule over a ts-sorted group (k_ung_tile): one pass over the referenced columns, a partial per
+    // (tile, pane segment) merged into pseudo-key slot tile mod kPseudoKeys (EKGPU_UNG=0: the k_part + k_agg path).
+    int ung_mode = 1;
+    int launch_ung(const DBatch& db, GroupDesc gd, const uint8_t* d_acc, int32_t* perr, int64_t* pmc,
+                   unsigned long long* pmh, bool any_fresh) {
+        if (any_fresh) {
+            hipLaunchKernelGGL(k_group_prep, dim3((gd.n_panes + 255) / 256), dim3(256), 0, stream, gd, perr, pmc, pmh);
+            hipLaunchKernelGGL(k_ung_zero, dim3(64, gd.n_panes), dim3(256), 0, stream, gd, dstate);
+        }
+        const int64_t rows = gd.hi - gd.lo;
+        int64_t tile = 8192;
+        while ((rows + tile - 1) / tile > (int64_t)kPseudoKeys) tile <<= 1;
+        const int64_t nt = std::max<int64_t>(1, (rows + tile - 1) / tile);
+        const int nvc = std::max(1, dp.n_vc);
+        const bool wh = dp.n_where > 0;
+        const int ph = phase_begin(EK_PHASE_AGGREGATE);
+#define EK_UNG(N, W) hipLaunchKernelGGL((k_ung_tile<N, W>), dim3((unsigned)nt), dim3(kUngBlock), 0, stream, d_plan, db, gd, d_acc, dstate, tile, perr)
+#define EK_UNG_N(W) switch (nvc) { case 1: EK_UNG(1, W); break; case 2: EK_UNG(2, W); break; case 3: EK_UNG(3, W); break; default: EK_UNG(4, W); break; }
+        if (wh) { EK_UNG_N(true) } else { EK_UNG_N(false) }
+#undef EK_UNG_N
+#undef EK_UNG
+        phase_end(ph);
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
         return 0;
     }
@@ -1560,8 +1589,12 @@ struct Engine {
         hipLaunchKernelGGL(k_chunk_max, dim3(nch), dim3(kBlock), 0, stream, ts, n, (int64_t*)runcm_d.p);
         hipLaunchKernelGGL(k_scan_max, dim3(1), dim3(1024), 0, stream, (int64_t*)runcm_d.p, nch, seed);
         hipLaunchKernelGGL(k_runmax, dim3(nch), dim3(kBlock), 0, stream, ts, n, (const int64_t*)runcm_d.p, (int64_t*)runmax_d.p);
+        runmax_p = (const int64_t*)runmax_d.p;
         return 0;
     }
+    // the running max of the current batch (arrival order): runmax_d, or the batch's own ts column when the batch is
+    // ts-sorted and starts at or above the carried max (then runmax[i] == ts[i]: no kernels, no copy)
+    const int64_t* runmax_p = nullptr;
 
     // one scalar device -> host (synchronous)
     int64_t fetch_i64(const void* dptr) {
@@ -1701,7 +1734,7 @@ struct Engine {
         if (int rc = ensure(mrg_col, (size_t)nq * 16)) return rc;
         int64_t* d_ends = (int64_t*)mrg_col.p;
         hipMemcpyAsync(d_ends, ends.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(k_fire_prefix, dim3((nq + 255) / 256), dim3(256), 0, stream, (const int64_t*)runmax_d.p, cur_nb,
+        hipLaunchKernelGGL(k_fire_prefix, dim3((nq + 255) / 256), dim3(256), 0, stream, runmax_p, cur_nb,
                            cur_arr_base, plan.late_tolerance_ms, (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)eb.arr.p,
                            eb.n, d_ends, nq, d_ends + nq);
         hipMemcpyAsync(pre.data(), d_ends + nq, (size_t)nq * 8, hipMemcpyDeviceToHost, stream);
@@ -1752,6 +1785,12 @@ struct Engine {
         return 0;
     }
 
+    int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
+    template <int N>
+    void km_walk1(bool sort, size_t lds, int nblk, const KmDesc& d, const Results& rv) {
+        if (sort) hipLaunchKernelGGL((k_km_walk<N, true, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+        else hipLaunchKernelGGL((k_km_walk<N, false, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
+    }
     template <int N>
     void km_walk(bool sort, bool write, int nblk, size_t lds, const KmDesc& d, const Results& rv) {
         if (sort) {
@@ -1777,27 +1816,39 @@ struct Engine {
         if (km_mode == 2 && !(K >= 16384 && (sort ? rows_kw <= 16.0 : overlap >= 4.0))) return 0;
         int end_bit = 1;
         while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)K) end_bit++;
+        const DBatch bv = buffer_view();
+        // one window over the whole span: the walk needs no positions; with one value column (no validity) the
+        // column itself is sorted by key (no position payload, no gather)
+        const bool one = nw == 1 && km_one;
+        const bool vsort = one && dp.n_vc == 1 && !bv.valid[dp.vc_col[0]];
         size_t tb = 0;
-        ekl_sort_pairs_u32(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
+        if (vsort) ekl_sort_pairs_u32_i64(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
+        else ekl_sort_pairs_u32(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
         for (int i = 0; i < 2; ++i) {
             if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
-            if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
+            if (!vsort)
+                if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
         }
+        if (vsort)
+            if (int rc = ensure(km_val[0], (size_t)n * 8)) return rc;
         if (int rc = ensure(km_tmp, tb)) return rc;
         if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
         if (int rc = ensure(km_flag, 16)) return rc;
         if (!h_kmf && hipHostMalloc((void**)&h_kmf, 16) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
         unsigned int* d_flag = (unsigned int*)km_flag.p;
         hipMemsetAsync(d_flag, 0, 16, stream);
-        const DBatch bv = buffer_view();
         const int ph = phase_begin(EK_PHASE_PARTITION);
         hipLaunchKernelGGL(k_km_keys, dim3((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                           d_plan, bv, lo, n, (uint32_t*)km_k[0].p, (uint32_t*)km_p[0].p, d_flag);
-        if (ekl_sort_pairs_u32(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p, (const uint32_t*)km_p[0].p,
-                               (uint32_t*)km_p[1].p, n, end_bit, stream))
+                           d_plan, bv, lo, n, (uint32_t*)km_k[0].p, vsort ? (uint32_t*)nullptr : (uint32_t*)km_p[0].p, d_flag);
+        if (vsort) {
+            if (ekl_sort_pairs_u32_i64(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p,
+                                       (const int64_t*)bv.col[dp.vc_col[0]] + lo, (int64_t*)km_val[0].p, n, end_bit, stream))
+                return fail(EK_ERR_DEVICE, "key sort failed");
+        } else if (ekl_sort_pairs_u32(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p, (const uint32_t*)km_p[0].p,
+                                      (uint32_t*)km_p[1].p, n, end_bit, stream))
             return fail(EK_ERR_DEVICE, "key sort failed");
         const uint32_t* sk = (const uint32_t*)km_k[1].p;
-        const uint32_t* spos = (const uint32_t*)km_p[1].p;
+        const uint32_t* spos = vsort ? nullptr : (const uint32_t*)km_p[1].p;
         uint32_t* kstart = (uint32_t*)km_start.p;
         hipLaunchKernelGGL(k_km_starts, dim3((unsigned)std::min<int64_t>(8192, (n + 1 + 255) / 256)), dim3(256), 0, stream, sk, n,
                            K, kstart);
@@ -1808,6 +1859,7 @@ struct Engine {
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major sort failed");
         if (h_kmf[0] > 0) return 0;                                                       // WHERE errors
         if (km_mode == 2 && !sort && (double)h_kmf[1] * overlap > (double)(1 << 22)) return 0;   // one key dominates
+        if (one && sort && h_kmf[1] > (unsigned)kKmSelMax) return 0;   // single pass: no (key, window) run too long
         // value columns in key order
         KmCols cols{};
         for (int v = 0; v < dp.n_vc; ++v) {
@@ -1854,7 +1906,7 @@ struct Engine {
         const size_t lds = (size_t)((3 * nw + 1) & ~1) * 4 + (sort ? (size_t)kKmSegMax * kKmBlock * 8 : 0);
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
         const dim3 gg((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
-        switch (nvc) {
+        if (!vsort) switch (nvc) {
         case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
@@ -1868,6 +1920,19 @@ struct Engine {
             default: km_walk<4>(sort, write, nblk, lds, d, rv); break;
             }
         };
+        if (one) {
+            switch (nvc) {
+            case 1: km_walk1<1>(sort, lds, nblk, d, rv); break;
+            case 2: km_walk1<2>(sort, lds, nblk, d, rv); break;
+            case 3: km_walk1<3>(sort, lds, nblk, d, rv); break;
+            default: km_walk1<4>(sort, lds, nblk, d, rv); break;
+            }
+            phase_end(ph2);
+            if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "key-major launch failed");
+            stats.windows_keymajor += nw;
+            *handled = true;
+            return 0;
+        }
         walk(false);
         if (sort) {
             hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
@@ -2249,7 +2314,7 @@ struct Engine {
         const int gg = (int)std::min<int64_t>(4096, (nt + 255) / 256);
         hipLaunchKernelGGL(k_gather8, dim3(gg), dim3(256), 0, stream, d_pos, nt, INT64_MAX, (const int64_t*)eb.rel.p,
                            (const int64_t*)nullptr, (const int64_t*)nullptr, g_rel);
-        hipLaunchKernelGGL(k_step_wm, dim3(gg), dim3(256), 0, stream, (const int64_t*)g_rel, nt, (const int64_t*)runmax_d.p,
+        hipLaunchKernelGGL(k_step_wm, dim3(gg), dim3(256), 0, stream, (const int64_t*)g_rel, nt, runmax_p,
                            cur_nb, cur_arr_base, cur_prevmax, plan.late_tolerance_ms, g_rel + nt, g_rel + 2 * nt);
         w_step.resize(nt);
         w_prev.resize(nt);
@@ -2367,8 +2432,8 @@ struct Engine {
     int64_t cur_arr_base = 0, cur_nb = 0, cur_prevmax = INT64_MIN;
     int64_t relstep_w(int64_t r) {
         const int64_t j = r - cur_arr_base;
-        if (j < 0 || !runmax_d.p) return W;
-        return fetch_i64((const int64_t*)runmax_d.p + j) - plan.late_tolerance_ms;
+        if (j < 0 || !runmax_p) return W;
+        return fetch_i64(runmax_p + j) - plan.late_tolerance_ms;
     }
 
     // SESSIONWINDOW(unit, L, timeout): getNextSessionWindow (event_window_trigger.go:77-110) over the released
@@ -2386,7 +2451,7 @@ struct Engine {
                 if (int rc = ensure(mrg_col, (size_t)n_new * 16)) return rc;
                 int64_t* g = (int64_t*)mrg_col.p;
                 hipLaunchKernelGGL(k_step_wm, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
-                                   (const int64_t*)eb.rel.p + rel_prev, n_new, (const int64_t*)runmax_d.p, cur_nb, cur_arr_base,
+                                   (const int64_t*)eb.rel.p + rel_prev, n_new, runmax_p, cur_nb, cur_arr_base,
                                    cur_prevmax, plan.late_tolerance_ms, g, g + n_new);
                 if (h_rwp.size() != o) h_rwp.assign(o, INT64_MIN);   // rows mirrored before (e.g. restored): unknown
                 h_rwp.resize(o + n_new);
@@ -2457,14 +2522,15 @@ struct Engine {
 
     // Event-time push in range mode, after the shared late-drop / watermark steps.
     int push_range(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t n_acc, int64_t min_acc,
-                   int64_t max_ts, int64_t arrival_base, int64_t M_prev, bool had_M) {
+                   int64_t max_ts, int64_t arrival_base, int64_t M_prev, bool had_M, int64_t batch_min) {
         const int64_t n = db.n;
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
         cur_arr_base = arrival_base;
         cur_nb = n;
         cur_prevmax = had_M ? M_prev : INT64_MIN;
         // running max of the batch: release steps (sliding) and the step at which W was reached
-        if (int rc = batch_runmax(ts, n, had_M ? M_prev : INT64_MIN)) return rc;
+        if (sorted && (!had_M || batch_min >= M_prev)) runmax_p = ts;
+        else if (int rc = batch_runmax(ts, n, had_M ? M_prev : INT64_MIN)) return rc;
         if (n_acc > 0) {
             if (sorted && !d_acc && (eb.n == 0 || !had_M || min_acc >= M_prev)) {
                 if (int rc = eb_append(db, start, n_acc, arrival_base)) return rc;
@@ -2476,7 +2542,7 @@ struct Engine {
         // the watermark's step: first arrival whose running max reached M (only if M advanced in this batch)
         if (!had_M || max_ts > M_prev) {
             if (int rc = ensure(bounds_idx, 8)) return rc;
-            hipLaunchKernelGGL(k_first_ge, dim3(1), dim3(64), 0, stream, (const int64_t*)runmax_d.p, n, max_ts, (int64_t*)bounds_idx.p);
+            hipLaunchKernelGGL(k_first_ge, dim3(1), dim3(64), 0, stream, runmax_p, n, max_ts, (int64_t*)bounds_idx.p);
             sW = arrival_base + fetch_i64(bounds_idx.p);
         }
         const int64_t rel_prev = eb_rel;
@@ -2489,10 +2555,12 @@ struct Engine {
         if (need_rel && eb_rel > rel_prev) {
             const int g = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
             hipLaunchKernelGGL(k_release_step, dim3(g), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                               (const int64_t*)eb.arr.p, rel_prev, eb_rel, (const int64_t*)runmax_d.p, n, arrival_base,
+                               (const int64_t*)eb.arr.p, rel_prev, eb_rel, runmax_p, n, arrival_base,
                                had_M ? M_prev : INT64_MIN, plan.late_tolerance_ms, (int64_t*)eb.rel.p);
         }
-        return range_triggers(rel_prev);
+        const int rc = range_triggers(rel_prev);
+        runmax_p = (const int64_t*)runmax_d.p;   // never an alias of a batch column past its push
+        return rc;
     }
 
     // Window-less rule (SELECT * ... WHERE): FilterOp.Apply per event (filter_operator.go:36-90). Each push
@@ -2736,7 +2804,7 @@ struct Engine {
             }
         }
         if (range_mode) {
-            const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M);
+            const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M, s.min_ts);
             return rc ? rc : record_time();
         }
         // a batch whose every accepted event was discarded still advanced the watermark: its windows close below

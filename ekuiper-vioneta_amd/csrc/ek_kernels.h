@@ -1510,6 +1510,156 @@ __global__ __launch_bounds__(kBlock) void k_finalize_merge(DPlan* __restrict__ p
     emit_rows(p, present, s, 0, w.out_base, w.idx, res, esh);
 }
 
+// ---------------------------------------------------------------- un-grouped rules over ts-sorted groups: one pass
+// Block tree merge of the per-thread partials through LDS (fixed order); thread 0 ends with the block's partial.
+template <int NVC, int B>
+__device__ __forceinline__ void block_merge_part(const DPlan& p, Part<NVC>& s) {
+    __shared__ int64_t t_cnt[B], t_vc[NVC][B], t_is[NVC][B];
+    __shared__ double t_fs[NVC][B], t_m2[NVC][B];
+    __shared__ uint64_t t_mn[NVC][B], t_mx[NVC][B];
+    const int t = threadIdx.x;
+    for (int stride = B / 2; stride > 0; stride >>= 1) {
+        if (t >= stride && t < 2 * stride) {
+            t_cnt[t] = s.cnt;
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                t_vc[v][t] = s.vcnt[v]; t_is[v][t] = s.isum[v]; t_fs[v][t] = s.fsum[v]; t_m2[v][t] = s.m2[v];
+                t_mn[v][t] = s.omn[v]; t_mx[v][t] = s.omx[v];
+            }
+        }
+        __syncthreads();
+        if (t < stride && t_cnt[t + stride] > 0) {
+            const int o = t + stride;
+            int64_t vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) { vc[v] = t_vc[v][o]; is[v] = t_is[v][o]; fs[v] = t_fs[v][o]; m2[v] = t_m2[v][o]; mn[v] = t_mn[v][o]; mx[v] = t_mx[v][o]; }
+            part_merge(p, s, t_cnt[o], vc, is, fs, m2, mn, mx);
+        }
+        __syncthreads();
+    }
+}
+
+// An un-grouped rule (pseudo keys) over a ts-sorted group: every pane is a contiguous row range, so one workgroup
+// per tile of rows folds each pane segment of its tile into ONE partial (accept mask, WHERE, a thread-local
+// two-pass M2 about the thread's own mean, then the block's Chan tree merge) and merges it into partial slot
+// (tile mod kPseudoKeys) of the pane — no staging round trip, every referenced column read once (count(*) alone
+// reads nothing). The host sizes the tiles so a launch has at most kPseudoKeys of them (distinct slots per pane)
+// and zeroes the slot counts of fresh panes first; k_finalize_merge folds a window's slots as before.
+constexpr int kUngBlock = 256;
+__global__ void k_ung_zero(GroupDesc gd, DState ds) {
+    const int r = blockIdx.y;
+    if (!gd.fresh[r]) return;
+    int64_t* c = ds.cnt + ((gd.q_lo + r) % gd.ring) * ds.K;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < (int64_t)kPseudoKeys; k += (int64_t)gridDim.x * blockDim.x) c[k] = 0;
+}
+
+template <int NVC, bool WHERE>
+__global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, DBatch b, GroupDesc gd,
+                                                        const uint8_t* __restrict__ acc, DState ds, int64_t tile,
+                                                        int32_t* __restrict__ pane_err) {
+    const DPlan& p = *pp;
+    const int64_t t0 = gd.lo + (int64_t)blockIdx.x * tile, t1 = min(gd.hi, t0 + tile);
+    int r = 0;
+    {   // first pane of the tile: the last r with pbnd[r] <= t0
+        int lo = 0, hi = gd.n_panes - 1;
+        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (gd.pbnd[mid] <= t0) lo = mid; else hi = mid - 1; }
+        r = lo;
+    }
+    const bool raw_count = p.n_vc == 0 && !WHERE && !gd.has_accept;
+    int col[NVC], fl[NVC];
+    bool isf[NVC];
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) { col[v] = v < p.n_vc ? p.vc_col[v] : 0; fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
+    for (; r < gd.n_panes && gd.pbnd[r] < t1; ++r) {
+        const int64_t s0 = max(t0, gd.pbnd[r]), s1 = min(t1, gd.pbnd[r + 1]);
+        if (s1 <= s0) continue;
+        Part<NVC> s{};
+        if (raw_count) {
+            if (threadIdx.x == 0) s.cnt = s1 - s0;
+        } else {
+            int64_t c = 0, vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
+            bool werr = false;
+            for (int64_t i = s0 + threadIdx.x; i < s1; i += kUngBlock) {
+                if (gd.has_accept && !acc[i]) continue;
+                if (WHERE) {
+                    const int w = where_decide_slow(p, b, i);
+                    if (w < 0) werr = true;
+                    if (w <= 0) continue;
+                }
+                c++;
+#pragma unroll
+                for (int v = 0; v < NVC; ++v) {
+                    if (!fl[v] || !col_valid(b, col[v], i)) continue;
+                    const int64_t raw = ((const int64_t*)b.col[col[v]])[i];
+                    const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
+                    vc[v]++;
+                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+                    fs[v] = __dadd_rn(fs[v], x);
+                    mn[v] = o < mn[v] ? o : mn[v];
+                    mx[v] = o > mx[v] ? o : mx[v];
+                }
+            }
+            if (werr) atomicOr(&pane_err[(gd.q_lo + r) % gd.ring], EK_WIN_WHERE_ERROR);
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {   // centred second pass over the thread's own rows (L1/L2-warm)
+                if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;
+                const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+                for (int64_t i = s0 + threadIdx.x; i < s1; i += kUngBlock) {
+                    if (gd.has_accept && !acc[i]) continue;
+                    if (WHERE && where_decide_slow(p, b, i) <= 0) continue;
+                    if (!col_valid(b, col[v], i)) continue;
+                    const int64_t raw = ((const int64_t*)b.col[col[v]])[i];
+                    const double d = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                    m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
+                }
+            }
+            if (c > 0) part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+        }
+        if (!raw_count) block_merge_part<NVC, kUngBlock>(p, s);
+        if (threadIdx.x == 0 && s.cnt > 0) {
+            const int64_t e = ((gd.q_lo + r) % gd.ring) * ds.K + (int64_t)(blockIdx.x % kPseudoKeys);
+            Part<NVC> a{};
+            const int64_t ac = ds.cnt[e];
+            if (ac) {
+                int64_t avc[NVC], ais[NVC];
+                double afs[NVC], am2[NVC];
+                uint64_t amn[NVC], amx[NVC];
+#pragma unroll
+                for (int v = 0; v < NVC; ++v) {
+                    const int f = fl[v];
+                    avc[v] = (f & NEED_CNT) ? ds.vcnt[v][e] : ac;
+                    ais[v] = (!isf[v] && (f & NEED_SUM)) ? ds.sum[v][e] : 0;
+                    afs[v] = isf[v] ? ((f & NEED_SUM) ? __longlong_as_double(ds.sum[v][e]) : 0.0) : ((f & NEED_FSUM) ? ds.fsum[v][e] : 0.0);
+                    am2[v] = (f & NEED_M2) ? ds.m2[v][e] : 0.0;
+                    amn[v] = (f & NEED_MIN) ? (uint64_t)ds.mn[v][e] : 0ull;
+                    amx[v] = (f & NEED_MAX) ? (uint64_t)ds.mx[v][e] : 0ull;
+                }
+                part_merge(p, a, ac, avc, ais, afs, am2, amn, amx);
+            }
+            part_merge(p, a, s.cnt, s.vcnt, s.isum, s.fsum, s.m2, s.omn, s.omx);
+            ds.cnt[e] = a.cnt;
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                const int f = fl[v];
+                if (f & NEED_CNT) ds.vcnt[v][e] = a.vcnt[v];
+                if (f & NEED_SUM) ds.sum[v][e] = isf[v] ? __double_as_longlong(a.fsum[v]) : a.isum[v];
+                if (f & NEED_FSUM) ds.fsum[v][e] = a.fsum[v];
+                if (f & NEED_M2) ds.m2[v][e] = a.m2[v];
+                if (f & NEED_MIN) ds.mn[v][e] = (int64_t)a.omn[v];
+                if (f & NEED_MAX) ds.mx[v][e] = (int64_t)a.omx[v];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- debug: window membership fingerprint
 // Per pane: number of accepted events (before WHERE) and Σ ek_mix64(arrival index); a window's
 // fingerprint is the sum over its panes (order-independent, exact in u64 arithmetic).

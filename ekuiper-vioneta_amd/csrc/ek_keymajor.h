@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kBlock) void k_km_keys(DPlan* __restrict__ pp, DBat
         if (wd <= 0 || k >= K) k = K;
         e += wd < 0;
         kout[i] = k;
-        pout[i] = (uint32_t)i;
+        if (pout) pout[i] = (uint32_t)i;
     }
     if (e) atomicAdd(nerr, e);
 }
@@ -145,12 +145,19 @@ __device__ __forceinline__ int km_having(const DPlan& p, const Part<NVC>& s, con
 }
 
 // WRITE = false: count the rows each (window, block) keeps; true: emit them (and raise window errors).
+// ONE (a launch of ONE window spanning the whole sorted span, WRITE = true): every row of a key is a member, so the
+// walk needs no positions, each key yields at most one row, and the rows are block-compacted with one atomic per
+// workgroup on the window's row counter — a single pass, no count pass / scan.
 // A key's membership [j0, j1) of its sorted rows only changes where a window start passes row j0 or a window end
 // passes row j1, so the thread folds, finalises and tests HAVING once per membership state and emits that row into
 // every window of the state's run [k, kend) — about two states per row instead of one fold per (key, window).
-template <int NVC, bool SORT, bool WRITE>
+template <int NVC, bool SORT, bool WRITE, bool ONE = false>
 __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, KmDesc d, Results res) {
     extern __shared__ uint32_t s_dyn[];
+    __shared__ uint32_t s_wc[kKmBlock / 64 + 1];
+    bool one_present = false;
+    int64_t one_v[EK_MAX_AGGS];
+    uint8_t one_t[EK_MAX_AGGS];
     const int nw = d.nw;
     uint32_t* s_h = s_dyn;                          // [nw] kept rows (count pass) / cursors (write pass)
     int32_t* s_a = (int32_t*)(s_dyn + nw);          // [nw] window starts (relative rows)
@@ -171,18 +178,24 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
 #pragma unroll
         for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
         int64_t j0 = s, j1 = s;
-        int k = s < e ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : nw;
+        int k = s < e ? (ONE ? 0 : km_first_gt(s_b, 0, nw, (int64_t)d.spos[s])) : nw;
         while (k < nw) {
-            const int64_t wa = s_a[k], wb = s_b[k];
-            while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
-            if (j0 == e) break;
-            if (j1 < j0) j1 = j0;
-            while (j1 < e && (int64_t)d.spos[j1] < wb) ++j1;
-            const int64_t p0 = d.spos[j0];
-            if (j1 == j0) { k = km_first_gt(s_b, k + 1, nw, p0); continue; }
-            // windows [k, kend) hold exactly rows [j0, j1) of this key
-            int kend = km_first_gt(s_a, k + 1, nw, p0);
-            if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
+            int kend = 1;
+            if constexpr (ONE) {
+                j0 = s;
+                j1 = e;
+            } else {
+                const int64_t wa = s_a[k], wb = s_b[k];
+                while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
+                if (j0 == e) break;
+                if (j1 < j0) j1 = j0;
+                while (j1 < e && (int64_t)d.spos[j1] < wb) ++j1;
+                const int64_t p0 = d.spos[j0];
+                if (j1 == j0) { k = km_first_gt(s_b, k + 1, nw, p0); continue; }
+                // windows [k, kend) hold exactly rows [j0, j1) of this key
+                kend = km_first_gt(s_a, k + 1, nw, p0);
+                if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
+            }
             // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
             int64_t vc[NVC], is[NVC];
             double fs[NVC], m2[NVC];
@@ -265,7 +278,18 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 const int hv = km_having(p, part, SORT ? &sr : nullptr);
                 if (WRITE && hv < 0) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
                 if (hv > 0) {
-                    if constexpr (!WRITE) {
+                    if constexpr (ONE) {
+                        one_present = true;
+#pragma unroll
+                        for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                            one_v[q] = 0;
+                            one_t[q] = EK_TAG_NULL;
+                            if (q >= p.n_aggs) continue;
+                            const Val av = agg_value(p, part, q, SORT ? &sr : nullptr);
+                            one_t[q] = av.tag == V_NULL ? EK_TAG_NULL : (av.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+                            one_v[q] = av.tag == V_F64 ? __double_as_longlong(av.f) : av.i;
+                        }
+                    } else if constexpr (!WRITE) {
                         for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
                     } else {
                         int64_t ov[EK_MAX_AGGS];
@@ -293,6 +317,28 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 }
             }
             k = kend;
+        }
+    }
+    if constexpr (ONE) {
+        const unsigned long long mask = __ballot(one_present);
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (lane == 0) s_wc[wv] = (uint32_t)__popcll(mask);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int w = 0; w < kKmBlock / 64; ++w) { const uint32_t c = s_wc[w]; s_wc[w] = run; run += c; }
+            s_wc[kKmBlock / 64] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[d.widx[0]], (unsigned long long)run) : 0u;
+        }
+        __syncthreads();
+        if (one_present) {
+            const int64_t pos = d.obase[0] + (int64_t)s_wc[kKmBlock / 64] + s_wc[wv] + __popcll(mask & ((1ull << lane) - 1ull));
+            res.key[pos] = (uint32_t)g;
+#pragma unroll
+            for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                if (q >= p.n_aggs) break;
+                res.tag[q][pos] = one_t[q];
+                res.val[q][pos] = one_v[q];
+            }
         }
     }
     if constexpr (!WRITE) {

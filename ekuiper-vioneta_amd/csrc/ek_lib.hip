@@ -20,3 +20,10 @@ int ekl_sort_pairs_u32(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s);
     return e == hipSuccess ? 0 : -1;
 }
+
+int ekl_sort_pairs_u32_i64(void* tmp, size_t* tmp_bytes, const uint32_t* kin, uint32_t* kout, const int64_t* vin,
+                           int64_t* vout, int64_t n, int end_bit, hipStream_t s) {
+    // stable: each key's values keep their buffer order (one-window key-major aggregation sorts the values directly)
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}

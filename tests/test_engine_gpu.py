@@ -207,3 +207,4 @@ def test_key_sharded_engines_union(oracle, engine_mod):
         for k, v in ref[e].items():
             g = union[k]
             assert g[1:] == v[1:] and abs(g[0] - v[0]) <= 1e-6 * abs(v[0])
+

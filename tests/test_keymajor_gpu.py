@@ -147,3 +147,57 @@ def test_km_auto_rule_picks_big_key_spaces(oracle, engine_mod):
         assert_windows_equal(rule.plan, got, exp.windows)
     finally:
         os.environ["EKGPU_KEYMAJOR"] = "1"
+
+
+def _push_per_window(oracle, engine_mod, rule, cols, window_ms, validity=None):
+    """One push per tumbling window's events: every push (but the first) fires exactly one window, so the
+    key-major launch holds ONE window (single pass: no positions, block-compacted rows)."""
+    exp = oracle.run(rule.plan, cols, validity)
+    ts = cols[1]
+    ends = np.arange((ts[0] // window_ms + 1) * window_ms, ts[-1] + 1, window_ms)
+    cuts = np.concatenate([[0], np.searchsorted(ts, ends), [len(ts)]]).astype(np.int64)
+    eng = engine_mod.Engine(rule.plan)
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        if hi > lo:
+            eng.push_host([c[lo:hi] for c in cols], None if validity is None else
+                          [None if v is None else v[lo:hi] for v in validity])
+    got = eng.poll()
+    st = eng.stats()
+    eng.close()
+    return got, exp, st
+
+
+@pytest.mark.parametrize("sql", [
+    # one value column, no validity: the column itself is sorted by key (no gather)
+    "SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9), count(*) FROM demo "
+    "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)",
+    # two value columns: positions sorted + gathered, still one pass
+    "SELECT deviceId, median(temperature), percentile_disc(humidity, 0.5), avg(humidity), stddev(temperature) "
+    "FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 2",
+])
+def test_km_one_window_per_push(oracle, engine_mod, sql):
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=20_000, debug_membership=True)
+    cols = R._iot(400_000, 20_000, seed=91, epm=50)
+    got, exp, st = _push_per_window(oracle, engine_mod, rule, cols, 1000)
+    assert len(exp.windows) >= 5 and st.windows_keymajor >= len(exp.windows)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_one_window_nulls_and_long_runs(oracle, engine_mod):
+    """Nullable value column (validity staged, positions path) and a key space small enough that a key's run exceeds
+    kKmSelMax: the one-window launch is declined before anything is written and the window-major path answers."""
+    schema = {"deviceId": "key", "ts": "bigint", "v": "bigint", "w": "float"}
+    rng = np.random.default_rng(17)
+    n = 120_000
+    ts = (1541152480000 + np.arange(n) // 40).astype(np.int64)
+    for keys in (20_000, 40):
+        k = rng.integers(0, keys, n).astype(np.uint32)
+        cols = [k, ts, rng.integers(-100, 100, n).astype(np.int64), rng.uniform(0, 1, n)]
+        valid = [None, None, None, (rng.random(n) > 0.2).astype(np.uint8)]
+        sql = ("SELECT deviceId, median(v), percentile_cont(w, 0.5), count(w), max(w) FROM s "
+               "GROUP BY deviceId, TUMBLINGWINDOW(ms, 500)")
+        rule = compile_rule(sql, schema, num_keys=keys, nullable=("w",), debug_membership=True)
+        got, exp, st = _push_per_window(oracle, engine_mod, rule, cols, 500, validity=valid)
+        assert len(exp.windows) >= 4
+        assert (st.windows_keymajor > 0) == (keys > 40)
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)

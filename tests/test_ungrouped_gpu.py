@@ -17,6 +17,9 @@ CASES = [
     "SELECT count(*), sum(temperature), min(temperature), stddev(humidity), var(temperature) FROM demo "
     "GROUP BY HOPPINGWINDOW(ss, 6, 2)",
     "SELECT count(*), avg(humidity) FROM demo WHERE temperature > 20 GROUP BY TUMBLINGWINDOW(ss, 2) HAVING count(*) > 10",
+    # count(*) alone over sorted batches: k_ung_tile reads no column at all
+    "SELECT count(*) FROM demo GROUP BY TUMBLINGWINDOW(ss, 10)",
+    "SELECT count(*) FROM demo GROUP BY HOPPINGWINDOW(ss, 4, 2) HAVING count(*) > 100",
 ]
 
 
@@ -41,4 +44,33 @@ def test_ungrouped_int_columns_out_of_order(oracle, engine_mod):
     rule = compile_rule(sql, schema, num_keys=0, late_tolerance_ms=20, debug_membership=True)
     got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=3)
     assert len(exp.windows) >= 3
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("ung", ["0", "1"])
+def test_ungrouped_tile_path_vs_partition_path(oracle, engine_mod, ung, monkeypatch):
+    """EKGPU_UNG=1 (default): sorted groups of an un-grouped rule fold tiles straight into the partial slots;
+    EKGPU_UNG=0: the k_part + k_agg route. Both equal the oracle, incl. a batch split inside a pane and many panes
+    per push."""
+    monkeypatch.setenv("EKGPU_UNG", ung)
+    sql = ("SELECT count(*), sum(temperature), min(humidity), max(humidity), var(temperature) FROM demo "
+           "WHERE humidity > 5 GROUP BY TUMBLINGWINDOW(ms, 500)")
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=0, debug_membership=True)
+    cols = list(iot_stream(500_000, 1000, events_per_ms=40))
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=7)
+    assert len(exp.windows) >= 20
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_ungrouped_hopping_gap_discard(oracle, engine_mod):
+    """Hopping discard mask (k_hop_drop) on a sorted un-grouped batch: the tile path skips the masked rows."""
+    n = 60_000
+    ts = 1541152480000 + np.arange(n, dtype=np.int64) // 10
+    ts[n // 2:] += 9_000            # a gap wider than the window: an empty hopping window discards the inputs
+    rng = np.random.default_rng(3)
+    cols = [rng.integers(0, 50, n).astype(np.uint32), ts, rng.uniform(0, 100, n), rng.uniform(0, 100, n)]
+    sql = "SELECT count(*), avg(temperature) FROM demo GROUP BY HOPPINGWINDOW(ss, 2, 1)"
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=0, debug_membership=True)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=1)
+    assert len(exp.windows) >= 5
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
