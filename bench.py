@@ -6,7 +6,8 @@
 
 A step = one pass of the hot path over one batch (ek_reset + the batch's ek_push_batch through the C ABI, inputs
 already resident in HBM); it triggers the batch's windows and writes their GROUP BY rows to HBM.
-`--config C3|C4a|C4b|C5` runs the other BASELINE configs at their per-GPU sizes.
+`--config C3|C4a|C4b|C5` runs the other BASELINE configs at their per-GPU sizes; `--config C1`
+times the columnar JSON ingest + WHERE (messages/s).
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): ONE global stream of N x the per-GPU events
 over N x the keys, key-hash sharded (mix64(key) % N, dense local ids per rank). Every rank runs its handle in
@@ -226,12 +227,87 @@ def ingest_inclusive(eng, cols, n, steps=2):
             "what": "pinned host columns -> H2D inside ek_push_batch, then ek_poll_results into host memory"}
 
 
+def bench_c1(args):
+    """C1: 1e6 schemaless JSON payloads {"temperature":T,"humidity":H}, T, H integers in [0, 100],
+    decoded on the GPU (ek_json_decode: every number -> float64, converter.go:507-520) and filtered by
+    SELECT * FROM demo WHERE temperature > 50 (ek_push_batch, window-less FilterOp). A step = decode + filter of the
+    whole micro-batch with the payload bytes already in HBM; `host_fed` repeats it from pinned host memory (H2D
+    included)."""
+    import numpy as np
+    import torch
+    from ekgpu.engine import Engine, JsonDecoder
+    from ekgpu.rule import compile_rule
+    n = args.events or 1_000_000
+    rng = np.random.default_rng(42 + 1)
+    t = rng.integers(0, 101, n)
+    h = rng.integers(0, 101, n)
+    msgs = [f'{{"temperature":{a},"humidity":{b}}}'.encode() for a, b in zip(t.tolist(), h.tolist())]
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.int64, count=n)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    blob = np.frombuffer(b"".join(msgs), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(blob.copy()).to(dev)
+    d_offs = torch.from_numpy(offs).to(dev)
+    dec = JsonDecoder.schemaless(["temperature", "humidity"])
+    rule = compile_rule("SELECT * FROM demo WHERE temperature > 50", {"temperature": "float", "humidity": "float"},
+                        is_event_time=False)
+    eng = Engine(rule.plan, device=0)
+
+    def step():
+        b = dec.decode_device(d_blob.data_ptr(), len(blob), d_offs.data_ptr(), n)
+        eng.reset()
+        eng.push_batch(b)
+
+    for _ in range(args.warmup):
+        step()
+    r = eng.poll_device()
+    rows = int(r.win_row_count[0]) if int(r.n_windows) else 0
+    eng.release(r)
+    assert rows == int((t > 50).sum()), (rows, int((t > 50).sum()))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    # host-fed: payload bytes + offsets in pinned host memory, copied by ek_json_decode
+    hb = torch.from_numpy(blob.copy()).pin_memory()
+    ho = torch.from_numpy(offs).pin_memory()
+    hb_np, ho_np = hb.numpy(), ho.numpy()
+    dec.decode(hb_np, ho_np)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        b = dec.decode(hb_np, ho_np)
+        eng.reset()
+        eng.push_batch(b)
+    eng.sync()
+    dth = (time.perf_counter() - t1) / args.steps
+    alg = len(blob) + 8 * (n + 1) + rows * (8 + 8 + 8)
+    out = {"metric": "messages/sec decoded and filtered (C1 JSON ingest + WHERE)", "value": n / dt, "unit": "messages/s",
+           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (1e6 schemaless JSON payloads, integer T/H uniform in [0, 100], seed 43)",
+           "config": {"workload": "C1: JSON decode + SELECT * FROM demo WHERE temperature > 50", "messages": n,
+                      "payload_bytes": int(len(blob)), "rows_out": rows},
+           "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "what": "payload bytes + offsets read + passing rows x (row index + 2 f64 columns) written, over ms_per_step"},
+           "host_fed": {"messages_per_s": n / dth, "ms_per_step": dth * 1e3,
+                        "what": "payloads in pinned host memory: H2D inside ek_json_decode, then the filter"}}
+    print(json.dumps(out), flush=True)
+    eng.close()
+    dec.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS) + ["C1"])
     ap.add_argument("--events", type=int, default=0, help="override the per-GPU event count")
     ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", N_EVENTS)))
     ap.add_argument("--no-cpu", action="store_true")
@@ -240,6 +316,8 @@ def main():
                     help="one process plays rank 0 of an N-GPU run in shard mode (no collective; a single-GPU check of "
                          "the shard path: C4a then sees only its own triggers)")
     args = ap.parse_args()
+    if args.config == "C1":
+        return bench_c1(args)
 
     import numpy as np
     import torch

@@ -1873,7 +1873,7 @@ struct Engine {
         const int nvc = std::max(1, dp.n_vc);
         const int nblk = (int)(((int64_t)K + kKmBlock - 1) / kKmBlock);
         if (int rc = ensure(km_ab, (size_t)nw * 28)) return rc;
-        if (int rc = ensure(km_bcnt, (size_t)nw * nblk * 4)) return rc;
+        if (int rc = ensure(km_bcnt, (size_t)nw * (nblk + 1) * 4)) return rc;
         km_hab.resize((size_t)nw * 3);
         int64_t* h_rab = km_hab.data();
         int64_t* h_rob = h_rab + 2 * nw;

@@ -38,7 +38,8 @@ struct KmDesc {
     const uint32_t* spos;          // relative positions in key order
     const int64_t* sval[kMaxVC];   // value columns gathered in key order
     const uint8_t* sok[kMaxVC];    // their validity (nullptr: all valid)
-    uint32_t* bcnt;                // [nw][nblk] kept rows per (window, block) -> exclusive offsets after k_km_scan
+    uint32_t* bcnt;                // [nw][nblk + 1] kept rows per (window, block) -> exclusive offsets after k_km_scan
+                                   // (the window's total at [nblk])
     int32_t* flags;                // [0] a (key, window) sub-run longer than kKmSelMax (order statistics), [1] scratch
 };
 
@@ -144,6 +145,102 @@ __device__ __forceinline__ int km_having(const DPlan& p, const Part<NVC>& s, con
     return h.i != 0 ? 1 : 0;
 }
 
+// Fold one (key, window run) membership state: rows [j0, j1) of the key's sorted rows. First pass (count, sums,
+// min, max), centred second pass (M2), then the order statistics. Returns true on an aggregate error.
+template <int NVC, bool SORT>
+__device__ __forceinline__ bool km_fold(const DPlan& p, const KmDesc& d, int64_t j0, int64_t j1, const int (&fl)[NVC],
+                                        const bool (&isf)[NVC], uint64_t* s_seg, Part<NVC>& part,
+                                        uint64_t (&sres)[kMaxSortAggs], uint8_t (&stag)[kMaxSortAggs]) {
+    // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
+    int64_t vc[NVC], is[NVC];
+    double fs[NVC], m2[NVC];
+    uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) {
+        vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull;
+        if (!fl[v]) continue;
+        const int64_t* __restrict__ val = d.sval[v];
+        const uint8_t* __restrict__ ok = d.sok[v];
+        for (int64_t j = j0; j < j1; ++j) {
+            if (ok && !ok[j]) continue;
+            const int64_t raw = val[j];
+            const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
+            const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
+            vc[v]++;
+            is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+            fs[v] = __dadd_rn(fs[v], x);
+            mn[v] = o < mn[v] ? o : mn[v];
+            mx[v] = o > mx[v] ? o : mx[v];
+        }
+        if ((fl[v] & NEED_M2) && vc[v] > 0) {   // stats._variance shape
+            const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+            for (int64_t j = j0; j < j1; ++j) {
+                if (ok && !ok[j]) continue;
+                const int64_t raw = val[j];
+                const double dd = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                m2[v] = __dadd_rn(m2[v], __dmul_rn(dd, dd));
+            }
+        }
+    }
+    part_merge(p, part, j1 - j0, vc, is, fs, m2, mn, mx);
+    bool agg_err = false;
+#pragma unroll
+    for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
+    if constexpr (SORT) {
+        // per sort column: the sub-run's valid values (ordered bits), insertion-sorted in this thread's LDS
+        // lane (interleaved, conflict-free) when at most kKmSegMax, else ranked by counting in memory
+        for (int sc = 0; sc < p.n_scol; ++sc) {
+            const int v = p.scol_vc[sc];
+            const int64_t* __restrict__ val = d.sval[v];
+            const uint8_t* __restrict__ ok = d.sok[v];
+            const bool fv = p.vc_is_float[v] != 0;
+            int64_t n = 0;
+            for (int64_t j = j0; j < j1; ++j) n += (!ok || ok[j]) ? 1 : 0;
+            if (n > kKmSelMax) { d.flags[0] = 1; agg_err = true; continue; }
+            const bool inl = n <= kKmSegMax;
+            if (inl) {
+                int m = 0;
+                for (int64_t j = j0; j < j1; ++j) {
+                    if (ok && !ok[j]) continue;
+                    const uint64_t x = fv ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
+                    int q = m;
+                    while (q > 0 && s_seg[(q - 1) * kKmBlock + threadIdx.x] > x) {
+                        s_seg[q * kKmBlock + threadIdx.x] = s_seg[(q - 1) * kKmBlock + threadIdx.x];
+                        --q;
+                    }
+                    s_seg[q * kKmBlock + threadIdx.x] = x;
+                    ++m;
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < kMaxSortAggs; ++a) {
+                if (a >= p.n_sagg || p.sagg_scol[a] != sc) continue;
+                const int ka = p.sagg_agg[a];
+                order_stat(p.agg_fn[ka], fv, p.agg_p[ka], n,
+                           [&](int64_t r) { return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r); },
+                           &sres[a], &stag[a]);
+                agg_err |= stag[a] == kTagErr;
+            }
+        }
+    }
+    return agg_err;
+}
+
+// the emitted values of a kept group
+template <int NVC>
+__device__ __forceinline__ void km_row(const DPlan& p, const Part<NVC>& part, const SortRes* sr, int64_t (&ov)[EK_MAX_AGGS],
+                                       uint8_t (&ot)[EK_MAX_AGGS]) {
+#pragma unroll
+    for (int q = 0; q < EK_MAX_AGGS; ++q) {
+        ov[q] = 0;
+        ot[q] = EK_TAG_NULL;
+        if (q >= p.n_aggs) continue;
+        const Val av = agg_value(p, part, q, sr);
+        ot[q] = av.tag == V_NULL ? EK_TAG_NULL : (av.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+        ov[q] = av.tag == V_F64 ? __double_as_longlong(av.f) : av.i;
+    }
+}
+
 // WRITE = false: count the rows each (window, block) keeps; true: emit them (and raise window errors).
 // ONE (a launch of ONE window spanning the whole sorted span, WRITE = true): every row of a key is a member, so the
 // walk needs no positions, each key yields at most one row, and the rows are block-compacted with one atomic per
@@ -165,7 +262,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
     for (int k = threadIdx.x; k < nw; k += kKmBlock) {
-        s_h[k] = 0;
+        // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
+        s_h[k] = (WRITE && !ONE) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
         s_a[k] = (int32_t)d.ab[2 * k];
         s_b[k] = (int32_t)d.ab[2 * k + 1];
     }
@@ -196,81 +294,10 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 kend = km_first_gt(s_a, k + 1, nw, p0);
                 if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
             }
-            // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
-            int64_t vc[NVC], is[NVC];
-            double fs[NVC], m2[NVC];
-            uint64_t mn[NVC], mx[NVC];
-#pragma unroll
-            for (int v = 0; v < NVC; ++v) {
-                vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull;
-                if (!fl[v]) continue;
-                const int64_t* __restrict__ val = d.sval[v];
-                const uint8_t* __restrict__ ok = d.sok[v];
-                for (int64_t j = j0; j < j1; ++j) {
-                    if (ok && !ok[j]) continue;
-                    const int64_t raw = val[j];
-                    const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
-                    const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
-                    vc[v]++;
-                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
-                    fs[v] = __dadd_rn(fs[v], x);
-                    mn[v] = o < mn[v] ? o : mn[v];
-                    mx[v] = o > mx[v] ? o : mx[v];
-                }
-                if ((fl[v] & NEED_M2) && vc[v] > 0) {   // stats._variance shape
-                    const double mean = __ddiv_rn(fs[v], (double)vc[v]);
-                    for (int64_t j = j0; j < j1; ++j) {
-                        if (ok && !ok[j]) continue;
-                        const int64_t raw = val[j];
-                        const double dd = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
-                        m2[v] = __dadd_rn(m2[v], __dmul_rn(dd, dd));
-                    }
-                }
-            }
-            Part<NVC> part{};
-            part_merge(p, part, j1 - j0, vc, is, fs, m2, mn, mx);
             uint64_t sres[kMaxSortAggs];
             uint8_t stag[kMaxSortAggs];
-            bool agg_err = false;
-#pragma unroll
-            for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
-            if constexpr (SORT) {
-                // per sort column: the sub-run's valid values (ordered bits), insertion-sorted in this thread's LDS
-                // lane (interleaved, conflict-free) when at most kKmSegMax, else ranked by counting in memory
-                for (int sc = 0; sc < p.n_scol; ++sc) {
-                    const int v = p.scol_vc[sc];
-                    const int64_t* __restrict__ val = d.sval[v];
-                    const uint8_t* __restrict__ ok = d.sok[v];
-                    const bool fv = p.vc_is_float[v] != 0;
-                    int64_t n = 0;
-                    for (int64_t j = j0; j < j1; ++j) n += (!ok || ok[j]) ? 1 : 0;
-                    if (n > kKmSelMax) { d.flags[0] = 1; agg_err = true; continue; }
-                    const bool inl = n <= kKmSegMax;
-                    if (inl) {
-                        int m = 0;
-                        for (int64_t j = j0; j < j1; ++j) {
-                            if (ok && !ok[j]) continue;
-                            const uint64_t x = fv ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
-                            int q = m;
-                            while (q > 0 && s_seg[(q - 1) * kKmBlock + threadIdx.x] > x) {
-                                s_seg[q * kKmBlock + threadIdx.x] = s_seg[(q - 1) * kKmBlock + threadIdx.x];
-                                --q;
-                            }
-                            s_seg[q * kKmBlock + threadIdx.x] = x;
-                            ++m;
-                        }
-                    }
-#pragma unroll
-                    for (int a = 0; a < kMaxSortAggs; ++a) {
-                        if (a >= p.n_sagg || p.sagg_scol[a] != sc) continue;
-                        const int ka = p.sagg_agg[a];
-                        order_stat(p.agg_fn[ka], fv, p.agg_p[ka], n,
-                                   [&](int64_t r) { return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r); },
-                                   &sres[a], &stag[a]);
-                        agg_err |= stag[a] == kTagErr;
-                    }
-                }
-            }
+            Part<NVC> part{};
+            const bool agg_err = km_fold<NVC, SORT>(p, d, j0, j1, fl, isf, s_seg, part, sres, stag);
             const SortRes sr{sres, stag, 0, 1};
             if (agg_err) {   // "run Select error" replaces each of these windows' output
                 if (WRITE) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_AGG_ERROR);
@@ -280,31 +307,15 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 if (hv > 0) {
                     if constexpr (ONE) {
                         one_present = true;
-#pragma unroll
-                        for (int q = 0; q < EK_MAX_AGGS; ++q) {
-                            one_v[q] = 0;
-                            one_t[q] = EK_TAG_NULL;
-                            if (q >= p.n_aggs) continue;
-                            const Val av = agg_value(p, part, q, SORT ? &sr : nullptr);
-                            one_t[q] = av.tag == V_NULL ? EK_TAG_NULL : (av.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
-                            one_v[q] = av.tag == V_F64 ? __double_as_longlong(av.f) : av.i;
-                        }
+                        km_row(p, part, SORT ? &sr : nullptr, one_v, one_t);
                     } else if constexpr (!WRITE) {
                         for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
                     } else {
                         int64_t ov[EK_MAX_AGGS];
                         uint8_t ot[EK_MAX_AGGS];
-#pragma unroll
-                        for (int q = 0; q < EK_MAX_AGGS; ++q) {
-                            ov[q] = 0;
-                            ot[q] = EK_TAG_NULL;
-                            if (q >= p.n_aggs) continue;
-                            const Val av = agg_value(p, part, q, SORT ? &sr : nullptr);
-                            ot[q] = av.tag == V_NULL ? EK_TAG_NULL : (av.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
-                            ov[q] = av.tag == V_F64 ? __double_as_longlong(av.f) : av.i;
-                        }
+                        km_row(p, part, SORT ? &sr : nullptr, ov, ot);
                         for (int kk = k; kk < kend; ++kk) {
-                            const int64_t pos = d.obase[kk] + (int64_t)d.bcnt[(int64_t)kk * d.nblk + blockIdx.x] + atomicAdd(&s_h[kk], 1u);
+                            const int64_t pos = d.obase[kk] + (int64_t)atomicAdd(&s_h[kk], 1u);
                             res.key[pos] = (uint32_t)g;
 #pragma unroll
                             for (int q = 0; q < EK_MAX_AGGS; ++q) {
@@ -343,14 +354,14 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     }
     if constexpr (!WRITE) {
         __syncthreads();
-        for (int k = threadIdx.x; k < nw; k += kKmBlock) d.bcnt[(int64_t)k * d.nblk + blockIdx.x] = s_h[k];
+        for (int k = threadIdx.x; k < nw; k += kKmBlock) d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] = s_h[k];
     }
 }
 
 // one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count
 __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
     const int k = blockIdx.x;
-    uint32_t* c = d.bcnt + (int64_t)k * d.nblk;
+    uint32_t* c = d.bcnt + (int64_t)k * (d.nblk + 1);
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -371,7 +382,10 @@ __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
         if (threadIdx.x == 1023) s_carry = carry + wb + x;
         __syncthreads();
     }
-    if (threadIdx.x == 0 && s_carry) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
+    if (threadIdx.x == 0) {
+        c[d.nblk] = s_carry;
+        if (s_carry) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
+    }
 }
 
 }  // namespace ek

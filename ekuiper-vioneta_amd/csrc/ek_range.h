@@ -459,11 +459,12 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
         if (t == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
         return;
     }
-    // exclusive scan of the slot counts (each thread H / kBlock consecutive slots); occupied slots -> group list
+    // one exclusive scan of the slot counts packed with the occupied-slot count (each thread H / kBlock consecutive
+    // slots): a slot's first row and its group index at once, no shared group counter to contend on
     {
         const int per = H / kBlock, s0 = t * per;
-        uint32_t sm = 0;
-        for (int k = s0; k < s0 + per; ++k) sm += s_off[k];
+        uint32_t sm = 0;   // occupied slots << 16 | rows (both <= kSmallWin)
+        for (int k = s0; k < s0 + per; ++k) { const uint32_t c = s_off[k]; sm += c | (c ? 0x10000u : 0u); }
         uint32_t x = sm;
         for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
         if (lane == 63) s_wsum[wv] = x;
@@ -472,10 +473,11 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
         for (int q = 0; q < wv; ++q) run += s_wsum[q];
         for (int k = s0; k < s0 + per; ++k) {
             const uint32_t c = s_off[k];
-            if (c) s_grp[atomicAdd(&s_ng, 1)] = (run << 16) | c;
-            s_off[k] = run;
-            run += c;
+            if (c) s_grp[run >> 16] = ((run & 0xFFFFu) << 16) | c;
+            s_off[k] = run & 0xFFFFu;
+            run += c | (c ? 0x10000u : 0u);
         }
+        if (t == kBlock - 1) s_ng = (int)(run >> 16);
     }
     __syncthreads();
 #pragma unroll
@@ -531,6 +533,7 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
             part_merge(p, s, c, vc, is, fs, m2, mn, mx);
             present = having_keep(p, s, &res.win_err[widx]);
         }
+        if (!__syncthreads_or(present)) continue;   // nothing kept in this round (HAVING): no compaction
         emit_rows(p, present, s, (int64_t)key, out, widx, res, esh);
     }
 }

@@ -301,6 +301,15 @@ class JsonDecoder:
             raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
         return out
 
+    def decode_device(self, blob_ptr: int, n_bytes: int, offsets_ptr: int, n_msgs: int) -> A.ek_batch:
+        """Payloads already in device memory (blob bytes + n_msgs + 1 int64 offsets): no H2D copy."""
+        out = A.ek_batch()
+        rc = lib().ek_json_decode(self.h, C.c_void_p(blob_ptr), n_bytes, C.c_void_p(offsets_ptr), n_msgs,
+                                  A.EK_MEM_DEVICE, C.byref(out))
+        if rc != 0:
+            raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
+        return out
+
     def errors(self):
         n = C.c_int64()
         lib().ek_json_errors(self.h, None, None, 0, C.byref(n))

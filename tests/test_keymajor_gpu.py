@@ -201,3 +201,16 @@ def test_km_one_window_nulls_and_long_runs(oracle, engine_mod):
         assert len(exp.windows) >= 4
         assert (st.windows_keymajor > 0) == (keys > 40)
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_write_pass_many_aggregates(oracle, engine_mod):
+    """The multi-window write pass (cursor per (window, block) starting at the block's offset) with many aggregates
+    over heavily overlapping sliding windows."""
+    sql = ("SELECT deviceId, count(*), sum(temperature), avg(humidity), min(temperature), max(humidity), "
+           "stddev(temperature), vars(humidity), count(humidity) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 4) OVER (WHEN trig = 1) HAVING count(*) > 1")
+    rule = compile_rule(sql, R.TRIG_SCHEMA, num_keys=5000, debug_membership=True)
+    cols = R._with_trig(R._iot(400_000, 5000, seed=37, epm=20), 3000)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=2)
+    assert len(got) > 100 and st.windows_keymajor > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
