@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "ekuiper-vioneta_amd"))
 from ekgpu import abi as A  # noqa: E402
 from ekgpu.results import result_to_python  # noqa: E402
 
-LIB_PATH = os.path.join(HERE, "libekoracle.so")
+# EKO_LIB: an alternative build of the same sources (tests/test_oracle_asan.py loads the ASan/UBSan one)
+LIB_PATH = os.environ.get("EKO_LIB") or os.path.join(HERE, "libekoracle.so")
 
 
 class eko_output(C.Structure):
