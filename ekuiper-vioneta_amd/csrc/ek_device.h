@@ -160,19 +160,17 @@ __device__ inline Val simple_eval(Val l, Val r, int op) {
 // touches per-lane scratch memory (a dynamically indexed array would live there). ek_create rejects deeper
 // programs.
 constexpr int kEvalDepth = 8;
+// Evaluation stack of eight values kept in registers as a shift register: the top is always s0, push shifts down,
+// pop shifts up. No access uses a runtime index, so nothing can be lowered to a private (scratch) array — a
+// switch over the slots was turned into an indexed load from a stack-allocated struct (136 B of scratch traffic per
+// HAVING / WHERE evaluation).
 struct EvalStack {
     Val s0, s1, s2, s3, s4, s5, s6, s7;
-    __device__ __forceinline__ Val get(int i) const {
-        switch (i) {
-        case 0: return s0; case 1: return s1; case 2: return s2; case 3: return s3;
-        case 4: return s4; case 5: return s5; case 6: return s6; default: return s7;
-        }
-    }
-    __device__ __forceinline__ void set(int i, Val v) {
-        switch (i) {
-        case 0: s0 = v; break; case 1: s1 = v; break; case 2: s2 = v; break; case 3: s3 = v; break;
-        case 4: s4 = v; break; case 5: s5 = v; break; case 6: s6 = v; break; default: s7 = v; break;
-        }
+    __device__ __forceinline__ void push(Val v) { s7 = s6; s6 = s5; s5 = s4; s4 = s3; s3 = s2; s2 = s1; s1 = s0; s0 = v; }
+    __device__ __forceinline__ Val pop() {
+        const Val v = s0;
+        s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7;
+        return v;
     }
 };
 
@@ -191,25 +189,32 @@ __device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, con
                 if (p.col_type[arg] == EK_COL_F64) v = Val{V_F64, 0, col_f64(*b, arg, row)};
                 else v = Val{V_I64, col_i64(p, *b, arg, row), 0.0};
             }
-            st.set(sp++, v);
+            st.push(v);
+            sp++;
         } else if (op == EK_OP_AGG) {
-            st.set(sp++, aggf(arg));
+            st.push(aggf(arg));
+            sp++;
         } else if (op == EK_OP_CONST_I64) {
-            st.set(sp++, Val{V_I64, prog[k].i64, 0.0});
+            st.push(Val{V_I64, prog[k].i64, 0.0});
+            sp++;
         } else if (op == EK_OP_CONST_F64) {
-            st.set(sp++, Val{V_F64, 0, prog[k].f64});
+            st.push(Val{V_F64, 0, prog[k].f64});
+            sp++;
         } else {
-            const Val r = st.get(--sp), l = st.get(--sp);
+            const Val r = st.pop();
+            const Val l = st.pop();
+            sp -= 2;
             Val res;
             if (l.tag == V_ERR) res = l;
             else if (op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mkb(false);
             else if (op == EK_OP_OR && l.tag == V_BOOL && l.i) res = mkb(true);
             else if (r.tag == V_ERR) res = r;
             else res = simple_eval(l, r, op);
-            st.set(sp++, res);
+            st.push(res);
+            sp++;
         }
     }
-    return sp ? st.get(sp - 1) : Val{V_NULL, 0, 0.0};
+    return sp ? st.s0 : Val{V_NULL, 0, 0.0};
 }
 struct NoAggs {
     __device__ __forceinline__ Val operator()(int) const { return Val{V_NULL, 0, 0.0}; }

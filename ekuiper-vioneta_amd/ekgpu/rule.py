@@ -281,6 +281,12 @@ class _Parser:
 def _fill_prog(dst, prog: List[Tuple]) -> int:
     if len(prog) > A.EK_MAX_PROG:
         raise RuleError("expression too long")
+    depth = top = 0   # the device evaluates with an 8-value register stack (ek_device.h EvalStack)
+    for ins in prog:
+        top += 1 if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG, A.EK_OP_CONST_I64, A.EK_OP_CONST_F64) else -1
+        depth = max(depth, top)
+    if depth > 8:
+        raise RuleError("expression nests too deeply (more than 8 pending operands)")
     for k, ins in enumerate(prog):
         dst[k].op = ins[0]
         if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG):
