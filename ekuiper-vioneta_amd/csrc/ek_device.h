@@ -50,6 +50,8 @@ struct DPlan {
     int32_t n_user_cols;          // columns of the caller's batch; [n_user_cols, n_columns) are derived (aggregate args)
     int32_t n_derived_prog[EK_MAX_DERIVED];
     ek_instr derived_prog[EK_MAX_DERIVED][EK_MAX_PROG];
+    int32_t n_first;              // EK_AGG_FIRST aggregates (non-aggregate select fields; range mode)
+    int32_t first_col[EK_MAX_AGGS];   // their source columns (the aggregate itself is the min buffer position)
     int32_t pseudo_keys;          // no GROUP BY in pane mode: rows spread over kPseudoKeys partial slots by row index
                                   // (merged per window by k_finalize_merge) instead of one partition
     ek_instr begin_prog[EK_MAX_PROG];

@@ -340,10 +340,12 @@ struct Engine {
                 return fail(EK_ERR_INVALID, "HAVING aggregate slot out of range");
         }
         wtype = plan.window_type;
-        bool sort_aggs = false;
-        for (int k = 0; k < plan.n_aggs; ++k)
+        bool sort_aggs = false, has_first = false;
+        for (int k = 0; k < plan.n_aggs; ++k) {
             sort_aggs |= plan.aggs[k].fn == EK_AGG_MEDIAN || plan.aggs[k].fn == EK_AGG_PERCENTILE_CONT ||
                          plan.aggs[k].fn == EK_AGG_PERCENTILE_DISC;
+            has_first |= plan.aggs[k].fn == EK_AGG_FIRST;
+        }
         n_out = plan.n_aggs;
         if (wtype == EK_WINDOW_NONE) {
             // a rule without window and aggregates: FilterOp (WHERE) + SELECT * per event (C1 shape)
@@ -403,6 +405,9 @@ struct Engine {
             if (plan.n_where > 0)
                 return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
                                                 "(FilterPlan above IncWindowPlan): not built");
+            if (has_first)
+                return fail(EK_ERR_UNSUPPORTED, "incremental windows emit the group's LAST row (window_inc_agg_op.go:443-457): "
+                                                "first-row select fields are not on that path");
             for (int k = 0; k < plan.n_aggs; ++k)
                 if (plan.aggs[k].fn != EK_AGG_COUNT_STAR && ((plan.nullable_mask >> plan.aggs[k].column) & 1u))
                     return fail(EK_ERR_UNSUPPORTED, "incremental aggregates over a nullable column (nil at a group's last row) are not built");
@@ -411,7 +416,7 @@ struct Engine {
         // earlier pushes, so the events are kept (range mode) instead of being folded into pane partials
         range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT ||
                      (wtype == EK_WINDOW_HOPPING && plan.is_event_time && plan.late_tolerance_ms > 0) ||
-                     wtype == EK_WINDOW_STATE || sort_aggs ||
+                     wtype == EK_WINDOW_STATE || sort_aggs || has_first ||
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
             return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
@@ -498,8 +503,32 @@ struct Engine {
             dp.agg_p[k] = a.param;
             dp.agg_vc[k] = -1;
             dp.agg_sidx[k] = -1;
-            if (a.fn < EK_AGG_COUNT_STAR || a.fn > EK_AGG_PERCENTILE_DISC) return fail(EK_ERR_INVALID, "bad aggregate %d", a.fn);
+            if (a.fn < EK_AGG_COUNT_STAR || a.fn > EK_AGG_FIRST) return fail(EK_ERR_INVALID, "bad aggregate %d", a.fn);
             if (a.fn == EK_AGG_COUNT_STAR) continue;
+            if (a.fn == EK_AGG_FIRST) {
+                // the group's first row = the minimum of the hidden position column (value = event-buffer index,
+                // buffer_view) over its rows; k_first_fetch reads the source column there
+                if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "first-row field column out of range");
+                if (rowpos_col < 0) {
+                    if (plan.n_columns >= EK_MAX_COLUMNS) return fail(EK_ERR_UNSUPPORTED, "too many columns for a first-row field");
+                    rowpos_col = plan.n_columns;
+                    dp.col_type[rowpos_col] = EK_COL_I64;
+                }
+                int v = -1;
+                for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == rowpos_col) v = x;
+                if (v < 0) {
+                    if (dp.n_vc >= kMaxVC) return fail(EK_ERR_UNSUPPORTED, "too many aggregated columns");
+                    v = dp.n_vc++;
+                    dp.vc_col[v] = rowpos_col;
+                    dp.vc_is_float[v] = 0;
+                    dp.vc_flags[v] = 0;
+                }
+                dp.agg_vc[k] = v;
+                dp.vc_flags[v] |= NEED_MIN;
+                dp.first_col[k] = a.column;
+                dp.n_first++;
+                continue;
+            }
             if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "aggregate column out of range");
             int v = -1;
             for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == a.column) v = x;
@@ -1239,6 +1268,37 @@ struct Engine {
     // Un-grouped rule over a ts-sorted group (k_ung_tile): one pass over the referenced columns, a partial per
     // (tile, pane segment) merged into pseudo-key slot tile mod kPseudoKeys (EKGPU_UNG=0: the k_part + k_agg path).
     int ung_mode = 1;
+    int rowpos_col = -1;      // hidden position column of first-row fields (buffer_view: event-buffer index)
+    DevBuf rowpos;            // its values 0, 1, 2, ... (grown with the buffer)
+    int64_t rowpos_n = 0;
+    int ensure_rowpos(int64_t n) {
+        if (rowpos_col < 0 || n <= rowpos_n) return 0;
+        const int64_t want = std::max<int64_t>(n, std::max<int64_t>(2 * rowpos_n, 1 << 16));
+        if (int rc = ensure(rowpos, (size_t)want * 8)) return rc;
+        hipLaunchKernelGGL(k_iota64, dim3((unsigned)std::min<int64_t>(8192, (want + 255) / 256)), dim3(256), 0, stream,
+                           (int64_t*)rowpos.p, (int64_t)0, want);
+        rowpos_n = want;
+        return 0;
+    }
+    // first-row select fields of the windows this fire emitted: swap each slot's position for the value
+    int first_fetch(const std::vector<int32_t>& slots, const std::vector<int64_t>& obase) {
+        std::vector<int32_t> ws;
+        std::vector<int64_t> wb;
+        for (size_t w = 0; w < slots.size(); ++w)
+            if (slots[w] >= 0) { ws.push_back(slots[w]); wb.push_back(obase[w]); }
+        if (ws.empty()) return 0;
+        const size_t nw = ws.size();
+        if (int rc = ensure(ff_d, nw * 12 + 16)) return rc;
+        int64_t* d_wb = (int64_t*)ff_d.p;
+        int32_t* d_ws = (int32_t*)(d_wb + nw);
+        hipMemcpyAsync(d_wb, wb.data(), nw * 8, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(d_ws, ws.data(), nw * 4, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_first_fetch, dim3((unsigned)nw), dim3(256), 0, stream, d_plan, buffer_view(), (const int32_t*)d_ws,
+                           (const int64_t*)d_wb, results_view());
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "first-row fetch failed");
+        return 0;
+    }
+    DevBuf ff_d;
     int launch_ung(const DBatch& db, GroupDesc gd, const uint8_t* d_acc, int32_t* perr, int64_t* pmc,
                    unsigned long long* pmh, bool any_fresh) {
         if (any_fresh) {
@@ -1414,6 +1474,7 @@ struct Engine {
             d.col[c] = eb.col[c].p;
             d.valid[c] = eb_valid_on[c] ? (const uint8_t*)eb.valid[c].p : nullptr;
         }
+        if (rowpos_col >= 0) d.col[rowpos_col] = rowpos.p;
         return d;
     }
 
@@ -1612,6 +1673,7 @@ struct Engine {
     int fire_windows(std::vector<PendWin>& pw) {
         const int nq = (int)pw.size();
         if (nq == 0) { hop_discard_pending = false; return 0; }
+        if (int rc = ensure_rowpos(eb.n)) return rc;
         if (int rc = ensure(rq_d, (size_t)nq * sizeof(RangeQ))) return rc;
         if (int rc = ensure(ab_d, (size_t)nq * 16)) return rc;
         std::vector<RangeQ> hq(nq);
@@ -1717,6 +1779,8 @@ struct Engine {
             if (members.empty()) continue;
             if (int rc = run_vgroup(members, V, obase, slots)) return rc;
         }
+        if (dp.n_first > 0)
+            if (int rc = first_fetch(slots, obase)) return rc;
         // windows never start below the last fired one's start (overlapping) or end (disjoint)
         const bool overlap = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_COUNT;
         eb_floor = std::max(eb_floor, overlap ? h_ab[2 * (nq - 1)] : h_ab[2 * (nq - 1) + 1]);
@@ -3834,7 +3898,7 @@ struct Engine {
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
                           &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d,
-                          &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag})
+                          &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag, &rowpos, &ff_d})
             release(*d);
         for (int v = 0; v < kMaxVC; ++v) { release(km_val[v]); release(km_ok[v]); }
         if (h_kmf) hipHostFree(h_kmf);

@@ -762,6 +762,10 @@ template <int NVC>
 __device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int k, const SortRes* sr = nullptr) {
     const int fn = p.agg_fn[k];
     if (fn == EK_AGG_COUNT_STAR) return Val{V_I64, s.cnt, 0.0};
+    if (fn == EK_AGG_FIRST) {   // the group's first row: min event-buffer position (k_first_fetch swaps in the value)
+        const int v = p.agg_vc[k];
+        return sel(s.vcnt, v) ? Val{V_I64, ord_to_i64(sel(s.omn, v)), 0.0} : Val{V_NULL, 0, 0.0};
+    }
     if (fn >= EK_AGG_MEDIAN) {
         if (!sr) return Val{V_ERR, 0, 0.0};
         const int e = p.agg_sidx[k] * sr->kk + sr->kl;

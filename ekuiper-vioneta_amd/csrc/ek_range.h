@@ -389,6 +389,35 @@ __global__ void k_arrivals_of(const int64_t* __restrict__ bidx, int64_t nb, int6
         out[k] = arr_base + bidx[k];
 }
 
+// ---------------------------------------------------------------- first-row select fields
+// A non-aggregate select field takes the column's value in the group's FIRST row (row.go:720-726: GroupedTuples
+// .Content[0]; the group keeps its rows in window order). Every aggregation path folds the hidden position column
+// (value = the row's event-buffer index, i.e. the window order) with MIN, so an emitted EK_AGG_FIRST slot holds the
+// first row's position; one block per window fired by this push then swaps in the source column's value there
+// (nil when that value is null).
+__global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* __restrict__ wslot,
+                              const int64_t* __restrict__ wbase, Results res) {
+    const DPlan& p = *pp;
+    const int32_t slot = wslot[blockIdx.x];
+    const int64_t base = wbase[blockIdx.x], cnt = res.win_cnt[slot];
+    for (int64_t r = base + threadIdx.x; r < base + cnt; r += blockDim.x) {
+        for (int q = 0; q < p.n_aggs; ++q) {
+            if (p.agg_fn[q] != EK_AGG_FIRST || res.tag[q][r] != EK_TAG_I64) continue;
+            const int64_t pos = res.val[q][r];
+            const int c = p.first_col[q];
+            if (!col_valid(b, c, pos)) {
+                res.tag[q][r] = EK_TAG_NULL;
+                res.val[q][r] = 0;
+            } else if (p.col_type[c] == EK_COL_F64) {
+                res.tag[q][r] = EK_TAG_F64;
+                res.val[q][r] = ((const int64_t*)b.col[c])[pos];
+            } else {
+                res.val[q][r] = col_i64(p, b, c, pos);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- small range windows: one workgroup per window
 // For a window of at most kSmallWin rows (COUNTWINDOW(1000), state windows, short sliding windows) the pane/bucket
 // partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here one

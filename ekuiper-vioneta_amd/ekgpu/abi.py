@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 5
+EKGPU_ABI_VERSION = 6
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -25,7 +25,7 @@ EK_COL_I64, EK_COL_F64, EK_COL_U32 = 1, 2, 3
 
 (EK_AGG_COUNT_STAR, EK_AGG_COUNT, EK_AGG_SUM, EK_AGG_AVG, EK_AGG_MIN, EK_AGG_MAX, EK_AGG_STDDEV,
  EK_AGG_STDDEVS, EK_AGG_VAR, EK_AGG_VARS, EK_AGG_MEDIAN, EK_AGG_PERCENTILE_CONT,
- EK_AGG_PERCENTILE_DISC) = range(1, 14)
+ EK_AGG_PERCENTILE_DISC, EK_AGG_FIRST) = range(1, 15)
 AGG_BY_NAME = {
     "count": EK_AGG_COUNT, "sum": EK_AGG_SUM, "avg": EK_AGG_AVG, "min": EK_AGG_MIN, "max": EK_AGG_MAX,
     "stddev": EK_AGG_STDDEV, "stddevs": EK_AGG_STDDEVS, "var": EK_AGG_VAR, "vars": EK_AGG_VARS,

@@ -482,7 +482,13 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
                 fields.append(OutputField(f.name, "dim", group_dims.index(cname)))
                 continue
             if f.slot != key_col:
-                raise RuleError(f"non-aggregate field {f.name} must be a GROUP BY dimension")
+                # a non-aggregate, non-dimension field: the column's value in the group's first row (row.go:720-726);
+                # lowered to the engine's EK_AGG_FIRST (range mode)
+                if len(p.aggs) >= A.EK_MAX_AGGS:
+                    raise RuleError("too many aggregate calls")
+                p.aggs.append((A.EK_AGG_FIRST, f.slot, 0.0))
+                fields.append(OutputField(f.name, "agg", len(p.aggs) - 1))
+                continue
             fields.append(OutputField(f.name, "key"))
         else:
             fields.append(f)

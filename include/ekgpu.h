@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 5
+#define EKGPU_ABI_VERSION 6
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -69,7 +69,9 @@ enum {
     EK_AGG_VARS = 10,           /* stats.SampleVariance             funcs_agg.go:275-297          */
     EK_AGG_MEDIAN = 11,         /* funcs_agg.go:29-55,415-428                                     */
     EK_AGG_PERCENTILE_CONT = 12,/* stats.Percentile(sorted, p*100)  funcs_agg.go:298-334          */
-    EK_AGG_PERCENTILE_DISC = 13 /* stats.PercentileNearestRank      funcs_agg.go:335-370          */
+    EK_AGG_PERCENTILE_DISC = 13,/* stats.PercentileNearestRank      funcs_agg.go:335-370          */
+    EK_AGG_FIRST = 14           /* a non-aggregate select field: the column's value in the group's
+                                   FIRST row (row.go:720-726, project_operator.go:136-207); ABI v6   */
 };
 
 /* Expression programs (WHERE / HAVING / OVER(WHEN ...)) in postfix form.

@@ -251,6 +251,10 @@ static void agg_eval(int fn, int is_float, int64_t n, const int64_t* iv, const d
     for (int64_t k = 0; k < n; ++k) if (!vnull[k]) { if (first < 0) first = k; cnt++; }
     switch (fn) {
     case EK_AGG_COUNT_STAR: o->tag = EK_TAG_I64; o->i = n; return;
+    case EK_AGG_FIRST:                                                 /* row.go:720-726: the group's first row */
+        if (n == 0 || vnull[0]) return;                                /* nil */
+        if (is_float) { o->tag = EK_TAG_F64; o->f = fv[0]; } else { o->tag = EK_TAG_I64; o->i = iv[0]; }
+        return;
     case EK_AGG_COUNT: o->tag = EK_TAG_I64; o->i = cnt; return;        /* getCount */
     case EK_AGG_SUM:                                                   /* funcs_agg.go:114-143 */
     case EK_AGG_AVG: {                                                 /* funcs_agg.go:56-86 */

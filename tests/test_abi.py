@@ -86,8 +86,12 @@ def test_compile_baseline_configs():
     r = compile_rule("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
                      "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)", IOT_SCHEMA, num_keys=100)
     assert r.plan.aggs[1].fn == A.EK_AGG_PERCENTILE_CONT and r.plan.aggs[1].param == 0.9
-    with pytest.raises(RuleError):
-        compile_rule("SELECT temperature FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", IOT_SCHEMA, num_keys=4)
+    # a non-aggregate, non-dimension field: the group's first row (row.go:720-726) -> EK_AGG_FIRST
+    r = compile_rule("SELECT temperature FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", IOT_SCHEMA, num_keys=4)
+    assert r.plan.n_aggs == 1 and r.plan.aggs[0].fn == A.EK_AGG_FIRST
+    with pytest.raises(RuleError):   # ... but not over a string column
+        compile_rule("SELECT name FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", dict(IOT_SCHEMA, name="string"),
+                     num_keys=4)
 
 
 def test_engine_without_gpu_fails_loudly():
