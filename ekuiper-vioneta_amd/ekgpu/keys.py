@@ -84,6 +84,9 @@ class StringDict:
             out[i] = c
         return out
 
+    def decode(self, codes) -> List[str]:
+        return [self.values[int(c)] for c in codes]
+
 
 def _canon_bits(col: np.ndarray) -> np.ndarray:
     """Value identity of a numeric column as int64: floats by bit pattern (so -0 and 0 stay apart, as "%v" prints

@@ -89,6 +89,21 @@ class CompiledRule:
             vout.append(None)
         return out, (vout if any(v is not None for v in vout) else None)
 
+    def decode_value(self, slot: int, values, tags) -> list:
+        """Result values of aggregate slot `slot` -> python values: a first-row field over a string column is a
+        dictionary code mapped back to its string; nil -> None."""
+        fn, c = self.plan.aggs[slot].fn, self.plan.aggs[slot].column
+        name = self.columns[c] if 0 <= c < len(self.columns) else None
+        out = []
+        for v, t in zip(values, tags):
+            if t == A.EK_TAG_NULL:
+                out.append(None)
+            elif fn == A.EK_AGG_FIRST and name in self.string_dicts:
+                out.append(self.string_dicts[name].values[int(v)])
+            else:
+                out.append(v)
+        return out
+
     def decode_keys(self, keys) -> list:
         """Result key ids -> the GROUP BY dimension values (the group's first row), as tuples."""
         if self.key_dict is not None:
@@ -494,7 +509,8 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
             fields.append(f)
     strings = {c for c, t in schema.items() if t == "string"}
     if strings:
-        used = {p.columns[c] for (_, c, _) in p.aggs if c >= 0 and c < len(p.columns)}
+        # a first-row field over a string column carries its dictionary code (decode_value maps it back)
+        used = {p.columns[c] for (fn, c, _) in p.aggs if c >= 0 and c < len(p.columns) and fn != A.EK_AGG_FIRST}
         for prog in [where, having, trigger, begin, emit] + [list(pr) for pr, _ in p.derived]:
             used |= {p.columns[ins[1]] for ins in prog if ins[0] == A.EK_OP_COL and ins[1] < len(p.columns)}
         if used & strings:

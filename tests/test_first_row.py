@@ -43,3 +43,18 @@ def test_oracle_project_kat_first_row(oracle):
         for key, tag, val in zip(w[0].keys, w[0].tags[0], w[0].values[0]):
             got[int(key)] = ("nil", None) if tag == A.EK_TAG_NULL else ("i", int(val))
         assert got == expect
+
+
+def test_first_row_string_field_lowering_and_oracle(oracle):
+    """A first-row field over a string column carries the column's dictionary code; decode_value maps it back."""
+    schema = {"k": "key", "ts": "bigint", "name": "string", "x": "float"}
+    rule = compile_rule("SELECT k, name, max(x) FROM s GROUP BY k, TUMBLINGWINDOW(ss, 1)", schema, num_keys=3)
+    assert rule.plan.aggs[1].fn == A.EK_AGG_FIRST
+    names = ["b", "a", "c", "b", "z"]
+    cols, _ = rule.device_columns([np.array([0, 1, 0, 1, 2], np.uint32),
+                                   np.array([T0, T0 + 1, T0 + 2, T0 + 3, T0 + 1000], np.int64), names,
+                                   np.array([1.0, 2.0, 3.0, 4.0, 5.0])])
+    run = oracle.run(rule.plan, cols)
+    w = [w for w in run.windows if len(w.keys)][0]
+    got = dict(zip((int(k) for k in w.keys), rule.decode_value(1, w.values[1], w.tags[1])))
+    assert got == {0: "b", 1: "a"}

@@ -81,3 +81,25 @@ def test_first_row_key_major_and_window_major(oracle, engine_mod, km, monkeypatc
     assert len(exp.windows) > 50
     assert (st.windows_keymajor > 0) == (km == "1")
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_first_row_string_field(oracle, engine_mod):
+    """A first-row field over a string column: the engine returns the dictionary code of the first row's string."""
+    schema = {"deviceId": "key", "ts": "bigint", "name": "string", "x": "float"}
+    n = 40_000
+    rng = np.random.default_rng(21)
+    words = np.array(["alpha", "beta", "gamma", "delta", "eps"])
+    raw = [rng.integers(0, 200, n).astype(np.uint32), (1541152480000 + np.arange(n) // 10).astype(np.int64),
+           list(words[rng.integers(0, 5, n)]), rng.uniform(0, 1, n)]
+    rule = compile_rule("SELECT deviceId, name, max(x) FROM s GROUP BY deviceId, TUMBLINGWINDOW(ms, 700)", schema,
+                        num_keys=200, debug_membership=True)
+    cols, _ = rule.device_columns(raw)
+    got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=2)
+    assert len(exp.windows) >= 3
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+    w = got[0]
+    first = {}
+    for i in range(n):   # the oracle-independent check of one window: the first row of each key in [start, end)
+        if w.start <= raw[1][i] < w.end and int(raw[0][i]) not in first:
+            first[int(raw[0][i])] = raw[2][i]
+    assert dict(zip(map(int, w.keys), rule.decode_value(1, w.values[1], w.tags[1]))) == first
