@@ -88,6 +88,60 @@ class StringDict:
         return [self.values[int(c)] for c in codes]
 
 
+class OrderedStringDict:
+    """Order-preserving int64 codes of a string column whose min / max the rule aggregates
+    (internal/binder/function/common_array_funcs.go:49,86: Go compares strings bytewise, which for UTF-8 is code point
+    order, i.e. Python's str order). A new string takes the midpoint between the codes of its sorted neighbours, so the
+    codes of strings already on the device never change and the engine's integer min / max over codes is the
+    lexicographic min / max. Codes start spread over +-2^61; a gap that can no longer be split (about 60 insertions
+    between the same two neighbours) raises, rather than re-coding data already pushed."""
+
+    LO, HI = -(1 << 61), 1 << 61
+
+    def __init__(self):
+        self.code: Dict[str, int] = {}
+        self.sorted: List[str] = []
+        self.codes: List[int] = []          # codes of self.sorted, ascending
+        self.by_code: Dict[int, str] = {}
+
+    def _add(self, s: str) -> int:
+        import bisect
+        i = bisect.bisect_left(self.sorted, s)
+        lo = self.codes[i - 1] if i > 0 else self.LO
+        hi = self.codes[i] if i < len(self.codes) else self.HI
+        if hi - lo < 2:
+            raise ValueError("ordered string dictionary: no code left between neighbours of %r" % s)
+        c = (lo + hi) // 2
+        self.sorted.insert(i, s)
+        self.codes.insert(i, c)
+        self.code[s] = c
+        self.by_code[c] = s
+        return c
+
+    def encode(self, col) -> np.ndarray:
+        out = np.empty(len(col), np.int64)
+        code = self.code
+        for i, s in enumerate(col):
+            c = code.get(s)
+            out[i] = c if c is not None else self._add(s)
+        return out
+
+    def decode(self, codes) -> List[str]:
+        return [self.by_code[int(c)] for c in codes]
+
+    @property
+    def values(self):
+        return _ByCode(self.by_code)
+
+
+class _ByCode:
+    def __init__(self, by_code):
+        self.by_code = by_code
+
+    def __getitem__(self, c):
+        return self.by_code[int(c)]
+
+
 def _canon_bits(col: np.ndarray) -> np.ndarray:
     """Value identity of a numeric column as int64: floats by bit pattern (so -0 and 0 stay apart, as "%v" prints
     them apart) with every NaN folded into one pattern ("NaN")."""

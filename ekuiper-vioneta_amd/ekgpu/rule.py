@@ -24,7 +24,7 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
 from . import abi as A
-from .keys import GroupKeyDict, StringDict
+from .keys import GroupKeyDict, OrderedStringDict, StringDict
 
 _TOKEN = re.compile(r"\s*(?:(\d+\.\d*|\.\d+|\d+(?:[eE][-+]?\d+)?)|([A-Za-z_][A-Za-z0-9_.]*)|(<=|>=|!=|<>|[=<>(),*+\-/%])|(\"[^\"]*\"|'[^']*'))")
 
@@ -98,7 +98,7 @@ class CompiledRule:
         for v, t in zip(values, tags):
             if t == A.EK_TAG_NULL:
                 out.append(None)
-            elif fn == A.EK_AGG_FIRST and name in self.string_dicts:
+            elif fn in (A.EK_AGG_FIRST, A.EK_AGG_MIN, A.EK_AGG_MAX) and name in self.string_dicts:
                 out.append(self.string_dicts[name].values[int(v)])
             else:
                 out.append(v)
@@ -508,13 +508,20 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
         else:
             fields.append(f)
     strings = {c for c, t in schema.items() if t == "string"}
+    # string columns aggregated by min / max (common_array_funcs.go:49,86): order-preserving int64 codes
+    # (OrderedStringDict), so the engine's integer min / max is the lexicographic one; first-row fields and count()
+    # over a string column need only its codes / validity
+    ordered = {p.columns[c] for (fn, c, _) in p.aggs
+               if fn in (A.EK_AGG_MIN, A.EK_AGG_MAX) and 0 <= c < len(p.columns) and p.columns[c] in strings}
+    for c in ordered:
+        plan.column_type[p.columns.index(c)] = A.EK_COL_I64
     if strings:
-        # a first-row field over a string column carries its dictionary code (decode_value maps it back)
-        used = {p.columns[c] for (fn, c, _) in p.aggs if c >= 0 and c < len(p.columns) and fn != A.EK_AGG_FIRST}
+        free = (A.EK_AGG_FIRST, A.EK_AGG_COUNT, A.EK_AGG_MIN, A.EK_AGG_MAX)
+        used = {p.columns[c] for (fn, c, _) in p.aggs if c >= 0 and c < len(p.columns) and fn not in free}
         for prog in [where, having, trigger, begin, emit] + [list(pr) for pr, _ in p.derived]:
             used |= {p.columns[ins[1]] for ins in prog if ins[0] == A.EK_OP_COL and ins[1] < len(p.columns)}
         if used & strings:
-            raise RuleError(f"string column(s) {sorted(used & strings)} may only be GROUP BY dimensions")
+            raise RuleError(f"string column(s) {sorted(used & strings)} may only be GROUP BY dimensions, min / max / count arguments or first-row fields")
     plan.n_aggs = len(p.aggs)
     for k, (fn, c, prm) in enumerate(p.aggs):
         plan.aggs[k].fn = fn
@@ -533,7 +540,7 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
         raise RuleError("num_keys (dictionary size of the GROUP BY key) is required")
     return CompiledRule(plan=plan, columns=list(schema.keys()), fields=fields, sql=sql,
                         group_dims=list(group_dims or []), schema=dict(schema),
-                        string_dicts={c: StringDict() for c in strings},
+                        string_dicts={c: (OrderedStringDict() if c in ordered else StringDict()) for c in strings},
                         options=dict(isEventTime=is_event_time, lateTolerance=late_tolerance_ms,
                                      planOptimizeStrategy=dict(enableIncrementalWindow=bool(incremental),
                                                                windowOption=dict(windowVersion=window_version))))

@@ -89,8 +89,8 @@ def test_compile_baseline_configs():
     # a non-aggregate, non-dimension field: the group's first row (row.go:720-726) -> EK_AGG_FIRST
     r = compile_rule("SELECT temperature FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", IOT_SCHEMA, num_keys=4)
     assert r.plan.n_aggs == 1 and r.plan.aggs[0].fn == A.EK_AGG_FIRST
-    with pytest.raises(RuleError):   # string columns: GROUP BY dimensions and first-row fields only
-        compile_rule("SELECT max(name) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", dict(IOT_SCHEMA, name="string"),
+    with pytest.raises(RuleError):   # string columns: dimensions, min / max / count arguments, first-row fields
+        compile_rule("SELECT sum(name) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss,10)", dict(IOT_SCHEMA, name="string"),
                      num_keys=4)
 
 

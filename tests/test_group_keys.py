@@ -96,7 +96,7 @@ def test_composite_rule_lowering():
     assert r.plan.key_column == len(SCHEMA) and r.plan.column_type[len(SCHEMA)] == A.EK_COL_U32
     assert [f.kind for f in r.fields] == ["dim", "dim", "agg", "agg", "agg"]
     with pytest.raises(RuleError):   # a string column inside an aggregate
-        compile_rule("SELECT count(color) FROM demo GROUP BY deviceId, color, TUMBLINGWINDOW(ss, 1)", SCHEMA, num_keys=10)
+        compile_rule("SELECT avg(color) FROM demo GROUP BY deviceId, color, TUMBLINGWINDOW(ss, 1)", SCHEMA, num_keys=10)
     # one key-typed dimension keeps the direct path
     r1 = compile_rule("SELECT k, count(*) FROM s GROUP BY k, TUMBLINGWINDOW(ss, 1)", {"k": "key", "ts": "bigint"}, num_keys=4)
     assert r1.key_dict is None and r1.plan.key_column == 0
