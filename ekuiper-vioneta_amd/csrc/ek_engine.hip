@@ -623,6 +623,7 @@ struct Engine {
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
+        eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
@@ -1432,6 +1433,24 @@ struct Engine {
     EvBuf eb, eb_alt;
     int64_t eb_base = 0;               // absolute stream position of buffer index 0
     bool eb_valid_on[EK_MAX_COLUMNS] = {};
+    // columns a range-mode kernel can read from the buffer (key, ts, aggregated / sorted value columns, WHERE /
+    // trigger / STATEWINDOW condition columns, first-row sources); eb_append skips the others (the buffer keeps
+    // their slot, contents unspecified and never read)
+    bool eb_need[EK_MAX_COLUMNS] = {};
+    void eb_need_init() {
+        for (int c = 0; c < EK_MAX_COLUMNS; ++c) eb_need[c] = false;
+        auto mark = [&](int c) { if (c >= 0 && c < EK_MAX_COLUMNS) eb_need[c] = true; };
+        mark(dp.key_col);
+        mark(dp.ts_col);
+        for (int v = 0; v < dp.n_vc; ++v) mark(dp.vc_col[v]);
+        for (int k = 0; k < plan.n_aggs; ++k) if (plan.aggs[k].fn == EK_AGG_FIRST) mark(plan.aggs[k].column);
+        auto prog = [&](const ek_instr* pr, int n) { for (int k = 0; k < n; ++k) if (pr[k].op == EK_OP_COL) mark(pr[k].arg); };
+        prog(plan.where_prog, plan.n_where);
+        prog(plan.trigger_prog, plan.n_trigger);
+        prog(plan.begin_prog, plan.n_begin);
+        prog(plan.emit_prog, plan.n_emit);
+        if (env_int("EKGPU_EB_ALL_COLUMNS", 0)) for (int c = 0; c < EK_MAX_COLUMNS; ++c) eb_need[c] = true;
+    }
     bool need_rel = false;             // sliding windows: per-event release step (closed right boundary)
     int64_t eb_rel = 0;                // released prefix (buffer index)
     int64_t eb_floor = 0;              // smallest buffer index a future window can start at
@@ -1530,8 +1549,9 @@ struct Engine {
         if (int rc = eb_reserve(cnt)) return rc;
         for (int c = 0; c < plan.n_columns; ++c) {
             const size_t es = col_es(c);
-            hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
-                           hipMemcpyDeviceToDevice, stream);
+            if (eb_need[c])
+                hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
+                               hipMemcpyDeviceToDevice, stream);
             if (eb_valid_on[c]) {
                 if (db.valid[c]) hipMemcpyAsync((uint8_t*)eb.valid[c].p + eb.n, db.valid[c] + start, (size_t)cnt, hipMemcpyDeviceToDevice, stream);
                 else fill_valid_ones(c, eb.n, cnt);
