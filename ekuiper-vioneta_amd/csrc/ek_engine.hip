@@ -623,6 +623,7 @@ struct Engine {
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
+        grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
@@ -1870,6 +1871,105 @@ struct Engine {
     }
 
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
+    int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
+    DevBuf grp_tiles, grp_cnt, grp_base;
+    std::vector<unsigned int> grp_h;
+    std::vector<int64_t> grp_hb;
+    std::vector<GrpTile> grp_ht;
+
+    // ek_keymajor.h k_grp_*: two MSD partition passes (8-bit digits of the key) into sub-buckets of 2^s2 keys,
+    // then one workgroup per sub-bucket groups its rows by key in LDS and emits. *ok = false: a sub-bucket holds
+    // more rows than kGrpCap (skewed keys) -> the caller's radix-sorted path (nothing was written).
+    int grp_run(const DBatch& bv, int64_t lo, int64_t n, int32_t wslot, int64_t wobase, bool sort, bool* ok) {
+        *ok = false;
+        int kb = 17;
+        while ((1ull << kb) < (uint64_t)K) kb++;
+        const int s1 = kb - 8, s2 = s1 - 8;
+        const int nb1 = (int)(((uint64_t)K - 1) >> s1) + 1, nsub = nb1 * 256;
+        const uint32_t* key0 = (const uint32_t*)bv.col[dp.key_col] + lo;
+        const int64_t* val0 = (const int64_t*)bv.col[dp.vc_col[0]] + lo;
+        for (int i = 0; i < 2; ++i) {
+            if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
+            if (int rc = ensure(km_val[i], (size_t)n * 8)) return rc;
+        }
+        const int64_t nt1 = (n + kGrpTile - 1) / kGrpTile;
+        const int64_t nt_cap = nt1 + nb1 + 1;
+        if (int rc = ensure(grp_tiles, (size_t)nt_cap * sizeof(GrpTile) * 2)) return rc;
+        if (int rc = ensure(grp_cnt, (size_t)(256 + nsub) * 2 * 4)) return rc;
+        if (int rc = ensure(grp_base, (size_t)(256 + nsub + 1) * 8)) return rc;
+        GrpTile* d_t1 = (GrpTile*)grp_tiles.p;
+        GrpTile* d_t2 = d_t1 + nt_cap;
+        unsigned int* tot1 = (unsigned int*)grp_cnt.p;
+        unsigned int* cur1 = tot1 + 256;
+        unsigned int* tot2 = cur1 + 256;
+        unsigned int* cur2 = tot2 + nsub;
+        int64_t* base1 = (int64_t*)grp_base.p;
+        int64_t* base2 = base1 + 256;
+        grp_ht.resize((size_t)nt1);
+        for (int64_t t = 0; t < nt1; ++t)
+            grp_ht[t] = GrpTile{t * kGrpTile, (int32_t)std::min<int64_t>(kGrpTile, n - t * kGrpTile), 0};
+        hipMemcpyAsync(d_t1, grp_ht.data(), (size_t)nt1 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
+        hipMemsetAsync(grp_cnt.p, 0, (size_t)(512 + 2 * nsub) * 4, stream);
+        const int ph = phase_begin(EK_PHASE_PARTITION);
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, K, tot1);
+        grp_h.resize(256);
+        hipMemcpyAsync(grp_h.data(), tot1, 256 * 4, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping histogram failed");
+        grp_hb.assign(256 + nsub + 1, 0);
+        int64_t acc = 0;
+        grp_ht.clear();
+        for (int b = 0; b < 256; ++b) {
+            grp_hb[b] = acc;
+            for (int64_t r = 0; r < grp_h[b]; r += kGrpTile)
+                grp_ht.push_back(GrpTile{acc + r, (int32_t)std::min<int64_t>(kGrpTile, grp_h[b] - r), b * 256});
+            acc += grp_h[b];
+        }
+        const int64_t nt2 = (int64_t)grp_ht.size();
+        hipMemcpyAsync(base1, grp_hb.data(), 256 * 8, hipMemcpyHostToDevice, stream);
+        if (nt2 > 0) hipMemcpyAsync(d_t2, grp_ht.data(), (size_t)nt2 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1, K,
+                           (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p);
+        if (nt2 > 0)
+            hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
+                               (const GrpTile*)d_t2, s2, K, tot2);
+        grp_h.resize((size_t)nsub);
+        hipMemcpyAsync(grp_h.data(), tot2, (size_t)nsub * 4, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping pass 1 failed");
+        acc = 0;
+        unsigned int mx = 0;
+        for (int i = 0; i < nsub; ++i) { grp_hb[256 + i] = acc; acc += grp_h[i]; mx = std::max(mx, grp_h[i]); }
+        grp_hb[256 + nsub] = acc;
+        if (mx > (unsigned int)kGrpCap) { phase_end(ph); return 0; }
+        hipMemcpyAsync(base2, grp_hb.data() + 256, (size_t)(nsub + 1) * 8, hipMemcpyHostToDevice, stream);
+        if (nt2 > 0)
+            hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
+                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, K, (const int64_t*)base2, cur2,
+                               (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p);
+        phase_end(ph);
+        GrpDesc g{};
+        g.base2 = base2;
+        g.keys = (const uint32_t*)km_k[1].p;
+        g.vals = (const int64_t*)km_val[1].p;
+        g.s1 = s1;
+        g.s2 = s2;
+        g.obase = wobase;
+        g.widx = wslot;
+        const Results rv = results_view();
+        const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
+        const size_t gl = grp_walk_lds(s2);
+        const dim3 gg((unsigned)nsub), gb(kGrpBlock);
+        if (dp.vc_is_float[0]) {
+            if (sort) hipLaunchKernelGGL((k_grp_walk<true, true>), gg, gb, gl, stream, d_plan, g, rv);
+            else hipLaunchKernelGGL((k_grp_walk<false, true>), gg, gb, gl, stream, d_plan, g, rv);
+        } else {
+            if (sort) hipLaunchKernelGGL((k_grp_walk<true, false>), gg, gb, gl, stream, d_plan, g, rv);
+            else hipLaunchKernelGGL((k_grp_walk<false, false>), gg, gb, gl, stream, d_plan, g, rv);
+        }
+        phase_end(ph2);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping walk failed");
+        *ok = true;
+        return 0;
+    }
     template <int N>
     void km_walk1(bool sort, size_t lds, int nblk, const KmDesc& d, const Results& rv) {
         if (sort) hipLaunchKernelGGL((k_km_walk<N, true, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
@@ -1901,6 +2001,17 @@ struct Engine {
         int end_bit = 1;
         while (end_bit < 32 && (1ull << end_bit) <= (uint64_t)K) end_bit++;
         const DBatch bv = buffer_view();
+        // one window, one value column without validity, no WHERE, 2^16 < K <= 2^27: MSD-partitioned grouping
+        if (nw == 1 && km_one && grp_on && dp.n_where == 0 && dp.n_vc == 1 && !bv.valid[dp.vc_col[0]] && K > 65536 &&
+            K <= (1u << 27)) {
+            bool ok = false;
+            if (int rc = grp_run(bv, lo, n, slots[wl[0]], obase[wl[0]], sort, &ok)) return rc;
+            if (ok) {
+                stats.windows_keymajor += 1;
+                *handled = true;
+                return 0;
+            }
+        }
         // one window over the whole span: the walk needs no positions; with one value column (no validity) the
         // column itself is sorted by key (no position payload, no gather)
         const bool one = nw == 1 && km_one;
@@ -3918,7 +4029,8 @@ struct Engine {
         }
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
                           &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d,
-                          &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag, &rowpos, &ff_d})
+                          &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag, &rowpos, &ff_d,
+                          &grp_tiles, &grp_cnt, &grp_base})
             release(*d);
         for (int v = 0; v < kMaxVC; ++v) { release(km_val[v]); release(km_ok[v]); }
         if (h_kmf) hipHostFree(h_kmf);

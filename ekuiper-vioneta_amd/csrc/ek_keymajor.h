@@ -358,6 +358,235 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     }
 }
 
+// ---------------------------------------------------------------- one window over a huge key space (C5 shape)
+// A window whose every row is a member and whose single value column is read without validity needs the rows
+// grouped by key, in no particular order inside a key (count / min / max / order statistics are order-free; the f64
+// sums stay within the north-star tolerance). Two MSD partition passes on 8-bit digits of the dense key
+// (k_grp_hist + k_grp_scatter: per 4096-row tile an LDS counting sort, one global reservation per (tile, digit),
+// runs written with consecutive lanes on consecutive addresses) cut the span into sub-buckets of 2^s2 keys; then
+// one workgroup per sub-bucket (k_grp_walk) loads its rows into LDS, counting-sorts them by key, and one thread per
+// key folds its LDS segment, sorts it in place for the order statistics, tests HAVING and emits (block-compacted).
+// 4 + 24 + 4 + 24 + 12 B per row instead of the radix sort's 3 passes + a random gather + a strided per-key walk.
+constexpr int kGrpTile = 4096;
+constexpr int kGrpBlock = 256;
+constexpr int kGrpCap = 4096;         // rows of one sub-bucket held in LDS by k_grp_walk (host-checked)
+
+struct GrpTile {
+    int64_t start;                    // first row of the tile in the pass's input
+    int32_t len;                      // rows (<= kGrpTile)
+    int32_t pre;                      // digit index offset (level 2: bucket * 256)
+};
+
+// totals per (pre + digit) of the tile's rows with key < K
+__global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restrict__ keys, const GrpTile* __restrict__ tiles,
+                                                        int shift, uint32_t K, unsigned int* __restrict__ tot) {
+    __shared__ unsigned int h[256];
+    const GrpTile t = tiles[blockIdx.x];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < t.len; i += kGrpBlock) {
+        const uint32_t k = keys[t.start + i];
+        if (k < K) atomicAdd(&h[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&tot[t.pre + threadIdx.x], h[threadIdx.x]);
+}
+
+// rows of a tile -> their (pre + digit) region: base[] exclusive region starts, cur[] reservation cursors
+__global__ __launch_bounds__(kGrpBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
+                                                           const GrpTile* __restrict__ tiles, int shift, uint32_t K,
+                                                           const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
+                                                           uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
+    __shared__ unsigned int h[256], lofs[257];
+    __shared__ int64_t gb[256];
+    __shared__ uint32_t s_key[kGrpTile];
+    __shared__ int64_t s_val[kGrpTile];
+    __shared__ uint8_t s_dig[kGrpTile];
+    __shared__ unsigned int wsum[kGrpBlock / 64];
+    const GrpTile t = tiles[blockIdx.x];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    constexpr int R = kGrpTile / kGrpBlock;
+    uint32_t k[R];
+    int64_t v[R];
+    int rk[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int i = threadIdx.x + j * kGrpBlock;
+        rk[j] = -1;
+        if (i >= t.len) continue;
+        k[j] = keys[t.start + i];
+        v[j] = vals[t.start + i];
+        if (k[j] < K) rk[j] = (int)atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const unsigned int c = h[threadIdx.x];
+    if (c) gb[threadIdx.x] = base[t.pre + threadIdx.x] + (int64_t)atomicAdd(&cur[t.pre + threadIdx.x], c);
+    lofs[threadIdx.x] = c;
+    __syncthreads();
+    block_excl_scan<kGrpBlock>(lofs, 256, wsum);   // lofs[256] = rows kept
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if (rk[j] < 0) continue;
+        const unsigned int d = (k[j] >> shift) & 255u;
+        const unsigned int p = lofs[d] + (unsigned int)rk[j];
+        s_key[p] = k[j];
+        s_val[p] = v[j];
+        s_dig[p] = (uint8_t)d;
+    }
+    __syncthreads();
+    const unsigned int m = lofs[256];
+    for (unsigned int p = threadIdx.x; p < m; p += kGrpBlock) {
+        const unsigned int d = s_dig[p];
+        const int64_t dst = gb[d] + (int64_t)(p - lofs[d]);
+        okeys[dst] = s_key[p];
+        ovals[dst] = s_val[p];
+    }
+}
+
+struct GrpDesc {
+    const int64_t* base2;             // [nsub + 1] sub-bucket row ranges in the level-2 output
+    const uint32_t* keys;
+    const int64_t* vals;
+    int s1, s2;                       // key = (bucket << s1) | (digit2 << s2) | local key
+    int64_t obase;                    // the window's result region
+    int32_t widx;
+    int32_t pad;
+};
+
+template <bool SORT, bool ISF>
+__global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, GrpDesc g, Results res) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char g_lds[];
+    const DPlan& p = *pp;
+    const int nloc = 1 << g.s2;                                   // keys of a sub-bucket (<= 2048)
+    int64_t* s_b = (int64_t*)g_lds;                               // [kGrpCap] values grouped by key
+    unsigned int* s_off = (unsigned int*)(s_b + kGrpCap);         // [nloc + 1] per-key counts -> offsets
+    unsigned int* s_cur = s_off + nloc + 1;                       // [nloc] scatter cursors
+    __shared__ unsigned int wsum[kGrpBlock / 64];
+    __shared__ uint32_t esh[20];
+    const int sb = blockIdx.x;
+    const int64_t r0 = g.base2[sb], r1 = g.base2[sb + 1];
+    const int m = (int)(r1 - r0);                                 // <= kGrpCap (host-checked)
+    if (m <= 0) return;                                           // uniform: no row, no emission
+    const uint32_t kbase = ((uint32_t)(sb >> 8) << g.s1) | ((uint32_t)(sb & 255) << g.s2);
+    const uint32_t mask = (uint32_t)nloc - 1u;
+    for (int i = threadIdx.x; i < nloc; i += kGrpBlock) s_off[i] = 0;
+    __syncthreads();
+    // counting sort by local key straight from the sub-bucket's rows (the keys are read twice, the second time from
+    // L2; no LDS staging copy, so four workgroups fit a CU)
+    for (int i = threadIdx.x; i < m; i += kGrpBlock) atomicAdd(&s_off[g.keys[r0 + i] & mask], 1u);
+    __syncthreads();
+    block_excl_scan<kGrpBlock>(s_off, nloc, wsum);
+    for (int i = threadIdx.x; i < nloc; i += kGrpBlock) s_cur[i] = s_off[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += kGrpBlock) s_b[atomicAdd(&s_cur[g.keys[r0 + i] & mask], 1u)] = g.vals[r0 + i];
+    __syncthreads();
+    constexpr bool isf = ISF;     // the value column's type (host-dispatched)
+    const int fl[1] = {p.vc_flags[0]};
+    for (int kb = 0; kb < nloc; kb += kGrpBlock) {
+        const int lk = kb + threadIdx.x;
+        bool present = false;
+        int64_t ov[EK_MAX_AGGS];
+        uint8_t ot[EK_MAX_AGGS];
+        if (lk < nloc) {
+            const int j0 = (int)s_off[lk], j1 = (int)s_off[lk + 1];
+            if (j1 > j0) {
+                int64_t vc[1] = {0}, is[1] = {0};
+                double fs[1] = {0.0}, m2[1] = {0.0};
+                uint64_t mn[1] = {~0ull}, mx[1] = {0ull};
+                for (int j = j0; j < j1; ++j) {
+                    const int64_t raw = s_b[j];
+                    const double x = isf ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = isf ? f64_to_ord(x) : i64_to_ord(raw);
+                    vc[0]++;
+                    is[0] = (int64_t)((uint64_t)is[0] + (uint64_t)raw);
+                    fs[0] = __dadd_rn(fs[0], x);
+                    mn[0] = o < mn[0] ? o : mn[0];
+                    mx[0] = o > mx[0] ? o : mx[0];
+                }
+                if ((fl[0] & NEED_M2) && vc[0] > 0) {
+                    const double mean = __ddiv_rn(fs[0], (double)vc[0]);
+                    for (int j = j0; j < j1; ++j) {
+                        const double dd = __dsub_rn(isf ? __longlong_as_double(s_b[j]) : (double)s_b[j], mean);
+                        m2[0] = __dadd_rn(m2[0], __dmul_rn(dd, dd));
+                    }
+                }
+                Part<1> part{};
+                part_merge(p, part, j1 - j0, vc, is, fs, m2, mn, mx);
+                uint64_t sres[kMaxSortAggs];
+                uint8_t stag[kMaxSortAggs];
+                bool agg_err = false;
+#pragma unroll
+                for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
+                if constexpr (SORT) {
+                    // the key's values in place, ascending by ordered bits (the segment belongs to this thread)
+                    for (int j = j0 + 1; j < j1; ++j) {
+                        const int64_t x = s_b[j];
+                        const uint64_t ox = isf ? f64_to_ord(__longlong_as_double(x)) : i64_to_ord(x);
+                        int q = j;
+                        while (q > j0) {
+                            const int64_t y = s_b[q - 1];
+                            const uint64_t oy = isf ? f64_to_ord(__longlong_as_double(y)) : i64_to_ord(y);
+                            if (oy <= ox) break;
+                            s_b[q] = y;
+                            --q;
+                        }
+                        s_b[q] = x;
+                    }
+#pragma unroll
+                    for (int a = 0; a < kMaxSortAggs; ++a) {
+                        if (a >= p.n_sagg) continue;
+                        const int ka = p.sagg_agg[a];
+                        order_stat(p.agg_fn[ka], isf, p.agg_p[ka], (int64_t)(j1 - j0),
+                                   [&](int64_t r) {
+                                       const int64_t x = s_b[j0 + (int)r];
+                                       return isf ? f64_to_ord(__longlong_as_double(x)) : i64_to_ord(x);
+                                   },
+                                   &sres[a], &stag[a]);
+                        agg_err |= stag[a] == kTagErr;
+                    }
+                }
+                const SortRes sr{sres, stag, 0, 1};
+                if (agg_err) {
+                    atomicOr(&res.win_err[g.widx], EK_WIN_AGG_ERROR);
+                } else {
+                    const int hv = km_having(p, part, SORT ? &sr : nullptr);
+                    if (hv < 0) atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
+                    if (hv > 0) {
+                        present = true;
+                        km_row(p, part, SORT ? &sr : nullptr, ov, ot);
+                    }
+                }
+            }
+        }
+        // block-compacted emission of this round's kept keys
+        const unsigned long long msk = __ballot(present);
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (!__syncthreads_or(present)) continue;
+        if (lane == 0) esh[wv] = (uint32_t)__popcll(msk);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int w = 0; w < kGrpBlock / 64; ++w) { const uint32_t c = esh[w]; esh[w] = run; run += c; }
+            esh[16] = (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[g.widx], (unsigned long long)run);
+        }
+        __syncthreads();
+        if (present) {
+            const int64_t pos = g.obase + (int64_t)esh[16] + esh[wv] + __popcll(msk & ((1ull << lane) - 1ull));
+            res.key[pos] = kbase | (uint32_t)lk;
+#pragma unroll
+            for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                if (q >= p.n_aggs) break;
+                res.tag[q][pos] = ot[q];
+                res.val[q][pos] = ov[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+inline size_t grp_walk_lds(int s2) { return (size_t)kGrpCap * 8 + ((size_t)(1 << s2) * 2 + 1) * 4 + 16; }
+
+
 // one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count
 __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
     const int k = blockIdx.x;

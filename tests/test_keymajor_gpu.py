@@ -214,3 +214,40 @@ def test_km_write_pass_many_aggregates(oracle, engine_mod):
     got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=2)
     assert len(got) > 100 and st.windows_keymajor > 0
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("grp", ["0", "1"])
+@pytest.mark.parametrize("sql,col", [
+    ("SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9), count(*) FROM demo "
+     "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)", "float"),
+    ("SELECT deviceId, median(v), percentile_disc(v, 0.25), avg(v), stddev(v) FROM demo "
+     "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 2", "int"),
+])
+def test_km_one_window_grouped_huge_keys(oracle, engine_mod, grp, sql, col, monkeypatch):
+    """K > 2^16, one window per push, one value column: EKGPU_GRP=1 (default) takes the MSD-partitioned grouping
+    (k_grp_*: two 8-bit digit passes, then LDS grouping per sub-bucket); =0 the radix-sorted key-major walk."""
+    monkeypatch.setenv("EKGPU_GRP", grp)
+    keys = 150_000
+    cols = R._iot(1_200_000, keys, seed=57, epm=300)
+    schema = dict(IOT_SCHEMA)
+    if col == "int":
+        cols = cols[:4] + [np.random.default_rng(2).integers(-1000, 1000, len(cols[0])).astype(np.int64)]
+        schema["v"] = "bigint"
+    rule = compile_rule(sql, schema, num_keys=keys, debug_membership=True)
+    got, exp, st = _push_per_window(oracle, engine_mod, rule, cols, 1000)
+    assert len(exp.windows) >= 3 and st.windows_keymajor >= len(exp.windows)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_one_window_grouped_skewed_falls_back(oracle, engine_mod):
+    """A hot key puts more than kGrpCap rows into one sub-bucket: the grouped path declines before writing anything
+    and the radix-sorted walk answers."""
+    keys = 100_000
+    cols = R._iot(600_000, keys, seed=58, epm=200)
+    cols[0][::7] = 12345                       # ~86 k rows of one key
+    rule = compile_rule("SELECT deviceId, max(temperature), count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)",
+                        IOT_SCHEMA, num_keys=keys, debug_membership=True)
+    os.environ["EKGPU_KEYMAJOR"] = "1"
+    got, exp, st = _push_per_window(oracle, engine_mod, rule, cols, 1000)
+    assert len(exp.windows) >= 2
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
