@@ -9,5 +9,5 @@ if [ -n "$TESTS" ] && [ "$TESTS" != "none" ]; then
 fi
 for c in ${CONFIGS:-C3 C4b C5 C2}; do
   timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu --no-ingest > gpurun_out/dev/$c.json 2> gpurun_out/dev/$c.err || { echo "$c failed"; tail -5 gpurun_out/dev/$c.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('gpurun_out/dev/$c.json')); r=d['roofline']; print('$c', round(d['ms_per_step'],3), 'ms', round(r['frac'],4), {k: round(v['launch_ms']*v['launches_per_step'],3) for k,v in r['kernels'].items()})"
+  python -c "import json,sys; d=json.load(open('gpurun_out/dev/$c.json')); r=d['roofline']; print('$c', round(d['ms_per_step'],3), 'ms', round(r['frac'],4), {k: round(v['launch_ms']*v['launches_per_step'],3) for k,v in r.get('kernels',{}).items()})"
 done
