@@ -436,10 +436,7 @@ __device__ __forceinline__ uint32_t sw_hash(uint32_t k) {
 }
 
 template <int NVC>
-#ifndef EK_SW_WPE
-#define EK_SW_WPE 6
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_SW_WPE))) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
+__global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
                                                      const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
                                                      const int64_t* __restrict__ obase, Results res, int max_n) {
     constexpr int R = kSmallWin / kBlock;      // rows per thread
