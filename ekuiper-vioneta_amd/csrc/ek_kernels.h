@@ -1407,8 +1407,15 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
                                                      DState ds, int32_t ring, const int32_t* __restrict__ pane_err,
                                                      Results res) {
     const DPlan& p = *pp;
-    const WinDesc w = wins[blockIdx.y];
-    const int64_t key = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    // XCD-aware order: dispatch slot `orig` runs on the XCD labelled orig % 8; the bijective swizzle gives every XCD
+    // a contiguous run of (key block-major, window-minor) work, so the consecutive windows of a key block — which
+    // share all but one (hopping: ppw - 1 of ppw) panes — are merged on one XCD and re-read its L2
+    const int64_t nwg = (int64_t)gridDim.x * gridDim.y;
+    const int64_t orig = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+    const int64_t xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int64_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const WinDesc w = wins[wgid % gridDim.y];
+    const int64_t key = (wgid / gridDim.y) * kBlock + threadIdx.x;
     int32_t werr = 0;
     for (int64_t q = w.q_first; q <= w.q_last; ++q) werr |= pane_err[q % ring];
     if (werr) {
