@@ -1895,55 +1895,58 @@ struct Engine {
         const int64_t nt1 = (n + kGrpTile - 1) / kGrpTile;
         const int64_t nt_cap = nt1 + nb1 + 1;
         if (int rc = ensure(grp_tiles, (size_t)nt_cap * sizeof(GrpTile) * 2)) return rc;
-        if (int rc = ensure(grp_cnt, (size_t)(256 + nsub) * 2 * 4)) return rc;
-        if (int rc = ensure(grp_base, (size_t)(256 + nsub + 1) * 8)) return rc;
+        constexpr int kRep1 = 64;   // counter replicas of the first pass (k_grp_hist)
+        const int n1 = kRep1 * 256;
+        if (int rc = ensure(grp_cnt, (size_t)(n1 + nsub) * 2 * 4)) return rc;
+        if (int rc = ensure(grp_base, (size_t)(n1 + nsub + 1) * 8)) return rc;
         GrpTile* d_t1 = (GrpTile*)grp_tiles.p;
         GrpTile* d_t2 = d_t1 + nt_cap;
         unsigned int* tot1 = (unsigned int*)grp_cnt.p;
-        unsigned int* cur1 = tot1 + 256;
-        unsigned int* tot2 = cur1 + 256;
+        unsigned int* cur1 = tot1 + n1;
+        unsigned int* tot2 = cur1 + n1;
         unsigned int* cur2 = tot2 + nsub;
         int64_t* base1 = (int64_t*)grp_base.p;
-        int64_t* base2 = base1 + 256;
+        int64_t* base2 = base1 + n1;
         grp_ht.resize((size_t)nt1);
         for (int64_t t = 0; t < nt1; ++t)
             grp_ht[t] = GrpTile{t * kGrpTile, (int32_t)std::min<int64_t>(kGrpTile, n - t * kGrpTile), 0};
         hipMemcpyAsync(d_t1, grp_ht.data(), (size_t)nt1 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
-        hipMemsetAsync(grp_cnt.p, 0, (size_t)(512 + 2 * nsub) * 4, stream);
+        hipMemsetAsync(grp_cnt.p, 0, (size_t)(2 * n1 + 2 * nsub) * 4, stream);
         const int ph = phase_begin(EK_PHASE_PARTITION);
-        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, K, tot1);
-        grp_h.resize(256);
-        hipMemcpyAsync(grp_h.data(), tot1, 256 * 4, hipMemcpyDeviceToHost, stream);
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, K,
+                           kRep1, tot1);
+        grp_h.resize(n1);
+        hipMemcpyAsync(grp_h.data(), tot1, (size_t)n1 * 4, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping histogram failed");
-        grp_hb.assign(256 + nsub + 1, 0);
+        grp_hb.assign(n1 + nsub + 1, 0);
         int64_t acc = 0;
         grp_ht.clear();
-        for (int b = 0; b < 256; ++b) {
-            grp_hb[b] = acc;
-            for (int64_t r = 0; r < grp_h[b]; r += kGrpTile)
-                grp_ht.push_back(GrpTile{acc + r, (int32_t)std::min<int64_t>(kGrpTile, grp_h[b] - r), b * 256});
-            acc += grp_h[b];
+        for (int b = 0; b < 256; ++b) {   // digit b's region holds its replicas' sub-regions one after another
+            const int64_t b0 = acc;
+            for (int q = 0; q < kRep1; ++q) { grp_hb[q * 256 + b] = acc; acc += grp_h[q * 256 + b]; }
+            for (int64_t r = b0; r < acc; r += kGrpTile)
+                grp_ht.push_back(GrpTile{r, (int32_t)std::min<int64_t>(kGrpTile, acc - r), b * 256});
         }
         const int64_t nt2 = (int64_t)grp_ht.size();
-        hipMemcpyAsync(base1, grp_hb.data(), 256 * 8, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(base1, grp_hb.data(), (size_t)n1 * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0) hipMemcpyAsync(d_t2, grp_ht.data(), (size_t)nt2 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1, K,
-                           (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p);
+                           kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p);
         if (nt2 > 0)
             hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const GrpTile*)d_t2, s2, K, tot2);
+                               (const GrpTile*)d_t2, s2, K, 1, tot2);
         grp_h.resize((size_t)nsub);
         hipMemcpyAsync(grp_h.data(), tot2, (size_t)nsub * 4, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping pass 1 failed");
         acc = 0;
         unsigned int mx = 0;
-        for (int i = 0; i < nsub; ++i) { grp_hb[256 + i] = acc; acc += grp_h[i]; mx = std::max(mx, grp_h[i]); }
-        grp_hb[256 + nsub] = acc;
+        for (int i = 0; i < nsub; ++i) { grp_hb[n1 + i] = acc; acc += grp_h[i]; mx = std::max(mx, grp_h[i]); }
+        grp_hb[n1 + nsub] = acc;
         if (mx > (unsigned int)kGrpCap) { phase_end(ph); return 0; }
-        hipMemcpyAsync(base2, grp_hb.data() + 256, (size_t)(nsub + 1) * 8, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(base2, grp_hb.data() + n1, (size_t)(nsub + 1) * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0)
             hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, K, (const int64_t*)base2, cur2,
+                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, K, 1, (const int64_t*)base2, cur2,
                                (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p);
         phase_end(ph);
         GrpDesc g{};

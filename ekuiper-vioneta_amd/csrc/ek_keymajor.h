@@ -377,24 +377,33 @@ struct GrpTile {
     int32_t pre;                      // digit index offset (level 2: bucket * 256)
 };
 
-// totals per (pre + digit) of the tile's rows with key < K
+// totals per (replica, pre + digit) of the tile's rows with key < K. A tile counts into replica blockIdx.x % rep
+// (stride 256): the first pass's tiles all share one set of 256 digits, and 64 replicas keep every counter's global
+// atomics (here and in k_grp_scatter's reservations) from serialising on one address; the host lays the replicas'
+// regions out consecutively inside each digit's region.
 __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restrict__ keys, const GrpTile* __restrict__ tiles,
-                                                        int shift, uint32_t K, unsigned int* __restrict__ tot) {
+                                                        int shift, uint32_t K, int rep, unsigned int* __restrict__ tot) {
     __shared__ unsigned int h[256];
     const GrpTile t = tiles[blockIdx.x];
     h[threadIdx.x] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < t.len; i += kGrpBlock) {
-        const uint32_t k = keys[t.start + i];
-        if (k < K) atomicAdd(&h[(k >> shift) & 255u], 1u);
+    constexpr int R = kGrpTile / kGrpBlock;
+    uint32_t k[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {                 // all of the tile's loads in flight before the first atomic
+        const int i = threadIdx.x + j * kGrpBlock;
+        k[j] = i < t.len ? keys[t.start + i] : K;
     }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (k[j] < K) atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&tot[t.pre + threadIdx.x], h[threadIdx.x]);
+    if (h[threadIdx.x]) atomicAdd(&tot[(blockIdx.x % rep) * 256 + t.pre + threadIdx.x], h[threadIdx.x]);
 }
 
-// rows of a tile -> their (pre + digit) region: base[] exclusive region starts, cur[] reservation cursors
+// rows of a tile -> their (replica, pre + digit) region: base[] exclusive region starts, cur[] reservation cursors
 __global__ __launch_bounds__(kGrpBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
-                                                           const GrpTile* __restrict__ tiles, int shift, uint32_t K,
+                                                           const GrpTile* __restrict__ tiles, int shift, uint32_t K, int rep,
                                                            const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
                                                            uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
     __shared__ unsigned int h[256], lofs[257];
@@ -421,7 +430,8 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_scatter(const uint32_t* __res
     }
     __syncthreads();
     const unsigned int c = h[threadIdx.x];
-    if (c) gb[threadIdx.x] = base[t.pre + threadIdx.x] + (int64_t)atomicAdd(&cur[t.pre + threadIdx.x], c);
+    const int ci = (int)(blockIdx.x % rep) * 256 + t.pre + threadIdx.x;
+    if (c) gb[threadIdx.x] = base[ci] + (int64_t)atomicAdd(&cur[ci], c);
     lofs[threadIdx.x] = c;
     __syncthreads();
     block_excl_scan<kGrpBlock>(lofs, 256, wsum);   // lofs[256] = rows kept
@@ -461,7 +471,6 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, 
     const int nloc = 1 << g.s2;                                   // keys of a sub-bucket (<= 2048)
     int64_t* s_b = (int64_t*)g_lds;                               // [kGrpCap] values grouped by key
     unsigned int* s_off = (unsigned int*)(s_b + kGrpCap);         // [nloc + 1] per-key counts -> offsets
-    unsigned int* s_cur = s_off + nloc + 1;                       // [nloc] scatter cursors
     __shared__ unsigned int wsum[kGrpBlock / 64];
     __shared__ uint32_t esh[20];
     const int sb = blockIdx.x;
@@ -472,14 +481,25 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, 
     const uint32_t mask = (uint32_t)nloc - 1u;
     for (int i = threadIdx.x; i < nloc; i += kGrpBlock) s_off[i] = 0;
     __syncthreads();
-    // counting sort by local key straight from the sub-bucket's rows (the keys are read twice, the second time from
-    // L2; no LDS staging copy, so four workgroups fit a CU)
-    for (int i = threadIdx.x; i < m; i += kGrpBlock) atomicAdd(&s_off[g.keys[r0 + i] & mask], 1u);
+    // counting sort by local key: every row's key and value are loaded into registers up front (all loads in flight
+    // at once instead of one latency per strided iteration), ranked by one LDS atomic, then placed after the scan
+    constexpr int R = kGrpCap / kGrpBlock;
+    uint32_t rkey[R];
+    int64_t rval[R];
+    unsigned int rrk[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const int i = threadIdx.x + j * kGrpBlock;
+        if (i < m) { rkey[j] = g.keys[r0 + i] & mask; rval[j] = g.vals[r0 + i]; }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (threadIdx.x + j * kGrpBlock < m) rrk[j] = atomicAdd(&s_off[rkey[j]], 1u);
     __syncthreads();
     block_excl_scan<kGrpBlock>(s_off, nloc, wsum);
-    for (int i = threadIdx.x; i < nloc; i += kGrpBlock) s_cur[i] = s_off[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < m; i += kGrpBlock) s_b[atomicAdd(&s_cur[g.keys[r0 + i] & mask], 1u)] = g.vals[r0 + i];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (threadIdx.x + j * kGrpBlock < m) s_b[s_off[rkey[j]] + rrk[j]] = rval[j];
     __syncthreads();
     constexpr bool isf = ISF;     // the value column's type (host-dispatched)
     const int fl[1] = {p.vc_flags[0]};
@@ -584,7 +604,7 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, 
         __syncthreads();
     }
 }
-inline size_t grp_walk_lds(int s2) { return (size_t)kGrpCap * 8 + ((size_t)(1 << s2) * 2 + 1) * 4 + 16; }
+inline size_t grp_walk_lds(int s2) { return (size_t)kGrpCap * 8 + ((size_t)(1 << s2) + 1) * 4 + 16; }
 
 
 // one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count
