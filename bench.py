@@ -102,6 +102,14 @@ def make_device_stream(n, keys, dev, seed=44, key_offset=0, events_per_ms=EVENTS
     return [key, ts, temp, hum]
 
 
+def disorder_ts(ts, seed, ms):
+    """`bench.py --disorder MS`: event i's ts moved back by a hash-chosen 0..MS ms, so the stream arrives out of
+    order by at most MS ms (a rule with lateTolerance >= MS drops nothing)."""
+    import torch
+    i = torch.arange(len(ts), dtype=torch.int64, device=ts.device)
+    return ts - (_tmix(i ^ (seed << 48)) & ((1 << 62) - 1)) % (ms + 1)
+
+
 def trig_column(i):
     """C4a trigger flag of global event i: 1 in 1e4 events (tests/test_fullsize_parity_gpu.py)."""
     import torch
@@ -351,6 +359,10 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="one process plays rank 0 of an N-GPU run in shard mode (no collective; a single-GPU check of "
                          "the shard path: C4a then sees only its own triggers)")
+    ap.add_argument("--disorder", type=int, default=0, metavar="MS",
+                    help="event-time configs: every ts moved back by a hash-chosen 0..MS ms (the stream arrives out of "
+                         "order) and the rule compiled with lateTolerance = MS, so nothing is late and the engine's "
+                         "unsorted path (watermark release, multi-tile partition) is the one timed")
     args = ap.parse_args()
     if args.config == "C1":
         return bench_c1(args)
@@ -382,11 +394,14 @@ def main():
         c = make_device_stream(cfg["n"], cfg["keys"], dev, seed=cfg["seed"], events_per_ms=cfg["epm"], t0=cfg["t0"])
         cols = config_columns(cfg, c)
         del c
+        if args.disorder > 0 and iet:
+            cols[1] = disorder_ts(cols[1], cfg["seed"], args.disorder)
         arr, n_glob, k_local = None, cfg["n"], cfg["keys"]
     else:
         cols, arr, n_glob, k_local = shard_stream(cfg, world, rank, dev)
     n = int(cols[0].numel())
-    rule = compile_rule(cfg["sql"], schema_of(cfg), num_keys=max(1, k_local), is_event_time=iet)
+    rule = compile_rule(cfg["sql"], schema_of(cfg), num_keys=max(1, k_local), is_event_time=iet,
+                        late_tolerance_ms=args.disorder if iet else 0)
     torch.cuda.synchronize()
     eng = Engine(rule.plan, device=local)
     ptrs = [x.data_ptr() for x in cols]
@@ -543,9 +558,12 @@ def main():
     }
     if global_count is not None:
         out["config"]["global_count"] = str(global_count)[:200]
-    if rank == 0 and world == 1 and args.config == "C2" and not args.no_ingest:
+    if args.disorder > 0 and iet:
+        out["config"]["disorder_ms"] = args.disorder
+        out["config"]["late_tolerance_ms"] = args.disorder
+    if rank == 0 and world == 1 and args.config == "C2" and not args.no_ingest and not args.disorder:
         out["ingest_inclusive"] = ingest_inclusive(eng, cols, n)
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "C2":
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == "C2" and not args.disorder:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -2950,12 +2950,14 @@ struct Engine {
             }
         } else if (!sorted) {
             int nch = (int)((n + kAccChunk - 1) / kAccChunk);
-            if (int rc = ensure(cmax, (size_t)nch * 8)) return rc;
+            if (int rc = ensure(cmax, (size_t)nch * 8 * 3)) return rc;   // chunk maxima + (count, min) partials
             if (int rc = ensure(acc, (size_t)n)) return rc;
+            int64_t* cpart = (int64_t*)cmax.p + nch;
             hipLaunchKernelGGL(k_chunk_max, dim3(nch), dim3(kBlock), 0, stream, ts, n, (int64_t*)cmax.p);
             hipLaunchKernelGGL(k_scan_max, dim3(1), dim3(1024), 0, stream, (int64_t*)cmax.p, nch, has_M ? M : kMinTs);
             hipLaunchKernelGGL(k_accept, dim3(nch), dim3(kBlock), 0, stream, ts, n, (const int64_t*)cmax.p, T,
-                               (uint8_t*)acc.p, (BatchStats*)bstats.p);
+                               (uint8_t*)acc.p, cpart);
+            hipLaunchKernelGGL(k_accept_reduce, dim3(1), dim3(1024), 0, stream, (const int64_t*)cpart, nch, (BatchStats*)bstats.p);
             hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "accept kernel failed");
             n_acc = h_stats->n_accepted;

@@ -153,61 +153,108 @@ __global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict_
     if (threadIdx.x == 0) cmax[blockIdx.x] = max(max(s[0], s[1]), max(s[2], s[3]));
 }
 
-// exclusive prefix max over chunk maxima, seeded with the carried stream max (single workgroup)
+// exclusive prefix max over chunk maxima, seeded with the carried stream max (single workgroup; the threads' partial
+// maxima are scanned with wave shuffles, not by one thread)
 __global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64_t seed) {
-    __shared__ int64_t part[1024];
-    int per = (nch + 1023) / 1024;
-    int b = threadIdx.x * per, e = min(nch, b + per);
+    __shared__ int64_t s_w[16];
+    const int per = (nch + 1023) / 1024;
+    const int b = threadIdx.x * per, e = min(nch, b + per);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int64_t m = INT64_MIN;
     for (int i = b; i < e; ++i) m = max(m, cmax[i]);
-    part[threadIdx.x] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t run = seed;
-        for (int t = 0; t < 1024; ++t) { int64_t v = part[t]; part[t] = run; run = max(run, v); }
+    int64_t x = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = max(x, y);
     }
+    int64_t run = __shfl_up(x, 1, 64);
+    if (lane == 0) run = INT64_MIN;
+    if (lane == 63) s_w[wv] = x;
     __syncthreads();
-    int64_t run = part[threadIdx.x];
-    for (int i = b; i < e; ++i) { int64_t v = cmax[i]; cmax[i] = run; run = max(run, v); }
+    run = max(run, seed);
+    for (int w = 0; w < wv; ++w) run = max(run, s_w[w]);
+    for (int i = b; i < e; ++i) { const int64_t v = cmax[i]; cmax[i] = run; run = max(run, v); }
 }
 
+// per-event acceptance of a 4096-event chunk; the chunk's (accepted count, min accepted ts) go to part[2 * chunk]
+// (reduced by k_accept_reduce: one atomic per wave on two counters serialised ~1.5 M atomics per 1e8 events)
 __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
-                                                   int64_t late_tol, uint8_t* acc, BatchStats* st) {
-    __shared__ int64_t tmax[kBlock];
-    int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
+                                                   int64_t late_tol, uint8_t* acc, int64_t* __restrict__ part) {
+    __shared__ int64_t s_w[kBlock / 64], s_c[kBlock / 64], s_m[kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int64_t v[kAccPerThread];
     int64_t lm = INT64_MIN;
+    if (base + kAccPerThread <= n && ((uintptr_t)ts & 15) == 0) {
 #pragma unroll
-    for (int k = 0; k < kAccPerThread; ++k) {
-        int64_t i = base + k;
-        v[k] = i < n ? ts[i] : INT64_MIN;
-        lm = max(lm, v[k]);
+        for (int k = 0; k < kAccPerThread; k += 2) {   // 16-B loads (base is 16-event aligned)
+            const longlong2 q = *(const longlong2*)(ts + base + k);
+            v[k] = q.x;
+            v[k + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kAccPerThread; ++k) v[k] = base + k < n ? ts[base + k] : INT64_MIN;
     }
-    tmax[threadIdx.x] = lm;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t run = excl[blockIdx.x];
-        for (int t = 0; t < kBlock; ++t) { int64_t x = tmax[t]; tmax[t] = run; run = max(run, x); }
+#pragma unroll
+    for (int k = 0; k < kAccPerThread; ++k) lm = max(lm, v[k]);
+    // exclusive prefix max of the threads' maxima over the block (wave shuffles + one LDS step)
+    int64_t x = lm;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = max(x, y);
     }
+    int64_t run = __shfl_up(x, 1, 64);
+    if (lane == 0) run = INT64_MIN;
+    if (lane == 63) s_w[wv] = x;
     __syncthreads();
-    int64_t run = tmax[threadIdx.x];
+    run = max(run, excl[blockIdx.x]);
+    for (int w = 0; w < wv; ++w) run = max(run, s_w[w]);
     int64_t cnt = 0, mn = INT64_MAX;
+    uint32_t pk[kAccPerThread / 4] = {};
 #pragma unroll
     for (int k = 0; k < kAccPerThread; ++k) {
-        int64_t i = base + k;
-        if (i < n) {
+        if (base + k < n) {
             // W_{i-1} = M_{i-1} - lateTol; no watermark yet (run == INT64_MIN) accepts everything
-            bool ok = (run == INT64_MIN) || (v[k] >= run - late_tol);
-            acc[i] = ok ? 1 : 0;
+            const bool ok = (run == INT64_MIN) || (v[k] >= run - late_tol);
+            pk[k >> 2] |= (ok ? 1u : 0u) << ((k & 3) * 8);
             if (ok) { cnt++; mn = min(mn, v[k]); }
             run = max(run, v[k]);
         }
     }
+    if (base + kAccPerThread <= n) {
+        *(uint4*)(acc + base) = make_uint4(pk[0], pk[1], pk[2], pk[3]);   // one 16-B store
+    } else {
+        for (int k = 0; k < kAccPerThread; ++k)
+            if (base + k < n) acc[base + k] = (uint8_t)((pk[k >> 2] >> ((k & 3) * 8)) & 1u);
+    }
     mn = wave_min64(mn);
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd((unsigned long long*)&st->n_accepted, (unsigned long long)cnt);
-        atomicMin((long long*)&st->min_accepted, (long long)mn);
+    if (lane == 0) { s_c[wv] = cnt; s_m[wv] = mn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t c = 0, m = INT64_MAX;
+        for (int w = 0; w < kBlock / 64; ++w) { c += s_c[w]; m = min(m, s_m[w]); }
+        part[2 * blockIdx.x] = c;
+        part[2 * blockIdx.x + 1] = m;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restrict__ part, int nch, BatchStats* st) {
+    __shared__ int64_t s_c[16], s_m[16];
+    int64_t c = 0, m = INT64_MAX;
+    for (int i = threadIdx.x; i < nch; i += 1024) { c += part[2 * i]; m = min(m, part[2 * i + 1]); }
+    m = wave_min64(m);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) { s_c[threadIdx.x >> 6] = c; s_m[threadIdx.x >> 6] = m; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t tc = 0, tm = INT64_MAX;
+        for (int w = 0; w < 16; ++w) { tc += s_c[w]; tm = min(tm, s_m[w]); }
+        st->n_accepted = tc;
+        st->min_accepted = tm;
     }
 }
 

@@ -2,7 +2,8 @@
 (oracle/ekoracle.c, the per-event restatement of the reference) on the same stream, every window compared
 with membership (count + Σ mix64(arrival)) and every row (tests/parity.py rule, vectorised).
 
-  C2  TUMBLINGWINDOW(ss,10) avg/max/count, 1e8 events / 64 Ki keys (the bench stream, seed 44)
+  C2  TUMBLINGWINDOW(ss,10) avg/max/count, 1e8 events / 64 Ki keys (the bench stream, seed 44); and 2e7 events
+      out of order by up to 50 ms with lateTolerance 50 ms (`bench.py --disorder 50`)
   C3  HOPPINGWINDOW(ss,60,5) sum/min/max/count, one of 8 shards: 2.5e7 events / 131 072 keys
   C4a SLIDINGWINDOW(ss,30) OVER (WHEN trig = 1) stddev/var/count HAVING count(*) > 1, 1e7 events / 1 M keys
   C4b COUNTWINDOW(1000) stddev/var/count HAVING count(*) > 1 (processing time), 1e8 events / 1 M keys
@@ -70,6 +71,25 @@ def test_c2_full_parity(engine_mod, pushes):
     got, exp, t_or, t_gpu = _run_both(engine_mod, rule, d, pushes=pushes)
     _report(f"C2 x{pushes}", n, got, t_or, t_gpu)
     assert len(exp.windows) == 99
+    assert_windows_equal_np(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("pushes", [1, 5])
+def test_c2_disordered_parity(engine_mod, pushes):
+    """`bench.py --disorder 50`: the C2 stream (2e7 events) with every ts moved back by up to 50 ms, lateTolerance
+    50 ms — the engine's unsorted path (watermark release, multi-tile partition) against the oracle's per-event
+    WatermarkOp (watermark_op.go:144-225)."""
+    from bench import disorder_ts
+    sql = ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo "
+           "GROUP BY deviceId, TUMBLINGWINDOW(ss, 10)")
+    n, keys = 20_000_000, 65536
+    rule = compile_rule(sql, IOT_SCHEMA, num_keys=keys, late_tolerance_ms=50, debug_membership=True)
+    d = _stream(n, keys, 100, seed=44)
+    d[1] = disorder_ts(d[1], 44, 50)
+    assert bool((d[1][1:] < d[1][:-1]).any())
+    got, exp, t_or, t_gpu = _run_both(engine_mod, rule, d, pushes=pushes)
+    _report(f"C2 disordered x{pushes}", n, got, t_or, t_gpu)
+    assert len(exp.windows) >= 19
     assert_windows_equal_np(rule.plan, got, exp.windows, check_members=True)
 
 
