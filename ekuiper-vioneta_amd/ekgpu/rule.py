@@ -317,9 +317,13 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
 def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True, late_tolerance_ms: int = 0,
                  timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
                  debug_membership: bool = False, nullable=(), incremental: bool = False,
-                 window_version: str = "") -> CompiledRule:
+                 window_version: str = "", sliding_send_twice: bool = False) -> CompiledRule:
     """schema: ordered {column: "bigint" | "float" | "key" | "string"}; the TIMESTAMP column must be bigint (epoch
-    ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring)."""
+    ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring).
+    sliding_send_twice: the rule option enableSlidingWindowSendTwice (a delayed sliding window also emits its first
+    part at the trigger, event_window_trigger.go:156-161) is not implemented and is rejected."""
+    if sliding_send_twice:
+        raise RuleError("enableSlidingWindowSendTwice is not supported by the GPU path")
     kw = dict(is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms, timestamp=timestamp,
               num_keys=num_keys, tz_offset_s=tz_offset_s, debug_membership=debug_membership, nullable=nullable,
               incremental=incremental, window_version=window_version)

@@ -136,3 +136,12 @@ def test_oracle_expression_argument_is_per_row(oracle):
     for w in exp.windows:
         a, b = (np.ascontiguousarray(w.values[k]).view(np.float64) for k in (0, 1))   # f64 bit patterns
         assert np.allclose(a, b * 1.8 + 32, rtol=1e-12, atol=1e-9)
+
+
+def test_sliding_send_twice_rejected():
+    """enableSlidingWindowSendTwice (event_window_trigger.go:156-161) is not modelled: the lowering refuses it."""
+    from ekgpu.rule import RuleError, compile_rule
+    sql = "SELECT count(*) FROM s GROUP BY SLIDINGWINDOW(ss, 10, 2)"
+    compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1)
+    with pytest.raises(RuleError):
+        compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1, sliding_send_twice=True)
