@@ -346,6 +346,24 @@ def bench_c1(args):
     dec.close()
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run would) before this process touches a GPU, and
+    exit with the first failing rank's code. Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -364,6 +382,13 @@ def main():
                          "order) and the rule compiled with lateTolerance = MS, so nothing is late and the engine's "
                          "unsorted path (watermark release, multi-tile partition) is the one timed")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (one rank per GPU): refusing to run",
+              file=sys.stderr, flush=True)
+        return 2
+    if env_world is None and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     if args.config == "C1":
         return bench_c1(args)
 
@@ -575,4 +600,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

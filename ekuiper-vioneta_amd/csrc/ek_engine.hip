@@ -3074,20 +3074,9 @@ struct Engine {
     DevBuf s_sync, s_klo, s_val[kMaxVC], s_ctab, s_tab, s_prof;
     int64_t s_max_chunks = 0;
 
-    template <int N, bool WH>
-    void launch_stream_t(const DBatch& db, const StreamDesc& sd, Results rv) {
-        hipLaunchKernelGGL((k_stream<N, WH>), dim3(stream_grid), dim3(kSBlock), stream_lds, stream, d_plan, db, sd, slay, dstate, rv,
-                           (int32_t*)pane_err.p);
-    }
     void launch_stream(const DBatch& db, const StreamDesc& sd) {
-        const Results rv = results_view();
-        const bool wh = dp.n_where > 0;
-        switch (std::max(1, dp.n_vc)) {
-        case 1: wh ? launch_stream_t<1, true>(db, sd, rv) : launch_stream_t<1, false>(db, sd, rv); break;
-        case 2: wh ? launch_stream_t<2, true>(db, sd, rv) : launch_stream_t<2, false>(db, sd, rv); break;
-        case 3: wh ? launch_stream_t<3, true>(db, sd, rv) : launch_stream_t<3, false>(db, sd, rv); break;
-        default: wh ? launch_stream_t<4, true>(db, sd, rv) : launch_stream_t<4, false>(db, sd, rv); break;
-        }
+        launch_stream_kernel(dp.n_vc, dp.n_where > 0, stream_grid, (size_t)stream_lds, stream, d_plan, db, sd, slay, dstate,
+                             results_view(), (int32_t*)pane_err.p);
     }
 
     StreamDesc stream_desc_base() {
@@ -3109,20 +3098,20 @@ struct Engine {
         if (env_int("EKGPU_STREAM_PROF", 0) && ensure(s_prof, (size_t)stream_grid * 64) == 0) sd.prof = (unsigned long long*)s_prof.p;
         return sd;
     }
-    size_t stream_sync_bytes() const { return ((size_t)(18 + kSXcd * s_max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15; }
+    size_t stream_sync_bytes() const { return ((size_t)(10 + kSXcd * s_max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15; }
 
     // Decide once per handle: plan shape, LDS budget, and a probe launch proving the grid is co-resident with
     // `owners` workgroups on each of the 8 XCDs (the kernel checks it before any side effect).
     int stream_setup() {
         stream_state = -1;
-        if (env_int("EKGPU_STREAM", 0) == 0 || range_mode || dp.pseudo_keys || dp.n_sagg > 0 || dp.n_vc < 1 || dp.n_vc > 4) return 0;
+        if (env_int("EKGPU_STREAM", 0) == 0 || range_mode || dp.pseudo_keys || dp.n_sagg > 0 || dp.n_vc < 1 || dp.n_vc > 2) return 0;
         for (int v = 0; v < dp.n_vc; ++v)
             if (dp.vc_flags[v] & (NEED_CNT | NEED_M2 | NEED_FSUM | NEED_SORT)) return 0;
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0 || cus % kSXcd) return 0;
-        stream_grid = 2 * cus;
-        stream_owners = stream_grid / kSXcd;
-        if (stream_owners > kSMaxOwners) return 0;
+        stream_grid = 2 * cus;                     // one producer + one consumer workgroup per CU
+        stream_owners = stream_grid / kSXcd / 2;   // consumers (= producers) per XCD
+        if (stream_owners > kSMaxOwners || stream_owners < 1) return 0;
         int64_t kpo = 1;
         const int64_t need = ((int64_t)K + stream_owners - 1) / stream_owners;
         stream_obits = 0;
@@ -3142,8 +3131,9 @@ struct Engine {
             o += 4 * (int)kpo;
             slay.bytes = (o + 15) & ~15;
         }
-        stream_lds = slay.bytes + kSTile * 10;
-        if (stream_lds > 72 * 1024) return 0;   // two workgroups per CU (with the kernel's static LDS)
+        // producer: the owner-sorted chunk (values + key-lows); consumer: the owner table; two workgroups per CU
+        stream_lds = std::max<int>(slay.bytes, kSTile * (8 * dp.n_vc + 2));
+        if (stream_lds > 78 * 1024) return 0;
         s_max_chunks = env_int("EKGPU_STREAM_MAX_CHUNKS", 1 << 16);
         if (int rc = ensure(s_sync, stream_sync_bytes())) return rc;
         if (int rc = ensure(s_klo, (size_t)kSXcd * kSRing * kSTile * 2)) return rc;
@@ -3180,17 +3170,25 @@ struct Engine {
     // Returns 1 (nothing launched) when the batch does not fit the launch's tables.
     int run_stream(const DBatch& db, const int64_t* b, int64_t qa, int64_t qb) {
         const int npn = (int)(qb - qa + 1);
-        // per-XCD pane lists (pane r -> XCD r % 8) and chunk prefixes on the kSTile-aligned per-pane grid
+        // per-XCD pane lists: contiguous pane ranges balanced by events (XCD x takes the panes whose first event
+        // falls in its eighth of the batch), and chunk prefixes on the kSTile-aligned per-pane grid
         std::vector<int32_t> xoff(kSXcd + 1, 0), xpane, xcpre;
-        std::vector<int32_t> cnt_per(kSXcd, 0);
-        for (int r = 0; r < npn; ++r) cnt_per[r % kSXcd]++;
+        std::vector<int32_t> cnt_per(kSXcd, 0), xof(npn);
+        {
+            const int64_t lo = b[0], span = std::max<int64_t>(1, b[npn] - b[0]);
+            for (int r = 0; r < npn; ++r) {
+                const int64_t mid = (b[r] + b[r + 1]) / 2 - lo;
+                xof[r] = (int)std::min<int64_t>(kSXcd - 1, mid * kSXcd / span);
+                cnt_per[xof[r]]++;
+            }
+        }
         for (int x = 0; x < kSXcd; ++x) xoff[x + 1] = xoff[x] + cnt_per[x];
         if (*std::max_element(cnt_per.begin(), cnt_per.end()) > kSMaxXPanes) return 1;
         xpane.resize(npn);
         xcpre.resize(npn + kSXcd);
         {
             std::vector<int32_t> fill(kSXcd, 0);
-            for (int r = 0; r < npn; ++r) { const int x = r % kSXcd; xpane[xoff[x] + fill[x]++] = r; }
+            for (int r = 0; r < npn; ++r) { const int x = xof[r]; xpane[xoff[x] + fill[x]++] = r; }
             for (int x = 0; x < kSXcd; ++x) {
                 int64_t c = 0;
                 int32_t* pre = xcpre.data() + xoff[x] + x;
@@ -3255,7 +3253,7 @@ struct Engine {
         sd.xoff = (const int32_t*)s_tab.p;
         sd.xpane = sd.xoff + xoff.size();
         sd.xcpre = sd.xpane + xpane.size();
-        hipMemsetAsync(s_sync.p, 0, ((size_t)(18 + kSXcd * sd.max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15, stream);
+        hipMemsetAsync(s_sync.p, 0, ((size_t)(10 + kSXcd * sd.max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15, stream);
         // fresh panes: zero their WHERE error flag and membership fingerprint (k_group_prep)
         hipLaunchKernelGGL(k_group_prep, dim3((npn + 255) / 256), dim3(256), 0, stream, gd, (int32_t*)pane_err.p,
                            (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
@@ -3278,9 +3276,10 @@ struct Engine {
             hipMemcpy(pr.data(), s_prof.p, pr.size() * 8, hipMemcpyDeviceToHost);
             double a[8] = {0};
             for (int g = 0; g < stream_grid; ++g) for (int k = 0; k < 8; ++k) a[k] += (double)pr[(size_t)g * 8 + k];
-            fprintf(stderr, "[k_stream per-WG avg] produce %.1f us, slot-wait %.1f us, consume %.1f us, finish %.1f us, idle %.1f us, "
-                            "n_produce %.1f, n_consume %.1f\n", a[0] / stream_grid / 100, a[1] / stream_grid / 100, a[2] / stream_grid / 100,
-                    a[3] / stream_grid / 100, a[4] / stream_grid / 100, a[5] / stream_grid, a[6] / stream_grid);
+            const double h = stream_grid / 2.0 * 100.0;   // per producer / per consumer, us
+            fprintf(stderr, "[k_stream avg] producer: slot-wait %.1f us, sort+store %.1f us, chunks %.1f | consumer: idle-poll %.1f us, "
+                            "fold %.1f us, finish %.1f us, batches %.1f\n", a[1] / h, a[2] / h, a[5] / (h / 100), a[3] / h, a[4] / h,
+                    a[7] / h, a[6] / (h / 100));
         }
         if (err) {
             stream_state = -1;

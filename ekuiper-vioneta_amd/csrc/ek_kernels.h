@@ -16,6 +16,12 @@
 #pragma once
 #include "ek_device.h"
 
+// linkage of the non-template kernels defined in this header: a translation unit that includes it only for the
+// device helpers (ek_stream.hip) defines EK_NT_KERNEL as static, so only the engine's unit exports them
+#ifndef EK_NT_KERNEL
+#define EK_NT_KERNEL
+#endif
+
 namespace ek {
 
 struct BatchStats {
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
     }
 }
 
-__global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
+EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
     int64_t mn = INT64_MAX, mx = INT64_MIN, mg = INT64_MIN;
     int uns = 0;
     for (int k = threadIdx.x; k < nb; k += 1024) {
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restr
 constexpr int kAccPerThread = 16;
 constexpr int kAccChunk = kBlock * kAccPerThread;  // 4096 events per block
 
-__global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict__ ts, int64_t n, int64_t* cmax) {
+EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict__ ts, int64_t n, int64_t* cmax) {
     int64_t base = (int64_t)blockIdx.x * kAccChunk;
     int64_t mx = INT64_MIN;
     for (int k = threadIdx.x; k < kAccChunk; k += kBlock) {
@@ -155,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict_
 
 // exclusive prefix max over chunk maxima, seeded with the carried stream max (single workgroup; the threads' partial
 // maxima are scanned with wave shuffles, not by one thread)
-__global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64_t seed) {
+EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64_t seed) {
     __shared__ int64_t s_w[16];
     const int per = (nch + 1023) / 1024;
     const int b = threadIdx.x * per, e = min(nch, b + per);
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64
 
 // per-event acceptance of a 4096-event chunk; the chunk's (accepted count, min accepted ts) go to part[2 * chunk]
 // (reduced by k_accept_reduce: one atomic per wave on two counters serialised ~1.5 M atomics per 1e8 events)
-__global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
                                                    int64_t late_tol, uint8_t* acc, int64_t* __restrict__ part) {
     __shared__ int64_t s_w[kBlock / 64], s_c[kBlock / 64], s_m[kBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ t
     }
 }
 
-__global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restrict__ part, int nch, BatchStats* st) {
+EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restrict__ part, int nch, BatchStats* st) {
     __shared__ int64_t s_c[16], s_m[16];
     int64_t c = 0, m = INT64_MAX;
     for (int i = threadIdx.x; i < nch; i += 1024) { c += part[2 * i]; m = min(m, part[2 * i + 1]); }
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restric
 // the grid E1 + k H; the largest one <= ts_i is e_max, and some triggered window is empty iff
 // e_max - L > W_{i-1} (the watermark before i, the exclusive running max of ts seeded with the carried stream max).
 // acc_out[i] = accepted(i) && !dropped(i); accepted = acc_in[i] (out-of-order batches) or i >= start (sorted).
-__global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
                                                      int64_t start, const uint8_t* acc_in, int64_t E1, int64_t H,
                                                      int64_t L, uint8_t* acc_out, BatchStats* st) {
     __shared__ int64_t tmax[kBlock];
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__
 // One wave per pane, 64-ary search: each round the 64 lanes probe 64 evenly spaced rows of the bracket and a ballot
 // narrows it 65-fold, so a 1e8-row batch costs 5 dependent load rounds instead of 27.
 constexpr int kBoundsBlock = 256;
-__global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi,
+EK_NT_KERNEL __global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi,
                                                               PaneGrid g, int64_t q_lo, int nb, int64_t* out) {
     const int lane = threadIdx.x & 63;
     const int k = blockIdx.x * (kBoundsBlock / 64) + (threadIdx.x >> 6);
@@ -337,7 +343,7 @@ __global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __r
 }
 
 // per-window result counters of the windows handed out by a poll: one launch instead of four fills
-__global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
+EK_NT_KERNEL __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         wcnt[i] = 0;
         werr[i] = 0;
@@ -347,7 +353,7 @@ __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wm
 }
 
 // first index in [lo, hi) with ts >= bound[k] (sorted batches)
-__global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
+EK_NT_KERNEL __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
                               int64_t* out) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nb) return;
@@ -709,7 +715,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
 
 // per group: zero the per-pane scalars (WHERE error flag, membership fingerprint) of freshly
 // claimed ring slots
-__global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
+EK_NT_KERNEL __global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r < gd.n_panes && gd.fresh[r]) {
         int64_t s = (gd.q_lo + r) % gd.ring;
@@ -912,7 +918,7 @@ __device__ __forceinline__ void part_run(const GroupDesc& gd, const uint32_t* ct
 }
 
 // Rows per partition (sort aggregates: the key-grouped scratch region of each partition), one thread each.
-__global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restrict__ ctab, int ls, int64_t* __restrict__ out) {
+EK_NT_KERNEL __global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restrict__ ctab, int ls, int64_t* __restrict__ out) {
     const int pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid >= gd.np) return;
     const int rel = pid / gd.nb, bucket = pid % gd.nb;
@@ -1606,7 +1612,7 @@ __device__ __forceinline__ void block_merge_part(const DPlan& p, Part<NVC>& s) {
 // reads nothing). The host sizes the tiles so a launch has at most kPseudoKeys of them (distinct slots per pane)
 // and zeroes the slot counts of fresh panes first; k_finalize_merge folds a window's slots as before.
 constexpr int kUngBlock = 256;
-__global__ void k_ung_zero(GroupDesc gd, DState ds) {
+EK_NT_KERNEL __global__ void k_ung_zero(GroupDesc gd, DState ds) {
     const int r = blockIdx.y;
     if (!gd.fresh[r]) return;
     int64_t* c = ds.cnt + ((gd.q_lo + r) % gd.ring) * ds.K;
@@ -1721,7 +1727,7 @@ __global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, 
 // ---------------------------------------------------------------- debug: window membership fingerprint
 // Per pane: number of accepted events (before WHERE) and Σ ek_mix64(arrival index); a window's
 // fingerprint is the sum over its panes (order-independent, exact in u64 arithmetic).
-__global__ __launch_bounds__(kBlock) void k_members(DPlan* __restrict__ pp, DBatch b, PaneGrid g, const uint8_t* acc,
+EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_members(DPlan* __restrict__ pp, DBatch b, PaneGrid g, const uint8_t* acc,
                                                     int has_acc, int64_t lo, int64_t hi, int64_t arrival_base,
                                                     const int64_t* __restrict__ arrival, int64_t qa, int64_t qb,
                                                     int32_t ring, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
@@ -1736,7 +1742,7 @@ __global__ __launch_bounds__(kBlock) void k_members(DPlan* __restrict__ pp, DBat
     }
 }
 
-__global__ void k_win_members(const WinDesc* __restrict__ wins, int32_t ring, const int64_t* __restrict__ pane_mcnt,
+EK_NT_KERNEL __global__ void k_win_members(const WinDesc* __restrict__ wins, int32_t ring, const int64_t* __restrict__ pane_mcnt,
                               const unsigned long long* __restrict__ pane_mhash, int64_t* wmc, unsigned long long* wmh) {
     if (threadIdx.x != 0) return;
     const WinDesc w = wins[blockIdx.x];

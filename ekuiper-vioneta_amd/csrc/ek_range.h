@@ -430,6 +430,39 @@ constexpr int kSmallWin = 2048;
 __host__ __device__ inline int sw_slots(int n) { int h = 256; while (h < 2 * n) h <<= 1; return h; }
 inline size_t sw_lds_bytes(int max_n) { return (size_t)sw_slots(max_n) * 8 + (size_t)max_n * 6 + 16; }
 
+// a window group's rows (indices into the window, distinct) into ascending order, so the group folds its values in
+// the window's row order: the f64 sums are the reference's sequential ones, whatever order the LDS atomics of the
+// scatter placed them in. Insertion sort for short groups, heap sort (in place, O(n log n)) for long ones.
+__device__ inline void sw_sort_rows(uint16_t* a, int n) {
+    if (n <= 24) {
+        for (int i = 1; i < n; ++i) {
+            const uint16_t x = a[i];
+            int j = i - 1;
+            while (j >= 0 && a[j] > x) { a[j + 1] = a[j]; --j; }
+            a[j + 1] = x;
+        }
+        return;
+    }
+    auto sift = [&](int r, int end) {
+        const uint16_t x = a[r];
+        while (2 * r + 1 < end) {
+            int c = 2 * r + 1;
+            if (c + 1 < end && a[c + 1] > a[c]) ++c;
+            if (a[c] <= x) break;
+            a[r] = a[c];
+            r = c;
+        }
+        a[r] = x;
+    };
+    for (int r = n / 2 - 1; r >= 0; --r) sift(r, n);
+    for (int end = n - 1; end > 0; --end) {
+        const uint16_t x = a[0];
+        a[0] = a[end];
+        a[end] = x;
+        sift(0, end);
+    }
+}
+
 __device__ __forceinline__ uint32_t sw_hash(uint32_t k) {
     k ^= k >> 16; k *= 0x7feb352du; k ^= k >> 15; k *= 0x846ca68bu; k ^= k >> 16;
     return k;
@@ -526,6 +559,7 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
         if (gi < ng) {
             const uint32_t gw = s_grp[gi];
             const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu), g1 = g0 + c;
+            sw_sort_rows(s_row + g0, c);   // the scatter's atomics placed them in no fixed order
             key = kcol ? kcol[a + s_row[g0]] : 0u;
             int64_t vc[NVC], is[NVC];
             double fs[NVC], m2[NVC];

@@ -67,16 +67,19 @@ def group_key_string(values: Sequence) -> str:
 
 
 class StringDict:
-    """Dense u32 codes of a string column (first-seen order)."""
+    """Dense u32 codes of a string column (first-seen order). Rows that are nil (None, or validity 0) take the
+    placeholder code 0 and are not entered in the dictionary (the engine never reads a nil row's value)."""
 
     def __init__(self):
         self.ids: Dict[str, int] = {}
         self.values: List[str] = []
 
-    def encode(self, col) -> np.ndarray:
-        out = np.empty(len(col), np.uint32)
+    def encode(self, col, valid=None) -> np.ndarray:
+        out = np.zeros(len(col), np.uint32)
         ids = self.ids
         for i, s in enumerate(col):
+            if s is None or (valid is not None and not valid[i]):
+                continue
             c = ids.get(s)
             if c is None:
                 c = ids[s] = len(self.values)
@@ -91,37 +94,65 @@ class StringDict:
 class OrderedStringDict:
     """Order-preserving int64 codes of a string column whose min / max the rule aggregates
     (internal/binder/function/common_array_funcs.go:49,86: Go compares strings bytewise, which for UTF-8 is code point
-    order, i.e. Python's str order). A new string takes the midpoint between the codes of its sorted neighbours, so the
-    codes of strings already on the device never change and the engine's integer min / max over codes is the
-    lexicographic min / max. Codes start spread over +-2^61; a gap that can no longer be split (about 60 insertions
-    between the same two neighbours) raises, rather than re-coding data already pushed."""
+    order, i.e. Python's str order). Codes already on the device never change, so the engine's integer min / max over
+    codes is the lexicographic min / max.
 
-    LO, HI = -(1 << 61), 1 << 61
+    Placement of a new string between its sorted neighbours' codes (lo, hi) — codes live in +-2^62:
+      * past either end, or right after / before the previously inserted string (a monotone run: ISO timestamps,
+        sequence ids, sorted names), the new code takes a share of the gap next to that neighbour that halves with
+        every step of the run down to 2^-20, so the rest of the gap stays open for the run: tens of millions of
+        strings of one monotone run fit;
+      * anywhere else it takes the midpoint.
+    Only an adversarial order (e.g. a zig-zag converging on one point, ~60 levels deep) can exhaust a gap; that
+    raises ValueError rather than re-coding values already pushed to the device. Nil rows (None, or validity 0)
+    take the placeholder code 0 and are not entered in the dictionary."""
+
+    LO, HI = -(1 << 62), 1 << 62
+    RUN_SHIFT = 20
 
     def __init__(self):
         self.code: Dict[str, int] = {}
         self.sorted: List[str] = []
         self.codes: List[int] = []          # codes of self.sorted, ascending
         self.by_code: Dict[int, str] = {}
+        self._last: Optional[str] = None     # the string inserted last (monotone-run detection)
+        self._dir, self._run = 0, 0          # direction and length of the current run
 
     def _add(self, s: str) -> int:
         import bisect
         i = bisect.bisect_left(self.sorted, s)
         lo = self.codes[i - 1] if i > 0 else self.LO
         hi = self.codes[i] if i < len(self.codes) else self.HI
-        if hi - lo < 2:
-            raise ValueError("ordered string dictionary: no code left between neighbours of %r" % s)
-        c = (lo + hi) // 2
+        gap = hi - lo
+        if gap < 2:
+            raise ValueError("ordered string dictionary: no code left between the neighbours of %r "
+                             "(adversarial insertion order)" % s)
+        ascending = i == len(self.sorted) or (i > 0 and self.sorted[i - 1] == self._last)
+        descending = i == 0 or (i < len(self.sorted) and self.sorted[i] == self._last)
+        run = self._run + 1 if (ascending and self._dir > 0) or (descending and self._dir < 0) else 0
+        step = max(1, gap >> min(self.RUN_SHIFT, run + 1))   # midpoint first; a growing run takes ever less
+        if not self.sorted:
+            c, self._dir = 0, 0
+        elif ascending:
+            c, self._dir = lo + step, 1
+        elif descending:
+            c, self._dir = hi - step, -1
+        else:
+            c, self._dir, run = lo + gap // 2, 0, 0
+        self._run = run
         self.sorted.insert(i, s)
         self.codes.insert(i, c)
         self.code[s] = c
         self.by_code[c] = s
+        self._last = s
         return c
 
-    def encode(self, col) -> np.ndarray:
-        out = np.empty(len(col), np.int64)
+    def encode(self, col, valid=None) -> np.ndarray:
+        out = np.zeros(len(col), np.int64)
         code = self.code
         for i, s in enumerate(col):
+            if s is None or (valid is not None and not valid[i]):
+                continue
             c = code.get(s)
             out[i] = c if c is not None else self._add(s)
         return out

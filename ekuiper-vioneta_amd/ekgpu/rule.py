@@ -23,6 +23,8 @@ import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
+
 from . import abi as A
 from .keys import GroupKeyDict, OrderedStringDict, StringDict
 
@@ -80,9 +82,20 @@ class CompiledRule:
             raise ValueError(f"expected {len(user)} columns ({user}), got {len(cols)}")
         validity = list(validity) if validity is not None else [None] * len(cols)
         out = []
-        for name, c in zip(user, cols):
-            out.append(self.string_dicts[name].encode(c) if name in self.string_dicts else c)
         vout = list(validity)
+        for j, (name, c) in enumerate(zip(user, cols)):
+            if name not in self.string_dicts:
+                out.append(c)
+                continue
+            # a nil string (None, or validity 0) is not a dictionary entry: placeholder code, validity 0
+            nil = np.fromiter((s is None for s in c), dtype=bool, count=len(c))
+            if nil.any():
+                if not (self.plan.nullable_mask >> self.columns.index(name)) & 1:
+                    raise ValueError(f"string column {name!r} holds nil values but is not declared nullable")
+                v = np.ones(len(c), np.uint8) if validity[j] is None else np.array(validity[j], np.uint8)
+                v[nil] = 0
+                vout[j] = v
+            out.append(self.string_dicts[name].encode(c, vout[j]))
         if self.key_dict is not None:
             idx = [user.index(d) for d in self.group_dims]
             out.append(self.key_dict.encode([cols[i] for i in idx], [validity[i] for i in idx]))
@@ -321,12 +334,19 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
     """schema: ordered {column: "bigint" | "float" | "key" | "string"}; the TIMESTAMP column must be bigint (epoch
     ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring).
     sliding_send_twice: the rule option enableSlidingWindowSendTwice (a delayed sliding window also emits its first
-    part at the trigger, event_window_trigger.go:156-161) is not implemented and is rejected."""
-    if sliding_send_twice:
-        raise RuleError("enableSlidingWindowSendTwice is not supported by the GPU path")
-    kw = dict(is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms, timestamp=timestamp,
-              num_keys=num_keys, tz_offset_s=tz_offset_s, debug_membership=debug_membership, nullable=nullable,
-              incremental=incremental, window_version=window_version)
+    part at the trigger, event_window_trigger.go:156-161) only changes a SLIDINGWINDOW with a delay: that case is not
+    implemented and is rejected; for every other window the option has no effect and is ignored."""
+    rule = _compile_rule(sql, schema, is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms,
+                         timestamp=timestamp, num_keys=num_keys, tz_offset_s=tz_offset_s,
+                         debug_membership=debug_membership, nullable=nullable, incremental=incremental,
+                         window_version=window_version)
+    if sliding_send_twice and rule.plan.window_type == A.EK_WINDOW_SLIDING and rule.plan.delay > 0:
+        raise RuleError("enableSlidingWindowSendTwice with a delayed SLIDINGWINDOW is not supported by the GPU path")
+    return rule
+
+
+def _compile_rule(sql, schema, **kw) -> CompiledRule:
+    num_keys = kw["num_keys"]
     try:
         return _compile(sql, dict(schema), **kw)
     except _Composite as c:

@@ -145,3 +145,8 @@ def test_sliding_send_twice_rejected():
     compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1)
     with pytest.raises(RuleError):
         compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1, sliding_send_twice=True)
+    # the option only changes a delayed sliding window: without a delay, and for other windows, it is ignored
+    for other in ("SLIDINGWINDOW(ss, 10)", "TUMBLINGWINDOW(ss, 10)", "HOPPINGWINDOW(ss, 10, 5)"):
+        r = compile_rule(f"SELECT count(*) FROM s GROUP BY {other}", {"a": "bigint", "ts": "bigint"}, num_keys=1,
+                         sliding_send_twice=True)
+        assert r.plan.delay == 0

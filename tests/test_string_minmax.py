@@ -29,6 +29,45 @@ def test_ordered_codes_follow_string_order():
     assert all(s.encode() < t.encode() for s, t in zip(d.sorted, d.sorted[1:]))   # Go's bytewise order
 
 
+@pytest.mark.parametrize("order", ["ascending", "descending", "ascending_inside_gap", "descending_inside_gap"])
+def test_ordered_codes_monotone_runs(order):
+    """Monotone runs (ISO timestamps, sequence ids) must not exhaust the code space (midpoint placement
+    failed at the 63rd ascending value)."""
+    d = OrderedStringDict()
+    vals = [f"id{i:07d}" for i in range(10_000)]
+    if order.startswith("descending"):
+        vals = vals[::-1]
+    if order.endswith("inside_gap"):
+        d.encode(["id", "iz"])            # every run value sorts between these two
+    codes = d.encode(vals)
+    srt = sorted(zip(vals, codes.tolist()))
+    assert all(a[1] < b[1] for a, b in zip(srt, srt[1:]))
+    assert d.decode(codes[:5]) == vals[:5]
+    # interleaved random insertions after the run still find room
+    rng = np.random.default_rng(0)
+    more = [f"id{int(x):07d}x" for x in rng.integers(0, 10_000, 2000)]
+    c2 = d.encode(more)
+    allv = sorted(set(zip(vals + more, codes.tolist() + c2.tolist())))
+    assert all(a[1] < b[1] for a, b in zip(allv, allv[1:]))
+
+
+def test_string_nil_rows_are_not_dictionary_entries():
+    """None (or validity 0) rows of a nullable string column take a placeholder code and validity 0."""
+    d = OrderedStringDict()
+    out = d.encode(["a", None, "b"])
+    assert len(d.sorted) == 2 and out[1] == 0
+    out = d.encode(["c", "zz"], np.array([1, 0], np.uint8))
+    assert "zz" not in d.code
+    rule = compile_rule("SELECT k, min(name), max(name) FROM s GROUP BY k, TUMBLINGWINDOW(ms, 300)", SCHEMA,
+                        num_keys=4, nullable=("name",))
+    cols, valid = rule.device_columns([np.zeros(3, np.uint32), np.full(3, T0, np.int64), ["q", None, "r"],
+                                       np.zeros(3)])
+    assert valid is not None and list(valid[2]) == [1, 0, 1]
+    strict = compile_rule("SELECT k, min(name) FROM s GROUP BY k, TUMBLINGWINDOW(ms, 300)", SCHEMA, num_keys=4)
+    with pytest.raises(ValueError):
+        strict.device_columns([np.zeros(2, np.uint32), np.full(2, T0, np.int64), ["q", None], np.zeros(2)])
+
+
 def _stream(n, keys, seed):
     rng = np.random.default_rng(seed)
     return [rng.integers(0, keys, n).astype(np.uint32), (T0 + np.arange(n) // 5).astype(np.int64), _words(rng, n),
