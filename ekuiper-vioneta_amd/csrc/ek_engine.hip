@@ -29,7 +29,7 @@
 #include "ek_lib.h"
 #include "ek_range.h"
 #include "ek_global.h"
-#include "ek_stream.h"
+#include "ek_stream_desc.h"
 #include "ek_keymajor.h"
 
 using namespace ek;
@@ -190,6 +190,19 @@ struct Engine {
     int chunk = 16384;
     LdsLayout lay{};
     int np_max = 8192;
+
+    // ---- processing time (execProcessingWindow under the caller's clock, ek_advance_time)
+    bool proc = false;                 // processing-time TUMBLING / HOPPING / SLIDING / SESSION
+    bool proc_pushdown = false;        // WHERE moved below the window (windowPlan.go:82-99): rows are pre-filtered
+    DPlan* d_plan_where = nullptr;     // the plan with WHERE, for the pre-filter (d_plan has n_where = 0 then)
+    bool clock_started = false;        // the rule's start: the first ek_advance_time, or the first row
+    int64_t clock_ms = 0;              // the clock (every timer due at or before it has fired)
+    // session timers (window_op.go:363-373,448-461): ticker due ps_tick, timeout due ps_to_due; next row to deliver
+    int64_t ps_tick = 0;
+    bool ps_to_exists = false, ps_to_armed = false;
+    int64_t ps_to_due = 0;
+    int64_t ps_next_abs = 0;
+    int64_t ps_last_nonmatch = INT64_MIN;   // SLIDING: ts of the latest delivered row not matching OVER (WHEN)
 
     // ---- stream state
     bool has_M = false;
@@ -384,7 +397,19 @@ struct Engine {
             if ((wtype <= EK_WINDOW_NONE || wtype > EK_WINDOW_SESSION) && !inc_count)
                 return fail(EK_ERR_UNSUPPORTED, "unsupported window type %d", wtype);
         } else if (wtype != EK_WINDOW_COUNT) {
-            return fail(EK_ERR_UNSUPPORTED, "processing-time windows other than COUNTWINDOW are wall-clock driven (use event time)");
+            // execProcessingWindow (window_op.go:235-470) under the caller's clock (ek_advance_time): tickers aligned
+            // to the rule's start, rows delivered at their arrival timestamps
+            if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING && wtype != EK_WINDOW_SLIDING && wtype != EK_WINDOW_SESSION)
+                return fail(EK_ERR_UNSUPPORTED, "unsupported processing-time window type %d", wtype);
+            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
+                return fail(EK_ERR_UNSUPPORTED, "delayed processing-time sliding windows fire from wall-clock timers per trigger: not built");
+            if (plan.incremental || plan.window_version == 2)
+                return fail(EK_ERR_UNSUPPORTED, "incremental / v2 processing-time windows are not built");
+            if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64 || (plan.nullable_mask & (1u << plan.ts_column)))
+                return fail(EK_ERR_INVALID, "processing-time windows need the rows' arrival timestamps (a non-nullable i64 column)");
+            proc = true;
+            // windowPlan.PushDownPredicate (windowPlan.go:82-99): WHERE below a processing-time TUMBLING / HOPPING / SESSION
+            proc_pushdown = plan.n_where > 0 && wtype != EK_WINDOW_SLIDING;
         }
         // incremental-aggregation window (planOptimizeStrategy.enableIncrementalWindow): the planner rewrites the
         // rule only when every aggregate is incremental and the window is COUNT (no interval) / SLIDING / HOPPING /
@@ -420,8 +445,9 @@ struct Engine {
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
             return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
-        need_rel = wtype == EK_WINDOW_SLIDING || (inc && wtype == EK_WINDOW_COUNT) ||
-                   (wtype == EK_WINDOW_SESSION && plan.late_tolerance_ms > 0);
+        need_rel = (wtype == EK_WINDOW_SLIDING && !proc) || (inc && wtype == EK_WINDOW_COUNT) ||
+                   (wtype == EK_WINDOW_SESSION && plan.late_tolerance_ms > 0 && !proc);
+        if (proc && plan.late_tolerance_ms != 0) return fail(EK_ERR_INVALID, "lateTolerance applies to event time only");
         if (plan.is_event_time) {
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64)
                 return fail(EK_ERR_INVALID, "event time needs an i64 timestamp column");
@@ -639,6 +665,11 @@ struct Engine {
         own_stream = true;
         hipEventCreate(&ev0);
         hipEventCreate(&ev1);
+        if (proc_pushdown) {
+            if (hipMalloc((void**)&d_plan_where, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
+            if (hipMemcpy(d_plan_where, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+            dp.n_where = 0;   // the pre-filter already dropped every row whose WHERE is not true
+        }
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
         if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
         if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
@@ -762,6 +793,13 @@ struct Engine {
         inc_pend.clear();
         gmode = 0;
         g_row_arr = nullptr;
+        clock_started = false;
+        clock_ms = kMinTs;
+        ps_tick = 0;
+        ps_to_exists = ps_to_armed = false;
+        ps_to_due = 0;
+        ps_next_abs = 0;
+        ps_last_nonmatch = INT64_MIN;
         g_wa = g_wt = nullptr;
         g_nwm = 0;
         g_trig.clear();
@@ -2214,6 +2252,8 @@ struct Engine {
         if (inc && wtype == EK_WINDOW_COUNT) return inc_count_triggers(rel_prev);
         if (wtype == EK_WINDOW_SLIDING && gmode) {
             if (int rc = global_slide_triggers(pw)) return rc;
+        } else if (wtype == EK_WINDOW_SLIDING && proc) {
+            if (int rc = proc_slide_triggers(rel_prev, pw)) return rc;
         } else if (wtype == EK_WINDOW_SLIDING) {
             const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
             if (n_new > 0) {
@@ -2308,7 +2348,9 @@ struct Engine {
                 E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
             }
             if (e1_known && has_W) {
-                hop_discard_pending = wtype == EK_WINDOW_HOPPING && !gmode;
+                // (processing time: a tick fires before any later row arrives, so the discard of an empty window
+                // never reaches a row the window could not hold; it is not applied)
+                hop_discard_pending = wtype == EK_WINDOW_HOPPING && !gmode && !proc;
                 while (win_end(next_win) <= W) {
                     const int64_t j = next_win++;
                     PendWin p{};
@@ -2321,6 +2363,8 @@ struct Engine {
                     pw.push_back(p);
                 }
             }
+        } else if (wtype == EK_WINDOW_SESSION && proc) {
+            if (int rc = proc_session_triggers(rel_prev, pw)) return rc;
         } else if (wtype == EK_WINDOW_SESSION) {
             if (int rc = session_triggers(rel_prev, pw)) return rc;
         } else if (wtype == EK_WINDOW_STATE) {
@@ -2718,6 +2762,310 @@ struct Engine {
         return 0;
     }
 
+    // ================================================================== processing time (ek_advance_time)
+    // WindowOperator.execProcessingWindow (window_op.go:235-470) with the caller's clock, as the reference's own tests
+    // drive it (pkg/timex mock clock, topotest/mock_topo.go:208-235): the rule opens at the first ek_advance_time (or
+    // at the first row); a row is delivered when the clock reaches its arrival timestamp, after every timer due at or
+    // before it; ek_advance_time(now) moves the clock without rows. Rows arrive in timestamp order.
+    //   TUMBLING / HOPPING: tickers from getAlignedWindowEndTime(start, rawInterval) every length / interval
+    //     (window_op.go:228-233,250-260,471-481); a tick scans the rows with ts < tick (time-related windows) - the
+    //     event-time pane / range machinery with E1 = the first tick and the watermark = the clock;
+    //   SLIDING (no delay): each row matching OVER (WHEN) scans at its own timestamp over the rows delivered so far
+    //     (window_op.go:353-379), [ts - length, ts] of the arrival prefix; a non-matching row garbage-collects the
+    //     rows with ts + length <= its ts (gcInputs, window_op.go:657-673), which only matters for a row exactly at
+    //     the left edge of a later trigger with the same timestamp;
+    //   SESSION: the timeout timer re-armed by every row, the ticker every length (window_op.go:363-373,448-461,483-492).
+    //   WHERE below TUMBLING / HOPPING / SESSION (windowPlan.go:82-99): rows are pre-filtered at delivery.
+    void start_clock(int64_t t0) {
+        clock_started = true;
+        clock_ms = t0;
+        if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_HOPPING) {
+            e1_known = true;
+            first_ts = 0;   // triggerTime is zero until the first scan: window_start falls back to end - length
+            E1 = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
+            grid.tumbling = wtype == EK_WINDOW_TUMBLING;
+            grid.origin = grid.tumbling ? E1 : E1 - L;
+            grid.P = P;
+        } else if (wtype == EK_WINDOW_SESSION) {
+            ps_tick = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
+        }
+    }
+
+    int push_proc(DBatch db) {
+        const int64_t n = db.n;
+        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+        const int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
+        if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
+        const int ph_s = phase_begin(EK_PHASE_STATS);
+        hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN, (BatchStats*)bstats_part.p);
+        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
+                           (BatchStats*)bstats.p);
+        phase_end(ph_s);
+        hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
+        const BatchStats s = *h_stats;
+        if (s.unsorted) return fail(EK_ERR_INVALID, "processing-time rows must arrive in timestamp order (their arrival times)");
+        if (!clock_started) start_clock(s.min_ts);
+        else if (s.min_ts < clock_ms)
+            return fail(EK_ERR_INVALID, "processing-time row at %lld is older than the clock (%lld)", (long long)s.min_ts,
+                        (long long)clock_ms);
+        const int64_t arrival_base = arrivals;
+        arrivals += n;
+        h_wdesc_used = 0;   // the stats sync above drained every earlier descriptor upload
+        h_desc_used = 0;
+        aux_used = 0;
+        if (proc_pushdown)
+            if (int rc = proc_prefilter(db, arrival_base)) { g_row_arr = nullptr; return rc; }
+        const int rc = proc_deliver(db, arrival_base, s.min_ts, s.max_ts);
+        g_row_arr = nullptr;
+        return rc;
+    }
+
+    // WHERE pushed below the window: the rows whose WHERE is true, compacted (stable), with their arrival indices as
+    // the batch's row arrivals (g_row_arr). A row whose WHERE errors is dropped and counted (FilterOp forwards its error).
+    DevBuf pf_cols[EK_MAX_COLUMNS], pf_valid[EK_MAX_COLUMNS], pf_arr;
+    int proc_prefilter(DBatch& db, int64_t arrival_base) {
+        const int64_t n = db.n;
+        if (int rc = ensure(flags_d, (size_t)n)) return rc;
+        if (int rc = ensure(trig_d, (size_t)n * 8)) return rc;
+        const int nb = (int)((n + kCompactTile - 1) / kCompactTile);
+        if (int rc = ensure(cnts_d, (size_t)(nb + 2) * 8)) return rc;
+        hipMemsetAsync((int64_t*)cnts_d.p + nb + 1, 0, 8, stream);
+        hipLaunchKernelGGL(k_filter_flags, dim3((int)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, stream, d_plan_where, db,
+                           (uint8_t*)flags_d.p, (unsigned long long*)((int64_t*)cnts_d.p + nb + 1));
+        hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (int64_t*)cnts_d.p);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+        hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n, (const int64_t*)cnts_d.p,
+                           (int64_t)0, (int64_t*)trig_d.p);
+        int64_t sel_err[2] = {0, 0};
+        hipMemcpyAsync(sel_err, (int64_t*)cnts_d.p + nb, 16, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "pre-filter failed");
+        const int64_t ns = sel_err[0];
+        stats.records_filter_error += sel_err[1];
+        DBatch fb{};
+        fb.n = ns;
+        const int g = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (ns + 255) / 256));
+        for (int c = 0; c < plan.n_columns; ++c) {
+            const int es = plan.column_type[c] == EK_COL_U32 ? 4 : 8;
+            if (int rc = ensure(pf_cols[c], (size_t)std::max<int64_t>(ns, 1) * es)) return rc;
+            uint8_t* vd = nullptr;
+            if (db.valid[c]) {
+                if (int rc = ensure(pf_valid[c], (size_t)std::max<int64_t>(ns, 1))) return rc;
+                vd = (uint8_t*)pf_valid[c].p;
+            }
+            if (ns > 0)
+                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)trig_d.p, ns, db.col[c], es,
+                                   db.valid[c], pf_cols[c].p, vd);
+            fb.col[c] = pf_cols[c].p;
+            fb.valid[c] = vd;
+        }
+        if (int rc = ensure(pf_arr, (size_t)std::max<int64_t>(ns, 1) * 8)) return rc;
+        if (ns > 0)
+            hipLaunchKernelGGL(k_offset_idx, dim3(g), dim3(256), 0, stream, (const int64_t*)trig_d.p, ns, arrival_base,
+                               (int64_t*)pf_arr.p);
+        g_row_arr = (const int64_t*)pf_arr.p;
+        db = fb;
+        return 0;
+    }
+
+    // the clock moves to max_ts delivering the batch's rows (timers due at or before each row fire first)
+    int proc_deliver(const DBatch& db, int64_t arrival_base, int64_t min_ts, int64_t max_ts) {
+        if (!has_M || max_ts > M) { M = max_ts; has_M = true; }
+        W = max_ts;
+        has_W = true;
+        int rc = 0;
+        if (range_mode) {
+            if (db.n > 0)
+                if (int r = eb_append(db, 0, db.n, arrival_base)) return r;
+            const int64_t rel_prev = eb_rel;
+            eb_rel = eb.n;
+            rc = range_triggers(rel_prev);
+            if (!rc && wtype == EK_WINDOW_SLIDING) rc = proc_slide_floor();
+        } else if (db.n > 0) {
+            const int64_t save = arrivals;
+            arrivals = arrival_base;
+            rc = process(db, true, 0, nullptr, min_ts, max_ts, g_row_arr);
+            arrivals = save;
+        } else {
+            rc = proc_close();
+        }
+        clock_ms = max_ts;
+        return rc;
+    }
+
+    // pane mode, no rows: every window whose tick is due fires (its panes can no longer receive rows)
+    int proc_close() {
+        if (!e1_known || W < win_end(next_win)) return 0;
+        const int64_t nclose = (W - win_end(next_win)) / H + 1;
+        if (int rc = ensure_results(nclose * Krows(), nclose)) return rc;
+        return finalize_ready(INT64_MAX);
+    }
+
+    int advance_time(int64_t now) {
+        if (!proc) return fail(EK_ERR_STATE, "ek_advance_time drives processing-time TUMBLING / HOPPING / SLIDING / SESSION windows");
+        if (!clock_started) { start_clock(now); return 0; }
+        if (now < clock_ms) return fail(EK_ERR_INVALID, "the clock cannot move back (%lld < %lld)", (long long)now, (long long)clock_ms);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream failed");
+        phase_used = 0;
+        hipEventRecord(ev0, stream);
+        h_wdesc_used = 0;
+        h_desc_used = 0;
+        aux_used = 0;
+        W = now;
+        has_W = true;
+        int rc = 0;
+        if (range_mode) {
+            rc = range_triggers(eb_rel);
+            if (!rc && wtype == EK_WINDOW_SLIDING) rc = proc_slide_floor();
+        } else {
+            rc = proc_close();
+        }
+        clock_ms = now;
+        return rc ? rc : record_time();
+    }
+
+    // SLIDING: one window per delivered row matching OVER (WHEN), over the rows delivered up to it:
+    // [lb(ts - length), row]; the left edge moves one ms in when a non-matching row with the same ts as the trigger
+    // arrived before it (its gcInputs dropped the rows with ts + length <= ts).
+    int proc_slide_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
+        const int64_t n_new = eb_rel - rel_prev;
+        if (n_new <= 0) return 0;
+        if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
+        if (int rc = ensure(trig_d, (size_t)n_new * 8)) return rc;
+        const int nb = (int)((n_new + kCompactTile - 1) / kCompactTile);
+        if (int rc = ensure(cnts_d, (size_t)(nb + 1) * 8)) return rc;
+        const DBatch bv = buffer_view();
+        hipLaunchKernelGGL(k_trigger_flags, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
+                           d_plan, bv, rel_prev, eb_rel, (uint8_t*)flags_d.p);
+        hipLaunchKernelGGL(k_flag_count, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new, (int64_t*)cnts_d.p);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, stream, (int64_t*)cnts_d.p, nb);
+        hipLaunchKernelGGL(k_flag_write, dim3(nb), dim3(kBlock), 0, stream, (const uint8_t*)flags_d.p, n_new,
+                           (const int64_t*)cnts_d.p, rel_prev, (int64_t*)trig_d.p);
+        const int64_t nt = fetch_i64((const int64_t*)cnts_d.p + nb);
+        std::vector<int64_t> pos(std::max<int64_t>(nt, 0)), tts(std::max<int64_t>(nt, 0));
+        if (nt > 0) hipMemcpyAsync(pos.data(), trig_d.p, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+        if (int rc = ensure(mrg_col, (size_t)(nt + 1) * 24)) return rc;
+        int64_t* g_ts = (int64_t*)mrg_col.p;
+        if (nt > 0) {
+            hipLaunchKernelGGL(k_gather8, dim3((int)std::min<int64_t>(4096, (nt + 255) / 256)), dim3(256), 0, stream,
+                               (const int64_t*)trig_d.p, nt, INT64_MAX, (const int64_t*)eb.col[dp.ts_col].p,
+                               (const int64_t*)nullptr, (const int64_t*)nullptr, g_ts);
+            hipMemcpyAsync(tts.data(), g_ts, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+        // the latest non-matching row before each trigger (its ts decides the gcInputs edge): the row just before the
+        // trigger unless that row is a trigger too (then the same as that trigger's); rows before this batch: carried
+        std::vector<int64_t> qpos;            // batch rows whose ts is needed (non-matching predecessors, the last row)
+        std::vector<int64_t> nm_ref(std::max<int64_t>(nt, 0));   // >= 0: index into qpos; -1: the carried value
+        for (int64_t k = 0; k < nt; ++k) {
+            if (k > 0 && pos[k - 1] == pos[k] - 1) { nm_ref[k] = nm_ref[k - 1]; continue; }
+            if (pos[k] - 1 >= rel_prev) { nm_ref[k] = (int64_t)qpos.size(); qpos.push_back(pos[k] - 1); }
+            else nm_ref[k] = -1;
+        }
+        const bool last_is_trig = nt > 0 && pos[nt - 1] == eb_rel - 1;
+        int64_t last_ref = -1;
+        if (!last_is_trig) { last_ref = (int64_t)qpos.size(); qpos.push_back(eb_rel - 1); }
+        std::vector<int64_t> qts(qpos.size());
+        if (!qpos.empty()) {
+            const int64_t nq = (int64_t)qpos.size();
+            int64_t* d_q = g_ts + nt;
+            hipMemcpyAsync(d_q, qpos.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_gather8, dim3((int)std::min<int64_t>(4096, (nq + 255) / 256)), dim3(256), 0, stream, d_q, nq,
+                               INT64_MAX, (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)nullptr, (const int64_t*)nullptr,
+                               d_q + nq);
+            hipMemcpyAsync(qts.data(), d_q + nq, (size_t)nq * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+        }
+        std::vector<int64_t> prevts(std::max<int64_t>(nt, 0));
+        for (int64_t k = 0; k < nt; ++k) prevts[k] = nm_ref[k] >= 0 ? qts[nm_ref[k]] : ps_last_nonmatch;
+        ps_last_nonmatch = last_is_trig ? prevts[nt - 1] : qts[last_ref];
+        for (int64_t k = 0; k < nt; ++k) {
+            const int64_t t = tts[k];
+            PendWin p{};
+            p.q.kind = RB_UPTO;
+            p.q.lo_ts = prevts[k] == t ? t - L + 1 : t - L;
+            p.q.pos = pos[k];
+            p.q.floor = eb_floor;
+            p.start = t - L;   // scan(): windowStart = t - length (window_op.go:697-707)
+            p.end = t;
+            pw.push_back(p);
+        }
+        return 0;
+    }
+    // rows older than clock - length can no longer be in a window (every later trigger is at or after the clock)
+    int proc_slide_floor() {
+        if (eb_rel <= eb_floor) return 0;
+        const int64_t bound = W - L;
+        if (int rc = ensure(bounds_val, 8)) return rc;
+        if (int rc = ensure(bounds_idx, 8)) return rc;
+        hipMemcpyAsync(bounds_val.p, &bound, 8, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p, eb_floor, eb_rel,
+                           (const int64_t*)bounds_val.p, 1, (int64_t*)bounds_idx.p);
+        eb_floor = std::max(eb_floor, fetch_i64((const int64_t*)bounds_idx.p));
+        return 0;
+    }
+
+    // SESSION: the delivered rows' timestamps are mirrored on the host and the timers replayed in due order:
+    // the ticker (due ps_tick, every length) closes the inputs when the first one is at least length old; the timeout
+    // (due ps_to_due, re-armed by every row) closes them. A close takes every input (all are older than the clock).
+    int proc_session_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
+        const int64_t n_new = eb_rel - rel_prev;
+        if (h_rts.empty()) { h_rts_base = eb_base + rel_prev; if (ps_next_abs < h_rts_base) ps_next_abs = h_rts_base; }
+        if (n_new > 0) {
+            const size_t o = h_rts.size();
+            h_rts.resize(o + n_new);
+            hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "session mirror copy failed");
+        }
+        int64_t floor_abs = eb_base + eb_floor;
+        const int64_t end_abs = eb_base + eb_rel;
+        auto close = [&](int64_t at, int64_t upto_abs) {
+            PendWin p{};
+            p.q.kind = RB_FIXED;
+            p.q.pos = floor_abs - eb_base;
+            p.q.rstep = upto_abs - eb_base;
+            int64_t ws = sess_has_trigger ? sess_trigger : 0;
+            if (ws <= 0) ws = at - L;
+            p.start = ws;
+            p.end = at;
+            pw.push_back(p);
+            floor_abs = upto_abs;
+            sess_trigger = at;
+            sess_has_trigger = true;
+        };
+        // timers due at or before `now` with `upto_abs` rows delivered (ticker first on a tie)
+        auto timers = [&](int64_t now, int64_t upto_abs) {
+            for (;;) {
+                const bool tk = ps_tick <= now;
+                const bool tm = ps_to_armed && ps_to_due <= now && (!tk || ps_to_due < ps_tick);
+                if (tm) {
+                    ps_to_armed = false;
+                    if (floor_abs < upto_abs) { close(ps_to_due, upto_abs); ps_to_exists = false; }
+                } else if (tk) {
+                    if (floor_abs < upto_abs && ps_tick - h_rts[floor_abs - h_rts_base] >= L) close(ps_tick, upto_abs);
+                    ps_tick += L;
+                } else {
+                    break;
+                }
+            }
+        };
+        for (int64_t r = ps_next_abs; r < end_abs; ++r) {
+            const int64_t t = h_rts[r - h_rts_base];
+            timers(t, r);
+            if (!ps_to_exists) { ps_to_exists = true; sess_trigger = t; sess_has_trigger = true; }
+            ps_to_armed = true;
+            ps_to_due = t + H;
+        }
+        ps_next_abs = end_abs;
+        timers(W, end_abs);
+        const int64_t drop = floor_abs - h_rts_base;
+        if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
+            h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+            h_rts_base = floor_abs;
+        }
+        return 0;
+    }
+
     // Event-time push in range mode, after the shared late-drop / watermark steps.
     int push_range(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t n_acc, int64_t min_acc,
                    int64_t max_ts, int64_t arrival_base, int64_t M_prev, bool had_M, int64_t batch_min) {
@@ -2909,6 +3257,10 @@ struct Engine {
             const int rc = state_scan(lo, eb_rel);
             return rc ? rc : record_time();
         }
+        if (proc) {
+            const int rc = push_proc(db);
+            return rc ? rc : record_time();
+        }
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
 
         // ---- 1. batch statistics (one pass over ts)
@@ -3093,12 +3445,13 @@ struct Engine {
         sd.sync = (uint32_t*)s_sync.p;
         sd.klo = (uint16_t*)s_klo.p;
         for (int v = 0; v < dp.n_vc; ++v) sd.val[v] = (int64_t*)s_val[v].p;
-        sd.ctab = (uint32_t*)s_ctab.p;
+        sd.ctab = (unsigned long long*)s_ctab.p;
         sd.prof = nullptr;
         if (env_int("EKGPU_STREAM_PROF", 0) && ensure(s_prof, (size_t)stream_grid * 64) == 0) sd.prof = (unsigned long long*)s_prof.p;
         return sd;
     }
-    size_t stream_sync_bytes() const { return ((size_t)(10 + kSXcd * s_max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15; }
+    size_t stream_sync_bytes() const { return ((size_t)(10 + kSXcd * kSRing) * 4 + 15) & ~(size_t)15; }
+    size_t stream_ctab_bytes() const { return (size_t)kSXcd * kSRing * stream_owners * 8; }
 
     // Decide once per handle: plan shape, LDS budget, and a probe launch proving the grid is co-resident with
     // `owners` workgroups on each of the 8 XCDs (the kernel checks it before any side effect).
@@ -3139,7 +3492,7 @@ struct Engine {
         if (int rc = ensure(s_klo, (size_t)kSXcd * kSRing * kSTile * 2)) return rc;
         for (int v = 0; v < dp.n_vc; ++v)
             if (int rc = ensure(s_val[v], (size_t)kSXcd * kSRing * kSTile * 8)) return rc;
-        if (int rc = ensure(s_ctab, (size_t)kSXcd * kSRing * (stream_owners + 1) * 4)) return rc;
+        if (int rc = ensure(s_ctab, stream_ctab_bytes())) return rc;
         // probe: an empty work list (every XCD has no pane)
         if (int rc = ensure(s_tab, 4096)) return rc;
         hipMemsetAsync(s_tab.p, 0, 4096, stream);
@@ -3148,6 +3501,7 @@ struct Engine {
         sd.xcpre = (const int32_t*)s_tab.p;
         sd.xpane = (const int32_t*)s_tab.p;
         hipMemsetAsync(s_sync.p, 0, stream_sync_bytes(), stream);
+        hipMemsetAsync(s_ctab.p, 0, stream_ctab_bytes(), stream);
         DBatch empty{};
         launch_stream(empty, sd);
         uint32_t err = 0;
@@ -3253,7 +3607,9 @@ struct Engine {
         sd.xoff = (const int32_t*)s_tab.p;
         sd.xpane = sd.xoff + xoff.size();
         sd.xcpre = sd.xpane + xpane.size();
-        hipMemsetAsync(s_sync.p, 0, ((size_t)(10 + kSXcd * sd.max_chunks + kSXcd * kSRing) * 4 + 15) & ~(size_t)15, stream);
+        // every launch starts from untagged run descriptors (a tag is a chunk index of this launch)
+        hipMemsetAsync(s_sync.p, 0, stream_sync_bytes(), stream);
+        hipMemsetAsync(s_ctab.p, 0, stream_ctab_bytes(), stream);
         // fresh panes: zero their WHERE error flag and membership fingerprint (k_group_prep)
         hipLaunchKernelGGL(k_group_prep, dim3((npn + 255) / 256), dim3(256), 0, stream, gd, (int32_t*)pane_err.p,
                            (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
@@ -4021,6 +4377,7 @@ struct Engine {
         release(wdesc); release(r_key); release(r_wcnt); release(r_werr); release(r_wmc); release(r_wmh);
         for (int k = 0; k < EK_MAX_AGGS; ++k) { release(r_val[k]); release(r_tag[k]); }
         if (d_plan) hipFree(d_plan);
+        if (d_plan_where) hipFree(d_plan_where);
         if (h_stats) hipHostFree(h_stats);
         if (h_small) hipHostFree(h_small);
         if (h_wdesc) hipHostFree(h_wdesc);
@@ -4134,6 +4491,11 @@ int ek_destroy(void* h) {
 int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g) {
     if (!h) return EK_ERR_INVALID;
     return ((Engine*)h)->push_global(batch, g);
+}
+
+int ek_advance_time(void* h, int64_t now_ms) {
+    if (!h) return EK_ERR_INVALID;
+    return static_cast<Engine*>(h)->advance_time(now_ms);
 }
 
 int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end) {

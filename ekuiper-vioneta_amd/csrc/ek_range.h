@@ -208,6 +208,21 @@ __global__ void k_filter_flags(DPlan* __restrict__ pp, DBatch b, uint8_t* __rest
     if ((threadIdx.x & 63) == 0 && e) atomicAdd(n_err, e);
 }
 
+// rows sel[0..ns) of one column (4- or 8-byte elements) and of its validity bytes, compacted (pushed-down WHERE)
+__global__ void k_compact_col(const int64_t* __restrict__ sel, int64_t ns, const void* __restrict__ src, int es,
+                              const uint8_t* __restrict__ vsrc, void* __restrict__ dst, uint8_t* __restrict__ vdst) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = sel[k];
+        if (es == 4) ((uint32_t*)dst)[k] = ((const uint32_t*)src)[i];
+        else ((int64_t*)dst)[k] = ((const int64_t*)src)[i];
+        if (vdst) vdst[k] = vsrc[i];
+    }
+}
+// out[k] = base + idx[k]
+__global__ void k_offset_idx(const int64_t* __restrict__ idx, int64_t n, int64_t base, int64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) out[k] = base + idx[k];
+}
+
 // SELECT * rows of the selected events: key = batch row, value c = column c (tag by type / validity)
 __global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ sel, int64_t ns, int64_t out_base,
                               int32_t widx, Results res) {

@@ -5,10 +5,10 @@
 // the Infinity Cache does not absorb that round trip (a just-written buffer reads back at the HBM rate,
 // tools/mb_mall.hip). Here one persistent launch keeps the staging inside each XCD's 4 MiB L2:
 //   * every XCD (HW_REG_XCC_ID) owns a contiguous range of the batch's panes, balanced by events; its panes are
-//     cut into 4096-row chunks on a per-pane grid, numbered j = 0, 1, ... in event order;
+//     cut into 2048-row chunks on a per-pane grid, numbered j = 0, 1, ... in event order;
 //   * half of the XCD's workgroups are PRODUCERS: producer i takes chunks i, i + P, i + 2P, ...; it loads a chunk
 //     once (16-byte key / value loads, the next chunk's loads issued before this one is partitioned), counting-
-//     sorts it in LDS by owner and writes the owner runs into ring slot j mod kSRing (kSRing x 72 KiB stays in L2);
+//     sorts it in LDS by owner and writes the owner runs into ring slot j mod kSRing (kSRing x 36 KiB stays in L2);
 //   * the other half are CONSUMERS: consumer o owns the key range [o << obits, (o + 1) << obits) and keeps its
 //     partial table of the current pane in LDS; it folds in its run of every chunk of the XCD in chunk order and
 //     finalises its key range of a pane after the pane's last chunk, exactly as k_agg does (direct emission of a
@@ -21,62 +21,15 @@
 // rewritten only after every consumer of the XCD has counted it folded in. Every spin is bounded; a grid that is
 // not co-resident (P producers + P consumers on each XCD) is detected before any side effect (sync->err = 1).
 #pragma once
-#include "ek_kernels.h"
+// constants, StreamDesc, xcc_id / ld_acq32 and the launcher declaration
+#include "ek_stream_desc.h"
 
 namespace ek {
-
-constexpr int kSBlock = 512;          // threads per workgroup (two per CU: one producer, one consumer)
-constexpr int kSTile = 4096;          // events per chunk
-constexpr int kSTileE = kSTile / kSBlock;
-#ifndef EK_SRING
-#define EK_SRING 32
-#endif
-constexpr int kSRing = EK_SRING;      // staging slots per XCD (32 x 72 KiB for two f64 columns: L2-resident)
-constexpr int kSXcd = 8;
-constexpr int kSMaxOwners = 64;       // consumers (= producers) per XCD
-constexpr int kSBatch = 32;           // chunks folded in per consume step (<= 63: one wave polls them)
-constexpr int kSU = 4;                // staged rows in flight per thread while folding in
-constexpr int kSMaxXPanes = 512;      // panes per XCD per launch
-
-struct StreamDesc {
-    int64_t nbatch;
-    int64_t q_lo;
-    int32_t n_panes;       // panes [q_lo, q_lo + n_panes) of the batch
-    int32_t ring;          // pane-state ring
-    int32_t key_col, n_where;
-    uint32_t num_keys;
-    int32_t owners;        // consumers (= producers) per XCD
-    int32_t obits;         // key range of a consumer = [o << obits, (o + 1) << obits)
-    int32_t max_chunks;    // per-XCD capacity of the chunk flags
-    int32_t nvc;
-    int32_t pad;
-    int64_t timeout;       // s_memrealtime ticks (100 MHz) a spin may last
-    const int64_t* pbnd;   // [n_panes + 1] first event of each pane
-    const int32_t* xpane;  // panes of each XCD (group-relative), x-major, [n_panes]
-    const int32_t* xoff;   // [kSXcd + 1] offsets into xpane
-    const int32_t* xcpre;  // per XCD x: chunk prefix over its panes at xcpre[xoff[x] + x + k], k = 0..count
-    const int64_t* dbase;  // per pane: direct-emission row base or -1
-    const int32_t* didx;   // per pane: window index (direct emission)
-    const uint8_t* fresh;  // per pane: 1 = write, 0 = merge into the pane state
-    uint32_t* sync;        // [0] arrived, [1] err, [2..10) members, then flags[8][max_chunks], cons[8][kSRing]
-    uint16_t* klo;         // [kSXcd][kSRing][kSTile]
-    int64_t* val[kMaxVC];  // [kSXcd][kSRing][kSTile]
-    uint32_t* ctab;        // [kSXcd][kSRing][owners + 1]
-    unsigned long long* prof;   // optional [grid][8] per-workgroup time split (EKGPU_STREAM_PROF)
-};
-
-__device__ __forceinline__ int xcc_id() {
-    // HW_REG_XCC_ID (hwreg 20), bits [3:0]
-    return (int)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 15);
-}
-__device__ __forceinline__ uint32_t ld_acq32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // LDS: consumer = [table: per key of the owner range, 8-byte fields then u32 counts];
 //      producer = [s_val: NVC x kSTile x 8][s_klo: kSTile x 2]
 template <int NVC, bool WHERE>
-__global__ __launch_bounds__(kSBlock) void k_stream(
+__global__ __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_stream(
     DPlan* __restrict__ pp, DBatch b, StreamDesc sd, LdsLayout lay, DState ds, Results res, int32_t* __restrict__ pane_err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const DPlan& p = *pp;
@@ -84,14 +37,12 @@ __global__ __launch_bounds__(kSBlock) void k_stream(
     __shared__ int s_i[8];
     __shared__ uint32_t s_tcnt[kSMaxOwners + 4];
     __shared__ uint32_t s_wsum[kSBlock / 64];
-    __shared__ uint32_t r_start[kSBatch], r_pre[kSBatch + 1];
-    static_assert(kSBatch <= 63, "one wave polls a consume batch");
+    static_assert(kSWaveBatch < 64, "one wave polls its batch");
     __shared__ uint32_t esh[20];
     uint32_t* g_arrived = sd.sync;
     uint32_t* g_err = sd.sync + 1;
     uint32_t* g_members = sd.sync + 2;
-    uint32_t* g_flags = sd.sync + 10;
-    uint32_t* g_cons = g_flags + (size_t)kSXcd * sd.max_chunks;
+    uint32_t* g_cons = sd.sync + 10;
     const int x = xcc_id();
     const int P = sd.owners;
 
@@ -117,7 +68,6 @@ __global__ __launch_bounds__(kSBlock) void k_stream(
     const int xo = sd.xoff[x], nxp = sd.xoff[x + 1] - xo;
     const int32_t* cpre = sd.xcpre + xo + x;     // [nxp + 1]
     const int c_total = nxp > 0 ? cpre[nxp] : 0;
-    uint32_t* flags = g_flags + (size_t)x * sd.max_chunks;
     uint32_t* cons = g_cons + (size_t)x * kSRing;
     int fl[NVC], vcol[NVC];
     bool isf[NVC];
@@ -222,8 +172,6 @@ __global__ __launch_bounds__(kSBlock) void k_stream(
             }
             __syncthreads();
             block_excl_scan<kSBlock>(s_tcnt, P, s_wsum);
-            uint32_t* ct = sd.ctab + ((size_t)x * kSRing + slot) * (P + 1);
-            for (int t = tid; t <= P; t += kSBlock) ct[t] = s_tcnt[t];
 #pragma unroll
             for (int jj = 0; jj < kSTileE; ++jj) {
                 if (lp[jj] < 0) continue;
@@ -251,10 +199,17 @@ __global__ __launch_bounds__(kSBlock) void k_stream(
                     else sd.val[v][region + s] = s_val[(size_t)v * kSTile + s];
                 }
             }
-            // publish: every storing wave drains (this also waits for the next chunk's loads), then one lane flags
+            // publish: every storing wave drains (this also waits for the next chunk's loads), then each consumer's
+            // run descriptor goes out tagged with the chunk: (j + 1) << 32 | offset << 16 | length, one 8-byte
+            // agent-scope atomic store per owner, so a consumer learns readiness and its run in one load
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(&flags[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid < P) {
+                const uint64_t d = ((uint64_t)(uint32_t)(j + 1) << 32) | ((uint64_t)s_tcnt[tid] << 16) |
+                                   (uint64_t)(s_tcnt[tid + 1] - s_tcnt[tid]);
+                __hip_atomic_store(sd.ctab + ((size_t)x * kSRing + slot) * P + tid, (unsigned long long)d, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
             pt[2] += __builtin_amdgcn_s_memrealtime() - t1;
             pt[5]++;
             cur = nxt;
@@ -367,104 +322,101 @@ __global__ __launch_bounds__(kSBlock) void k_stream(
 
         zero_table();
         __syncthreads();
-        int next_c = 0, cur_k = 0;
-        uint64_t idle_since = __builtin_amdgcn_s_memrealtime();
-        while (next_c < c_total) {
-            const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
-            // wave 0: lane t polls chunk next_c + t (within the current pane); g = the leading run of published chunks
-            if (tid < 64) {
-                const int want = min(cpre[cur_k + 1], next_c + kSBatch) - next_c;
-                const bool set = tid < want && ld_acq32(&flags[next_c + tid]) != 0u;
+        // Every wave folds in its own chunks independently (no workgroup barrier inside a pane): wave w takes chunks
+        // c0 + w, c0 + w + kSWaves, ... of the pane, polls up to kSWaveBatch of them at once (one tagged descriptor
+        // per lane), folds the ready ones' runs with all its lanes (LDS atomics on the shared table) and counts
+        // them consumed. The workgroup meets only at a pane's end, to finalise the pane.
+        constexpr int kSWaves = kSBlock / 64;
+        const int lane = tid & 63, wv = tid >> 6;
+        __shared__ uint32_t w_start[kSWaves][kSWaveBatch], w_pre[kSWaves][kSWaveBatch + 1];
+        for (int k = 0; k < nxp; ++k) {
+            const int c1 = cpre[k + 1];
+            int j = cpre[k] + wv;
+            uint64_t idle_since = __builtin_amdgcn_s_memrealtime();
+            bool failed = false;
+            while (j < c1) {
+                const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+                const int jj = j + kSWaves * lane;
+                uint64_t d = 0;
+                if (lane < kSWaveBatch && jj < c1)
+                    d = __hip_atomic_load(sd.ctab + ((size_t)x * kSRing + jj % kSRing) * P + owner, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                const bool set = lane < kSWaveBatch && jj < c1 && (uint32_t)(d >> 32) == (uint32_t)(jj + 1);
                 const unsigned long long m = __ballot(set);
-                if (tid == 0) {
-                    s_i[2] = (int)__builtin_ctzll(~m);
-                    s_i[5] = s_i[2] == 0 ? (int)ld_acq32(g_err) : 0;
+                const int g = (int)__builtin_ctzll(~m);   // kSWaveBatch < 64: ~m is never 0
+                if (g == 0) {
+                    if (ld_acq32(g_err) || timed_out(idle_since)) { failed = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    pt[3] += __builtin_amdgcn_s_memrealtime() - tc0;
+                    continue;
                 }
-            }
-            __syncthreads();
-            const int g = s_i[2];
-            if (g == 0) {
-                const int e = s_i[5];
-                __syncthreads();
-                if (e || timed_out(idle_since)) { if (tid == 0) atomicOr(g_err, 2u); return; }
-                __builtin_amdgcn_s_sleep(1);
-                pt[3] += __builtin_amdgcn_s_memrealtime() - tc0;
-                continue;
-            }
-            if (tid < g) {
-                const int slot = (next_c + tid) % kSRing;
-                const uint32_t* ct = sd.ctab + ((size_t)x * kSRing + slot) * (P + 1);
-                const uint32_t o0 = __builtin_nontemporal_load(ct + owner), o1 = __builtin_nontemporal_load(ct + owner + 1);
-                r_start[tid] = (uint32_t)(((size_t)x * kSRing + slot) * kSTile) + o0;
-                r_pre[tid + 1] = o1 - o0;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                r_pre[0] = 0;
-                for (int t = 0; t < g; ++t) r_pre[t + 1] += r_pre[t];
-            }
-            __syncthreads();
-            const uint32_t total = r_pre[g];
-            for (uint32_t v0 = 0; v0 < total; v0 += kSBlock * kSU) {
-                int kl[kSU];
-                int64_t raw[NVC][kSU];
+                const uint32_t len = lane < g ? (uint32_t)(d & 0xFFFFu) : 0u;
+                uint32_t incl = len;
+                for (int o = 1; o < kSWaveBatch; o <<= 1) { const uint32_t y = __shfl_up(incl, o, 64); if (lane >= o) incl += y; }
+                if (lane < g) {
+                    w_start[wv][lane] = (uint32_t)(((size_t)x * kSRing + jj % kSRing) * kSTile) + (uint32_t)((d >> 16) & 0xFFFFu);
+                    w_pre[wv][lane] = incl - len;
+                }
+                const uint32_t total = __shfl(incl, g - 1, 64);
+                for (uint32_t v0 = 0; v0 < total; v0 += 64 * kSU) {
+                    int kl[kSU];
+                    int64_t raw[NVC][kSU];
 #pragma unroll
-                for (int u = 0; u < kSU; ++u) {
-                    const uint32_t v = v0 + u * kSBlock + tid;
-                    kl[u] = -1;
-                    if (v < total) {
-                        int lo = 0, hi = g - 1;   // run of row v: last j with r_pre[j] <= v
-                        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (r_pre[mid] <= v) lo = mid; else hi = mid - 1; }
-                        const size_t pos = (size_t)r_start[lo] + (v - r_pre[lo]);
-                        kl[u] = (int)__builtin_nontemporal_load(sd.klo + pos);
+                    for (int u = 0; u < kSU; ++u) {
+                        const uint32_t v = v0 + u * 64 + lane;
+                        kl[u] = -1;
+                        if (v < total) {
+                            int r = 0;   // run of row v: last r with w_pre[r] <= v
+                            while (r + 1 < g && w_pre[wv][r + 1] <= v) ++r;
+                            const size_t pos = (size_t)w_start[wv][r] + (v - w_pre[wv][r]);
+                            kl[u] = (int)__builtin_nontemporal_load(sd.klo + pos);
 #pragma unroll
-                        for (int w = 0; w < NVC; ++w) raw[w][u] = fl[w] ? __builtin_nontemporal_load(sd.val[w] + pos) : 0;
+                            for (int w = 0; w < NVC; ++w) raw[w][u] = fl[w] ? __builtin_nontemporal_load(sd.val[w] + pos) : 0;
+                        }
                     }
-                }
 #pragma unroll
-                for (int u = 0; u < kSU; ++u) {
-                    if (kl[u] < 0) break;
-                    atomicAdd(&lcnt[kl[u]], 1u);
+                    for (int u = 0; u < kSU; ++u) {
+                        if (kl[u] < 0) break;
+                        atomicAdd(&lcnt[kl[u]], 1u);
 #pragma unroll
-                    for (int w = 0; w < NVC; ++w) {
-                        const int f = fl[w];
-                        if (f == 0) continue;
-                        if (isf[w]) {
-                            const double xv = __longlong_as_double(raw[w][u]);
-                            if (f & NEED_SUM) atomicAdd(&((double*)(lds + lay.off_sum[w]))[kl[u]], xv);
-                            if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[w]))[kl[u]], (unsigned long long)~f64_to_ord(xv));
-                            if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[w]))[kl[u]], (unsigned long long)f64_to_ord(xv));
-                        } else {
-                            if (f & NEED_SUM) atomicAdd(&((unsigned long long*)(lds + lay.off_sum[w]))[kl[u]], (unsigned long long)raw[w][u]);
-                            if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[w]))[kl[u]], (unsigned long long)~i64_to_ord(raw[w][u]));
-                            if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[w]))[kl[u]], (unsigned long long)i64_to_ord(raw[w][u]));
+                        for (int w = 0; w < NVC; ++w) {
+                            const int f = fl[w];
+                            if (f == 0) continue;
+                            if (isf[w]) {
+                                const double xv = __longlong_as_double(raw[w][u]);
+                                if (f & NEED_SUM) atomicAdd(&((double*)(lds + lay.off_sum[w]))[kl[u]], xv);
+                                if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[w]))[kl[u]], (unsigned long long)~f64_to_ord(xv));
+                                if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[w]))[kl[u]], (unsigned long long)f64_to_ord(xv));
+                            } else {
+                                if (f & NEED_SUM) atomicAdd(&((unsigned long long*)(lds + lay.off_sum[w]))[kl[u]], (unsigned long long)raw[w][u]);
+                                if (f & NEED_MIN) atomicMax(&((unsigned long long*)(lds + lay.off_min[w]))[kl[u]], (unsigned long long)~i64_to_ord(raw[w][u]));
+                                if (f & NEED_MAX) atomicMax(&((unsigned long long*)(lds + lay.off_max[w]))[kl[u]], (unsigned long long)i64_to_ord(raw[w][u]));
+                            }
                         }
                     }
                 }
+                // the wave's loads of these slots have returned (their values went into the LDS atomics): free them
+                if (lane < g) atomicAdd(&cons[jj % kSRing], 1u);
+                j += kSWaves * g;
+                idle_since = __builtin_amdgcn_s_memrealtime();
+                pt[4] += idle_since - tc0;
+                pt[6]++;
             }
-            __syncthreads();   // every run of these slots has been read (loads returned into the LDS atomics)
-            if (tid < g) atomicAdd(&cons[(next_c + tid) % kSRing], 1u);
-            next_c += g;
+            if (failed) atomicOr(g_err, 2u);
+            __syncthreads();   // every wave has folded in its chunks of the pane
+            if (tid == 0) s_i[6] = (int)ld_acq32(g_err);
+            __syncthreads();
+            if (s_i[6]) return;   // (uniform: one read for the whole workgroup)
             const uint64_t tc1 = __builtin_amdgcn_s_memrealtime();
-            pt[4] += tc1 - tc0;
-            pt[6]++;
-            if (next_c == cpre[cur_k + 1]) {
-                finish_pane(sd.xpane[xo + cur_k]);
-                __syncthreads();
-                zero_table();
-                cur_k++;
-                __syncthreads();
-                pt[7] += __builtin_amdgcn_s_memrealtime() - tc1;
-            }
-            idle_since = __builtin_amdgcn_s_memrealtime();
+            finish_pane(sd.xpane[xo + k]);
+            __syncthreads();
+            zero_table();
+            __syncthreads();
+            pt[7] += __builtin_amdgcn_s_memrealtime() - tc1;
         }
     }
     if (sd.prof && tid == 0)
         for (int k = 0; k < 8; ++k) sd.prof[(size_t)blockIdx.x * 8 + k] = pt[k];
 }
-
-// ek_stream.hip: k_stream<nvc (1..2), where> on `grid` workgroups of kSBlock threads with `lds` dynamic bytes
-void launch_stream_kernel(int nvc, bool where, int grid, size_t lds, hipStream_t s, DPlan* p, const DBatch& db,
-                          const StreamDesc& sd, const LdsLayout& lay, const DState& ds, const Results& rv, int32_t* perr);
 
 }  // namespace ek

@@ -56,6 +56,8 @@ def lib():
         L.ek_push_batch_global.restype = C.c_int
         L.ek_advance_watermark.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
         L.ek_advance_watermark.restype = C.c_int
+        L.ek_advance_time.argtypes = [C.c_void_p, C.c_int64]
+        L.ek_advance_time.restype = C.c_int
         L.ek_shard_triggers.argtypes = [C.c_void_p, C.POINTER(A.ek_batch), C.POINTER(A.ek_global_ctx), C.c_void_p,
                                         C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         L.ek_shard_triggers.restype = C.c_int
@@ -86,7 +88,7 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_release_results", "ek_reset", "ek_sync", "ek_set_stream", "ek_get_stats", "ek_last_error",
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
-                    "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers"]
+                    "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -191,6 +193,11 @@ class Engine:
 
     def advance_watermark(self, wm_ms: int, arrivals_end: int):
         self._check(lib().ek_advance_watermark(self.h, int(wm_ms), int(arrivals_end)))
+
+    def advance_time(self, now_ms: int):
+        """Processing-time windows: move the handle's clock to now_ms (the first call, before any row, is the rule's
+        start); every window the clock closes becomes pollable."""
+        self._check(lib().ek_advance_time(self.h, int(now_ms)))
 
     def shard_triggers(self, columns, ctx: A.ek_global_ctx, validity=None):
         """(global arrival, ts) of this handle's accepted trigger rows of the batch (ek_shard_triggers)."""

@@ -502,6 +502,11 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
         raise RuleError(f"unexpected token {p.peek()!r}")
     plan.window_type = wtype
     plan.key_column = key_col
+    if not is_event_time and timestamp and wtype in (A.EK_WINDOW_TUMBLING, A.EK_WINDOW_HOPPING, A.EK_WINDOW_SLIDING,
+                                                     A.EK_WINDOW_SESSION):
+        # processing-time time windows: the TIMESTAMP column carries each row's arrival time (the timestamp the
+        # reference stamps at ingest); the engine's clock reaches it before the row is delivered (ek_advance_time)
+        plan.ts_column = p.col(timestamp)
     if wtype == A.EK_WINDOW_NONE:
         # window-less rule: FilterOp + projection of every column (SELECT *, the C1 shape)
         if p.aggs or key_col >= 0 or having:

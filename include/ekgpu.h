@@ -320,6 +320,16 @@ typedef struct {
     int32_t pad2;
 } ek_global_ctx;
 
+/* ---------------------------------------------------------------- processing-time clock
+ * Processing-time TUMBLING / HOPPING / SLIDING (no delay) / SESSION windows (WindowOperator.execProcessingWindow,
+ * window_op.go:235-470) run under the caller's clock, the way the reference's tests drive them with its mock clock
+ * (pkg/timex/time.go:31-100): every row carries its arrival time in the plan's ts_column (non-decreasing); the clock
+ * reaches a row's timestamp before the row is delivered, so every ticker / timeout due at or before it fires first.
+ * ek_advance_time(h, now) moves the clock with no rows: the first call (before any row) is the rule's start, which
+ * aligns the tickers (getAlignedWindowEndTime(start, rawInterval)); without it the first row's time is the start.
+ * The clock never moves back (EK_ERR_INVALID). Windows the clock closes are polled like any other. */
+int ek_advance_time(void* h, int64_t now_ms);
+
 /* One micro-batch of a shard: the rows owned by this handle plus the global context above. */
 int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g);
 /* A WatermarkTuple with no new rows (event_window_trigger.go:126-146): the global watermark reached wm_ms after

@@ -1267,6 +1267,98 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     return 0;
 }
 
+/* ------------------------------------------------------------------ processing time (deterministic clock)
+ * WindowOperator.execProcessingWindow (window_op.go:235-470) for TUMBLING / HOPPING / SLIDING (no delay) / SESSION,
+ * driven by a clock the way the reference's own tests drive it (pkg/timex/time.go:31-100 mock clock;
+ * topotest/mock_topo.go:208-235,263-268): the rule opens at start_ms; before row i is delivered the clock is set to
+ * its timestamp ts_i (the row's arrival time) and every timer due at or before ts_i fires first, in due order (a
+ * ticker before a session timeout due at the same instant); after the last row the clock moves to end_ms.
+ *   tickers (getFirstTimer + setupTicker, window_op.go:228-233,250-260,471-481): the first tick at
+ *     getAlignedWindowEndTime(start_ms, rawInterval) (rawInterval = length for tumbling / session, interval for
+ *     hopping, planner.go:394-400), then every length (tumbling, session) or interval (hopping);
+ *   tick (window_op.go:483-499): scan(tick); a session window scans only when it has inputs and the first one is at
+ *     least `length` before the tick;
+ *   rows (window_op.go:343-419): appended to the inputs; SLIDING: a row matching OVER (WHEN) scans at its own
+ *     timestamp, any other row garbage-collects the inputs that expired (gcInputs, window_op.go:657-673: ts + length
+ *     <= t); SESSION: the timeout timer is (re)armed at ts + timeout, the first row of a session sets triggerTime;
+ *   session timeout (window_op.go:448-461): scan(now) over the whole inputs, then every input is dropped.
+ * WHERE: windowPlan.PushDownPredicate (windowPlan.go:82-99) moves it below a processing-time TUMBLING / HOPPING /
+ * SESSION window: a row whose WHERE is not true never reaches the window (an evaluation error drops the row; the
+ * reference forwards that error by itself, not as a window result). Rows must arrive with non-decreasing ts. */
+int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
+                 int64_t start_ms, int64_t end_ms, eko_output* out) {
+    memset(out, 0, sizeof *out);
+    if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
+    const int wt = p->window_type;
+    if (p->is_event_time || !(wt == EK_WINDOW_TUMBLING || wt == EK_WINDOW_HOPPING || wt == EK_WINDOW_SLIDING || wt == EK_WINDOW_SESSION)) {
+        set_status(out, EK_ERR_UNSUPPORTED, "processing-time clock runs are for TUMBLING / HOPPING / SLIDING / SESSION"); return out->status;
+    }
+    if (p->incremental || p->window_version == 2) { set_status(out, EK_ERR_UNSUPPORTED, "incremental / v2 windows are not restated in processing time"); return out->status; }
+    if (wt == EK_WINDOW_SLIDING && p->delay != 0) { set_status(out, EK_ERR_UNSUPPORTED, "delayed processing-time sliding windows are not restated"); return out->status; }
+    if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "processing-time rows need their arrival timestamp column"); return out->status; }
+    dataset d = { p, n, columns, validity, NULL };
+    outbuf ob; memset(&ob, 0, sizeof ob);
+    int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
+    for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
+    for (int64_t i = 0; i < n; ++i)
+        if ((i > 0 && ts[i] < ts[i - 1]) || ts[i] < start_ms) {
+            free(ts); set_status(out, EK_ERR_INVALID, "processing-time rows must arrive with non-decreasing timestamps after the start"); return out->status;
+        }
+    winop o; memset(&o, 0, sizeof o);
+    o.d = &d; o.ob = &ob; o.wtype = wt; o.ts = ts;
+    const int64_t u = unit_ms(p->time_unit);
+    o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = (int64_t)p->delay * u;
+    o.raw_interval = wt == EK_WINDOW_HOPPING ? p->interval : p->length;
+    o.unit = p->time_unit; o.tz = p->tz_offset_s;
+    const int pushdown = p->n_where > 0 && wt != EK_WINDOW_SLIDING;
+    const int has_tick = wt != EK_WINDOW_SLIDING;
+    int64_t tick = has_tick ? eko_aligned_window_end(start_ms, o.raw_interval, o.unit, o.tz) : MAXT_MS;
+    const int64_t period = wt == EK_WINDOW_HOPPING ? o.I : o.L;
+    int to_exists = 0, to_armed = 0;
+    int64_t to_due = 0;
+    /* every timer due at or before `now`, in due order (ticker first on a tie) */
+#define EKO_ADVANCE(now)                                                                                        \
+    for (;;) {                                                                                                  \
+        const int tk = has_tick && tick <= (now);                                                               \
+        const int tm = wt == EK_WINDOW_SESSION && to_armed && to_due <= (now) && (!tk || to_due < tick);        \
+        if (tm) {                                                                                               \
+            to_armed = 0;                                                                                       \
+            if (o.inputs.n > 0) { scan(&o, to_due, o.L + o.D, 1); o.inputs.n = 0; to_exists = 0; }              \
+        } else if (tk) {                                                                                        \
+            if (wt != EK_WINDOW_SESSION || (o.inputs.n > 0 && tick - ts[o.inputs.a[0]] >= o.L))                 \
+                scan(&o, tick, o.L + o.D, 1);                                                                   \
+            tick += period;                                                                                     \
+        } else break;                                                                                           \
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        EKO_ADVANCE(ts[i])
+        if (pushdown) {
+            val_t r = eval_prog(p->where_prog, p->n_where, &d, i, NULL);
+            if (!(r.tag == V_BOOL && r.i)) continue;
+        }
+        v_push(&o.inputs, i);
+        if (wt == EK_WINDOW_SESSION) {
+            if (!to_exists) { to_exists = 1; o.trigger_time = ts[i]; o.has_trigger = 1; }
+            to_armed = 1;
+            to_due = ts[i] + o.I;
+        } else if (wt == EK_WINDOW_SLIDING) {
+            if (match_trigger(&o, i)) {
+                scan(&o, ts[i], o.L + o.D, 1);
+            } else {
+                int64_t g = 0;   /* gcInputs(inputs, ts + 1ns): drop the prefix with ts_k + length <= ts */
+                while (g < o.inputs.n && ts[o.inputs.a[g]] + o.L <= ts[i]) g++;
+                v_erase_front(&o.inputs, g);
+            }
+        }
+    }
+    EKO_ADVANCE(end_ms)
+#undef EKO_ADVANCE
+    free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
+    free(ts);
+    finish_output(p, &ob, out);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ shard model (multi-GPU protocol)
  * One key-hash shard of a rule: the shard's own rows (global arrival indices g->row_arrival) plus the global
  * WatermarkTuples (wm list), the global window anchor (origin) and the global sliding triggers — exactly what

@@ -38,6 +38,12 @@ int eko_run(const ek_plan* plan, int64_t n_rows, const void* const* columns,
             const uint8_t* const* validity, eko_output* out);
 void eko_free(eko_output* out);
 
+/* Processing-time TUMBLING / HOPPING / SLIDING / SESSION under a deterministic clock (execProcessingWindow with the
+ * reference's mock clock): the rule opens at start_ms, each row is delivered when the clock reaches its timestamp
+ * (its arrival time), and the clock finally moves to end_ms. */
+int eko_run_proc(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,
+                 int64_t start_ms, int64_t end_ms, eko_output* out);
+
 /* Shard model of the multi-GPU protocol: one key-hash shard's rows (global arrivals g->row_arrival) with the
  * global WatermarkTuples / window anchor / sliding triggers of the whole stream (g: host memory). */
 int eko_run_shard(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,

@@ -57,6 +57,9 @@ def lib():
         _lib.eko_run_shard.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                        C.POINTER(A.ek_global_ctx), C.POINTER(eko_output)]
         _lib.eko_run_shard.restype = C.c_int
+        _lib.eko_run_proc.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                      C.c_int64, C.c_int64, C.POINTER(eko_output)]
+        _lib.eko_run_proc.restype = C.c_int
         _lib.eko_shard_triggers.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                             C.POINTER(A.ek_global_ctx), C.c_void_p, C.c_void_p]
         _lib.eko_shard_triggers.restype = C.c_int64
@@ -113,6 +116,20 @@ def run(plan: A.ek_plan, columns: List[np.ndarray], validity: Optional[List[Opti
     n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
     out = eko_output()
     rc = L.eko_run(C.byref(plan), n, cptr, vptr, C.byref(out))
+    if rc != 0:
+        msg = out.error.decode()
+        raise RuntimeError(f"oracle error {rc}: {msg}")
+    return _collect(L, out)
+
+
+def run_proc(plan: A.ek_plan, columns: List[np.ndarray], start_ms: int, end_ms: int,
+             validity: Optional[List[Optional[np.ndarray]]] = None) -> OracleRun:
+    """Processing-time windows under a deterministic clock (eko_run_proc): the rule opens at start_ms, every row is
+    delivered at its timestamp (arrival time), then the clock moves to end_ms."""
+    L = lib()
+    n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
+    out = eko_output()
+    rc = L.eko_run_proc(C.byref(plan), n, cptr, vptr, int(start_ms), int(end_ms), C.byref(out))
     if rc != 0:
         msg = out.error.decode()
         raise RuntimeError(f"oracle error {rc}: {msg}")

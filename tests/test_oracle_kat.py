@@ -108,6 +108,26 @@ def test_window_rule_kat(oracle, case):
             assert w.start == exp["window_start"] and w.end == exp["window_end"]
 
 
+# ------------------------------------------------------------------ processing time (mock clock)
+@pytest.mark.parametrize("case", _load("kat_window_proc.json")["tests"], ids=lambda c: c["name"])
+def test_processing_window_kat(oracle, case):
+    """window_rule_test.go TestWindow (processing time) under the reference's mock clock: the rule opens at the first
+    row's second, rows arrive at their timestamps, the run ends at the last row (eko_run_proc)."""
+    g = _load("kat_window_proc.json")
+    cols = _stream_cols(g["streams"][case["stream"]])
+    rule = compile_rule(case["sql"], SCHEMA, is_event_time=False, num_keys=4)
+    start = int(cols[0][0]) // 1000 * 1000
+    run = oracle.run_proc(rule.plan, cols, start, int(cols[0][-1]))
+    assert len(run.windows) == case["windows_out"]
+    for w, members, exp in zip(run.windows, run.members, case["windows"]):
+        assert sorted(int(m) for m in members) == exp["members"]
+        assert w.end == exp["window_end"]
+        if "window_start" in exp:
+            assert w.start == exp["window_start"]
+        if "count" in exp:
+            assert (w.value(0, 0) if len(w.keys) else None) == exp["count"]
+
+
 # ------------------------------------------------------------------ STATEWINDOW (WindowV2Operator)
 def test_state_window_kat(oracle):
     """window_v2_op_test.go:40-91 TestStateWindow: rows a = 1, 2, 6 under statewindow(a > 1, a > 5)."""
