@@ -165,38 +165,72 @@ def global_tuples(cfg, world, n_glob):
             "origin_known": True, "origin_ts": cfg["t0"], "origin_arrival": 0}
 
 
-def cpu_baseline(sample_events):
+CPU_SAMPLE = {"C2": 100_000_000, "C3": 15_000_000, "C4a": 1_000_000, "C4b": 50_000_000, "C5": 30_000_000}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(name, cfg, sample_events):
     """The CPU oracle (C restatement of the reference per-tuple path, oracle/ekoracle.c) on the first
-    `sample_events` events of the C2 stream: single thread (the reference runs a rule's window -> aggregate chain
-    in one goroutine, operations.go:63-74), and as P key-hash shards on P host threads (reference semantics on all
-    of this job's host cores)."""
+    `sample_events` events of the config's stream (the same synthetic generator, numpy side): single thread (the
+    reference runs a rule's window -> aggregate chain in one goroutine, operations.go:63-74), and for rules that
+    shard by key without changing their windows (tumbling / hopping GROUP BY key: C2, C3, C5) also as P key-hash
+    shards on P host threads (reference semantics on all of this job's host cores). COUNTWINDOW
+    blocks (C4b) and OVER (WHEN) triggers (C4a) are global over the stream, so those report one thread only."""
     import threading
     import numpy as np
     from oracle import ekoracle
     from ekgpu.rule import compile_rule
-    from ekgpu.synth import IOT_SCHEMA, iot_stream
+    from ekgpu.synth import iot_stream
     ekoracle.build()
-    rule = compile_rule(C2_SQL, IOT_SCHEMA, num_keys=N_KEYS)
-    key, ts, temp, hum = iot_stream(sample_events, N_KEYS, events_per_ms=EVENTS_PER_MS)
+    iet = not cfg.get("processing_time")
+    keys = cfg["keys"]
+    key, ts, temp, hum = iot_stream(sample_events, keys, seed=cfg["seed"], events_per_ms=cfg["epm"], t0=cfg["t0"])
+    cols = [key, ts, temp, hum]
+    if cfg.get("trig"):
+        i = np.arange(sample_events, dtype=np.int64)
+        cols.append(((((i * 0x9E3779B1) >> 7) % 10_000) == 0).astype(np.int64))
+    if cfg.get("sentinel"):   # C5: the event at the window end that closes the one window
+        end = cfg["t0"] + 60_000
+        cols = [np.append(cols[0], np.uint32(0)), np.append(cols[1], np.int64(end)), np.append(cols[2], 50.0),
+                np.append(cols[3], 50.0)]
+    rules = [compile_rule(cfg["sql"], schema_of(cfg), num_keys=keys, is_event_time=iet)]
+    if cfg.get("global_count"):
+        rules.append(compile_rule(cfg["global_count"], schema_of(cfg), num_keys=1, is_event_time=iet))
     t = time.perf_counter()
-    run = ekoracle.run(rule.plan, [key, ts, temp, hum])
+    nwin = 0
+    for r in rules:
+        nwin += len(ekoracle.run(r.plan, cols).windows)
     dt = time.perf_counter() - t
-    out = {"value": sample_events / dt, "unit": "events/s", "cores": 1, "kind": "port",
-           "sample": f"first {sample_events} events of the C2 stream ({len(run.windows)} windows closed), "
+    out = {"value": sample_events / dt, "unit": "events/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+           "sample": f"first {sample_events} events of the {name} stream ({nwin} windows closed), "
                      f"oracle/ekoracle.c single-threaded, {dt:.1f} s"}
+    if cfg.get("trig") or cfg.get("processing_time"):
+        return out
     P = max(1, int(os.environ.get("EKGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", "8"))))
-    shard = (key % P).astype(np.int64)
+    shard = (cols[0] % P).astype(np.int64)
     parts = []
     for r in range(P):
         m = shard == r
-        parts.append([(key[m] // P).astype(np.uint32), ts[m], temp[m], hum[m]])
+        parts.append([(cols[0][m] // P).astype(np.uint32)] + [c[m] for c in cols[1:]])
     del shard
-    prule = compile_rule(C2_SQL, IOT_SCHEMA, num_keys=(N_KEYS + P - 1) // P)
+    prules = [compile_rule(cfg["sql"], schema_of(cfg), num_keys=(keys + P - 1) // P, is_event_time=iet)]
     errs = []
 
     def work(c):
         try:
-            ekoracle.run(prule.plan, c)
+            for r in prules:
+                ekoracle.run(r.plan, c)
+            if cfg.get("global_count"):   # the shard's partial count(*); the P partials add up on the host
+                ekoracle.run(rules[1].plan, c)
         except Exception as e:   # noqa: BLE001  (reported, not swallowed)
             errs.append(e)
     th = [threading.Thread(target=work, args=(c,)) for c in parts]
@@ -371,7 +405,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS) + ["C1"])
     ap.add_argument("--events", type=int, default=0, help="override the per-GPU event count")
-    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", N_EVENTS)))
+    ap.add_argument("--cpu-sample", type=int, default=int(os.environ.get("EKGPU_CPU_SAMPLE", "0")),
+                    help="events of the CPU baseline sample (default: CPU_SAMPLE of the config, ~10 s single-threaded)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -588,8 +623,8 @@ def main():
         out["config"]["late_tolerance_ms"] = args.disorder
     if rank == 0 and world == 1 and args.config == "C2" and not args.no_ingest and not args.disorder:
         out["ingest_inclusive"] = ingest_inclusive(eng, cols, n)
-    if rank == 0 and world == 1 and not args.no_cpu and args.config == "C2" and not args.disorder:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+    if rank == 0 and world == 1 and not args.no_cpu and not args.disorder:
+        out["cpu_baseline"] = cpu_baseline(args.config, cfg, min(cfg["n"], args.cpu_sample or CPU_SAMPLE[args.config]))
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -29,7 +29,6 @@
 #include "ek_lib.h"
 #include "ek_range.h"
 #include "ek_global.h"
-#include "ek_stream_desc.h"
 #include "ek_keymajor.h"
 
 using namespace ek;
@@ -1085,23 +1084,6 @@ struct Engine {
         }
 
         const int64_t* bidx = sorted ? h_small + (q_hi - q_lo + 2) : nullptr;
-        if (sorted && stream_usable(db, d_acc)) {
-            // every pane of the batch in one XCD-resident streaming launch (pane bounds: bidx[0..nq], start..n)
-            const int64_t nq = q_hi - q_lo + 1;
-            std::vector<int64_t> pb(nq + 1);
-            for (int64_t k = 0; k <= nq; ++k) pb[k] = bidx[k];
-            pb[0] = start;
-            pb[nq] = n;
-            const int rc = run_stream(db, pb.data(), q_lo, q_hi);
-            if (rc < 0) return rc;
-            if (rc == 0) {
-                if (plan.debug_membership)
-                    hipLaunchKernelGGL(k_members, dim3(256), dim3(kBlock), 0, stream, d_plan, db, grid, d_acc, (int)(d_acc != nullptr),
-                                       start, n, arrivals, d_arrival, q_lo, q_hi, ring, (int64_t*)pane_mcnt.p,
-                                       (unsigned long long*)pane_mhash.p);
-                return finalize_ready(q_hi);
-            }
-        }
         for (const Grp& g : groups) {
             if (g.hi > g.lo) {
                 // pane boundaries of the group (sorted batches): pbnd[k] = first event of pane qa + k
@@ -3391,10 +3373,6 @@ struct Engine {
 
     int record_time() {
         hipEventRecord(ev1, stream);
-        if (stream_launched) {
-            hipEventSynchronize(ev1);
-            if (int rc = stream_check()) return rc;
-        }
         if (hipEventSynchronize(ev1) == hipSuccess) {
             float ms = 0;
             hipEventElapsedTime(&ms, ev0, ev1);
@@ -3413,237 +3391,6 @@ struct Engine {
     }
 
 
-
-    // ================================================================== XCD-resident streaming path (ek_stream.h)
-    // One persistent launch partitions and aggregates a ts-sorted batch with the staging kept in each XCD's L2 /
-    // the Infinity Cache (no HBM round trip), for pane-mode plans whose aggregates need only count / sum / min /
-    // max of non-nullable columns (every C2 / C3 shape). OFF by default (EKGPU_STREAM=1 enables it): measured on
-    // C2 it takes 1.84 ms against 1.20 ms for k_part + k_agg, because every workgroup folds in every chunk of its
-    // XCD serially with its own production (tuning log); parity-tested in tests/test_stream_gpu.py.
-    int stream_state = 0;               // 0 not probed, 1 usable, -1 disabled for this handle
-    int stream_owners = 0, stream_grid = 0, stream_obits = 0, stream_lds = 0;
-    LdsLayout slay{};
-    DevBuf s_sync, s_klo, s_val[kMaxVC], s_ctab, s_tab, s_prof;
-    int64_t s_max_chunks = 0;
-
-    void launch_stream(const DBatch& db, const StreamDesc& sd) {
-        launch_stream_kernel(dp.n_vc, dp.n_where > 0, stream_grid, (size_t)stream_lds, stream, d_plan, db, sd, slay, dstate,
-                             results_view(), (int32_t*)pane_err.p);
-    }
-
-    StreamDesc stream_desc_base() {
-        StreamDesc sd{};
-        sd.key_col = dp.key_col;
-        sd.n_where = dp.n_where;
-        sd.num_keys = dp.num_keys;
-        sd.owners = stream_owners;
-        sd.obits = stream_obits;
-        sd.max_chunks = (int32_t)s_max_chunks;
-        sd.nvc = dp.n_vc;
-        sd.ring = ring;
-        sd.timeout = (int64_t)env_int("EKGPU_STREAM_TIMEOUT_MS", 1000) * 100000;   // s_memrealtime: 100 MHz
-        sd.sync = (uint32_t*)s_sync.p;
-        sd.klo = (uint16_t*)s_klo.p;
-        for (int v = 0; v < dp.n_vc; ++v) sd.val[v] = (int64_t*)s_val[v].p;
-        sd.ctab = (unsigned long long*)s_ctab.p;
-        sd.prof = nullptr;
-        if (env_int("EKGPU_STREAM_PROF", 0) && ensure(s_prof, (size_t)stream_grid * 64) == 0) sd.prof = (unsigned long long*)s_prof.p;
-        return sd;
-    }
-    size_t stream_sync_bytes() const { return ((size_t)(10 + kSXcd * kSRing) * 4 + 15) & ~(size_t)15; }
-    size_t stream_ctab_bytes() const { return (size_t)kSXcd * kSRing * stream_owners * 8; }
-
-    // Decide once per handle: plan shape, LDS budget, and a probe launch proving the grid is co-resident with
-    // `owners` workgroups on each of the 8 XCDs (the kernel checks it before any side effect).
-    int stream_setup() {
-        stream_state = -1;
-        if (env_int("EKGPU_STREAM", 0) == 0 || range_mode || dp.pseudo_keys || dp.n_sagg > 0 || dp.n_vc < 1 || dp.n_vc > 2) return 0;
-        for (int v = 0; v < dp.n_vc; ++v)
-            if (dp.vc_flags[v] & (NEED_CNT | NEED_M2 | NEED_FSUM | NEED_SORT)) return 0;
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0 || cus % kSXcd) return 0;
-        stream_grid = 2 * cus;                     // one producer + one consumer workgroup per CU
-        stream_owners = stream_grid / kSXcd / 2;   // consumers (= producers) per XCD
-        if (stream_owners > kSMaxOwners || stream_owners < 1) return 0;
-        int64_t kpo = 1;
-        const int64_t need = ((int64_t)K + stream_owners - 1) / stream_owners;
-        stream_obits = 0;
-        while (kpo < need) { kpo <<= 1; stream_obits++; }
-        if (kpo > 65536) return 0;
-        // LDS table for kpo keys (8-byte fields first, then the u32 counts)
-        slay = LdsLayout{};
-        {
-            int o = 0;
-            for (int v = 0; v < dp.n_vc; ++v) {
-                const int f = dp.vc_flags[v];
-                if (f & NEED_SUM) { slay.off_sum[v] = o; o += 8 * (int)kpo; }
-                if (f & NEED_MIN) { slay.off_min[v] = o; o += 8 * (int)kpo; }
-                if (f & NEED_MAX) { slay.off_max[v] = o; o += 8 * (int)kpo; }
-            }
-            slay.off_cnt = o;
-            o += 4 * (int)kpo;
-            slay.bytes = (o + 15) & ~15;
-        }
-        // producer: the owner-sorted chunk (values + key-lows); consumer: the owner table; two workgroups per CU
-        stream_lds = std::max<int>(slay.bytes, kSTile * (8 * dp.n_vc + 2));
-        if (stream_lds > 78 * 1024) return 0;
-        s_max_chunks = env_int("EKGPU_STREAM_MAX_CHUNKS", 1 << 16);
-        if (int rc = ensure(s_sync, stream_sync_bytes())) return rc;
-        if (int rc = ensure(s_klo, (size_t)kSXcd * kSRing * kSTile * 2)) return rc;
-        for (int v = 0; v < dp.n_vc; ++v)
-            if (int rc = ensure(s_val[v], (size_t)kSXcd * kSRing * kSTile * 8)) return rc;
-        if (int rc = ensure(s_ctab, stream_ctab_bytes())) return rc;
-        // probe: an empty work list (every XCD has no pane)
-        if (int rc = ensure(s_tab, 4096)) return rc;
-        hipMemsetAsync(s_tab.p, 0, 4096, stream);
-        StreamDesc sd = stream_desc_base();
-        sd.xoff = (const int32_t*)s_tab.p;
-        sd.xcpre = (const int32_t*)s_tab.p;
-        sd.xpane = (const int32_t*)s_tab.p;
-        hipMemsetAsync(s_sync.p, 0, stream_sync_bytes(), stream);
-        hipMemsetAsync(s_ctab.p, 0, stream_ctab_bytes(), stream);
-        DBatch empty{};
-        launch_stream(empty, sd);
-        uint32_t err = 0;
-        hipMemcpyAsync(&err, (uint32_t*)s_sync.p + 1, 4, hipMemcpyDeviceToHost, stream);
-        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream probe failed");
-        if (err == 0) stream_state = 1;
-        return 0;
-    }
-
-    bool stream_usable(const DBatch& db, const uint8_t* d_acc) {
-        if (d_acc) return false;
-        if (stream_state == 0 && stream_setup() != 0) return false;
-        if (stream_state <= 0) return false;
-        for (int v = 0; v < dp.n_vc; ++v)
-            if (db.valid[dp.vc_col[v]]) return false;
-        return true;
-    }
-
-    // Every pane [qa, qb] of a sorted batch (pane r = rows [b[r], b[r+1])) in one k_stream launch.
-    // Returns 1 (nothing launched) when the batch does not fit the launch's tables.
-    int run_stream(const DBatch& db, const int64_t* b, int64_t qa, int64_t qb) {
-        const int npn = (int)(qb - qa + 1);
-        // per-XCD pane lists: contiguous pane ranges balanced by events (XCD x takes the panes whose first event
-        // falls in its eighth of the batch), and chunk prefixes on the kSTile-aligned per-pane grid
-        std::vector<int32_t> xoff(kSXcd + 1, 0), xpane, xcpre;
-        std::vector<int32_t> cnt_per(kSXcd, 0), xof(npn);
-        {
-            const int64_t lo = b[0], span = std::max<int64_t>(1, b[npn] - b[0]);
-            for (int r = 0; r < npn; ++r) {
-                const int64_t mid = (b[r] + b[r + 1]) / 2 - lo;
-                xof[r] = (int)std::min<int64_t>(kSXcd - 1, mid * kSXcd / span);
-                cnt_per[xof[r]]++;
-            }
-        }
-        for (int x = 0; x < kSXcd; ++x) xoff[x + 1] = xoff[x] + cnt_per[x];
-        if (*std::max_element(cnt_per.begin(), cnt_per.end()) > kSMaxXPanes) return 1;
-        xpane.resize(npn);
-        xcpre.resize(npn + kSXcd);
-        {
-            std::vector<int32_t> fill(kSXcd, 0);
-            for (int r = 0; r < npn; ++r) { const int x = xof[r]; xpane[xoff[x] + fill[x]++] = r; }
-            for (int x = 0; x < kSXcd; ++x) {
-                int64_t c = 0;
-                int32_t* pre = xcpre.data() + xoff[x] + x;
-                for (int k = 0; k < cnt_per[x]; ++k) {
-                    pre[k] = (int32_t)c;
-                    const int r = xpane[xoff[x] + k];
-                    const int64_t A = b[r] & ~(int64_t)(kSTile - 1);
-                    c += b[r + 1] > b[r] ? (b[r + 1] - 1 - A) / kSTile + 1 : 1;
-                }
-                pre[cnt_per[x]] = (int32_t)c;
-                if (c > s_max_chunks) return 1;
-            }
-        }
-        // pane descriptors: the group layout of run_group ([pbnd n+1][dbase n][didx n][fresh n])
-        const size_t aux_words = aux_layout_words(npn);
-        int64_t* aux = desc_alloc(aux_words);
-        if (!aux) return fail(EK_ERR_NOMEM, "pinned");
-        int64_t* h_pbnd = aux;
-        int64_t* h_dbase = h_pbnd + npn + 1;
-        int32_t* h_didx = (int32_t*)(h_dbase + npn);
-        uint8_t* h_fresh = (uint8_t*)(h_didx + 2 * ((npn + 1) / 2));
-        if (int rc = claim_slots(qa, qb, h_fresh, false)) return rc;
-        for (int k = 0; k <= npn; ++k) h_pbnd[k] = b[k];
-        for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
-        if (wtype == EK_WINDOW_TUMBLING && has_W) {
-            for (int r = 0; r < npn; ++r) {
-                const int64_t q = qa + r;
-                if (!h_fresh[r] || win_end(q) > W || q < next_win) continue;
-                if (int rc = register_until(q)) return rc;
-                WinInfo& wi = win_info(q);
-                wi.direct = true;
-                h_dbase[r] = wi.out_base;
-                h_didx[r] = wi.slot;
-            }
-        }
-        GroupDesc gd{};
-        gd.q_lo = qa;
-        gd.n_panes = npn;
-        gd.ring = ring;
-        if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
-        // the XCD lists: one more pinned block
-        const size_t lw = (size_t)(xoff.size() + xpane.size() + xcpre.size() + 1) / 2 + 2;
-        int64_t* hl = desc_alloc(lw);
-        if (!hl) return fail(EK_ERR_NOMEM, "pinned");
-        int32_t* h32 = (int32_t*)hl;
-        memcpy(h32, xoff.data(), xoff.size() * 4);
-        memcpy(h32 + xoff.size(), xpane.data(), xpane.size() * 4);
-        memcpy(h32 + xoff.size() + xpane.size(), xcpre.data(), xcpre.size() * 4);
-        if (int rc = ensure(s_tab, lw * 8)) return rc;
-        hipMemcpyAsync(s_tab.p, hl, lw * 8, hipMemcpyHostToDevice, stream);
-        StreamDesc sd = stream_desc_base();
-        int64_t cmax = 1;
-        for (int x = 0; x < kSXcd; ++x) cmax = std::max<int64_t>(cmax, xcpre[xoff[x] + x + cnt_per[x]]);
-        sd.max_chunks = (int32_t)((cmax + 3) & ~3);   // the flag block of this launch (zeroed below)
-        sd.nbatch = db.n;
-        sd.q_lo = qa;
-        sd.n_panes = npn;
-        sd.pbnd = gd.pbnd;
-        sd.dbase = gd.dbase;
-        sd.didx = gd.didx;
-        sd.fresh = gd.fresh;
-        sd.xoff = (const int32_t*)s_tab.p;
-        sd.xpane = sd.xoff + xoff.size();
-        sd.xcpre = sd.xpane + xpane.size();
-        // every launch starts from untagged run descriptors (a tag is a chunk index of this launch)
-        hipMemsetAsync(s_sync.p, 0, stream_sync_bytes(), stream);
-        hipMemsetAsync(s_ctab.p, 0, stream_ctab_bytes(), stream);
-        // fresh panes: zero their WHERE error flag and membership fingerprint (k_group_prep)
-        hipLaunchKernelGGL(k_group_prep, dim3((npn + 255) / 256), dim3(256), 0, stream, gd, (int32_t*)pane_err.p,
-                           (int64_t*)pane_mcnt.p, (unsigned long long*)pane_mhash.p);
-        const int ph = phase_begin(EK_PHASE_PARTITION);
-        launch_stream(db, sd);
-        phase_end(ph);
-        if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "stream kernel launch failed");
-        stream_launched = true;
-        return 0;
-    }
-    bool stream_launched = false;
-    // after the push's final sync: a stream launch that found the grid not co-resident or timed out
-    int stream_check() {
-        if (!stream_launched) return 0;
-        stream_launched = false;
-        uint32_t err = 0;
-        hipMemcpy(&err, (uint32_t*)s_sync.p + 1, 4, hipMemcpyDeviceToHost);
-        if (s_prof.p && env_int("EKGPU_STREAM_PROF", 0)) {
-            std::vector<unsigned long long> pr((size_t)stream_grid * 8);
-            hipMemcpy(pr.data(), s_prof.p, pr.size() * 8, hipMemcpyDeviceToHost);
-            double a[8] = {0};
-            for (int g = 0; g < stream_grid; ++g) for (int k = 0; k < 8; ++k) a[k] += (double)pr[(size_t)g * 8 + k];
-            const double h = stream_grid / 2.0 * 100.0;   // per producer / per consumer, us
-            fprintf(stderr, "[k_stream avg] producer: slot-wait %.1f us, sort+store %.1f us, chunks %.1f | consumer: idle-poll %.1f us, "
-                            "fold %.1f us, finish %.1f us, batches %.1f\n", a[1] / h, a[2] / h, a[5] / (h / 100), a[3] / h, a[4] / h,
-                    a[7] / h, a[6] / (h / 100));
-        }
-        if (err) {
-            stream_state = -1;
-            return fail(EK_ERR_DEVICE, "streaming aggregation kernel %s (code %u); the handle falls back to the two-kernel path, "
-                                       "re-run the stream", err == 1 ? "was not co-resident" : "timed out", err);
-        }
-        return 0;
-    }
 
     // ================================================================== SHARD mode (global watermark)
     // One key-hash shard of a rule (include/ekgpu.h, ek_push_batch_global): the rows of this handle carry their

@@ -17,7 +17,7 @@
 #include "ek_device.h"
 
 // linkage of the non-template kernels defined in this header: a translation unit that includes it only for the
-// device helpers (ek_stream.hip) defines EK_NT_KERNEL as static, so only the engine's unit exports them
+// device helpers defines EK_NT_KERNEL as static, so only the engine's unit exports them
 #ifndef EK_NT_KERNEL
 #define EK_NT_KERNEL
 #endif
