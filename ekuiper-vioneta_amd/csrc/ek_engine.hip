@@ -644,10 +644,12 @@ struct Engine {
             lay.bytes = (int32_t)std::max<size_t>((size_t)((o + 15) & ~15), (sparse_lds_bytes(dp.n_vc) + 15) & ~(size_t)15);
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
+        sorted_chunk = env_int("EKGPU_SORTED_CHUNK", kTile);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
+        km_packed = env_int("EKGPU_KM_PACKED", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
@@ -1137,7 +1139,7 @@ struct Engine {
         // chunk size of this group: halve while a chunk would span more panes than k_part sorts in LDS
         // sorted groups start from single-tile chunks (keys read once, k_part's count pass skipped) and
         // grow the chunk only while a pane would span more chunk runs than k_agg walks
-        int64_t csz = pbnd_host ? std::min<int64_t>(kTile, chunk) : chunk;
+        int64_t csz = pbnd_host ? std::min<int64_t>(sorted_chunk, chunk) : chunk;
         int mp = max_panes_in_chunk(pbnd_host, gd, csz);
         while (pbnd_host && csz < chunk && max_chunks_in_pane(pbnd_host, gd, csz) > kMaxRuns) {
             csz <<= 1;
@@ -1290,6 +1292,7 @@ struct Engine {
     // Un-grouped rule over a ts-sorted group (k_ung_tile): one pass over the referenced columns, a partial per
     // (tile, pane segment) merged into pseudo-key slot tile mod kPseudoKeys (EKGPU_UNG=0: the k_part + k_agg path).
     int ung_mode = 1;
+    int64_t sorted_chunk = kTile;   // first chunk size tried for a sorted group (single-tile chunks: no count pass)
     int rowpos_col = -1;      // hidden position column of first-row fields (buffer_view: event-buffer index)
     DevBuf rowpos;            // its values 0, 1, 2, ... (grown with the buffer)
     int64_t rowpos_n = 0;
@@ -1891,6 +1894,8 @@ struct Engine {
     }
 
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
+    int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
+    DevBuf km_rbase, km_rec;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
     std::vector<unsigned int> grp_h;
@@ -2158,7 +2163,23 @@ struct Engine {
             if (h_kmf[2]) { phase_end(ph2); return 0; }   // a (key, window) run too long for one thread: window-major path
         }
         hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);
+        // packed emission: the windows' kept totals -> record offsets (one sync to size the record buffer)
+        const bool packed = km_packed && dp.n_aggs <= kKmRecAggs;
+        int64_t nrec = 0;
+        if (packed) {
+            if (int rc = ensure(km_rbase, (size_t)(nw + 1) * 8)) return rc;
+            hipLaunchKernelGGL(k_km_rbase, dim3(1), dim3(1024), 0, stream, d, (int64_t*)km_rbase.p);
+            nrec = fetch_i64((int64_t*)km_rbase.p + nw);
+            if (int rc = ensure(km_rec, (size_t)std::max<int64_t>(nrec, 1) * 32)) return rc;
+            d.rbase = (const int64_t*)km_rbase.p;
+            d.rec = (uint4*)km_rec.p;
+        }
         walk(true);
+        if (packed && nrec > 0) {
+            const int64_t per = (nrec + nw - 1) / nw;
+            const dim3 gu((unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (per + kBlock - 1) / kBlock)), (unsigned)nw);
+            hipLaunchKernelGGL(k_km_unpack, gu, dim3(kBlock), 0, stream, d, dp.n_aggs, rv);
+        }
         phase_end(ph2);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major aggregation failed");
         stats.windows_keymajor += nw;

@@ -58,6 +58,22 @@ __device__ __forceinline__ int64_t ub_i64(const int64_t* a, int64_t lo, int64_t 
     return lo;
 }
 
+// Galloping searches from lo (the answer is usually a few rows away: a ts-sorted batch releases an event at its own
+// arrival or at the end of its equal-ts run): O(log distance) probes near lo instead of a binary search over the
+// whole remaining batch (whose first probes miss every cache). Same results as lb_i64 / ub_i64.
+__device__ __forceinline__ int64_t gallop_lb(const int64_t* a, int64_t lo, int64_t hi, int64_t x) {
+    if (lo >= hi || a[lo] >= x) return lo;
+    int64_t prev = lo, step = 1;
+    while (lo + step < hi && a[lo + step] < x) { prev = lo + step; step <<= 1; }
+    return lb_i64(a, prev + 1, min(hi, lo + step), x);
+}
+__device__ __forceinline__ int64_t gallop_ub(const int64_t* a, int64_t lo, int64_t hi, int64_t x) {
+    if (lo >= hi || a[lo] > x) return lo;
+    int64_t prev = lo, step = 1;
+    while (lo + step < hi && a[lo + step] <= x) { prev = lo + step; step <<= 1; }
+    return ub_i64(a, prev + 1, min(hi, lo + step), x);
+}
+
 // Release step of buffered events [i0, i1): the arrival index of the watermark advance that released the
 // event (watermark_op.go:157-214: released at the first advance W_j > W_{j-1} at or after its arrival with
 // W_j >= ts). runmax[0..nb) = batch running max (arrival arr_base + j), prevmax = stream max before the
@@ -70,12 +86,12 @@ __global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* _
         const int64_t ls = max((int64_t)0, barr[i] - arr_base);
         int64_t r = INT64_MAX;
         if (ls < nb) {
-            const int64_t j0 = lb_i64(runmax, ls, nb, x);
+            const int64_t j0 = gallop_lb(runmax, ls, nb, x);
             if (j0 < nb) {
                 const int64_t prev = j0 > 0 ? runmax[j0 - 1] : prevmax;
                 if (runmax[j0] > prev) r = arr_base + j0;
                 else {
-                    const int64_t j1 = ub_i64(runmax, j0 + 1, nb, runmax[j0]);
+                    const int64_t j1 = gallop_ub(runmax, j0 + 1, nb, runmax[j0]);
                     if (j1 < nb) r = arr_base + j1;
                 }
             }
