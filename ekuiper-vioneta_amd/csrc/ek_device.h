@@ -56,6 +56,7 @@ struct DPlan {
                                   // (merged per window by k_finalize_merge) instead of one partition
     ek_instr begin_prog[EK_MAX_PROG];
     ek_instr emit_prog[EK_MAX_PROG];
+    int32_t having_star;          // HAVING reads no aggregate but count(*): decidable from a group's row count alone
 };
 
 // Columns of one micro-batch (device pointers).

@@ -522,6 +522,12 @@ struct Engine {
         }
         dp.n_aggs = plan.n_aggs;
         dp.inc = inc ? 1 : 0;
+        dp.having_star = plan.n_having > 0 ? 1 : 0;
+        for (int i = 0; i < plan.n_having; ++i)
+            if (plan.having_prog[i].op == EK_OP_AGG &&
+                (plan.having_prog[i].arg < 0 || plan.having_prog[i].arg >= plan.n_aggs ||
+                 plan.aggs[plan.having_prog[i].arg].fn != EK_AGG_COUNT_STAR))
+                dp.having_star = 0;
         for (int k = 0; k < plan.n_aggs; ++k) {
             const ek_agg_spec& a = plan.aggs[k];
             dp.agg_fn[k] = a.fn;
@@ -2075,7 +2081,7 @@ struct Engine {
         uint32_t* kstart = (uint32_t*)km_start.p;
         hipLaunchKernelGGL(k_km_starts, dim3((unsigned)std::min<int64_t>(8192, (n + 1 + 255) / 256)), dim3(256), 0, stream, sk, n,
                            K, kstart);
-        hipLaunchKernelGGL(k_km_maxrun, dim3((unsigned)std::min<int64_t>(4096, ((int64_t)K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_km_maxrun, dim3((unsigned)std::min<int64_t>(256, ((int64_t)K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            stream, (const uint32_t*)kstart, K, d_flag + 1);
         phase_end(ph);
         hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);

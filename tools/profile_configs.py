@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Per-config rocprofv3 summaries -> profiles/r02_*:
-  r02_kernels_<cfg>.csv  rocprofv3 --kernel-trace --stats of `bench.py --config <cfg> --steps S --warmup W`
-  r02_pmc_<cfg>.json     FETCH_SIZE / WRITE_SIZE passes (each its own run, --steps 1 --warmup 1): HBM bytes of the
+"""Per-config rocprofv3 summaries -> profiles/<round>_* (round = $EKGPU_ROUND, default r03):
+  <round>_kernels_<cfg>.csv  rocprofv3 --kernel-trace --stats of `bench.py --config <cfg> --steps S --warmup W`
+  <round>_pmc_<cfg>.json     FETCH_SIZE / WRITE_SIZE passes (each its own run, --steps 1 --warmup 1): HBM bytes of the
                          engine's kernels (ek::*) per step; FETCH_SIZE doubled (gfx950: it reports half the bytes of
                          wide coalesced reads, MI355X_MICROARCH.md "HBM"), sizes KiB -> bytes.
 usage: profile_configs.py <cfg> <events_per_gpu> <steps_in_pmc_runs> <trace_dir> <pmc_fetch_dir> <pmc_write_dir>
@@ -15,6 +15,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROUND = os.environ.get("EKGPU_ROUND", "r03")
 
 
 def counters(d):
@@ -35,7 +36,7 @@ def main():
     cfg, events, steps, tdir, fdir, wdir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5], sys.argv[6]
     stats = glob.glob(os.path.join(tdir, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
-        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"r02_kernels_{cfg}.csv"))
+        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{ROUND}_kernels_{cfg}.csv"))
     f, fn = counters(fdir)
     w, wn = counters(wdir)
     kern = {}
@@ -51,7 +52,7 @@ def main():
            "note": "PMC passes over `steps_profiled` pushes (warmup + timed); FETCH_SIZE doubled (gfx950), KiB -> bytes",
            "hbm_read_bytes_per_step": tot_r / steps, "hbm_write_bytes_per_step": tot_w / steps,
            "hbm_bytes_per_step": (tot_r + tot_w) / steps, "kernels": kern}
-    json.dump(out, open(os.path.join(ROOT, "profiles", f"r02_pmc_{cfg}.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"{ROUND}_pmc_{cfg}.json"), "w"), indent=1)
     print(cfg, f"{out['hbm_bytes_per_step'] / 1e9:.3f} GB/step", {k: round((v['read_bytes_per_step'] + v['write_bytes_per_step']) / 1e9, 3) for k, v in kern.items()})
 
 
