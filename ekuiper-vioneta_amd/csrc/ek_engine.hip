@@ -656,6 +656,7 @@ struct Engine {
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
         km_packed = env_int("EKGPU_KM_PACKED", 1);
+        count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
@@ -1767,7 +1768,7 @@ struct Engine {
             hipMemcpyAsync(slot_d.p, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
             hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)eb.arr.p,
                                (const int64_t*)ab_d.p, (const int32_t*)slot_d.p, (int64_t*)r_wmc.p,
-                               (unsigned long long*)r_wmh.p);
+                               (unsigned long long*)r_wmh.p, (int64_t)0);
             hipStreamSynchronize(stream);   // slots/ab host vectors are reused
         }
         // small windows: one workgroup each (k_small_win); no order statistics on that path
@@ -1794,10 +1795,10 @@ struct Engine {
                 Results rv = results_view();
                 const int ph = phase_begin(EK_PHASE_AGGREGATE);
                 switch (std::max(1, dp.n_vc)) {
-                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
-                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
-                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
-                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n); break;
+                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
                 }
                 phase_end(ph);
                 // the host vectors above are reused by the next fire: keep them alive until the copies ran
@@ -1901,6 +1902,7 @@ struct Engine {
 
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
     int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
+    int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
     DevBuf km_rbase, km_rec;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
@@ -3163,7 +3165,142 @@ struct Engine {
 
     // COUNTWINDOW(n[, m]) in processing time (window_op.go:390-418, TupleList 502-551): every m-th arrival
     // emits the last n arrivals when at least n are buffered; arrival order, no watermark.
+    // Small windows read straight from `src` (a batch in arrival order): hab = each window's row range in src, in
+    // trigger order. Registers the windows like fire_windows and aggregates them with k_small_win.
+    int fire_direct_small(const DBatch& src, const std::vector<int64_t>& hab, int64_t arr_base) {
+        const int nq = (int)(hab.size() / 2);
+        if (nq == 0) return 0;
+        // consecutive equal-size windows (COUNTWINDOW blocks) and no membership fingerprint: arithmetic layout
+        bool arith = !plan.debug_membership;
+        for (int w = 1; w < nq && arith; ++w)
+            arith = hab[2 * w] == hab[2 * w - 1] && hab[2 * w + 1] - hab[2 * w] == hab[1] - hab[0];
+        if (arith) {
+            const int64_t len = hab[1] - hab[0], rowcap = std::min<int64_t>(K, len);
+            if (int rc = ensure_results(rowcap * nq, nq)) return rc;
+            SwArith ar{};
+            ar.a0 = hab[0];
+            ar.len = (int32_t)len;
+            ar.rowcap = rowcap;
+            ar.ob0 = r_rows_used;
+            ar.slot0 = (int32_t)wins.size();
+            for (int w = 0; w < nq; ++w) {
+                WinInfo wi{};
+                wi.j = range_wins++;
+                wi.out_base = r_rows_used;
+                wi.slot = (int32_t)wins.size();
+                wi.direct = true;
+                r_rows_used += rowcap;
+                wins.push_back(wi);
+            }
+            stats.windows_out += nq;
+            const size_t swl = sw_lds_bytes((int)len);
+            Results rv = results_view();
+            const int ph = phase_begin(EK_PHASE_AGGREGATE);
+            switch (std::max(1, dp.n_vc)) {
+            case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
+            case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
+            case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
+            default: hipLaunchKernelGGL(k_small_win<4>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
+            }
+            phase_end(ph);
+            if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");
+            return 0;
+        }
+        if (int rc = ensure(ab_d, (size_t)nq * 16)) return rc;
+        hipMemcpyAsync(ab_d.p, hab.data(), (size_t)nq * 16, hipMemcpyHostToDevice, stream);
+        int64_t rows = 0;
+        int max_n = 1;
+        for (int w = 0; w < nq; ++w) {
+            rows += std::min<int64_t>(K, hab[2 * w + 1] - hab[2 * w]);
+            max_n = std::max<int>(max_n, (int)(hab[2 * w + 1] - hab[2 * w]));
+        }
+        if (int rc = ensure_results(rows, nq)) return rc;
+        std::vector<int32_t> slots(nq), wl(nq);
+        std::vector<int64_t> obase(nq);
+        for (int w = 0; w < nq; ++w) {
+            WinInfo wi{};
+            wi.j = range_wins++;
+            wi.out_base = r_rows_used;
+            wi.slot = (int32_t)wins.size();
+            wi.direct = true;
+            r_rows_used += std::min<int64_t>(K, hab[2 * w + 1] - hab[2 * w]);
+            wins.push_back(wi);
+            slots[w] = wi.slot;
+            obase[w] = wi.out_base;
+            wl[w] = w;
+        }
+        stats.windows_out += nq;
+        if (int rc = ensure(sw_d, (size_t)nq * 4 + (size_t)nq * 12 + 16)) return rc;
+        int32_t* d_wl = (int32_t*)sw_d.p;
+        int32_t* d_slot = d_wl + nq;
+        int64_t* d_ob = (int64_t*)(((uintptr_t)(d_slot + nq) + 7) & ~(uintptr_t)7);
+        hipMemcpyAsync(d_wl, wl.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(d_slot, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(d_ob, obase.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
+        if (plan.debug_membership)
+            hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)nullptr, (const int64_t*)ab_d.p,
+                               (const int32_t*)d_slot, (int64_t*)r_wmc.p, (unsigned long long*)r_wmh.p, arr_base);
+        const size_t swl = sw_lds_bytes(max_n);
+        Results rv = results_view();
+        const int ph = phase_begin(EK_PHASE_AGGREGATE);
+        switch (std::max(1, dp.n_vc)) {
+        case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+        case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+        case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+        default: hipLaunchKernelGGL(k_small_win<4>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
+        }
+        phase_end(ph);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");   // host lists reused
+        return 0;
+    }
+
+    // COUNTWINDOW(n) (tumbling, processing time) over a batch holding whole windows (window_op.go:390-418): the window
+    // that spans the carried rows and the batch head goes through the event buffer; every window wholly inside the
+    // batch is aggregated straight from the batch's columns (no copy into the buffer); only the rows of the next,
+    // unfinished window are appended. Windows, arrivals and membership are those of the buffered path.
+    bool count_direct_ok(const DBatch& db) const {
+        const int64_t len = plan.length;
+        return count_direct && plan.interval <= 0 && !inc && !need_rel && !gmode && rowpos_col < 0 && dp.n_sagg == 0 &&
+               small_win_on && len >= 1 && len <= kSmallWin && db.n >= 2 * len;
+    }
+    int push_count_direct(const DBatch& db) {
+        const int64_t n = db.n, len = plan.length, A0 = arrivals, A1 = A0 + n;
+        int64_t k = std::max<int64_t>(count_k, 1);   // next window: [k len - len, k len)
+        int64_t e = k * len;
+        if (e > A1) return 1;
+        if (e - len < A0) {   // the window the carried rows began: the batch head completes it in the buffer
+            const int64_t hcut = e - A0;
+            if (int rc = eb_append(db, 0, hcut, A0)) return rc;
+            eb_rel = eb.n;
+            std::vector<PendWin> pw(1);
+            pw[0].q.kind = RB_FIXED;
+            pw[0].q.pos = e - len - eb_base;
+            pw[0].q.rstep = e - eb_base;
+            if (int rc = fire_windows(pw)) return rc;
+            ++k;
+            e += len;
+        }
+        std::vector<int64_t> hab;
+        for (; e <= A1; ++k, e += len) { hab.push_back(e - len - A0); hab.push_back(e - A0); }
+        if (int rc = fire_direct_small(db, hab, A0)) return rc;
+        count_k = k;
+        // every buffered row is consumed: the buffer restarts at the next window's first arrival with its rows
+        const int64_t s_next = k * len - len;
+        eb.n = 0;
+        eb_base = s_next;
+        eb_rel = 0;
+        eb_floor = 0;
+        if (int rc = eb_append(db, s_next - A0, A1 - s_next, A0)) return rc;
+        arrivals = A1;
+        eb_rel = eb.n;
+        return 0;
+    }
+
     int push_count(const DBatch& db) {
+        if (count_direct_ok(db)) {
+            const int rc = push_count_direct(db);
+            if (rc <= 0) return rc;   // 1: the batch holds no whole window, buffered path
+        }
         const int64_t n = db.n;
         const int64_t arrival_base = arrivals;
         if (int rc = eb_append(db, 0, n, arrival_base)) return rc;

@@ -365,12 +365,13 @@ __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* 
 }
 
 // debug_membership for range windows: count and Σ ek_mix64(arrival) over [a, b) (one block per window)
+// (barr == nullptr: row i's arrival is arr_base + i — windows read straight from a batch in arrival order)
 __global__ __launch_bounds__(kBlock) void k_range_members(const int64_t* __restrict__ barr, const int64_t* __restrict__ ab,
                                                           const int32_t* __restrict__ slot, int64_t* wmc,
-                                                          unsigned long long* wmh) {
+                                                          unsigned long long* wmh, int64_t arr_base) {
     const int64_t a = ab[2 * blockIdx.x], b = ab[2 * blockIdx.x + 1];
     unsigned long long h = 0;
-    for (int64_t i = a + threadIdx.x; i < b; i += kBlock) h += d_mix64((uint64_t)barr[i]);
+    for (int64_t i = a + threadIdx.x; i < b; i += kBlock) h += d_mix64(barr ? (uint64_t)barr[i] : (uint64_t)(arr_base + i));
     for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
     __shared__ unsigned long long s[kBlock / 64];
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = h;
@@ -499,17 +500,33 @@ __device__ __forceinline__ uint32_t sw_hash(uint32_t k) {
     return k;
 }
 
+// Windows laid out arithmetically (consecutive COUNTWINDOW blocks of one batch): window w = rows [a0 + w len, + len),
+// result slot slot0 + w, result region ob0 + w rowcap — no per-window lists to upload.
+struct SwArith {
+    int64_t a0, ob0, rowcap;
+    int32_t len, slot0;
+};
+
+// HAVING decision (1 keep, 0 drop, -1 non-bool: a window error) of a group's partial, without side effects
+template <int NVC>
+__device__ __forceinline__ int having_decide(const DPlan& p, const Part<NVC>& s) {
+    if (p.n_having <= 0) return 1;
+    const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, [&](int k) { return agg_value(p, s, k); });
+    if (h.tag != V_BOOL) return -1;
+    return h.i != 0 ? 1 : 0;
+}
+
 template <int NVC>
 __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
                                                      const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
-                                                     const int64_t* __restrict__ obase, Results res, int max_n) {
+                                                     const int64_t* __restrict__ obase, Results res, int max_n, SwArith ar) {
     constexpr int R = kSmallWin / kBlock;      // rows per thread
     const DPlan& p = *pp;
-    const int w = wlist[blockIdx.x];
-    const int64_t a = ab[2 * w];
-    const int n = (int)(ab[2 * w + 1] - a);   // 1 <= n <= kSmallWin (host-checked)
-    const int32_t widx = slots[w];
-    const int64_t out = obase[w];
+    const int w = wlist ? wlist[blockIdx.x] : (int)blockIdx.x;
+    const int64_t a = wlist ? ab[2 * w] : ar.a0 + (int64_t)w * ar.len;
+    const int n = wlist ? (int)(ab[2 * w + 1] - a) : ar.len;   // 1 <= n <= kSmallWin (host-checked)
+    const int32_t widx = wlist ? slots[w] : ar.slot0 + w;
+    const int64_t out = wlist ? obase[w] : ar.ob0 + (int64_t)w * ar.rowcap;
     // dynamic LDS sized by the launch's largest window (sw_lds_bytes): slots = the power of two >= 2 max_n
     extern __shared__ uint32_t s_dyn[];
     const int Hmax = sw_slots(max_n);
@@ -518,13 +535,21 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
     uint32_t* s_grp = s_off + Hmax;            // [max_n] occupied slots: (first row in s_row) << 16 | rows
     uint16_t* s_row = (uint16_t*)(s_grp + max_n);   // [max_n] window rows grouped by slot
     __shared__ uint32_t s_wsum[kBlock / 64];
-    __shared__ int s_err, s_ng;
+    __shared__ int s_err, s_ng, s_h1;
     __shared__ uint32_t esh[20];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     int H = 256;
     while (H < 2 * n) H <<= 1;
     for (int k = t; k < H; k += kBlock) { s_key[k] = ~0u; s_off[k] = 0; }
-    if (t == 0) { s_err = 0; s_ng = 0; }
+    if (t == 0) {
+        s_err = 0;
+        s_ng = 0;
+        if (p.having_star) {   // HAVING over count(*) alone: the decision for a one-row group, evaluated once
+            Part<NVC> cp{};
+            cp.cnt = 1;
+            s_h1 = having_decide(p, cp);
+        }
+    }
     __syncthreads();
     const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
     int my[R];
@@ -587,7 +612,19 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
         Part<NVC> s{};
         bool present = false;
         uint32_t key = 0;
-        if (gi < ng) {
+        int hs = 1;   // HAVING over count(*) alone (C4b: count(*) > 1): decided from the group's row count, before any fold
+        if (gi < ng && p.having_star) {
+            const int64_t c = (int64_t)(s_grp[gi] & 0xFFFFu);
+            int d = s_h1;
+            if (c != 1) {
+                Part<NVC> cp{};
+                cp.cnt = c;
+                d = having_decide(p, cp);
+            }
+            if (d < 0) atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
+            hs = d > 0 ? 1 : 0;
+        }
+        if (gi < ng && hs) {
             const uint32_t gw = s_grp[gi];
             const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu), g1 = g0 + c;
             sw_sort_rows(s_row + g0, c);   // the scatter's atomics placed them in no fixed order

@@ -127,6 +127,26 @@ def test_count_window(oracle, engine_mod, n, m):
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
 
 
+def test_count_window_direct_uneven_batches(oracle, engine_mod):
+    """COUNTWINDOW(1000): batches holding whole windows are aggregated straight from the batch (the window spanning
+    the carried rows and the batch head goes through the event buffer); small batches (< 2 windows) take the
+    buffered path; mostly one-row groups over a large key space, HAVING count(*) > 1 decided from the row count."""
+    sql = ("SELECT deviceId, stddev(temperature), var(temperature) FROM demo "
+           "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1")
+    cols = _iot(60_500, 20_000, seed=67, epm=10)
+    cuts = [0, 700, 5_300, 6_100, 9_999, 10_000, 31_234, 32_000, 33_500, 60_500]
+    for members in (True, False):   # without the fingerprint the direct windows launch with arithmetic ranges
+        rule = compile_rule(sql, IOT_SCHEMA, num_keys=20_000, is_event_time=False, debug_membership=members)
+        exp = oracle.run(rule.plan, cols)
+        eng = engine_mod.Engine(rule.plan)
+        for lo, hi in zip(cuts, cuts[1:]):
+            eng.push_host([c[lo:hi] for c in cols])
+        got = eng.poll()
+        eng.close()
+        assert len(got) == len(exp.windows) == 60
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=members)
+
+
 def test_count_window_rejected_in_event_time(engine_mod):
     rule = compile_rule("SELECT count(*) FROM demo GROUP BY COUNTWINDOW(10)", IOT_SCHEMA)
     with pytest.raises(engine_mod.EngineError) as e:

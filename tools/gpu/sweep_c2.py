@@ -22,7 +22,7 @@ def main():
                                                                events_per_ms=cfg["epm"], t0=cfg["t0"]))
     n = int(cols[0].numel())
     ptrs = [c.data_ptr() for c in cols]
-    rule = compile_rule(cfg["sql"], bench.schema_of(cfg), num_keys=cfg["keys"])
+    rule = compile_rule(cfg["sql"], bench.schema_of(cfg), num_keys=cfg["keys"], is_event_time=not cfg.get("processing_time"))
     steps = int(os.environ.get("SWEEP_STEPS", "10"))
     ref_rows = None
     for spec in sys.argv[1:] or [""]:
