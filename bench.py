@@ -168,6 +168,55 @@ def global_tuples(cfg, world, n_glob):
 CPU_SAMPLE = {"C2": 100_000_000, "C3": 15_000_000, "C4a": 1_000_000, "C4b": 50_000_000, "C5": 30_000_000}
 
 
+def device_router(ts, arr, tol, dist, want_list):
+    """The rule's WatermarkOp over the WHOLE global stream (ekgpu.shard.GlobalWatermark, watermark_op.go:144-225),
+    computed by the ranks from their own rows, inside the timed step: F[v] = first global arrival with ts == v
+    (scatter-min on each rank, one all_reduce MIN over the stream's ts range); the running max advances exactly at
+    the arrivals F[v] < min_{u > v} F[u] (no earlier arrival reached v), which are the WatermarkTuples (wm = v - tol);
+    each rank checks its rows against the tuple before them (accepted iff ts >= mark - tol) and one all_reduce MIN
+    gives all_accepted. Returns the tuple dict make_ctx takes: the full tuple list when `want_list` (range-mode
+    windows) or when some row is late, else only the batch's last tuple with the all_accepted / max_wm_step hints
+    (a pane-mode shard needs nothing else, include/ekgpu.h ek_global_ctx)."""
+    import numpy as np
+    import torch
+    i64max = torch.iinfo(torch.int64).max
+    dev = ts.device
+    mm = torch.stack([-ts.min(), ts.max()]) if ts.numel() else torch.tensor([-i64max, -i64max], device=dev)
+    dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+    lo, hi = -int(mm[0]), int(mm[1])
+    F = torch.full((hi - lo + 1,), i64max, dtype=torch.int64, device=dev)
+    if ts.numel():
+        F.scatter_reduce_(0, ts - lo, arr, reduce="amin", include_self=True)
+    dist.all_reduce(F, op=dist.ReduceOp.MIN)
+    S = torch.flip(torch.cummin(torch.flip(F, [0]), 0).values, [0])
+    nxt = torch.cat([S[1:], torch.tensor([i64max], dtype=torch.int64, device=dev)])
+    tv = torch.nonzero(F < nxt).squeeze(1)
+    t_arr = F[tv].contiguous()
+    t_mark = tv + lo
+    k = torch.searchsorted(t_arr, arr) - 1
+    zero_mark = -62135596800000 + tol          # the stream mark before the first event (watermark_op.go:55-58)
+    mb = torch.where(k >= 0, t_mark[k.clamp(min=0)], torch.full_like(k, zero_mark))
+    acc = torch.tensor([int(bool((ts >= mb - tol).all())) if ts.numel() else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(acc, op=dist.ReduceOp.MIN)
+    wm_ts = t_mark - tol
+    steps = wm_ts[1:] - wm_ts[:-1]
+    j = torch.searchsorted(wm_ts, torch.tensor([lo], dtype=torch.int64, device=dev))
+    jj = int(j.clamp(max=len(wm_ts) - 1))
+    head = torch.stack([acc[0], steps.max() if steps.numel() else torch.tensor(0, device=dev), t_arr[jj], F[0],
+                        t_arr[-1], wm_ts[-1]]).cpu().tolist()
+    all_acc, max_step, o_arr, first_lo = bool(head[0]), int(head[1]), int(head[2]), int(head[3])
+    out = {"arrivals_end": None, "all_accepted": all_acc, "max_wm_step": max_step,
+           # the first window's anchor: the earliest event (ts = lo) is released at the first tuple reaching it
+           "origin_known": all_acc and first_lo <= o_arr, "origin_ts": lo, "origin_arrival": o_arr}
+    if want_list or not all_acc:
+        out["wm_arrival"] = t_arr.cpu().numpy()
+        out["wm_ts"] = wm_ts.cpu().numpy()
+    else:
+        out["wm_arrival"] = np.array([int(head[4])], np.int64)
+        out["wm_ts"] = np.array([int(head[5])], np.int64)
+    return out
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -433,10 +482,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if os.environ.get("EKGPU_BENCH_ONE_DEVICE"):   # rehearsal of the N-rank path on one GPU (with a gloo backend)
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("EKGPU_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.sim_world > 1 and world == 1:
@@ -490,13 +541,24 @@ def main():
                         "origin_ts": cfg["t0"], "origin_arrival": 0}
             sent_ctx = make_ctx(sent_tup, np.zeros(0, np.int64))
 
+    want_list = bool(cfg.get("trig") or cfg.get("sentinel"))   # range-mode windows take the full tuple list
+    ts_dev = cols[1]
+
     def step():
+        nonlocal ctx, tup
         eng.reset()
         if world == 1:
             eng.push_device(n, ptrs)
             if sent_ptrs:
                 eng.push_device(1, sent_ptrs)
         else:
+            if iet and dist is not None:
+                # the router (global WatermarkOp) runs inside the timed step, on the ranks' own rows
+                tup = device_router(ts_dev, arr, args.disorder, dist, want_list)
+                tup["arrivals_end"] = n_glob
+                ctx = make_ctx(tup, np.zeros(0, np.int64))
+                ctx.row_arrival = arr.data_ptr()
+                ctx.memory = 1
             g = ctx
             if cfg.get("trig"):
                 from ekgpu.dist import exchange_triggers

@@ -1993,7 +1993,7 @@ struct Engine {
         const Results rv = results_view();
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
         const size_t gl = grp_walk_lds(s2);
-        const dim3 gg((unsigned)nsub), gb(kGrpBlock);
+        const dim3 gg((unsigned)nsub), gb(kGrpWalkBlock);
         if (dp.vc_is_float[0]) {
             if (sort) hipLaunchKernelGGL((k_grp_walk<true, true>), gg, gb, gl, stream, d_plan, g, rv);
             else hipLaunchKernelGGL((k_grp_walk<false, true>), gg, gb, gl, stream, d_plan, g, rv);

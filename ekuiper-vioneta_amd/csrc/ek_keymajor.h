@@ -463,6 +463,7 @@ __global__ __launch_bounds__(kBlock) void k_km_unpack(KmDesc d, int n_aggs, Resu
 constexpr int kGrpTile = 4096;
 constexpr int kGrpBlock = 256;
 constexpr int kGrpCap = 4096;         // rows of one sub-bucket held in LDS by k_grp_walk (host-checked)
+constexpr int kGrpWalkBlock = 512;    // k_grp_walk: 8 rows per thread in registers (16 at 256 threads held 153 VGPRs: 3 waves/SIMD)
 
 struct GrpTile {
     int64_t start;                    // first row of the tile in the pass's input
@@ -558,13 +559,13 @@ struct GrpDesc {
 };
 
 template <bool SORT, bool ISF>
-__global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, GrpDesc g, Results res) {
+__global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ pp, GrpDesc g, Results res) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_lds[];
     const DPlan& p = *pp;
     const int nloc = 1 << g.s2;                                   // keys of a sub-bucket (<= 2048)
     int64_t* s_b = (int64_t*)g_lds;                               // [kGrpCap] values grouped by key
     unsigned int* s_off = (unsigned int*)(s_b + kGrpCap);         // [nloc + 1] per-key counts -> offsets
-    __shared__ unsigned int wsum[kGrpBlock / 64];
+    __shared__ unsigned int wsum[kGrpWalkBlock / 64];
     __shared__ uint32_t esh[20];
     const int sb = blockIdx.x;
     const int64_t r0 = g.base2[sb], r1 = g.base2[sb + 1];
@@ -572,31 +573,31 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, 
     if (m <= 0) return;                                           // uniform: no row, no emission
     const uint32_t kbase = ((uint32_t)(sb >> 8) << g.s1) | ((uint32_t)(sb & 255) << g.s2);
     const uint32_t mask = (uint32_t)nloc - 1u;
-    for (int i = threadIdx.x; i < nloc; i += kGrpBlock) s_off[i] = 0;
+    for (int i = threadIdx.x; i < nloc; i += kGrpWalkBlock) s_off[i] = 0;
     __syncthreads();
     // counting sort by local key: every row's key and value are loaded into registers up front (all loads in flight
     // at once instead of one latency per strided iteration), ranked by one LDS atomic, then placed after the scan
-    constexpr int R = kGrpCap / kGrpBlock;
+    constexpr int R = kGrpCap / kGrpWalkBlock;
     uint32_t rkey[R];
     int64_t rval[R];
     unsigned int rrk[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const int i = threadIdx.x + j * kGrpBlock;
+        const int i = threadIdx.x + j * kGrpWalkBlock;
         if (i < m) { rkey[j] = g.keys[r0 + i] & mask; rval[j] = g.vals[r0 + i]; }
     }
 #pragma unroll
     for (int j = 0; j < R; ++j)
-        if (threadIdx.x + j * kGrpBlock < m) rrk[j] = atomicAdd(&s_off[rkey[j]], 1u);
+        if (threadIdx.x + j * kGrpWalkBlock < m) rrk[j] = atomicAdd(&s_off[rkey[j]], 1u);
     __syncthreads();
-    block_excl_scan<kGrpBlock>(s_off, nloc, wsum);
+    block_excl_scan<kGrpWalkBlock>(s_off, nloc, wsum);
 #pragma unroll
     for (int j = 0; j < R; ++j)
-        if (threadIdx.x + j * kGrpBlock < m) s_b[s_off[rkey[j]] + rrk[j]] = rval[j];
+        if (threadIdx.x + j * kGrpWalkBlock < m) s_b[s_off[rkey[j]] + rrk[j]] = rval[j];
     __syncthreads();
     constexpr bool isf = ISF;     // the value column's type (host-dispatched)
     const int fl[1] = {p.vc_flags[0]};
-    for (int kb = 0; kb < nloc; kb += kGrpBlock) {
+    for (int kb = 0; kb < nloc; kb += kGrpWalkBlock) {
         const int lk = kb + threadIdx.x;
         bool present = false;
         int64_t ov[EK_MAX_AGGS];
@@ -680,7 +681,7 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_walk(DPlan* __restrict__ pp, 
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t run = 0;
-            for (int w = 0; w < kGrpBlock / 64; ++w) { const uint32_t c = esh[w]; esh[w] = run; run += c; }
+            for (int w = 0; w < kGrpWalkBlock / 64; ++w) { const uint32_t c = esh[w]; esh[w] = run; run += c; }
             esh[16] = (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[g.widx], (unsigned long long)run);
         }
         __syncthreads();
