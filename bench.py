@@ -130,6 +130,18 @@ def schema_of(cfg):
     return dict(IOT_SCHEMA, trig="bigint") if cfg.get("trig") else IOT_SCHEMA
 
 
+def block_stream(cfg, world, rank, dev):
+    """COUNTWINDOW rules shard by window blocks, not by key: window k is the arrivals [k n, (k + 1) n) of the
+    global stream (window_op.go:390-418) and aggregates every key of that block only, so rank r takes the
+    contiguous arrivals [r N, (r + 1) N) (N = per-GPU events, a multiple of n) and runs the single-GPU path on them:
+    its windows are exactly the global windows r N / n ... (r + 1) N / n - 1 (no watermark, no exchange). Key-hash
+    shards would cut every window into `world` pieces of n / world rows."""
+    n_per = cfg["n"]
+    c = make_device_stream(n_per * world, cfg["keys"] * world, dev, seed=cfg["seed"], events_per_ms=cfg["epm"] * world,
+                           t0=cfg["t0"], lo=rank * n_per, hi=(rank + 1) * n_per)
+    return config_columns(cfg, c), n_per * world, cfg["keys"] * world
+
+
 def shard_stream(cfg, world, rank, dev):
     """Rank `rank`'s rows of the global stream (world x events, world x keys, world x rate): local columns with
     dense key ids, their global arrival indices, and the number of global events."""
@@ -424,6 +436,20 @@ def bench_c1(args):
                         "what": "payload bytes + offsets read + passing rows x (row index + 2 f64 columns) written, over ms_per_step"},
            "host_fed": {"messages_per_s": n / dth, "ms_per_step": dth * 1e3,
                         "what": "payloads in pinned host memory: H2D inside ek_json_decode, then the filter"}}
+    if not args.no_cpu:
+        # CPU baseline: the same payloads decoded one message at a time (json.loads: every number float64, as the
+        # schemaless converter.go:507-520) and filtered by WHERE temperature > 50 (filter_operator.go:36-90)
+        t2 = time.perf_counter()
+        kept = 0
+        for m in msgs:
+            d = json.loads(m)
+            t_ = d.get("temperature")
+            if t_ is not None and float(t_) > 50:
+                kept += 1
+        dtc = time.perf_counter() - t2
+        assert kept == rows
+        out["cpu_baseline"] = {"value": n / dtc, "unit": "messages/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"all {n} payloads, json.loads + WHERE per message (Python 3, C json decoder), {dtc:.1f} s"}
     print(json.dumps(out), flush=True)
     eng.close()
     dec.close()
@@ -508,8 +534,12 @@ def main():
         if args.disorder > 0 and iet:
             cols[1] = disorder_ts(cols[1], cfg["seed"], args.disorder)
         arr, n_glob, k_local = None, cfg["n"], cfg["keys"]
+    elif cfg.get("processing_time"):
+        cols, n_glob, k_local = block_stream(cfg, world, rank, dev)
+        arr = None
     else:
         cols, arr, n_glob, k_local = shard_stream(cfg, world, rank, dev)
+    blocks = world > 1 and bool(cfg.get("processing_time"))   # window-block shards: the single-GPU path per rank
     n = int(cols[0].numel())
     rule = compile_rule(cfg["sql"], schema_of(cfg), num_keys=max(1, k_local), is_event_time=iet,
                         late_tolerance_ms=args.disorder if iet else 0)
@@ -527,7 +557,7 @@ def main():
         crule = compile_rule(cfg["global_count"], schema_of(cfg), num_keys=1, is_event_time=iet)
         cnt_eng = Engine(crule.plan, device=local)
     ctx = None
-    if world > 1:
+    if world > 1 and not blocks:
         tup = global_tuples(cfg, world, n_glob) if iet else {
             "wm_arrival": np.zeros(0, np.int64), "wm_ts": np.zeros(0, np.int64), "arrivals_end": n_glob,
             "origin_known": False, "origin_ts": 0, "origin_arrival": 0}
@@ -547,7 +577,7 @@ def main():
     def step():
         nonlocal ctx, tup
         eng.reset()
-        if world == 1:
+        if world == 1 or blocks:
             eng.push_device(n, ptrs)
             if sent_ptrs:
                 eng.push_device(1, sent_ptrs)
@@ -645,7 +675,7 @@ def main():
                                         "achieved_gbs": kb_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None}
     dominant = max(kernels.items(), key=lambda kv: kv[1]["launch_ms"] * kv[1]["launches_per_step"])[0] if kernels else None
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", f"r02_pmc_{args.config}.json")
+    pmc = os.path.join(ROOT, "profiles", f"r03_pmc_{args.config}.json")
     if os.path.exists(pmc):
         pm = json.load(open(pmc))
         if pm.get("events_per_gpu") == n and world == 1:
@@ -667,7 +697,8 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['sql']}", "events_per_gpu": cfg["n"], "keys_per_gpu": cfg["keys"],
                    "events_total": n_glob, "events_rank0": n, "windows_emitted": n_windows, "rows_per_step_rank0": rows,
                    "event_rate": f"{cfg['epm'] * world} events per ms of event time" if iet else "processing time",
-                   "parallelism": f"key-hash shards x{world}" + (" (shard mode: global WatermarkTuples, global arrivals"
+                   "parallelism": f"window-block shards x{world} (COUNTWINDOW: contiguous global arrivals per rank)" if blocks else
+                                  f"key-hash shards x{world}" + (" (shard mode: global WatermarkTuples, global arrivals"
                                                                   + (", trigger all_gather" if cfg.get("trig") else "")
                                                                   + (", count(*) all_gather" if cfg.get("global_count") else "")
                                                                   + ")" if world > 1 else "")},

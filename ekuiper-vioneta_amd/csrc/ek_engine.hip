@@ -665,7 +665,9 @@ struct Engine {
         // chunk-local partitions k_part can sort through LDS: 8 B each next to the 4096-row staging (~13 K)
         np_max = env_int("EKGPU_NP_MAX", 13000);
         max_panes_group = env_int("EKGPU_MAX_GROUP_PANES", 4096);
-        ring = (int)(2 * ppw + 16);
+        // pane-state ring: pane mode only (range-mode windows aggregate from the event buffer; a COUNTWINDOW(1000) ring
+        // of 2 ppw + 16 slots held 2016 x K x 24 B — 387 GB at 8 M keys)
+        ring = range_mode ? 4 : (int)(2 * ppw + 16);
 
         // ---- HIP resources
         if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
