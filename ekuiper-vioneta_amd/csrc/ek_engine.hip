@@ -657,6 +657,7 @@ struct Engine {
         km_one = env_int("EKGPU_KM_ONE", 1);
         km_packed = env_int("EKGPU_KM_PACKED", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
+        append_fused = env_int("EKGPU_APPEND_FUSED", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
@@ -1580,11 +1581,22 @@ struct Engine {
         for (int c = 0; c < plan.n_columns; ++c)
             if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
         if (int rc = eb_reserve(cnt)) return rc;
+        // the kept columns (and the arrival numbers) in one k_append launch; misaligned columns by hipMemcpyAsync
+        AppendDesc ad{};
         for (int c = 0; c < plan.n_columns; ++c) {
             const size_t es = col_es(c);
-            if (eb_need[c])
-                hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
-                               hipMemcpyDeviceToDevice, stream);
+            if (eb_need[c] && cnt > 0) {
+                char* dst = (char*)eb.col[c].p + eb.n * es;
+                const char* src = (const char*)db.col[c] + start * es;
+                if (append_fused && ad.nc < kAppendCols && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0) {
+                    ad.src[ad.nc] = (const uint4*)src;
+                    ad.dst[ad.nc] = (uint4*)dst;
+                    ad.bytes[ad.nc] = (int64_t)cnt * (int64_t)es;
+                    ad.nc++;
+                } else {
+                    hipMemcpyAsync(dst, src, (size_t)cnt * es, hipMemcpyDeviceToDevice, stream);
+                }
+            }
             if (eb_valid_on[c]) {
                 if (db.valid[c]) hipMemcpyAsync((uint8_t*)eb.valid[c].p + eb.n, db.valid[c] + start, (size_t)cnt, hipMemcpyDeviceToDevice, stream);
                 else fill_valid_ones(c, eb.n, cnt);
@@ -1592,9 +1604,19 @@ struct Engine {
         }
         if (g_row_arr) {   // shard mode: the rows' global arrival indices
             if (cnt > 0) hipMemcpyAsync((int64_t*)eb.arr.p + eb.n, g_row_arr + start, (size_t)cnt * 8, hipMemcpyDeviceToDevice, stream);
-        } else {
+        } else if (ad.nc > 0) {
+            ad.arr = (int64_t*)eb.arr.p + eb.n;
+            ad.arr_base = arr_base + start;
+            ad.n = cnt;
+        } else if (cnt > 0) {
             const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
             hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
+        }
+        if (ad.nc > 0) {
+            int64_t mv = 0;
+            for (int c = 0; c < ad.nc; ++c) mv = std::max<int64_t>(mv, ad.bytes[c] >> 4);
+            const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (mv + 1023) / 1024));
+            hipLaunchKernelGGL(k_append, dim3((unsigned)gx, (unsigned)(ad.nc + (ad.arr ? 1 : 0))), dim3(256), 0, stream, ad);
         }
         if (need_rel) hipMemsetAsync((int64_t*)eb.rel.p + eb.n, 0x7f, (size_t)cnt * 8, stream);   // "not released"
         eb.n += cnt;
@@ -1905,6 +1927,7 @@ struct Engine {
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
     int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
+    int append_fused = 1;   // EKGPU_APPEND_FUSED=0: event-buffer appends by one hipMemcpyAsync per column + k_iota64
     DevBuf km_rbase, km_rec;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
@@ -1965,7 +1988,7 @@ struct Engine {
         const int64_t nt2 = (int64_t)grp_ht.size();
         hipMemcpyAsync(base1, grp_hb.data(), (size_t)n1 * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0) hipMemcpyAsync(d_t2, grp_ht.data(), (size_t)nt2 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1, K,
+        hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt1), dim3(kGrpScatBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1, K,
                            kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p);
         if (nt2 > 0)
             hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
@@ -1980,7 +2003,7 @@ struct Engine {
         if (mx > (unsigned int)kGrpCap) { phase_end(ph); return 0; }
         hipMemcpyAsync(base2, grp_hb.data() + n1, (size_t)(nsub + 1) * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0)
-            hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
+            hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt2), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[0].p,
                                (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, K, 1, (const int64_t*)base2, cur2,
                                (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p);
         phase_end(ph);
@@ -1994,19 +2017,28 @@ struct Engine {
         g.widx = wslot;
         const Results rv = results_view();
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
-        const size_t gl = grp_walk_lds(s2);
+        // register depth (and LDS slab) sized to the largest sub-bucket of this launch
+        const int rdep = mx <= 8u * kGrpWalkBlock ? 8 : mx <= 12u * kGrpWalkBlock ? 12 : 16;
+        const size_t gl = grp_walk_lds(s2, rdep);
         const dim3 gg((unsigned)nsub), gb(kGrpWalkBlock);
-        if (dp.vc_is_float[0]) {
-            if (sort) hipLaunchKernelGGL((k_grp_walk<true, true>), gg, gb, gl, stream, d_plan, g, rv);
-            else hipLaunchKernelGGL((k_grp_walk<false, true>), gg, gb, gl, stream, d_plan, g, rv);
-        } else {
-            if (sort) hipLaunchKernelGGL((k_grp_walk<true, false>), gg, gb, gl, stream, d_plan, g, rv);
-            else hipLaunchKernelGGL((k_grp_walk<false, false>), gg, gb, gl, stream, d_plan, g, rv);
-        }
+        const bool isf = dp.vc_is_float[0] != 0;
+        if (rdep == 8) grp_walk_launch<8>(sort, isf, gg, gb, gl, g, rv);
+        else if (rdep == 12) grp_walk_launch<12>(sort, isf, gg, gb, gl, g, rv);
+        else grp_walk_launch<16>(sort, isf, gg, gb, gl, g, rv);
         phase_end(ph2);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping walk failed");
         *ok = true;
         return 0;
+    }
+    template <int R>
+    void grp_walk_launch(bool sort, bool isf, dim3 gg, dim3 gb, size_t gl, const GrpDesc& g, const Results& rv) {
+        if (isf) {
+            if (sort) hipLaunchKernelGGL((k_grp_walk<true, true, R>), gg, gb, gl, stream, d_plan, g, rv);
+            else hipLaunchKernelGGL((k_grp_walk<false, true, R>), gg, gb, gl, stream, d_plan, g, rv);
+        } else {
+            if (sort) hipLaunchKernelGGL((k_grp_walk<true, false, R>), gg, gb, gl, stream, d_plan, g, rv);
+            else hipLaunchKernelGGL((k_grp_walk<false, false, R>), gg, gb, gl, stream, d_plan, g, rv);
+        }
     }
     template <int N>
     void km_walk1(bool sort, size_t lds, int nblk, const KmDesc& d, const Results& rv) {
@@ -2701,7 +2733,7 @@ struct Engine {
             const size_t o = h_rts.size();
             h_rts.resize(o + n_new);
             hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
-            if (need_rel) {
+            if (need_rel && !gmode) {
                 // the watermark before each new row's release step (k_step_wm over the batch's running max)
                 if (int rc = ensure(mrg_col, (size_t)n_new * 16)) return rc;
                 int64_t* g = (int64_t*)mrg_col.p;
@@ -2742,8 +2774,27 @@ struct Engine {
             *ticked = false;
             return INT64_MAX;
         };
+        if (gmode) {
+            // shard mode: the sessions the router closed over the whole stream (GlobalSession), each over this
+            // shard's released rows with ts < end (a session window is not overlapping: window_op.go:605-655)
+            for (const GSess& gs : g_sess) {
+                const int64_t i0 = std::max<int64_t>(0, floor_abs - h_rts_base);
+                const int64_t b_abs = i0 >= (int64_t)h_rts.size()
+                    ? floor_abs
+                    : h_rts_base + (std::lower_bound(h_rts.begin() + i0, h_rts.end(), gs.end) - h_rts.begin());
+                PendWin p{};
+                p.q.kind = RB_FIXED;
+                p.q.pos = floor_abs - eb_base;
+                p.q.rstep = b_abs - eb_base;
+                p.start = gs.start;
+                p.end = gs.end;
+                pw.push_back(p);
+                floor_abs = b_abs;
+            }
+            g_sess.clear();
+        }
         bool ticked = false;
-        int64_t we = next_session(floor_abs, &ticked);
+        int64_t we = gmode ? INT64_MAX : next_session(floor_abs, &ticked);
         while (we != INT64_MAX && we <= W) {
             const int64_t i0 = floor_abs - h_rts_base;
             const bool has_inputs = i0 < (int64_t)h_rts.size();
@@ -3577,11 +3628,13 @@ struct Engine {
     DevBuf g_wm_d, g_arr_d, g_acc_d;
     struct GTrig { int64_t a, t; };
     std::vector<GTrig> g_trig;          // accepted global sliding triggers not released yet (arrival order)
+    struct GSess { int64_t start, end; };
+    std::vector<GSess> g_sess;          // sessions the router closed in this push (ek_global_ctx sess_*), in order
 
     int global_check() {
         if (plan.is_event_time) {
-            if (inc || plan.window_version == 2 || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_STATE)
-                return fail(EK_ERR_UNSUPPORTED, "shard mode: session, state, v2 and incremental windows depend on every row "
+            if (inc || plan.window_version == 2 || wtype == EK_WINDOW_STATE)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: state, v2 and incremental windows depend on every row "
                                                 "of the stream (not shardable by key)");
             if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
                 return fail(EK_ERR_UNSUPPORTED, "shard mode: delayed sliding windows are not built");
@@ -3621,6 +3674,14 @@ struct Engine {
         if ((g->n_wm > 0 && (!g->wm_arrival || !g->wm_ts)) || (g->n_trig > 0 && (!g->trig_arrival || !g->trig_ts)))
             return fail(EK_ERR_INVALID, "missing watermark / trigger list");
         if (n > 0 && !g->row_arrival) return fail(EK_ERR_INVALID, "missing row arrivals");
+        if (g->n_sess < 0 || (g->n_sess > 0 && (!g->sess_start || !g->sess_end)))
+            return fail(EK_ERR_INVALID, "missing session list");
+        g_sess.clear();
+        if (wtype == EK_WINDOW_SESSION)
+            for (int64_t k = 0; k < g->n_sess; ++k) {
+                if (g->sess_end[k] <= (k ? g->sess_end[k - 1] : INT64_MIN)) return fail(EK_ERR_INVALID, "session ends must advance");
+                g_sess.push_back(GSess{g->sess_start[k], g->sess_end[k]});
+            }
         g_wa = g->wm_arrival;
         g_wt = g->wm_ts;
         g_nwm = g->n_wm;

@@ -495,55 +495,60 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restri
     if (h[threadIdx.x]) atomicAdd(&tot[(blockIdx.x % rep) * 256 + t.pre + threadIdx.x], h[threadIdx.x]);
 }
 
-// rows of a tile -> their (replica, pre + digit) region: base[] exclusive region starts, cur[] reservation cursors
-__global__ __launch_bounds__(kGrpBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
-                                                           const GrpTile* __restrict__ tiles, int shift, uint32_t K, int rep,
-                                                           const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
-                                                           uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
+// rows of a tile -> their (replica, pre + digit) region: base[] exclusive region starts, cur[] reservation cursors.
+// 512 threads (8 rows each): the 52 KB of LDS staging allow two workgroups per CU, so 16 waves keep loads in flight
+// (256 threads left 8 waves per CU and ran the pass at 2.7 TB/s). The digit is re-derived from the staged key.
+constexpr int kGrpScatBlock = 512;
+__global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
+                                                               const GrpTile* __restrict__ tiles, int shift, uint32_t K, int rep,
+                                                               const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
+                                                               uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
     __shared__ unsigned int h[256], lofs[257];
     __shared__ int64_t gb[256];
     __shared__ uint32_t s_key[kGrpTile];
     __shared__ int64_t s_val[kGrpTile];
-    __shared__ uint8_t s_dig[kGrpTile];
-    __shared__ unsigned int wsum[kGrpBlock / 64];
+    __shared__ unsigned int wsum[kGrpScatBlock / 64];
     const GrpTile t = tiles[blockIdx.x];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
-    constexpr int R = kGrpTile / kGrpBlock;
+    constexpr int R = kGrpTile / kGrpScatBlock;
     uint32_t k[R];
     int64_t v[R];
     int rk[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const int i = threadIdx.x + j * kGrpBlock;
+        const int i = threadIdx.x + j * kGrpScatBlock;
         rk[j] = -1;
         if (i >= t.len) continue;
         k[j] = keys[t.start + i];
         v[j] = vals[t.start + i];
-        if (k[j] < K) rk[j] = (int)atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        if (threadIdx.x + j * kGrpScatBlock < t.len && k[j] < K) rk[j] = (int)atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        const unsigned int c = h[threadIdx.x];
+        const int ci = (int)(blockIdx.x % rep) * 256 + t.pre + threadIdx.x;
+        if (c) gb[threadIdx.x] = base[ci] + (int64_t)atomicAdd(&cur[ci], c);
+        lofs[threadIdx.x] = c;
     }
     __syncthreads();
-    const unsigned int c = h[threadIdx.x];
-    const int ci = (int)(blockIdx.x % rep) * 256 + t.pre + threadIdx.x;
-    if (c) gb[threadIdx.x] = base[ci] + (int64_t)atomicAdd(&cur[ci], c);
-    lofs[threadIdx.x] = c;
-    __syncthreads();
-    block_excl_scan<kGrpBlock>(lofs, 256, wsum);   // lofs[256] = rows kept
+    block_excl_scan<kGrpScatBlock>(lofs, 256, wsum);   // lofs[256] = rows kept
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         if (rk[j] < 0) continue;
-        const unsigned int d = (k[j] >> shift) & 255u;
-        const unsigned int p = lofs[d] + (unsigned int)rk[j];
+        const unsigned int p = lofs[(k[j] >> shift) & 255u] + (unsigned int)rk[j];
         s_key[p] = k[j];
         s_val[p] = v[j];
-        s_dig[p] = (uint8_t)d;
     }
     __syncthreads();
     const unsigned int m = lofs[256];
-    for (unsigned int p = threadIdx.x; p < m; p += kGrpBlock) {
-        const unsigned int d = s_dig[p];
+    for (unsigned int p = threadIdx.x; p < m; p += kGrpScatBlock) {
+        const uint32_t kk = s_key[p];
+        const unsigned int d = (kk >> shift) & 255u;
         const int64_t dst = gb[d] + (int64_t)(p - lofs[d]);
-        okeys[dst] = s_key[p];
+        okeys[dst] = kk;
         ovals[dst] = s_val[p];
     }
 }
@@ -558,18 +563,22 @@ struct GrpDesc {
     int32_t pad;
 };
 
-template <bool SORT, bool ISF>
+// R: rows per thread held in registers (R * kGrpWalkBlock >= the launch's largest sub-bucket, host-chosen). With
+// SORT, every row's rank inside its key's segment (values below it, ties broken by position) is counted from the
+// grouped LDS copy with independent reads, then the row is stored at its rank: the segments come out sorted with no
+// dependent per-key insertion chain (the time of a wave is its longest segment, not that segment squared).
+template <bool SORT, bool ISF, int R>
 __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ pp, GrpDesc g, Results res) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_lds[];
     const DPlan& p = *pp;
     const int nloc = 1 << g.s2;                                   // keys of a sub-bucket (<= 2048)
-    int64_t* s_b = (int64_t*)g_lds;                               // [kGrpCap] values grouped by key
-    unsigned int* s_off = (unsigned int*)(s_b + kGrpCap);         // [nloc + 1] per-key counts -> offsets
+    int64_t* s_b = (int64_t*)g_lds;                               // [R * kGrpWalkBlock] values grouped by key
+    unsigned int* s_off = (unsigned int*)(s_b + R * kGrpWalkBlock);   // [nloc + 1] per-key counts -> offsets
     __shared__ unsigned int wsum[kGrpWalkBlock / 64];
     __shared__ uint32_t esh[20];
     const int sb = blockIdx.x;
     const int64_t r0 = g.base2[sb], r1 = g.base2[sb + 1];
-    const int m = (int)(r1 - r0);                                 // <= kGrpCap (host-checked)
+    const int m = (int)(r1 - r0);                                 // <= R * kGrpWalkBlock (host-checked)
     if (m <= 0) return;                                           // uniform: no row, no emission
     const uint32_t kbase = ((uint32_t)(sb >> 8) << g.s1) | ((uint32_t)(sb & 255) << g.s2);
     const uint32_t mask = (uint32_t)nloc - 1u;
@@ -577,7 +586,7 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
     __syncthreads();
     // counting sort by local key: every row's key and value are loaded into registers up front (all loads in flight
     // at once instead of one latency per strided iteration), ranked by one LDS atomic, then placed after the scan
-    constexpr int R = kGrpCap / kGrpWalkBlock;
+    static_assert(R * kGrpWalkBlock <= kGrpCap, "sub-bucket rows beyond the LDS slab");
     uint32_t rkey[R];
     int64_t rval[R];
     unsigned int rrk[R];
@@ -596,12 +605,38 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
         if (threadIdx.x + j * kGrpWalkBlock < m) s_b[s_off[rkey[j]] + rrk[j]] = rval[j];
     __syncthreads();
     constexpr bool isf = ISF;     // the value column's type (host-dispatched)
+    if constexpr (SORT) {
+        // rank of each row inside its segment by ordered bits; equal ordered bits are equal values, so the tie
+        // order only has to make the ranks a permutation
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (threadIdx.x + j * kGrpWalkBlock >= m) continue;
+            const int a = (int)s_off[rkey[j]], b = (int)s_off[rkey[j] + 1];
+            const int me = a + (int)rrk[j];
+            const uint64_t ox = isf ? f64_to_ord(__longlong_as_double(rval[j])) : i64_to_ord(rval[j]);
+            unsigned int r = 0;
+            for (int q = a; q < b; ++q) {
+                const int64_t y = s_b[q];
+                const uint64_t oy = isf ? f64_to_ord(__longlong_as_double(y)) : i64_to_ord(y);
+                r += (oy < ox || (oy == ox && q < me)) ? 1u : 0u;
+            }
+            rrk[j] = (unsigned int)a + r;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            if (threadIdx.x + j * kGrpWalkBlock < m) s_b[rrk[j]] = rval[j];
+        __syncthreads();
+    }
     const int fl[1] = {p.vc_flags[0]};
     for (int kb = 0; kb < nloc; kb += kGrpWalkBlock) {
         const int lk = kb + threadIdx.x;
         bool present = false;
-        int64_t ov[EK_MAX_AGGS];
-        uint8_t ot[EK_MAX_AGGS];
+        Part<1> part{};
+        uint64_t sres[kMaxSortAggs];
+        uint8_t stag[kMaxSortAggs];
+#pragma unroll
+        for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
         if (lk < nloc) {
             const int j0 = (int)s_off[lk], j1 = (int)s_off[lk + 1];
             if (j1 > j0) {
@@ -625,28 +660,9 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                         m2[0] = __dadd_rn(m2[0], __dmul_rn(dd, dd));
                     }
                 }
-                Part<1> part{};
                 part_merge(p, part, j1 - j0, vc, is, fs, m2, mn, mx);
-                uint64_t sres[kMaxSortAggs];
-                uint8_t stag[kMaxSortAggs];
                 bool agg_err = false;
-#pragma unroll
-                for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
-                if constexpr (SORT) {
-                    // the key's values in place, ascending by ordered bits (the segment belongs to this thread)
-                    for (int j = j0 + 1; j < j1; ++j) {
-                        const int64_t x = s_b[j];
-                        const uint64_t ox = isf ? f64_to_ord(__longlong_as_double(x)) : i64_to_ord(x);
-                        int q = j;
-                        while (q > j0) {
-                            const int64_t y = s_b[q - 1];
-                            const uint64_t oy = isf ? f64_to_ord(__longlong_as_double(y)) : i64_to_ord(y);
-                            if (oy <= ox) break;
-                            s_b[q] = y;
-                            --q;
-                        }
-                        s_b[q] = x;
-                    }
+                if constexpr (SORT) {   // the segment is sorted ascending by ordered bits (rank placement above)
 #pragma unroll
                     for (int a = 0; a < kMaxSortAggs; ++a) {
                         if (a >= p.n_sagg) continue;
@@ -666,10 +682,7 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                 } else {
                     const int hv = km_having(p, part, SORT ? &sr : nullptr);
                     if (hv < 0) atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
-                    if (hv > 0) {
-                        present = true;
-                        km_row(p, part, SORT ? &sr : nullptr, ov, ot);
-                    }
+                    present = hv > 0;
                 }
             }
         }
@@ -685,7 +698,11 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
             esh[16] = (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[g.widx], (unsigned long long)run);
         }
         __syncthreads();
-        if (present) {
+        if (present) {   // the row's values are computed only now: nothing of them lives across the barriers
+            int64_t ov[EK_MAX_AGGS];
+            uint8_t ot[EK_MAX_AGGS];
+            const SortRes sr{sres, stag, 0, 1};
+            km_row(p, part, SORT ? &sr : nullptr, ov, ot);
             const int64_t pos = g.obase + (int64_t)esh[16] + esh[wv] + __popcll(msk & ((1ull << lane) - 1ull));
             res.key[pos] = kbase | (uint32_t)lk;
 #pragma unroll
@@ -698,7 +715,8 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
         __syncthreads();
     }
 }
-inline size_t grp_walk_lds(int s2) { return (size_t)kGrpCap * 8 + ((size_t)(1 << s2) + 1) * 4 + 16; }
+// dynamic LDS of k_grp_walk<.., R>: the R * kGrpWalkBlock value slab, then the nloc + 1 offsets
+inline size_t grp_walk_lds(int s2, int R) { return (size_t)R * kGrpWalkBlock * 8 + ((size_t)(1 << s2) + 1) * 4 + 16; }
 
 
 // one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count

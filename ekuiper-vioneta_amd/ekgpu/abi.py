@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 6
+EKGPU_ABI_VERSION = 7
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -155,6 +155,10 @@ class ek_global_ctx(C.Structure):
         ("n_trig", C.c_int64),
         ("memory", C.c_int32),
         ("pad2", C.c_int32),
+        ("sess_start", C.c_void_p),
+        ("sess_end", C.c_void_p),
+        ("sess_wm", C.c_void_p),
+        ("n_sess", C.c_int64),
     ]
 
 

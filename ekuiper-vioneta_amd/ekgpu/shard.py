@@ -116,6 +116,113 @@ class GlobalWatermark:
                 "origin_known": self.origin_known, "origin_ts": self.origin_ts, "origin_arrival": self.origin_arrival}
 
 
+_UNIT_MS = {1: 86_400_000, 2: 3_600_000, 3: 60_000, 4: 1000, 5: 1}   # EK_UNIT_DD .. EK_UNIT_MS
+
+
+def _aligned_end(ts: int, interval: int, unit: int, tz_s: int) -> int:
+    """getAlignedWindowEndTime (window_op.go:194-227): the end of the window holding ts on the unit's grid."""
+    off = tz_s * 1000
+    local = ts + off
+    day0 = (local // 86_400_000) * 86_400_000
+    if unit == 1:                                    # dd
+        return day0 + interval * 86_400_000 - off
+    # hh: hours of the day; mi: minutes of the hour; ss: seconds of the minute; ms: millis of the second
+    b0 = {2: day0, 3: (local // 3_600_000) * 3_600_000, 4: (local // 60_000) * 60_000,
+          5: (local // 1000) * 1000}[unit]
+    step = _UNIT_MS[unit]
+    part = (local - b0) // step
+    gap = interval * (part // interval + 1) if part > interval else interval
+    return b0 + gap * step - off
+
+
+class GlobalSession:
+    """A SESSIONWINDOW(unit, length, timeout) rule's window boundaries over the WHOLE stream, run by the router
+    beside GlobalWatermark: the WatermarkOp release (watermark_op.go:157-204: at each WatermarkTuple the buffered
+    accepted events with ts <= watermark, in (ts, arrival) order), then the window node's EventRow and
+    WatermarkTuple branches for a session (event_window_trigger.go:77-110 getNextSessionWindow, :124-196), on
+    timestamps only. Every session it closes is (start, end, watermark of the closing tuple); a key-hash shard
+    fires each over its own rows with ts < end (window_op.go:605-655 handleInputs: a session window is not
+    overlapping, its content is the remaining inputs before the end), so the shards' union is the stream's
+    windows. Host restatement of the same loop as oracle/ekoracle.c next_session / win_on_watermark."""
+
+    def __init__(self, plan):
+        u = _UNIT_MS[int(plan.time_unit)]
+        self.L = int(plan.length) * u
+        self.timeout = int(plan.interval) * u
+        self.raw = int(plan.length)
+        self.unit = int(plan.time_unit)
+        self.tz = int(plan.tz_offset_s)
+        self.pending = []            # heap of (ts, arrival): accepted, not released
+        self.inputs = []             # released ts not yet consumed by a session (release order = ts order)
+        self.has_trigger = False
+        self.trigger_time = 0
+        self.last_ticked = False
+
+    def _next(self, now):
+        inp = self.inputs
+        if inp:
+            et = inp[0]
+            tick = _aligned_end(et, self.raw, self.unit, self.tz)
+            p = None
+            for t in inp:
+                r = None
+                if p is not None and t - p > self.timeout:
+                    r = p + self.timeout
+                if t > tick:
+                    if tick - self.L > et and (r is None or tick < r):
+                        return tick, True
+                    tick += self.L
+                if r is not None:
+                    return r, False
+                p = t
+            if p is not None and now - p > self.timeout:
+                return p + self.timeout, False
+        return None, False
+
+    def step(self, ts: np.ndarray, wm: dict) -> dict:
+        """One global micro-batch (ts in arrival order, wm = GlobalWatermark.track's result for it): adds the
+        sessions its tuples closed to wm as sess_start / sess_end / sess_wm."""
+        import heapq
+        ts = np.asarray(ts, dtype=np.int64)
+        base = int(wm["arrivals_end"]) - len(ts)
+        acc = np.asarray(wm["accepted"], bool)
+        ev_a = (base + np.nonzero(acc)[0]).tolist()
+        ev_t = ts[acc].tolist()
+        out_s, out_e, out_w = [], [], []
+        j = 0
+        for a_k, w in zip(np.asarray(wm["wm_arrival"]).tolist(), np.asarray(wm["wm_ts"]).tolist()):
+            while j < len(ev_a) and ev_a[j] <= a_k:
+                heapq.heappush(self.pending, (ev_t[j], ev_a[j]))
+                j += 1
+            while self.pending and self.pending[0][0] <= w:
+                t, _ = heapq.heappop(self.pending)
+                if not self.has_trigger:
+                    self.has_trigger, self.trigger_time = True, t
+                self.inputs.append(t)
+            we, ticked = self._next(w)
+            while we is not None and we <= w:
+                if not self.last_ticked and self.inputs:
+                    self.has_trigger, self.trigger_time = True, self.inputs[0]
+                ws = self.trigger_time if self.has_trigger else ZERO_MS
+                if ws <= 0:
+                    ws = we - self.L
+                k = 0
+                while k < len(self.inputs) and self.inputs[k] < we:
+                    k += 1
+                del self.inputs[:k]
+                out_s.append(ws), out_e.append(we), out_w.append(w)
+                self.has_trigger, self.trigger_time = True, we
+                self.last_ticked = ticked
+                we, ticked = self._next(w)
+        for i in range(j, len(ev_a)):   # accepted after the batch's last tuple: released by a later one
+            heapq.heappush(self.pending, (ev_t[i], ev_a[i]))
+        wm = dict(wm)
+        wm["sess_start"] = np.asarray(out_s, np.int64)
+        wm["sess_end"] = np.asarray(out_e, np.int64)
+        wm["sess_wm"] = np.asarray(out_w, np.int64)
+        return wm
+
+
 def make_ctx(wm: dict, row_arrival: np.ndarray, trig_arrival=None, trig_ts=None):
     """An ek_global_ctx over host arrays (the arrays are attached to the struct to keep them alive)."""
     from . import abi as A
@@ -139,7 +246,14 @@ def make_ctx(wm: dict, row_arrival: np.ndarray, trig_arrival=None, trig_ts=None)
     g.trig_ts = tt.ctypes.data if len(tt) else None
     g.n_trig = len(ta)
     g.memory = A.EK_MEM_HOST
-    g._keep = (ra, wa, wt, ta, tt)
+    ss = np.ascontiguousarray(wm.get("sess_start", np.zeros(0)), dtype=np.int64)
+    se = np.ascontiguousarray(wm.get("sess_end", np.zeros(0)), dtype=np.int64)
+    sw = np.ascontiguousarray(wm.get("sess_wm", np.zeros(0)), dtype=np.int64)
+    g.sess_start = ss.ctypes.data if len(ss) else None
+    g.sess_end = se.ctypes.data if len(se) else None
+    g.sess_wm = sw.ctypes.data if len(sw) else None
+    g.n_sess = len(ss)
+    g._keep = (ra, wa, wt, ta, tt, ss, se, sw)
     return g
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 6
+#define EKGPU_ABI_VERSION 7
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -287,9 +287,12 @@ int ek_import_state(void* h, const void* buf, int64_t size);
  * WHOLE stream and broadcasts its WatermarkTuples; every shard receives only its own rows, each with its
  * global arrival index. A handle enters this mode at its first ek_push_batch_global / ek_advance_watermark
  * (before any ek_push_batch) and stays in it until ek_reset; its own rows no longer move its watermark.
- * Built for event-time TUMBLING / HOPPING / SLIDING (no delay) and processing-time COUNTWINDOW (global
- * arrival blocks); other windows -> EK_ERR_UNSUPPORTED (session gaps and state windows depend on every row
- * of the stream). Global un-grouped aggregates are merged across shards by the caller (ekgpu/dist.py). */
+ * Built for event-time TUMBLING / HOPPING / SLIDING (no delay) / SESSION and processing-time COUNTWINDOW
+ * (global arrival blocks); other windows -> EK_ERR_UNSUPPORTED (state windows depend on every row of the
+ * stream). A SESSIONWINDOW's gaps depend on every row's timestamp: the router runs getNextSessionWindow over
+ * the whole stream (ekgpu/shard.py GlobalSession, event_window_trigger.go:77-180) and hands every shard the
+ * sessions it closed (sess_*); a shard fires each over its own rows with ts < sess_end. Global un-grouped
+ * aggregates are merged across shards by the caller (ekgpu/dist.py). */
 typedef struct {
     const int64_t* row_arrival;   /* per row of the batch: global arrival index, strictly increasing       */
     int64_t arrivals_end;         /* global arrivals after this batch (>= last row_arrival + 1)           */
@@ -318,6 +321,12 @@ typedef struct {
     int32_t memory;               /* EK_MEM_HOST or EK_MEM_DEVICE: where row_arrival lives (the other arrays
                                    * are always host memory) */
     int32_t pad2;
+    /* SESSIONWINDOW (ABI v7): the sessions the WHOLE stream's WatermarkTuples of this batch closed, in order:
+     * window [sess_start[k], sess_end[k]) fired at the tuple of watermark sess_wm[k] (a value of wm_ts) */
+    const int64_t* sess_start;
+    const int64_t* sess_end;
+    const int64_t* sess_wm;
+    int64_t n_sess;
 } ek_global_ctx;
 
 /* ---------------------------------------------------------------- processing-time clock

@@ -793,6 +793,9 @@ typedef struct {
     int shard;
     int origin_known;
     int64_t origin_ts, origin_arrival, cur_wm_arrival;
+    /* shard model, SESSIONWINDOW: the router's global session list (ek_global_ctx sess_*) and the next one */
+    const int64_t *sess_start, *sess_end, *sess_wm;
+    int64_t n_sess, i_sess;
 } winop;
 
 static int64_t ev_ts(const winop* o, int64_t e) { return o->ts[e]; }
@@ -947,6 +950,16 @@ static void win_on_watermark(winop* o, int64_t wm) {
             scan(o, o->delay_ts.a[0], o->D, 0);
             v_erase_front(&o->delay_ts, 1);
         }
+    }
+    if (o->shard && o->wtype == EK_WINDOW_SESSION) {
+        /* shard model: the sessions the WHOLE stream's tuple closed (ekgpu/shard.py GlobalSession), each over
+         * this shard's inputs with ts < end (handleInputs of a non-overlapping window, window_op.go:605-655) */
+        while (o->i_sess < o->n_sess && o->sess_wm[o->i_sess] <= wm) {
+            o->trigger_time = o->sess_start[o->i_sess]; o->has_trigger = 1;
+            scan(o, o->sess_end[o->i_sess], o->L, 1);
+            o->i_sess++;
+        }
+        return;
     }
     int64_t we = o->next_end;
     int ticked = 0;
@@ -1370,13 +1383,15 @@ int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const 
  *   hopping:  the "empty window discards every input" quirk (window_op.go:605-655) for lateTolerance 0, decided
  *             per event: event i reaches no window iff ts_i > W_{i-1} and e_max(ts_i) - L > W_{i-1}
  *   count:    processing-time COUNTWINDOW blocks over the GLOBAL arrival order (window_op.go:390-418)
+ *   session:  the sessions the router closed over the WHOLE stream (g->sess_*), each at its tuple, over the
+ *             shard's inputs with ts < end
  * The union of the shards' rows (and the sum of their membership fingerprints) is compared with eko_run on the
  * whole stream by the tests. */
 int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
                   const ek_global_ctx* g, eko_output* out) {
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION || !g) { set_status(out, EK_ERR_INVALID, "bad plan / context"); return out->status; }
-    if (p->incremental || p->window_version == 2 || p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_STATE ||
+    if (p->incremental || p->window_version == 2 || p->window_type == EK_WINDOW_STATE ||
         p->window_type == EK_WINDOW_NONE || (p->window_type == EK_WINDOW_SLIDING && p->delay != 0) ||
         (p->window_type == EK_WINDOW_HOPPING && p->late_tolerance_ms != 0) ||
         (p->window_type == EK_WINDOW_COUNT && p->is_event_time)) {
@@ -1416,6 +1431,13 @@ int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const
     o.next_end = MAXT_MS; o.prev_end = ZERO_MS;
     o.shard = 1;
     o.origin_known = g->origin_known; o.origin_ts = g->origin_ts; o.origin_arrival = g->origin_arrival;
+    if (p->window_type == EK_WINDOW_SESSION) {
+        if (g->n_sess > 0 && (!g->sess_start || !g->sess_end || !g->sess_wm)) {
+            free(ts); set_status(out, EK_ERR_INVALID, "missing session list"); return out->status;
+        }
+        o.I = (int64_t)p->interval * u;   /* the session timeout */
+        o.sess_start = g->sess_start; o.sess_end = g->sess_end; o.sess_wm = g->sess_wm; o.n_sess = g->n_sess;
+    }
     const int64_t H = p->window_type == EK_WINDOW_HOPPING ? o.I : o.L;
     int64_t last_wm = ZERO_MS;
     vec64 buf; memset(&buf, 0, sizeof buf);   /* own rows (< n) and trigger ghosts (>= n), release order */

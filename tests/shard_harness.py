@@ -4,7 +4,7 @@ shards' union with the single-stream oracle on EVERY window (start/end/status, m
 import numpy as np
 
 from ekgpu import abi as A
-from ekgpu.shard import GlobalWatermark, ShardDictionary, make_ctx, merge_triggers, shard_of
+from ekgpu.shard import GlobalSession, GlobalWatermark, ShardDictionary, make_ctx, merge_triggers, shard_of
 
 T0 = 1541152480000
 SCHEMA = {"deviceId": "key", "ts": "bigint", "temperature": "float", "humidity": "float", "trig": "bigint"}
@@ -25,6 +25,11 @@ CASES = {
                      "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1", 0, False, "sorted"),
     "tumbling_median": ("SELECT deviceId, median(temperature), count(*) FROM demo "
                         "GROUP BY deviceId, TUMBLINGWINDOW(ss, 2)", 0, True, "ooo"),
+    # sessions closed by the timeout (bursts separated by 8 s gaps) and by the length ticks (a continuous stream)
+    "session_gaps": ("SELECT deviceId, avg(temperature), max(humidity), count(*) FROM demo "
+                     "GROUP BY deviceId, SESSIONWINDOW(ss, 5, 2)", 0, True, "gaps"),
+    "session_ooo_tol": ("SELECT deviceId, sum(temperature), min(humidity), count(*) FROM demo "
+                        "GROUP BY deviceId, SESSIONWINDOW(ss, 1, 1)", 300, True, "ooo"),
 }
 
 
@@ -49,11 +54,17 @@ def global_stream(kind, n=40_000, keys=300, seed=7):
     return [key, ts.astype(np.int64), temp, hum, trig]
 
 
-def route(cols, world, batches, late_tol, is_event_time):
-    """Per rank, per batch: (local cols, row_arrival, wm dict). Dictionaries are per rank (dense local ids)."""
+def route(cols, world, batches, late_tol, is_event_time, sql=None):
+    """Per rank, per batch: (local cols, row_arrival, wm dict). Dictionaries are per rank (dense local ids).
+    A SESSIONWINDOW rule (sql) also gets the router's global session list (GlobalSession) in every wm dict."""
     n = len(cols[0])
     cuts = np.linspace(0, n, batches + 1).astype(np.int64)
     gw = GlobalWatermark(late_tol)
+    gs = None
+    if sql is not None and "SESSIONWINDOW" in sql.upper():
+        from ekgpu.rule import compile_rule
+        gs = GlobalSession(compile_rule(sql, SCHEMA, num_keys=1, late_tolerance_ms=late_tol,
+                                        is_event_time=is_event_time).plan)
     owner = shard_of(cols[0], world)
     dicts = [ShardDictionary() for _ in range(world)]
     out = [[] for _ in range(world)]
@@ -61,6 +72,8 @@ def route(cols, world, batches, late_tol, is_event_time):
         lo, hi = cuts[b], cuts[b + 1]
         if is_event_time:
             wm = gw.track(cols[1][lo:hi])
+            if gs is not None:
+                wm = gs.step(cols[1][lo:hi], wm)
         else:
             gw.arrivals += hi - lo
             wm = {"wm_arrival": np.zeros(0, np.int64), "wm_ts": np.zeros(0, np.int64), "arrivals_end": gw.arrivals,
@@ -82,6 +95,9 @@ def whole_ctx(batches_of_rank, trig=None):
           "arrivals_end": batches_of_rank[-1][2]["arrivals_end"]}
     last = batches_of_rank[-1][2]
     wm.update(origin_known=last["origin_known"], origin_ts=last["origin_ts"], origin_arrival=last["origin_arrival"])
+    if "sess_end" in last:
+        for f in ("sess_start", "sess_end", "sess_wm"):
+            wm[f] = np.concatenate([b[2][f] for b in batches_of_rank])
     ta, tt = trig if trig is not None else (None, None)
     return cols, arr, make_ctx(wm, arr, ta, tt)
 

@@ -5,7 +5,8 @@ on its own rows, the lists are all-gathered). Each rank runs the shard model of 
 eko_run_shard, the CPU restatement of ek_push_batch_global); rank 0 checks that the union of the shards equals
 the single-stream oracle on EVERY window — including the windows closed by the global watermark, out-of-order
 streams with late events, lateTolerance > 0, hopping windows across event-time gaps, COUNTWINDOW(1000) over the
-global arrival order and SLIDINGWINDOW ... OVER (WHEN ...)."""
+global arrival order, SLIDINGWINDOW ... OVER (WHEN ...) and SESSIONWINDOW (the router's global session list,
+ekgpu.shard.GlobalSession)."""
 import os
 import socket
 
@@ -37,7 +38,7 @@ def _worker(rank, world, port, case, q):
     try:
         sql, tol, iet, kind = H.CASES[case]
         cols = H.global_stream(kind)
-        per_rank, dicts = H.route(cols, world, batches=5, late_tol=tol, is_event_time=iet)
+        per_rank, dicts = H.route(cols, world, batches=5, late_tol=tol, is_event_time=iet, sql=sql)
         mine = per_rank[rank]
         rule = compile_rule(sql, H.SCHEMA, num_keys=max(1, len(dicts[rank].global_of)), late_tolerance_ms=tol,
                             is_event_time=iet)

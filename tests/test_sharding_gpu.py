@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 def _run_engines(engine_mod, case, world, batches=5, debug=True):
     sql, tol, iet, kind = H.CASES[case]
     cols = H.global_stream(kind)
-    per_rank, dicts = H.route(cols, world, batches=batches, late_tol=tol, is_event_time=iet)
+    per_rank, dicts = H.route(cols, world, batches=batches, late_tol=tol, is_event_time=iet, sql=sql)
     rules = [compile_rule(sql, H.SCHEMA, num_keys=max(1, len(dicts[r].global_of)), late_tolerance_ms=tol,
                           is_event_time=iet, debug_membership=debug) for r in range(world)]
     engs = [engine_mod.Engine(rules[r].plan) for r in range(world)]
@@ -99,8 +99,8 @@ def test_advance_watermark_closes_windows(oracle, engine_mod):
 def test_shard_mode_rejections(engine_mod):
     """Windows whose content depends on every row of the stream are not shardable; local and shard pushes
     do not mix on one handle."""
-    sess = compile_rule("SELECT deviceId, count(*) FROM demo GROUP BY deviceId, SESSIONWINDOW(ss, 10, 2)", H.SCHEMA,
-                        num_keys=4)
+    sess = compile_rule("SELECT deviceId, count(*) FROM demo GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 99)",
+                        H.SCHEMA, num_keys=4)
     eng = engine_mod.Engine(sess.plan)
     wm = {"wm_arrival": np.zeros(0, np.int64), "wm_ts": np.zeros(0, np.int64), "arrivals_end": 0,
           "origin_known": False, "origin_ts": 0, "origin_arrival": 0}
