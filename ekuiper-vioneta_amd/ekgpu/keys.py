@@ -66,6 +66,42 @@ def group_key_string(values: Sequence) -> str:
     return "".join(go_v(v) + "," for v in values)
 
 
+def _factorize(col, valid=None):
+    """(codes, uniques) of a column, hashed in C (pandas.factorize): uniques in first-seen order over the non-nil
+    rows, codes[i] = -1 for nil rows (None, or validity 0). The dictionaries below loop over the distinct values
+    only, not over the rows."""
+    import pandas as pd
+    a = col if isinstance(col, np.ndarray) and col.dtype.kind in "iuf" else np.asarray(col, dtype=object)
+    n = len(a)
+    keep = None
+    if valid is not None:
+        keep = np.asarray(valid, np.uint8) != 0
+    if a.dtype == object:
+        nn = np.not_equal(a, None)
+        keep = nn if keep is None else keep & nn
+    if keep is None or keep.all():
+        codes, uniques = pd.factorize(a, use_na_sentinel=False)
+        codes = np.asarray(codes, np.int64)
+    else:
+        idx = np.nonzero(keep)[0]
+        sub, uniques = pd.factorize(a[idx], use_na_sentinel=False)
+        codes = np.full(n, -1, np.int64)
+        codes[idx] = sub
+    return codes, np.asarray(uniques, dtype=object)
+
+
+def _first_rows(codes: np.ndarray) -> np.ndarray:
+    """First row of every code of a first-seen-order factorisation: the rows where the running max of the codes
+    grows (nil rows carry -1 and never do)."""
+    if len(codes) == 0:
+        return np.zeros(0, np.int64)
+    run = np.maximum.accumulate(codes)
+    grow = np.empty(len(codes), bool)
+    grow[0] = codes[0] >= 0
+    grow[1:] = run[1:] > run[:-1]
+    return np.nonzero(grow)[0]
+
+
 class StringDict:
     """Dense u32 codes of a string column (first-seen order). Rows that are nil (None, or validity 0) take the
     placeholder code 0 and are not entered in the dictionary (the engine never reads a nil row's value)."""
@@ -75,17 +111,17 @@ class StringDict:
         self.values: List[str] = []
 
     def encode(self, col, valid=None) -> np.ndarray:
-        out = np.zeros(len(col), np.uint32)
+        codes, uniq = _factorize(col, valid)
         ids = self.ids
-        for i, s in enumerate(col):
-            if s is None or (valid is not None and not valid[i]):
-                continue
+        m = np.zeros(len(uniq) + 1, np.uint32)       # slot -1 (nil) -> placeholder 0
+        for u in range(len(uniq)):                    # first-seen order
+            s = uniq[u]
             c = ids.get(s)
             if c is None:
                 c = ids[s] = len(self.values)
                 self.values.append(s)
-            out[i] = c
-        return out
+            m[u] = c
+        return m[codes]
 
     def decode(self, codes) -> List[str]:
         return [self.values[int(c)] for c in codes]
@@ -148,14 +184,14 @@ class OrderedStringDict:
         return c
 
     def encode(self, col, valid=None) -> np.ndarray:
-        out = np.zeros(len(col), np.int64)
+        codes, uniq = _factorize(col, valid)
         code = self.code
-        for i, s in enumerate(col):
-            if s is None or (valid is not None and not valid[i]):
-                continue
+        m = np.zeros(len(uniq) + 1, np.int64)        # slot -1 (nil) -> placeholder 0
+        for u in range(len(uniq)):                    # insertion in first-seen order
+            s = uniq[u]
             c = code.get(s)
-            out[i] = c if c is not None else self._add(s)
-        return out
+            m[u] = c if c is not None else self._add(s)
+        return m[codes]
 
     def decode(self, codes) -> List[str]:
         return [self.by_code[int(c)] for c in codes]
@@ -223,12 +259,28 @@ class GroupKeyDict:
             vals.append((a, None if v is None else np.asarray(v, np.uint8)))
         out = np.empty(n, np.uint32)
         if self.by_string:
-            for i in range(n):
-                row = tuple(None if (m is not None and not m[i]) else (a[i].item() if hasattr(a[i], "item") else a[i])
-                            for a, m in vals)
+            # one code per dimension (nil its own code), the rows' code tuples factorised, and the key string built
+            # once per distinct tuple in first-seen order (distinct tuples can still share a string: "%v," collisions)
+            if n == 0:
+                return out
+            comb = np.zeros(n, np.int64)
+            for a, m in vals:
+                codes, uniq = _factorize(a if a.dtype == object else _canon_bits(a), m)
+                card = len(uniq) + 1
+                if int(comb.max()) + 1 > (1 << 62) // card:
+                    comb = _factorize(comb)[0]   # re-densify before the product could overflow
+                comb = comb * card + (codes + 1)
+            tcodes, _ = _factorize(comb)
+            tfirst = _first_rows(tcodes)
+            m_id = np.empty(len(tfirst), np.uint32)
+            for u in range(len(tfirst)):                # first-seen order
+                i = int(tfirst[u])
+                row = tuple(None if (mm is not None and not mm[i]) else (a[i].item() if hasattr(a[i], "item") else a[i])
+                            for a, mm in vals)
                 k = group_key_string(row)
                 j = self.ids.get(k)
-                out[i] = self._new(k, row) if j is None else j
+                m_id[u] = self._new(k, row) if j is None else j
+            out[:] = m_id[tcodes]
             return out
         # numeric dimensions: key on the value tuples (nil -> its own value)
         fields = []
