@@ -657,7 +657,6 @@ struct Engine {
         km_one = env_int("EKGPU_KM_ONE", 1);
         km_packed = env_int("EKGPU_KM_PACKED", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
-        append_fused = env_int("EKGPU_APPEND_FUSED", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
@@ -1581,22 +1580,11 @@ struct Engine {
         for (int c = 0; c < plan.n_columns; ++c)
             if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
         if (int rc = eb_reserve(cnt)) return rc;
-        // the kept columns (and the arrival numbers) in one k_append launch; misaligned columns by hipMemcpyAsync
-        AppendDesc ad{};
         for (int c = 0; c < plan.n_columns; ++c) {
             const size_t es = col_es(c);
-            if (eb_need[c] && cnt > 0) {
-                char* dst = (char*)eb.col[c].p + eb.n * es;
-                const char* src = (const char*)db.col[c] + start * es;
-                if (append_fused && ad.nc < kAppendCols && ((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0) {
-                    ad.src[ad.nc] = (const uint4*)src;
-                    ad.dst[ad.nc] = (uint4*)dst;
-                    ad.bytes[ad.nc] = (int64_t)cnt * (int64_t)es;
-                    ad.nc++;
-                } else {
-                    hipMemcpyAsync(dst, src, (size_t)cnt * es, hipMemcpyDeviceToDevice, stream);
-                }
-            }
+            if (eb_need[c])
+                hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
+                               hipMemcpyDeviceToDevice, stream);
             if (eb_valid_on[c]) {
                 if (db.valid[c]) hipMemcpyAsync((uint8_t*)eb.valid[c].p + eb.n, db.valid[c] + start, (size_t)cnt, hipMemcpyDeviceToDevice, stream);
                 else fill_valid_ones(c, eb.n, cnt);
@@ -1604,19 +1592,9 @@ struct Engine {
         }
         if (g_row_arr) {   // shard mode: the rows' global arrival indices
             if (cnt > 0) hipMemcpyAsync((int64_t*)eb.arr.p + eb.n, g_row_arr + start, (size_t)cnt * 8, hipMemcpyDeviceToDevice, stream);
-        } else if (ad.nc > 0) {
-            ad.arr = (int64_t*)eb.arr.p + eb.n;
-            ad.arr_base = arr_base + start;
-            ad.n = cnt;
-        } else if (cnt > 0) {
+        } else {
             const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
             hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
-        }
-        if (ad.nc > 0) {
-            int64_t mv = 0;
-            for (int c = 0; c < ad.nc; ++c) mv = std::max<int64_t>(mv, ad.bytes[c] >> 4);
-            const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (mv + 1023) / 1024));
-            hipLaunchKernelGGL(k_append, dim3((unsigned)gx, (unsigned)(ad.nc + (ad.arr ? 1 : 0))), dim3(256), 0, stream, ad);
         }
         if (need_rel) hipMemsetAsync((int64_t*)eb.rel.p + eb.n, 0x7f, (size_t)cnt * 8, stream);   // "not released"
         eb.n += cnt;
@@ -1927,7 +1905,6 @@ struct Engine {
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
     int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
-    int append_fused = 1;   // EKGPU_APPEND_FUSED=0: event-buffer appends by one hipMemcpyAsync per column + k_iota64
     DevBuf km_rbase, km_rec;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;

@@ -17,45 +17,6 @@ __global__ void k_iota64(int64_t* __restrict__ out, int64_t base, int64_t n) {
         out[i] = base + i;
 }
 
-// One launch appends a batch's kept columns to the event buffer (and, with arr != nullptr, the rows' arrival
-// numbers arr_base + i): column blockIdx.y, 16-byte chunks, four loads in flight per thread before the stores.
-// Every src / dst is 16-byte aligned (host-checked; a misaligned column goes through hipMemcpyAsync instead).
-constexpr int kAppendCols = 8;
-struct AppendDesc {
-    const uint4* src[kAppendCols];
-    uint4* dst[kAppendCols];
-    int64_t bytes[kAppendCols];
-    int32_t nc;
-    int32_t pad;
-    int64_t* arr;
-    int64_t arr_base;
-    int64_t n;
-};
-__global__ __launch_bounds__(256) void k_append(AppendDesc d) {
-    const int c = blockIdx.y;
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    if (c == d.nc) {
-        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < d.n; i += stride) d.arr[i] = d.arr_base + i;
-        return;
-    }
-    const uint4* __restrict__ src = d.src[c];
-    uint4* __restrict__ dst = d.dst[c];
-    const int64_t nv = d.bytes[c] >> 4;
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < nv; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], e = src[i + 2 * stride], f = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = e;
-        dst[i + 3 * stride] = f;
-    }
-    for (; i < nv; i += stride) dst[i] = src[i];
-    if (blockIdx.x == 0 && threadIdx.x < (d.bytes[c] & 15)) {
-        const int64_t o = (nv << 4) + threadIdx.x;
-        ((unsigned char*)dst)[o] = ((const unsigned char*)src)[o];
-    }
-}
-
 // Inclusive running max of ts in arrival order (the stream max M_j of watermark_op.go:217-225 after
 // event j), seeded per kAccChunk chunk with the exclusive prefix max from k_chunk_max + k_scan_max.
 __global__ __launch_bounds__(kBlock) void k_runmax(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
