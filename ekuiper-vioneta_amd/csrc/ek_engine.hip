@@ -4382,34 +4382,53 @@ int ek_create(const ek_plan* plan, int device, void** out_handle) {
     return 0;
 }
 
+// Every entry point runs on the handle's device whatever the calling thread's current device is (a Go node may call
+// from any OS thread; the bench runs two rules on two host threads), and gives the caller its device back.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(void* h) {
+        if (!h) return;
+        const int dev = ((Engine*)h)->device;
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() { if (prev >= 0) hipSetDevice(prev); }
+};
+
 int ek_push_batch(void* h, const ek_batch* batch) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->push(batch);
 }
 
 int ek_poll_results(void* h, int32_t memory, ek_result* out) {
     if (!h || !out) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->poll(memory, out);
 }
 
 int ek_release_results(void* h, ek_result* res) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     if (res) memset(res, 0, sizeof *res);
     return ((Engine*)h)->release_results();
 }
 
 int ek_reset(void* h) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->reset();
 }
 
 int ek_sync(void* h) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return hipStreamSynchronize(((Engine*)h)->stream) == hipSuccess ? 0 : EK_ERR_DEVICE;
 }
 
 int ek_set_stream(void* h, void* s) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     Engine* e = (Engine*)h;
     hipStreamSynchronize(e->stream);
     if (s) {
@@ -4435,22 +4454,26 @@ const char* ek_last_error(void* h) {
 }
 
 int ek_destroy(void* h) {
+    DeviceGuard dg(h);
     delete (Engine*)h;
     return 0;
 }
 
 int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->push_global(batch, g);
 }
 
 int ek_advance_time(void* h, int64_t now_ms) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return static_cast<Engine*>(h)->advance_time(now_ms);
 }
 
 int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     Engine* e = (Engine*)h;
     const int64_t a = std::max<int64_t>(0, arrivals_end - 1);
     ek_global_ctx g{};
@@ -4465,16 +4488,19 @@ int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end) {
 int ek_shard_triggers(void* h, const ek_batch* batch, const ek_global_ctx* g, int64_t* out_arrival, int64_t* out_ts,
                       int64_t cap, int64_t* n_out) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->shard_triggers(batch, g, out_arrival, out_ts, cap, n_out);
 }
 
 int ek_export_state(void* h, void* buf, int64_t cap, int64_t* size) {
     if (!h || !size) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->export_state(buf, cap, size);
 }
 
 int ek_import_state(void* h, const void* buf, int64_t size) {
     if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
     return ((Engine*)h)->import_state(buf, size);
 }
 
