@@ -30,6 +30,7 @@
 #include "ek_range.h"
 #include "ek_global.h"
 #include "ek_keymajor.h"
+#include "ek_launch.h"
 
 using namespace ek;
 
@@ -50,25 +51,6 @@ struct WinInfo {
     int32_t slot;        // index into win_cnt / win_err device arrays
     bool direct;         // rows emitted by k_agg (whole tumbling pane inside one group)
 };
-
-// NVC-specialised launches (value columns referenced by aggregates: 1..kMaxVC)
-template <int N>
-void launch_agg(dim3 g, size_t lds, hipStream_t s, DPlan* p, GroupDesc gd, LdsLayout lay, const uint32_t* ctab, int ls,
-                int64_t rs, Staging st, DState ds, Results res, const int32_t* pane_err, const int64_t* pbase,
-                uint64_t* scratch, int64_t scr_stride) {
-    if (pbase)
-        hipLaunchKernelGGL((k_agg<N, true>), g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err,
-                           pbase, scratch, scr_stride);
-    else
-        hipLaunchKernelGGL((k_agg<N, false>), g, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err,
-                           pbase, scratch, scr_stride);
-}
-template <int N>
-void launch_fin(dim3 g, hipStream_t s, DPlan* p, const WinDesc* w, DState ds, int32_t ring, const int32_t* pe, Results res,
-                bool merge) {
-    if (merge) hipLaunchKernelGGL(k_finalize_merge<N>, dim3(g.y), dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
-    else hipLaunchKernelGGL(k_finalize<N>, g, dim3(kBlock), 0, s, p, w, ds, ring, pe, res);
-}
 
 int64_t floordiv_h(int64_t a, int64_t b) {
     int64_t q = a / b;
@@ -1007,12 +989,7 @@ struct Engine {
             Results rv = results_view();
             const WinDesc* wd = (const WinDesc*)wdesc.p;
             const int ph = phase_begin(EK_PHASE_FINALIZE);
-            switch (nvc) {
-            case 1: launch_fin<1>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
-            case 2: launch_fin<2>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
-            case 3: launch_fin<3>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
-            default: launch_fin<4>(grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv, dp.pseudo_keys != 0); break;
-            }
+            ek::launch_fin(nvc, dp.pseudo_keys != 0, grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv);
             phase_end(ph);
         }
         if (plan.debug_membership) {
@@ -1258,14 +1235,7 @@ struct Engine {
             uint32_t* ct = (uint32_t*)chist.p;
             dim3 gp(gd.nch);
             const int ph = phase_begin(EK_PHASE_PARTITION);
-#define EK_PART(M, W, N) hipLaunchKernelGGL((k_part<M, W, N>), gp, dim3(kPartBlock), lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, perr)
-#define EK_PART_N(M, W) switch (nvc) { case 1: EK_PART(M, W, 1); break; case 2: EK_PART(M, W, 2); break; \
-                                       case 3: EK_PART(M, W, 3); break; default: EK_PART(M, W, 4); break; }
-#define EK_PART_W(M) if (wh) { EK_PART_N(M, true) } else { EK_PART_N(M, false) }
-            if (mode == 0) { EK_PART_W(0) } else if (mode == 1) { EK_PART_W(1) } else { EK_PART_W(2) }
-#undef EK_PART_W
-#undef EK_PART_N
-#undef EK_PART
+            ek::launch_part(mode, wh, nvc, gp, lds_p, stream, d_plan, db, grid, gd, d_acc, st, ct, ls, rs, perr);
             phase_end(ph);
         }
         {
@@ -1286,12 +1256,8 @@ struct Engine {
                 pbase = (const int64_t*)sort_pbase.p;
                 scr = (uint64_t*)sort_scr.p;
             }
-            switch (nvc) {
-            case 1: launch_agg<1>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
-            case 2: launch_agg<2>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
-            case 3: launch_agg<3>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
-            default: launch_agg<4>(ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr, scr_stride); break;
-            }
+            ek::launch_agg(nvc, pbase != nullptr, ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
+                       scr_stride);
             phase_end(ph);
         }
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
@@ -1346,11 +1312,7 @@ struct Engine {
         const int nvc = std::max(1, dp.n_vc);
         const bool wh = dp.n_where > 0;
         const int ph = phase_begin(EK_PHASE_AGGREGATE);
-#define EK_UNG(N, W) hipLaunchKernelGGL((k_ung_tile<N, W>), dim3((unsigned)nt), dim3(kUngBlock), 0, stream, d_plan, db, gd, d_acc, dstate, tile, perr)
-#define EK_UNG_N(W) switch (nvc) { case 1: EK_UNG(1, W); break; case 2: EK_UNG(2, W); break; case 3: EK_UNG(3, W); break; default: EK_UNG(4, W); break; }
-        if (wh) { EK_UNG_N(true) } else { EK_UNG_N(false) }
-#undef EK_UNG_N
-#undef EK_UNG
+        ek::launch_ung(nvc, wh, dim3((unsigned)nt), stream, d_plan, db, gd, d_acc, dstate, tile, perr);
         phase_end(ph);
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "kernel launch failed");
         return 0;
@@ -1723,6 +1685,13 @@ struct Engine {
     bool hop_discard_pending = false;   // fire_windows applies the hopping empty-window discard to this set
 
     // Resolve the ranges of `pw` on the device, register the windows, launch their aggregation.
+    // k_small_win over nb windows (one wave each; see ek_range.h), specialised by value columns, WHERE and rows per lane
+    void small_win_launch(int nb, const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot,
+                          const int64_t* ob, int max_n, SwArith ar) {
+        ek::launch_small_win(std::max(1, dp.n_vc), dp.n_where > 0, max_n <= 16 * kSwLanes ? 16 : kSwRows, nb, sw_lds_bytes(max_n),
+                         stream, d_plan, src, ab, wl, slot, ob, results_view(), max_n, ar);
+    }
+
     int fire_windows(std::vector<PendWin>& pw) {
         const int nq = (int)pw.size();
         if (nq == 0) { hop_discard_pending = false; return 0; }
@@ -1785,7 +1754,6 @@ struct Engine {
                 const int nw = (int)wl.size();
                 int max_n = 1;
                 for (int w : wl) max_n = std::max<int>(max_n, (int)(h_ab[2 * w + 1] - h_ab[2 * w]));
-                const size_t swl = sw_lds_bytes(max_n);
                 if (int rc = ensure(sw_d, (size_t)nw * 4 + (size_t)nq * 12 + 16)) return rc;
                 int32_t* d_wl = (int32_t*)sw_d.p;
                 int32_t* d_slot = d_wl + nw;
@@ -1793,15 +1761,8 @@ struct Engine {
                 hipMemcpyAsync(d_wl, wl.data(), (size_t)nw * 4, hipMemcpyHostToDevice, stream);
                 hipMemcpyAsync(d_slot, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
                 hipMemcpyAsync(d_ob, obase.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
-                const DBatch bv = buffer_view();
-                Results rv = results_view();
                 const int ph = phase_begin(EK_PHASE_AGGREGATE);
-                switch (std::max(1, dp.n_vc)) {
-                case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-                case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-                case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-                default: hipLaunchKernelGGL(k_small_win<4>, dim3(nw), dim3(kBlock), swl, stream, d_plan, bv, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-                }
+                small_win_launch(nw, buffer_view(), (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{});
                 phase_end(ph);
                 // the host vectors above are reused by the next fire: keep them alive until the copies ran
                 hipStreamSynchronize(stream);
@@ -1999,40 +1960,12 @@ struct Engine {
         const size_t gl = grp_walk_lds(s2, rdep);
         const dim3 gg((unsigned)nsub), gb(kGrpWalkBlock);
         const bool isf = dp.vc_is_float[0] != 0;
-        if (rdep == 8) grp_walk_launch<8>(sort, isf, gg, gb, gl, g, rv);
-        else if (rdep == 12) grp_walk_launch<12>(sort, isf, gg, gb, gl, g, rv);
-        else grp_walk_launch<16>(sort, isf, gg, gb, gl, g, rv);
+        ek::launch_grp_walk(sort, isf, rdep, gg, gb, gl, stream, d_plan, g, rv);
         phase_end(ph2);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping walk failed");
         *ok = true;
         return 0;
     }
-    template <int R>
-    void grp_walk_launch(bool sort, bool isf, dim3 gg, dim3 gb, size_t gl, const GrpDesc& g, const Results& rv) {
-        if (isf) {
-            if (sort) hipLaunchKernelGGL((k_grp_walk<true, true, R>), gg, gb, gl, stream, d_plan, g, rv);
-            else hipLaunchKernelGGL((k_grp_walk<false, true, R>), gg, gb, gl, stream, d_plan, g, rv);
-        } else {
-            if (sort) hipLaunchKernelGGL((k_grp_walk<true, false, R>), gg, gb, gl, stream, d_plan, g, rv);
-            else hipLaunchKernelGGL((k_grp_walk<false, false, R>), gg, gb, gl, stream, d_plan, g, rv);
-        }
-    }
-    template <int N>
-    void km_walk1(bool sort, size_t lds, int nblk, const KmDesc& d, const Results& rv) {
-        if (sort) hipLaunchKernelGGL((k_km_walk<N, true, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-        else hipLaunchKernelGGL((k_km_walk<N, false, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-    }
-    template <int N>
-    void km_walk(bool sort, bool write, int nblk, size_t lds, const KmDesc& d, const Results& rv) {
-        if (sort) {
-            if (write) hipLaunchKernelGGL((k_km_walk<N, true, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-            else hipLaunchKernelGGL((k_km_walk<N, true, false>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-        } else {
-            if (write) hipLaunchKernelGGL((k_km_walk<N, false, true>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-            else hipLaunchKernelGGL((k_km_walk<N, false, false>), dim3(nblk), dim3(kKmBlock), lds, stream, d_plan, d, rv);
-        }
-    }
-
     int km_run(const std::vector<int>& wl, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots,
                bool* handled) {
         *handled = false;
@@ -2154,21 +2087,9 @@ struct Engine {
         case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         }
-        auto walk = [&](bool write) {
-            switch (nvc) {
-            case 1: km_walk<1>(sort, write, nblk, lds, d, rv); break;
-            case 2: km_walk<2>(sort, write, nblk, lds, d, rv); break;
-            case 3: km_walk<3>(sort, write, nblk, lds, d, rv); break;
-            default: km_walk<4>(sort, write, nblk, lds, d, rv); break;
-            }
-        };
+        auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
         if (one) {
-            switch (nvc) {
-            case 1: km_walk1<1>(sort, lds, nblk, d, rv); break;
-            case 2: km_walk1<2>(sort, lds, nblk, d, rv); break;
-            case 3: km_walk1<3>(sort, lds, nblk, d, rv); break;
-            default: km_walk1<4>(sort, lds, nblk, d, rv); break;
-            }
+            ek::launch_km_walk(nvc, sort, true, true, nblk, lds, stream, d_plan, d, rv);
             phase_end(ph2);
             if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "key-major launch failed");
             stats.windows_keymajor += nw;
@@ -3223,15 +3144,8 @@ struct Engine {
                 wins.push_back(wi);
             }
             stats.windows_out += nq;
-            const size_t swl = sw_lds_bytes((int)len);
-            Results rv = results_view();
             const int ph = phase_begin(EK_PHASE_AGGREGATE);
-            switch (std::max(1, dp.n_vc)) {
-            case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
-            case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
-            case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
-            default: hipLaunchKernelGGL(k_small_win<4>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)nullptr, (const int32_t*)nullptr, (const int32_t*)nullptr, (const int64_t*)nullptr, rv, (int)len, ar); break;
-            }
+            small_win_launch(nq, src, nullptr, nullptr, nullptr, nullptr, (int)len, ar);
             phase_end(ph);
             if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");
             return 0;
@@ -3270,15 +3184,8 @@ struct Engine {
         if (plan.debug_membership)
             hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)nullptr, (const int64_t*)ab_d.p,
                                (const int32_t*)d_slot, (int64_t*)r_wmc.p, (unsigned long long*)r_wmh.p, arr_base);
-        const size_t swl = sw_lds_bytes(max_n);
-        Results rv = results_view();
         const int ph = phase_begin(EK_PHASE_AGGREGATE);
-        switch (std::max(1, dp.n_vc)) {
-        case 1: hipLaunchKernelGGL(k_small_win<1>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-        case 2: hipLaunchKernelGGL(k_small_win<2>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-        case 3: hipLaunchKernelGGL(k_small_win<3>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-        default: hipLaunchKernelGGL(k_small_win<4>, dim3(nq), dim3(kBlock), swl, stream, d_plan, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, rv, max_n, SwArith{}); break;
-        }
+        small_win_launch(nq, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{});
         phase_end(ph);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");   // host lists reused
         return 0;

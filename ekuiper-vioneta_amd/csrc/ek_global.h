@@ -30,6 +30,7 @@ __device__ __forceinline__ int64_t wm_before(const WmList& w, int64_t a) {
 // Acceptance of the rows of a shard batch: ts >= the watermark before the row's arrival; for hopping windows
 // with lateTolerance 0 (hop != 0) also the empty-window discard of k_hop_drop with that watermark as W_{i-1}.
 // Counts accepted rows, their min ts and the discarded rows into st (zeroed by k_stats_reduce).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_accept_global(const int64_t* __restrict__ ts, const int64_t* __restrict__ arr,
                                                           int64_t n, WmList w, int hop, int64_t E1, int64_t H, int64_t L,
                                                           uint8_t* __restrict__ acc, BatchStats* st) {
@@ -53,9 +54,11 @@ __global__ __launch_bounds__(kBlock) void k_accept_global(const int64_t* __restr
         if (drops) atomicAdd((unsigned long long*)&st->n_dropped, (unsigned long long)drops);
     }
 }
+#endif
 
 // Release step of buffer rows [i0, i1) (all released by this batch's tuples): the arrival index of the first
 // tuple at or after the row's arrival whose watermark reaches its ts (INT64_MAX if none).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_release_step_global(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t i0,
                                       int64_t i1, WmList w, int64_t* __restrict__ brel) {
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
@@ -69,11 +72,14 @@ __global__ void k_release_step_global(const int64_t* __restrict__ bts, const int
         brel[i] = k < w.n ? w.arr[k] : INT64_MAX;
     }
 }
+#endif
 
 // flags[i] &= acc[i] (trigger rows that the global watermark accepts)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_and_flags(uint8_t* __restrict__ flags, const uint8_t* __restrict__ acc, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         flags[i] = flags[i] && acc[i];
 }
+#endif
 
 }  // namespace ek

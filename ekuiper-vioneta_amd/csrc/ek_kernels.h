@@ -16,11 +16,8 @@
 #pragma once
 #include "ek_device.h"
 
-// linkage of the non-template kernels defined in this header: a translation unit that includes it only for the
-// device helpers defines EK_NT_KERNEL as static, so only the engine's unit exports them
-#ifndef EK_NT_KERNEL
-#define EK_NT_KERNEL
-#endif
+// The non-template kernels of the ek_*.h headers are compiled by the engine's unit only: the units that instantiate the
+// big template kernel families (ek_tpl_*.hip, compiled in parallel) define EK_NO_PLAIN_KERNELS before including them.
 
 namespace ek {
 
@@ -115,7 +112,8 @@ __global__ __launch_bounds__(kBlock) void k_stats(const int64_t* __restrict__ ts
     }
 }
 
-EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(1024) void k_stats_reduce(const BatchStats* __restrict__ part, int nb, BatchStats* st) {
     int64_t mn = INT64_MAX, mx = INT64_MIN, mg = INT64_MIN;
     int uns = 0;
     for (int k = threadIdx.x; k < nb; k += 1024) {
@@ -140,12 +138,14 @@ EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_stats_reduce(const BatchS
         st->min_accepted = INT64_MAX;
     }
 }
+#endif
 
 // ---------------------------------------------------------------- late-event drop (out-of-order batches)
 constexpr int kAccPerThread = 16;
 constexpr int kAccChunk = kBlock * kAccPerThread;  // 4096 events per block
 
-EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict__ ts, int64_t n, int64_t* cmax) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t* __restrict__ ts, int64_t n, int64_t* cmax) {
     int64_t base = (int64_t)blockIdx.x * kAccChunk;
     int64_t mx = INT64_MIN;
     for (int k = threadIdx.x; k < kAccChunk; k += kBlock) {
@@ -158,10 +158,12 @@ EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_chunk_max(const int64_t
     __syncthreads();
     if (threadIdx.x == 0) cmax[blockIdx.x] = max(max(s[0], s[1]), max(s[2], s[3]));
 }
+#endif
 
 // exclusive prefix max over chunk maxima, seeded with the carried stream max (single workgroup; the threads' partial
 // maxima are scanned with wave shuffles, not by one thread)
-EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64_t seed) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, int nch, int64_t seed) {
     __shared__ int64_t s_w[16];
     const int per = (nch + 1023) / 1024;
     const int b = threadIdx.x * per, e = min(nch, b + per);
@@ -182,10 +184,12 @@ EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_scan_max(int64_t* cmax, i
     for (int w = 0; w < wv; ++w) run = max(run, s_w[w]);
     for (int i = b; i < e; ++i) { const int64_t v = cmax[i]; cmax[i] = run; run = max(run, v); }
 }
+#endif
 
 // per-event acceptance of a 4096-event chunk; the chunk's (accepted count, min accepted ts) go to part[2 * chunk]
 // (reduced by k_accept_reduce: one atomic per wave on two counters serialised ~1.5 M atomics per 1e8 events)
-EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBlock) void k_accept(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
                                                    int64_t late_tol, uint8_t* acc, int64_t* __restrict__ part) {
     __shared__ int64_t s_w[kBlock / 64], s_c[kBlock / 64], s_m[kBlock / 64];
     const int64_t base = (int64_t)blockIdx.x * kAccChunk + (int64_t)threadIdx.x * kAccPerThread;
@@ -247,8 +251,10 @@ EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_accept(const int64_t* _
         part[2 * blockIdx.x + 1] = m;
     }
 }
+#endif
 
-EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restrict__ part, int nch, BatchStats* st) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(1024) void k_accept_reduce(const int64_t* __restrict__ part, int nch, BatchStats* st) {
     __shared__ int64_t s_c[16], s_m[16];
     int64_t c = 0, m = INT64_MAX;
     for (int i = threadIdx.x; i < nch; i += 1024) { c += part[2 * i]; m = min(m, part[2 * i + 1]); }
@@ -263,6 +269,7 @@ EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_accept_reduce(const int64
         st->min_accepted = tm;
     }
 }
+#endif
 
 // Hopping windows with lateTolerance 0: the empty-window discard of window_op.go:605-655 (handleInputs). When the
 // watermark step of event i triggers a hopping window [e - L, e) that holds no released event, handleInputs finds
@@ -272,7 +279,8 @@ EK_NT_KERNEL __global__ __launch_bounds__(1024) void k_accept_reduce(const int64
 // the grid E1 + k H; the largest one <= ts_i is e_max, and some triggered window is empty iff
 // e_max - L > W_{i-1} (the watermark before i, the exclusive running max of ts seeded with the carried stream max).
 // acc_out[i] = accepted(i) && !dropped(i); accepted = acc_in[i] (out-of-order batches) or i >= start (sorted).
-EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
                                                      int64_t start, const uint8_t* acc_in, int64_t E1, int64_t H,
                                                      int64_t L, uint8_t* acc_out, BatchStats* st) {
     __shared__ int64_t tmax[kBlock];
@@ -312,12 +320,14 @@ EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_hop_drop(const int64_t*
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if ((threadIdx.x & 63) == 0 && cnt) atomicAdd((unsigned long long*)&st->n_dropped, (unsigned long long)cnt);
 }
+#endif
 
 // first index in [lo, hi) with ts >= start of pane q_lo + k (sorted batches; k = 0 -> lo for pane 0 of tumbling).
 // One wave per pane, 64-ary search: each round the 64 lanes probe 64 evenly spaced rows of the bracket and a ballot
 // narrows it 65-fold, so a 1e8-row batch costs 5 dependent load rounds instead of 27.
 constexpr int kBoundsBlock = 256;
-EK_NT_KERNEL __global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __restrict__ ts, int64_t lo, int64_t hi,
                                                               PaneGrid g, int64_t q_lo, int nb, int64_t* out) {
     const int lane = threadIdx.x & 63;
     const int k = blockIdx.x * (kBoundsBlock / 64) + (threadIdx.x >> 6);
@@ -341,9 +351,11 @@ EK_NT_KERNEL __global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const
     const unsigned long long below = __ballot(m < b && ts[m] < x);
     if (lane == 0) out[k] = a + __popcll(below);
 }
+#endif
 
 // per-window result counters of the windows handed out by a poll: one launch instead of four fills
-EK_NT_KERNEL __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         wcnt[i] = 0;
         werr[i] = 0;
@@ -351,9 +363,11 @@ EK_NT_KERNEL __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr
         wmh[i] = 0;
     }
 }
+#endif
 
 // first index in [lo, hi) with ts >= bound[k] (sorted batches)
-EK_NT_KERNEL __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
                               int64_t* out) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nb) return;
@@ -361,6 +375,7 @@ EK_NT_KERNEL __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64
     while (a < b) { int64_t m = (a + b) >> 1; if (ts[m] < x) a = m + 1; else b = m; }
     out[k] = a;
 }
+#endif
 
 // ---------------------------------------------------------------- partition pass
 struct GroupDesc {
@@ -715,7 +730,8 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
 
 // per group: zero the per-pane scalars (WHERE error flag, membership fingerprint) of freshly
 // claimed ring slots
-EK_NT_KERNEL __global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r < gd.n_panes && gd.fresh[r]) {
         int64_t s = (gd.q_lo + r) % gd.ring;
@@ -724,6 +740,7 @@ EK_NT_KERNEL __global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64
         pane_mhash[s] = 0;
     }
 }
+#endif
 
 // ---------------------------------------------------------------- per-partition aggregation
 // LDS layout per partition (kk = 1 << kbits keys): 8-byte fields first, then u32 counts.
@@ -918,7 +935,8 @@ __device__ __forceinline__ void part_run(const GroupDesc& gd, const uint32_t* ct
 }
 
 // Rows per partition (sort aggregates: the key-grouped scratch region of each partition), one thread each.
-EK_NT_KERNEL __global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restrict__ ctab, int ls, int64_t* __restrict__ out) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restrict__ ctab, int ls, int64_t* __restrict__ out) {
     const int pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid >= gd.np) return;
     const int rel = pid / gd.nb, bucket = pid % gd.nb;
@@ -932,6 +950,7 @@ EK_NT_KERNEL __global__ void k_part_sizes(GroupDesc gd, const uint32_t* __restri
     }
     out[pid] = t;
 }
+#endif
 
 // ---------------------------------------------------------------- order statistics (median, percentile_*)
 // Element of rank r (0-based, ascending) of a short segment of ordered keys: O(n^2) counting, one thread.
@@ -1612,12 +1631,14 @@ __device__ __forceinline__ void block_merge_part(const DPlan& p, Part<NVC>& s) {
 // reads nothing). The host sizes the tiles so a launch has at most kPseudoKeys of them (distinct slots per pane)
 // and zeroes the slot counts of fresh panes first; k_finalize_merge folds a window's slots as before.
 constexpr int kUngBlock = 256;
-EK_NT_KERNEL __global__ void k_ung_zero(GroupDesc gd, DState ds) {
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_ung_zero(GroupDesc gd, DState ds) {
     const int r = blockIdx.y;
     if (!gd.fresh[r]) return;
     int64_t* c = ds.cnt + ((gd.q_lo + r) % gd.ring) * ds.K;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < (int64_t)kPseudoKeys; k += (int64_t)gridDim.x * blockDim.x) c[k] = 0;
 }
+#endif
 
 template <int NVC, bool WHERE>
 __global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, DBatch b, GroupDesc gd,
@@ -1727,7 +1748,8 @@ __global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, 
 // ---------------------------------------------------------------- debug: window membership fingerprint
 // Per pane: number of accepted events (before WHERE) and Σ ek_mix64(arrival index); a window's
 // fingerprint is the sum over its panes (order-independent, exact in u64 arithmetic).
-EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_members(DPlan* __restrict__ pp, DBatch b, PaneGrid g, const uint8_t* acc,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBlock) void k_members(DPlan* __restrict__ pp, DBatch b, PaneGrid g, const uint8_t* acc,
                                                     int has_acc, int64_t lo, int64_t hi, int64_t arrival_base,
                                                     const int64_t* __restrict__ arrival, int64_t qa, int64_t qb,
                                                     int32_t ring, int64_t* pane_mcnt, unsigned long long* pane_mhash) {
@@ -1741,8 +1763,10 @@ EK_NT_KERNEL __global__ __launch_bounds__(kBlock) void k_members(DPlan* __restri
         atomicAdd(&pane_mhash[q % ring], (unsigned long long)d_mix64((uint64_t)a));
     }
 }
+#endif
 
-EK_NT_KERNEL __global__ void k_win_members(const WinDesc* __restrict__ wins, int32_t ring, const int64_t* __restrict__ pane_mcnt,
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_win_members(const WinDesc* __restrict__ wins, int32_t ring, const int64_t* __restrict__ pane_mcnt,
                               const unsigned long long* __restrict__ pane_mhash, int64_t* wmc, unsigned long long* wmh) {
     if (threadIdx.x != 0) return;
     const WinDesc w = wins[blockIdx.x];
@@ -1752,5 +1776,6 @@ EK_NT_KERNEL __global__ void k_win_members(const WinDesc* __restrict__ wins, int
     wmc[w.idx] = c;
     wmh[w.idx] = h;
 }
+#endif
 
 }  // namespace ek

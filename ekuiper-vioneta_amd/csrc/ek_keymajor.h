@@ -53,6 +53,7 @@ constexpr int kKmRecAggs = 3;      // record: key u32 | 4 tag bytes | 3 x 8-byte
 // (key, relative position) of every row of the span; rows that fail WHERE (or carry an out-of-range key) get the
 // sentinel key nkeys and sort last. WHERE errors are counted: the caller falls back to the window-major path,
 // which attributes them per window (filter_operator.go:63-77).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_km_keys(DPlan* __restrict__ pp, DBatch b, int64_t lo, int64_t n,
                                                     uint32_t* __restrict__ kout, uint32_t* __restrict__ pout,
                                                     unsigned int* __restrict__ nerr) {
@@ -71,8 +72,10 @@ __global__ __launch_bounds__(kBlock) void k_km_keys(DPlan* __restrict__ pp, DBat
     }
     if (e) atomicAdd(nerr, e);
 }
+#endif
 
 // kstart[g] = first sorted row with key >= g, for g in [0, K] (kstart[K] = rows that passed WHERE).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_km_starts(const uint32_t* __restrict__ sk, int64_t n, uint32_t K, uint32_t* __restrict__ kstart) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
         // row i starts every key in (sk[i - 1], sk[i]] (keys <= K; the span's end closes (sk[n - 1], K])
@@ -81,9 +84,11 @@ __global__ void k_km_starts(const uint32_t* __restrict__ sk, int64_t n, uint32_t
         for (uint32_t g = g0; g <= g1; ++g) kstart[g] = (uint32_t)i;
     }
 }
+#endif
 
 // longest key run (rows of one key over the whole span) -> atomicMax(*out)
 // (one atomic per workgroup on a grid of at most 256: per-wave atomics on the one word serialised, 0.18 ms on C4a)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_km_maxrun(const uint32_t* __restrict__ kstart, uint32_t K, unsigned int* out) {
     __shared__ unsigned int s_m[kBlock / 64];
     unsigned int m = 0;
@@ -97,6 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_km_maxrun(const uint32_t* __restrict
         if (m) atomicMax(out, m);
     }
 }
+#endif
 
 struct KmCols {
     int64_t* val[kMaxVC];
@@ -403,6 +409,7 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
 
 // rbase[k] = exclusive prefix over the launch's windows of their kept rows (bcnt[k][nblk] after k_km_scan);
 // rbase[nw] = the total (one workgroup)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(1024) void k_km_rbase(KmDesc d, int64_t* __restrict__ rbase) {
     __shared__ int64_t s_w[16];
     __shared__ int64_t s_carry;
@@ -426,8 +433,10 @@ __global__ __launch_bounds__(1024) void k_km_rbase(KmDesc d, int64_t* __restrict
     }
     if (threadIdx.x == 0) rbase[d.nw] = s_carry;
 }
+#endif
 
 // records -> result columns: window blockIdx.y's rows i = 0 .. kept - 1 land at obase + i (coalesced stores)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_km_unpack(KmDesc d, int n_aggs, Results res) {
     const int k = blockIdx.y;
     const int64_t cnt = d.rbase[k + 1] - d.rbase[k];
@@ -450,6 +459,7 @@ __global__ __launch_bounds__(kBlock) void k_km_unpack(KmDesc d, int n_aggs, Resu
         }
     }
 }
+#endif
 
 // ---------------------------------------------------------------- one window over a huge key space (C5 shape)
 // A window whose every row is a member and whose single value column is read without validity needs the rows
@@ -475,6 +485,7 @@ struct GrpTile {
 // (stride 256): the first pass's tiles all share one set of 256 digits, and 64 replicas keep every counter's global
 // atomics (here and in k_grp_scatter's reservations) from serialising on one address; the host lays the replicas'
 // regions out consecutively inside each digit's region.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restrict__ keys, const GrpTile* __restrict__ tiles,
                                                         int shift, uint32_t K, int rep, unsigned int* __restrict__ tot) {
     __shared__ unsigned int h[256];
@@ -494,11 +505,13 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restri
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&tot[(blockIdx.x % rep) * 256 + t.pre + threadIdx.x], h[threadIdx.x]);
 }
+#endif
 
 // rows of a tile -> their (replica, pre + digit) region: base[] exclusive region starts, cur[] reservation cursors.
 // 512 threads (8 rows each): the 52 KB of LDS staging allow two workgroups per CU, so 16 waves keep loads in flight
 // (256 threads left 8 waves per CU and ran the pass at 2.7 TB/s). The digit is re-derived from the staged key.
 constexpr int kGrpScatBlock = 512;
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
                                                                const GrpTile* __restrict__ tiles, int shift, uint32_t K, int rep,
                                                                const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
@@ -552,6 +565,7 @@ __global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* _
         ovals[dst] = s_val[p];
     }
 }
+#endif
 
 struct GrpDesc {
     const int64_t* base2;             // [nsub + 1] sub-bucket row ranges in the level-2 output
@@ -720,6 +734,7 @@ inline size_t grp_walk_lds(int s2, int R) { return (size_t)R * kGrpWalkBlock * 8
 
 
 // one workgroup per window: exclusive scan of its per-block counts in place; the total is the window's row count
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
     const int k = blockIdx.x;
     uint32_t* c = d.bcnt + (int64_t)k * (d.nblk + 1);
@@ -748,5 +763,6 @@ __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
         if (s_carry) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
     }
 }
+#endif
 
 }  // namespace ek

@@ -12,13 +12,16 @@
 
 namespace ek {
 
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_iota64(int64_t* __restrict__ out, int64_t base, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = base + i;
 }
+#endif
 
 // Inclusive running max of ts in arrival order (the stream max M_j of watermark_op.go:217-225 after
 // event j), seeded per kAccChunk chunk with the exclusive prefix max from k_chunk_max + k_scan_max.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_runmax(const int64_t* __restrict__ ts, int64_t n, const int64_t* excl,
                                                    int64_t* __restrict__ out) {
     __shared__ int64_t tmax[kBlock];
@@ -46,6 +49,7 @@ __global__ __launch_bounds__(kBlock) void k_runmax(const int64_t* __restrict__ t
         if (i < n) out[i] = run;
     }
 }
+#endif
 
 // first j in [lo, hi) with a[j] >= x (hi if none); a non-decreasing
 __device__ __forceinline__ int64_t lb_i64(const int64_t* a, int64_t lo, int64_t hi, int64_t x) {
@@ -78,6 +82,7 @@ __device__ __forceinline__ int64_t gallop_ub(const int64_t* a, int64_t lo, int64
 // event (watermark_op.go:157-214: released at the first advance W_j > W_{j-1} at or after its arrival with
 // W_j >= ts). runmax[0..nb) = batch running max (arrival arr_base + j), prevmax = stream max before the
 // batch (INT64_MIN if none), W_j = runmax[j] - late_tol. Events not released in this batch get INT64_MAX.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t i0,
                                int64_t i1, const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base,
                                int64_t prevmax, int64_t late_tol, int64_t* __restrict__ brel) {
@@ -99,9 +104,11 @@ __global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* _
         brel[i] = r;
     }
 }
+#endif
 
 // Released prefix of the buffer after a batch (single thread): events with ts < W, plus those with
 // ts == W that arrived no later than the step sW at which the watermark reached W.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n, int64_t W,
                           int64_t sW, int64_t* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -109,16 +116,20 @@ __global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __rest
     const int64_t q = ub_i64(bts, p, n, W);
     out[0] = ub_i64(barr, p, q, sW);   // arrivals are increasing inside one ts run
 }
+#endif
 
 // first j in [0, n) with runmax[j] >= x (n if none) — the step at which the stream max reached x
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_first_ge(const int64_t* __restrict__ a, int64_t n, int64_t x, int64_t* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     out[0] = lb_i64(a, 0, n, x);
 }
+#endif
 
 // Released prefix of the buffer at the WatermarkTuple that fires each window end (hopping windows): the first step j
 // of the batch whose watermark runmax[j] - late_tol reaches the end, then the k_rel_end bound at (W_j, arrival j).
 // handleInputs (window_op.go:605-655) drops every input present at that tuple when the window finds no member.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base, int64_t late_tol,
                               const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n,
                               const int64_t* __restrict__ ends, int nq, int64_t* __restrict__ out) {
@@ -131,10 +142,12 @@ __global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, in
     const int64_t q = ub_i64(bts, p, n, W);
     out[w] = ub_i64(barr, p, q, arr_base + j);
 }
+#endif
 
 // Derived columns (expression arguments of aggregates, GroupedTuples.AggregateEval row.go:712-718): per row the
 // valuer's arithmetic over the batch's own columns (eval_prog); nil -> validity 0. The programs cannot error (host
 // lowering: / and % only by non-zero constants).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_derive(DPlan* __restrict__ pp, DBatch b, int64_t n, int64_t* __restrict__ out0, int64_t* __restrict__ out1,
                          int64_t* __restrict__ out2, int64_t* __restrict__ out3, uint8_t* __restrict__ v0, uint8_t* __restrict__ v1,
                          uint8_t* __restrict__ v2, uint8_t* __restrict__ v3) {
@@ -153,9 +166,11 @@ __global__ void k_derive(DPlan* __restrict__ pp, DBatch b, int64_t n, int64_t* _
         }
     }
 }
+#endif
 
 // SLIDINGWINDOW trigger flags over buffer rows [i0, i1): 1 when OVER (WHEN cond) holds
 // (window_op.go:741-768: nil, error or non-bool -> no trigger); every row triggers without OVER.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {
     const DPlan& p = *pp;
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
@@ -167,9 +182,11 @@ __global__ void k_trigger_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, in
         flags[i - i0] = f;
     }
 }
+#endif
 
 // STATEWINDOW conditions of rows [i0, i1) of the buffer (isMatchCondition, window_v2_op.go:212-238: nil, an
 // error or a non-bool is false): bit 0 = begin condition true, bit 1 = emit condition true
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_state_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int64_t i1, uint8_t* __restrict__ flags) {
     const DPlan& p = *pp;
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
@@ -189,10 +206,12 @@ __global__ void k_state_flags(DPlan* __restrict__ pp, DBatch b, int64_t i0, int6
         flags[i - i0] = f;
     }
 }
+#endif
 
 // Watermarks around the release step r of each listed row (incremental event-time windows): w_step = the
 // watermark whose WatermarkTuple follows the row (emission), w_prev = the one before its step (the last gc).
 // runmax[0..nb) = batch running max (arrival arr_base + j); prevmax = stream max before the batch.
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_step_wm(const int64_t* __restrict__ rel, int64_t n, const int64_t* __restrict__ runmax, int64_t nb,
                           int64_t arr_base, int64_t prevmax, int64_t late_tol, int64_t* __restrict__ w_step,
                           int64_t* __restrict__ w_prev) {
@@ -203,15 +222,19 @@ __global__ void k_step_wm(const int64_t* __restrict__ rel, int64_t n, const int6
         w_prev[k] = pm == INT64_MIN ? INT64_MIN : pm - late_tol;
     }
 }
+#endif
 
 // gather of the flag bytes at compacted positions (positions are absolute: base_idx + i)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_gather_flags(const int64_t* __restrict__ pos, int64_t n, int64_t base_idx, const uint8_t* __restrict__ flags,
                                uint8_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
         out[k] = flags[pos[k] - base_idx];
 }
+#endif
 
 // FilterOp over a window-less batch (filter_operator.go:36-90): 1 keep; nil/false drop; error drop + count
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_filter_flags(DPlan* __restrict__ pp, DBatch b, uint8_t* __restrict__ flags, unsigned long long* n_err) {
     const DPlan& p = *pp;
     unsigned long long e = 0;
@@ -223,8 +246,10 @@ __global__ void k_filter_flags(DPlan* __restrict__ pp, DBatch b, uint8_t* __rest
     for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
     if ((threadIdx.x & 63) == 0 && e) atomicAdd(n_err, e);
 }
+#endif
 
 // rows sel[0..ns) of one column (4- or 8-byte elements) and of its validity bytes, compacted (pushed-down WHERE)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_compact_col(const int64_t* __restrict__ sel, int64_t ns, const void* __restrict__ src, int es,
                               const uint8_t* __restrict__ vsrc, void* __restrict__ dst, uint8_t* __restrict__ vdst) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns; k += (int64_t)gridDim.x * blockDim.x) {
@@ -234,12 +259,16 @@ __global__ void k_compact_col(const int64_t* __restrict__ sel, int64_t ns, const
         if (vdst) vdst[k] = vsrc[i];
     }
 }
+#endif
 // out[k] = base + idx[k]
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_offset_idx(const int64_t* __restrict__ idx, int64_t n, int64_t base, int64_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) out[k] = base + idx[k];
 }
+#endif
 
 // SELECT * rows of the selected events: key = batch row, value c = column c (tag by type / validity)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ sel, int64_t ns, int64_t out_base,
                               int32_t widx, Results res) {
     const DPlan& p = *pp;
@@ -255,9 +284,11 @@ __global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* _
         if (k == 0) res.win_cnt[widx] = ns;
     }
 }
+#endif
 
 // Per-block counts of set flags (stable compaction, pass 1)
 constexpr int kCompactTile = 4096;
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict__ flags, int64_t n, int64_t* cnt) {
     const int64_t base = (int64_t)blockIdx.x * kCompactTile;
     int64_t c = 0;
@@ -271,8 +302,10 @@ __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict
     __syncthreads();
     if (threadIdx.x == 0) cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
+#endif
 
 // exclusive scan of nb block counts (single workgroup); cnt[nb] = total
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(1024) void k_scan_counts(int64_t* cnt, int nb) {
     __shared__ int64_t part[1024];
     const int per = (nb + 1023) / 1024;
@@ -290,8 +323,10 @@ __global__ __launch_bounds__(1024) void k_scan_counts(int64_t* cnt, int nb) {
     int64_t run = part[threadIdx.x];
     for (int k = b0; k < b1; ++k) { int64_t x = cnt[k]; cnt[k] = run; run += x; }
 }
+#endif
 
 // pass 2: write base + i of every set flag, in order (one wave-ordered sweep per block)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict__ flags, int64_t n, const int64_t* cnt,
                                                        int64_t base_idx, int64_t* __restrict__ out) {
     const int64_t base = (int64_t)blockIdx.x * kCompactTile;
@@ -311,6 +346,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_write(const uint8_t* __restrict
         __syncthreads();
     }
 }
+#endif
 
 // Window range descriptor (host -> device): content = [max(floor, lo(lo_ts)), hi(...)) of the buffer.
 enum : int32_t { RB_LB = 0, RB_SLIDE = 1, RB_FIXED = 2, RB_UPTO = 3, RB_CAP = 4, RB_ARR = 5 };
@@ -325,6 +361,7 @@ struct RangeQ {
     int32_t pad;
 };
 
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* __restrict__ brel,
                                 const int64_t* __restrict__ barr, int64_t n_rel, const RangeQ* __restrict__ q, int nq,
                                 int64_t* __restrict__ ab) {
@@ -363,9 +400,11 @@ __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* 
     ab[2 * w] = a;
     ab[2 * w + 1] = b;
 }
+#endif
 
 // debug_membership for range windows: count and Σ ek_mix64(arrival) over [a, b) (one block per window)
 // (barr == nullptr: row i's arrival is arr_base + i — windows read straight from a batch in arrival order)
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kBlock) void k_range_members(const int64_t* __restrict__ barr, const int64_t* __restrict__ ab,
                                                           const int32_t* __restrict__ slot, int64_t* wmc,
                                                           unsigned long long* wmh, int64_t arr_base) {
@@ -381,9 +420,11 @@ __global__ __launch_bounds__(kBlock) void k_range_members(const int64_t* __restr
         wmh[slot[blockIdx.x]] = s[0] + s[1] + s[2] + s[3];
     }
 }
+#endif
 
 // Gather rows of the merge input (sources: [0, ntail) = saved buffer tail, [ntail, ..) = batch rows
 // listed in bidx) into the destination column in sorted order (perm from the radix sort).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_gather8(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const int64_t* __restrict__ tail,
                           const int64_t* __restrict__ batch, const int64_t* __restrict__ bidx, int64_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
@@ -391,6 +432,8 @@ __global__ void k_gather8(const int64_t* __restrict__ perm, int64_t n, int64_t n
         out[k] = s < ntail ? tail[s] : batch[bidx[s - ntail]];
     }
 }
+#endif
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_gather4(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const uint32_t* __restrict__ tail,
                           const uint32_t* __restrict__ batch, const int64_t* __restrict__ bidx, uint32_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
@@ -398,6 +441,8 @@ __global__ void k_gather4(const int64_t* __restrict__ perm, int64_t n, int64_t n
         out[k] = s < ntail ? tail[s] : batch[bidx[s - ntail]];
     }
 }
+#endif
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_gather1(const int64_t* __restrict__ perm, int64_t n, int64_t ntail, const uint8_t* __restrict__ tail,
                           const uint8_t* __restrict__ batch, const int64_t* __restrict__ bidx, uint8_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
@@ -405,7 +450,9 @@ __global__ void k_gather1(const int64_t* __restrict__ perm, int64_t n, int64_t n
         out[k] = s < ntail ? (tail ? tail[s] : (uint8_t)1) : (batch ? batch[bidx[s - ntail]] : (uint8_t)1);
     }
 }
+#endif
 // merge keys: ts of the saved tail rows and of the batch rows listed in bidx, and source ids 0..n-1
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_merge_keys(const int64_t* __restrict__ tail_ts, int64_t ntail, const int64_t* __restrict__ bts,
                              const int64_t* __restrict__ bidx, int64_t nb, int64_t tmin, uint64_t* __restrict__ keys,
                              int64_t* __restrict__ src) {
@@ -416,10 +463,13 @@ __global__ void k_merge_keys(const int64_t* __restrict__ tail_ts, int64_t ntail,
         src[k] = k;
     }
 }
+#endif
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_arrivals_of(const int64_t* __restrict__ bidx, int64_t nb, int64_t arr_base, int64_t* __restrict__ out) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (int64_t)gridDim.x * blockDim.x)
         out[k] = arr_base + bidx[k];
 }
+#endif
 
 // ---------------------------------------------------------------- first-row select fields
 // A non-aggregate select field takes the column's value in the group's FIRST row (row.go:720-726: GroupedTuples
@@ -427,6 +477,7 @@ __global__ void k_arrivals_of(const int64_t* __restrict__ bidx, int64_t nb, int6
 // (value = the row's event-buffer index, i.e. the window order) with MIN, so an emitted EK_AGG_FIRST slot holds the
 // first row's position; one block per window fired by this push then swaps in the source column's value there
 // (nil when that value is null).
+#ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* __restrict__ wslot,
                               const int64_t* __restrict__ wbase, Results res) {
     const DPlan& p = *pp;
@@ -449,18 +500,25 @@ __global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* _
         }
     }
 }
+#endif
 
-// ---------------------------------------------------------------- small range windows: one workgroup per window
+// ---------------------------------------------------------------- small range windows: one wave64 per window
 // For a window of at most kSmallWin rows (COUNTWINDOW(1000), state windows, short sliding windows) the pane/bucket
-// partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here one
-// workgroup owns the whole window: it loads the window's rows [a, b) of the event buffer, applies WHERE (an error
-// replaces the window's output, filter_operator.go:63-77), groups the rows by key through an LDS hash table (linear
-// probing, 2n..4n slots) and a counting sort of the rows by slot, then the first thread of every group folds the
-// group's rows (aggregate_operator.go:34-82; exact two-pass M2), applies HAVING and emits (block-compacted).
-// A handful of barriers per window instead of the log^2 stages of a sorting network.
+// partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here ONE WAVE
+// owns the whole window (a 64-thread workgroup, so its barriers are a wave's own LDS waits): it loads the window's
+// rows [a, a + n) (every key load of a lane issued before the first use), applies WHERE (an error replaces the
+// window's output, filter_operator.go:63-77), groups the rows by key through an LDS hash table (linear probing, 2n..4n
+// slots, 16-bit row counts packed two per word), scans the slot counts into group offsets (slots whose group HAVING
+// over count(*) drops are skipped before any row is placed), places the kept rows by slot, and one lane per group
+// folds the group's rows in window order (aggregate_operator.go:34-82; exact two-pass M2), applies HAVING and emits
+// (wave ballot compaction, the window's row count stored once: no atomics on the result counter).
+// LDS per window: 6 B per slot + 2 B per row (14 KB for n = 1000), so ~11 windows are in flight per CU, each
+// progressing on its own instead of four waves waiting on each other's barriers.
 constexpr int kSmallWin = 2048;
-__host__ __device__ inline int sw_slots(int n) { int h = 256; while (h < 2 * n) h <<= 1; return h; }
-inline size_t sw_lds_bytes(int max_n) { return (size_t)sw_slots(max_n) * 8 + (size_t)max_n * 6 + 16; }
+constexpr int kSwLanes = 64;                    // threads per k_small_win workgroup (one wave)
+constexpr int kSwRows = kSmallWin / kSwLanes;   // rows per lane, at most (RM: 16 for windows up to 1024 rows, else 32)
+__host__ __device__ inline int sw_slots(int n) { int h = 128; while (h < 2 * n) h <<= 1; return h; }
+inline size_t sw_lds_bytes(int max_n) { return (size_t)sw_slots(max_n) * 6 + (((size_t)max_n * 2 + 15) & ~(size_t)15); }
 
 // a window group's rows (indices into the window, distinct) into ascending order, so the group folds its values in
 // the window's row order: the f64 sums are the reference's sequential ones, whatever order the LDS atomics of the
@@ -515,119 +573,171 @@ __device__ __forceinline__ int having_decide(const DPlan& p, const Part<NVC>& s)
     if (h.tag != V_BOOL) return -1;
     return h.i != 0 ? 1 : 0;
 }
-
+// HAVING over count(*) alone, decided from a group's row count c (the decisions for 1 and 2 rows are cached)
 template <int NVC>
-__global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
-                                                     const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
-                                                     const int64_t* __restrict__ obase, Results res, int max_n, SwArith ar) {
-    constexpr int R = kSmallWin / kBlock;      // rows per thread
+__device__ __forceinline__ int having_star_decide(const DPlan& p, int c, int h1, int h2) {
+    if (c == 1) return h1;
+    if (c == 2) return h2;
+    Part<NVC> cp{};
+    cp.cnt = c;
+    return having_decide(p, cp);
+}
+
+template <int NVC, bool WHERE, int RM>
+__global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
+                                                       const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
+                                                       const int64_t* __restrict__ obase, Results res, int max_n, SwArith ar) {
     const DPlan& p = *pp;
+    const int lane = threadIdx.x;
     const int w = wlist ? wlist[blockIdx.x] : (int)blockIdx.x;
     const int64_t a = wlist ? ab[2 * w] : ar.a0 + (int64_t)w * ar.len;
     const int n = wlist ? (int)(ab[2 * w + 1] - a) : ar.len;   // 1 <= n <= kSmallWin (host-checked)
     const int32_t widx = wlist ? slots[w] : ar.slot0 + w;
     const int64_t out = wlist ? obase[w] : ar.ob0 + (int64_t)w * ar.rowcap;
-    // dynamic LDS sized by the launch's largest window (sw_lds_bytes): slots = the power of two >= 2 max_n
+    // dynamic LDS sized by the launch's largest window (sw_lds_bytes): Hmax = the power of two >= 2 max_n
     extern __shared__ uint32_t s_dyn[];
     const int Hmax = sw_slots(max_n);
-    uint32_t* s_key = s_dyn;                   // [Hmax] slot -> key (~0u: free)
-    uint32_t* s_off = s_key + Hmax;            // [Hmax] slot -> rows, then exclusive offset, then scatter cursor
-    uint32_t* s_grp = s_off + Hmax;            // [max_n] occupied slots: (first row in s_row) << 16 | rows
-    uint16_t* s_row = (uint16_t*)(s_grp + max_n);   // [max_n] window rows grouped by slot
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    __shared__ int s_err, s_ng, s_h1;
-    __shared__ uint32_t esh[20];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    int H = 256;
-    while (H < 2 * n) H <<= 1;
-    for (int k = t; k < H; k += kBlock) { s_key[k] = ~0u; s_off[k] = 0; }
-    if (t == 0) {
-        s_err = 0;
-        s_ng = 0;
-        if (p.having_star) {   // HAVING over count(*) alone: the decision for a one-row group, evaluated once
-            Part<NVC> cp{};
-            cp.cnt = 1;
-            s_h1 = having_decide(p, cp);
-        }
-    }
-    __syncthreads();
+    uint32_t* s_key = s_dyn;                           // [Hmax] slot -> key (~0u: free); then group g -> off << 16 | rows
+    uint32_t* s_cnt = s_key + Hmax;                    // [Hmax / 2] two u16 per word: slot rows, then slot cursor
+    uint16_t* s_row = (uint16_t*)(s_cnt + Hmax / 2);   // [max_n] kept window rows grouped by slot
+    const int H = sw_slots(n);
+    for (int k = lane; k < H; k += kSwLanes) s_key[k] = ~0u;
+    for (int k = lane; k < H / 2; k += kSwLanes) s_cnt[k] = 0u;
     const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
-    int my[R];
+    const int nj = (n + kSwLanes - 1) / kSwLanes;
+    // every key load of the lane in flight at once; sl[j] = the key, then its slot (-1: not a member / WHERE false)
+    int sl[RM];
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-        const int k = t + j * kBlock;
-        my[j] = -1;
-        if (k >= n) continue;
-        const int64_t i = a + k;
-        const int wd = p.n_where > 0 ? where_decide_slow(p, b, i) : 1;
-        if (wd < 0) s_err = 1;
-        if (wd <= 0) continue;
-        const uint32_t key = kcol ? kcol[i] : 0u;
-        uint32_t h = sw_hash(key) & (uint32_t)(H - 1);
-        while (true) {
-            const uint32_t old = atomicCAS(&s_key[h], ~0u, key);
-            if (old == ~0u || old == key) break;
-            h = (h + 1) & (uint32_t)(H - 1);
+    for (int j = 0; j < RM; ++j) {
+        const int k = lane + j * kSwLanes;
+        sl[j] = (j < nj && k < n) ? (int)(kcol ? kcol[a + k] : 0u) : -1;
+    }
+    uint32_t live = 0;   // bit j: row lane + 64 j is a member of a group
+#pragma unroll
+    for (int j = 0; j < RM; ++j) {
+        const int k = lane + j * kSwLanes;
+        if (j < nj && k < n) live |= 1u << j;
+    }
+    if (WHERE) {
+        bool err = false;
+#pragma unroll
+        for (int j = 0; j < RM; ++j) {
+            if (!((live >> j) & 1u)) continue;
+            const int wd = where_decide_slow(p, b, a + lane + j * kSwLanes);
+            err |= wd < 0;
+            if (wd <= 0) live &= ~(1u << j);
         }
-        my[j] = (int)h;
-        atomicAdd(&s_off[h], 1u);
+        if (__any(err)) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
+            if (lane == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
+            return;
+        }
     }
     __syncthreads();
-    if (s_err) {
-        if (t == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
+    // insertion: one probe of every pending row per round (their CAS round trips overlap), then the row counts
+    {
+        uint32_t pend = live;
+        int h[RM];
+#pragma unroll
+        for (int j = 0; j < RM; ++j) h[j] = (int)(sw_hash((uint32_t)sl[j]) & (uint32_t)(H - 1));
+        while (__any(pend != 0u)) {
+#pragma unroll
+            for (int j = 0; j < RM; ++j) {
+                if (!((pend >> j) & 1u)) continue;
+                const uint32_t key = (uint32_t)sl[j];
+                const uint32_t old = atomicCAS(&s_key[h[j]], ~0u, key);
+                if (old == ~0u || old == key) pend &= ~(1u << j);
+                else h[j] = (h[j] + 1) & (H - 1);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RM; ++j) {
+            sl[j] = ((live >> j) & 1u) ? h[j] : -1;
+            if (sl[j] >= 0) atomicAdd(&s_cnt[sl[j] >> 1], 1u << ((sl[j] & 1) * 16));
+        }
+    }
+    __syncthreads();
+    // slot scan: kept rows and kept groups before each lane's slots; a slot whose group HAVING drops gets the cursor
+    // 0x8000 (its rows are then skipped by the placement below)
+    int h1 = 1, h2 = 1;
+    if (p.having_star) {
+        Part<NVC> cp{};
+        cp.cnt = 1;
+        h1 = having_decide(p, cp);
+        cp.cnt = 2;
+        h2 = having_decide(p, cp);
+    }
+    const int per = H / kSwLanes;   // slots per lane (even)
+    const int s0 = lane * per;
+    uint32_t x = 0;                 // kept groups << 16 | kept rows of this lane's slots
+    bool herr = false;
+    for (int q = 0; q < per; q += 2) {
+        const uint32_t wd = s_cnt[(s0 + q) >> 1];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
+            if (c == 0) continue;
+            int d = 1;
+            if (p.having_star) {
+                d = having_star_decide<NVC>(p, c, h1, h2);
+                herr |= d < 0;
+            }
+            if (d > 0) x += 0x10000u + (uint32_t)c;
+        }
+    }
+    if (__any(herr) && lane == 0) atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < kSwLanes; o <<= 1) { const uint32_t y = __shfl_up(inc, o, kSwLanes); if (lane >= o) inc += y; }
+    const uint32_t tot = __shfl(inc, kSwLanes - 1, kSwLanes);
+    const int ng = (int)(tot >> 16);
+    if (ng == 0) {   // nothing kept (C4b: most windows hold no key twice)
+        if (lane == 0) res.win_cnt[widx] = 0;
         return;
     }
-    // one exclusive scan of the slot counts packed with the occupied-slot count (each thread H / kBlock consecutive
-    // slots): a slot's first row and its group index at once, no shared group counter to contend on
     {
-        const int per = H / kBlock, s0 = t * per;
-        uint32_t sm = 0;   // occupied slots << 16 | rows (both <= kSmallWin)
-        for (int k = s0; k < s0 + per; ++k) { const uint32_t c = s_off[k]; sm += c | (c ? 0x10000u : 0u); }
-        uint32_t x = sm;
-        for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
-        if (lane == 63) s_wsum[wv] = x;
-        __syncthreads();
-        uint32_t run = x - sm;
-        for (int q = 0; q < wv; ++q) run += s_wsum[q];
-        for (int k = s0; k < s0 + per; ++k) {
-            const uint32_t c = s_off[k];
-            if (c) s_grp[run >> 16] = ((run & 0xFFFFu) << 16) | c;
-            s_off[k] = run & 0xFFFFu;
-            run += c | (c ? 0x10000u : 0u);
+        uint32_t run = inc - x;
+        for (int q = 0; q < per; q += 2) {
+            const uint32_t wd = s_cnt[(s0 + q) >> 1];
+            uint32_t cur = 0;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
+                int d = c > 0 ? 1 : 0;
+                if (c > 0 && p.having_star) d = having_star_decide<NVC>(p, c, h1, h2);
+                if (d > 0) {
+                    s_key[run >> 16] = ((run & 0xFFFFu) << 16) | (uint32_t)c;
+                    cur |= (run & 0xFFFFu) << (16 * hh);
+                    run += 0x10000u + (uint32_t)c;
+                } else {
+                    cur |= 0x8000u << (16 * hh);
+                }
+            }
+            s_cnt[(s0 + q) >> 1] = cur;
         }
-        if (t == kBlock - 1) s_ng = (int)(run >> 16);
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-        if (my[j] >= 0) s_row[atomicAdd(&s_off[my[j]], 1u)] = (uint16_t)(t + j * kBlock);
+    for (int j = 0; j < RM; ++j) {
+        if (sl[j] < 0) continue;
+        const uint32_t sh = (uint32_t)(sl[j] & 1) * 16;
+        const uint32_t pos = (atomicAdd(&s_cnt[sl[j] >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        if (pos < 0x8000u) s_row[pos] = (uint16_t)(lane + j * kSwLanes);
+    }
     __syncthreads();
-    const int ng = s_ng;
     int fl[NVC], col[NVC];
     bool isf[NVC];
 #pragma unroll
     for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; col[v] = v < p.n_vc ? p.vc_col[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
-    for (int base = 0; base < ng; base += kBlock) {
-        const int gi = base + t;
+    int64_t emitted = 0;
+    for (int base = 0; base < ng; base += kSwLanes) {
+        const int gi = base + lane;
         Part<NVC> s{};
         bool present = false;
         uint32_t key = 0;
-        int hs = 1;   // HAVING over count(*) alone (C4b: count(*) > 1): decided from the group's row count, before any fold
-        if (gi < ng && p.having_star) {
-            const int64_t c = (int64_t)(s_grp[gi] & 0xFFFFu);
-            int d = s_h1;
-            if (c != 1) {
-                Part<NVC> cp{};
-                cp.cnt = c;
-                d = having_decide(p, cp);
-            }
-            if (d < 0) atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
-            hs = d > 0 ? 1 : 0;
-        }
-        if (gi < ng && hs) {
-            const uint32_t gw = s_grp[gi];
+        if (gi < ng) {
+            const uint32_t gw = s_key[gi];
             const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu), g1 = g0 + c;
-            sw_sort_rows(s_row + g0, c);   // the scatter's atomics placed them in no fixed order
+            sw_sort_rows(s_row + g0, c);   // the placement's atomics put them in no fixed order
             key = kcol ? kcol[a + s_row[g0]] : 0u;
             int64_t vc[NVC], is[NVC];
             double fs[NVC], m2[NVC];
@@ -640,11 +750,11 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
                 for (int v = 0; v < NVC; ++v) {
                     if (!fl[v] || !col_valid(b, col[v], r)) continue;
                     const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
-                    const double x = isf[v] ? __longlong_as_double(raw) : (double)raw;
-                    const uint64_t o = isf[v] ? f64_to_ord(x) : i64_to_ord(raw);
+                    const double xv = isf[v] ? __longlong_as_double(raw) : (double)raw;
+                    const uint64_t o = isf[v] ? f64_to_ord(xv) : i64_to_ord(raw);
                     vc[v]++;
                     is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
-                    fs[v] = __dadd_rn(fs[v], x);
+                    fs[v] = __dadd_rn(fs[v], xv);
                     mn[v] = o < mn[v] ? o : mn[v];
                     mx[v] = o > mx[v] ? o : mx[v];
                 }
@@ -662,11 +772,24 @@ __global__ __launch_bounds__(kBlock) void k_small_win(DPlan* __restrict__ pp, DB
                 }
             }
             part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-            present = having_keep(p, s, &res.win_err[widx]);
+            // HAVING over count(*) alone was decided by the slot scan; any other HAVING here
+            present = p.having_star ? true : having_keep(p, s, &res.win_err[widx]);
         }
-        if (!__syncthreads_or(present)) continue;   // nothing kept in this round (HAVING): no compaction
-        emit_rows(p, present, s, (int64_t)key, out, widx, res, esh);
+        const unsigned long long m = __ballot(present);
+        if (present) {
+            const int64_t pos = out + emitted + __popcll(m & ((1ull << lane) - 1ull));
+            res.key[pos] = key;
+#pragma unroll
+            for (int k = 0; k < EK_MAX_AGGS; ++k) {
+                if (k >= p.n_aggs) break;
+                const Val v = agg_value(p, s, k);
+                res.tag[k][pos] = v.tag == V_NULL ? EK_TAG_NULL : (v.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+                res.val[k][pos] = v.tag == V_F64 ? __double_as_longlong(v.f) : v.i;
+            }
+        }
+        emitted += __popcll(m);
     }
+    if (lane == 0) res.win_cnt[widx] = emitted;
 }
 
 }  // namespace ek

@@ -1,0 +1,34 @@
+// ek_tpl_small.hip — instantiations of k_small_win (one wave per small range window, ek_range.h) and its launcher:
+// the rules without WHERE here, those with WHERE in ek_tpl_small_w.hip (two parallel jobs).
+#ifndef EK_SW_WHERE
+#define EK_SW_WHERE false
+#define EK_SW_FN launch_small_win_nowhere
+#endif
+#define EK_NO_PLAIN_KERNELS
+#include "ek_launch.h"
+
+namespace ek {
+
+void EK_SW_FN(int nvc, int rm, int nb, size_t lds, hipStream_t s, DPlan* p, const DBatch& src, const int64_t* ab,
+              const int32_t* wl, const int32_t* slot, const int64_t* ob, const Results& res, int max_n, const SwArith& ar) {
+#define EK_SW(N, R) hipLaunchKernelGGL((k_small_win<N, EK_SW_WHERE, R>), dim3(nb), dim3(kSwLanes), lds, s, p, src, ab, wl, slot, ob, res, max_n, ar)
+#define EK_SW_N(R) switch (nvc) { case 1: EK_SW(1, R); break; case 2: EK_SW(2, R); break; \
+                                  case 3: EK_SW(3, R); break; default: EK_SW(4, R); break; }
+    if (rm <= 16) { EK_SW_N(16) } else { EK_SW_N(kSwRows) }
+#undef EK_SW_N
+#undef EK_SW
+}
+
+#if !EK_SW_WHERE
+void launch_small_win_where(int nvc, int rm, int nb, size_t lds, hipStream_t s, DPlan* p, const DBatch& src, const int64_t* ab,
+                            const int32_t* wl, const int32_t* slot, const int64_t* ob, const Results& res, int max_n,
+                            const SwArith& ar);
+void launch_small_win(int nvc, bool where, int rm, int nb, size_t lds, hipStream_t s, DPlan* p, const DBatch& src,
+                      const int64_t* ab, const int32_t* wl, const int32_t* slot, const int64_t* ob, const Results& res,
+                      int max_n, const SwArith& ar) {
+    if (where) launch_small_win_where(nvc, rm, nb, lds, s, p, src, ab, wl, slot, ob, res, max_n, ar);
+    else launch_small_win_nowhere(nvc, rm, nb, lds, s, p, src, ab, wl, slot, ob, res, max_n, ar);
+}
+#endif
+
+}  // namespace ek
