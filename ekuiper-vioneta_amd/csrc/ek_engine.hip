@@ -174,7 +174,8 @@ struct Engine {
 
     // ---- processing time (execProcessingWindow under the caller's clock, ek_advance_time)
     bool proc = false;                 // processing-time TUMBLING / HOPPING / SLIDING / SESSION
-    bool proc_pushdown = false;        // WHERE moved below the window (windowPlan.go:82-99): rows are pre-filtered
+    bool proc_pushdown = false;        // WHERE / FILTER moved below the window (windowPlan.go:82-99): rows are pre-filtered
+    bool pre_filter = false;           // a FilterOp in front of the window (pushed-down WHERE and / or the window FILTER)
     DPlan* d_plan_where = nullptr;     // the plan with WHERE, for the pre-filter (d_plan has n_where = 0 then)
     bool clock_started = false;        // the rule's start: the first ek_advance_time, or the first row
     int64_t clock_ms = 0;              // the clock (every timer due at or before it has fired)
@@ -286,6 +287,14 @@ struct Engine {
                 if (pr[k].op == EK_OP_COL && !col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "condition column out of range");
                 if (pr[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in a window condition");
             }
+        // the window's FILTER (WHERE ...) clause (ABI v8): a row condition over the stream's columns
+        if (plan.n_filter < 0 || plan.n_filter > EK_MAX_PROG || !prog_depth_ok(plan.filter_prog, plan.n_filter))
+            return fail(EK_ERR_INVALID, "malformed window FILTER program");
+        for (int k = 0; k < plan.n_filter; ++k) {
+            if (plan.filter_prog[k].op == EK_OP_COL && !col_ok(plan.filter_prog[k].arg)) return fail(EK_ERR_INVALID, "FILTER column out of range");
+            if (plan.filter_prog[k].op == EK_OP_AGG) return fail(EK_ERR_INVALID, "aggregate in a window FILTER");
+        }
+        if (plan.n_filter > 0 && plan.window_type == EK_WINDOW_NONE) return fail(EK_ERR_INVALID, "FILTER belongs to a window");
         // derived columns (expression arguments of aggregates): validated here, then appended to the engine's copy of
         // the plan as ordinary columns [user_cols, user_cols + n_derived) computed per batch by k_derive
         user_cols = plan.n_columns;
@@ -382,15 +391,20 @@ struct Engine {
             // to the rule's start, rows delivered at their arrival timestamps
             if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING && wtype != EK_WINDOW_SLIDING && wtype != EK_WINDOW_SESSION)
                 return fail(EK_ERR_UNSUPPORTED, "unsupported processing-time window type %d", wtype);
-            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
-                return fail(EK_ERR_UNSUPPORTED, "delayed processing-time sliding windows fire from wall-clock timers per trigger: not built");
             if (plan.incremental || plan.window_version == 2)
                 return fail(EK_ERR_UNSUPPORTED, "incremental / v2 processing-time windows are not built");
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64 || (plan.nullable_mask & (1u << plan.ts_column)))
                 return fail(EK_ERR_INVALID, "processing-time windows need the rows' arrival timestamps (a non-nullable i64 column)");
             proc = true;
             // windowPlan.PushDownPredicate (windowPlan.go:82-99): WHERE below a processing-time TUMBLING / HOPPING / SESSION
-            proc_pushdown = plan.n_where > 0 && wtype != EK_WINDOW_SLIDING;
+            // rows a FilterOp drops before they reach the window, compacted at delivery (proc_prefilter): WHERE AND the
+            // window FILTER pushed below TUMBLING / HOPPING / SESSION (windowPlan.PushDownPredicate, windowPlan.go:82-99),
+            // the FILTER op alone before SLIDING (planner.go:388-392; WHERE stays above the window)
+            proc_pushdown = (plan.n_where > 0 && wtype != EK_WINDOW_SLIDING) || plan.n_filter > 0;
+            if (wtype == EK_WINDOW_SLIDING && plan.delay > 0) {
+                slide_delay = (int64_t)plan.delay * unit_ms(plan.time_unit);
+                send_twice = plan.sliding_send_twice != 0;
+            }
         }
         // incremental-aggregation window (planOptimizeStrategy.enableIncrementalWindow): the planner rewrites the
         // rule only when every aggregate is incremental and the window is COUNT (no interval) / SLIDING / HOPPING /
@@ -411,6 +425,8 @@ struct Engine {
             if (plan.n_where > 0)
                 return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
                                                 "(FilterPlan above IncWindowPlan): not built");
+            if (plan.n_filter > 0)
+                return fail(EK_ERR_UNSUPPORTED, "a window FILTER with incremental window aggregates is not built");
             if (has_first)
                 return fail(EK_ERR_UNSUPPORTED, "incremental windows emit the group's LAST row (window_inc_agg_op.go:443-457): "
                                                 "first-row select fields are not on that path");
@@ -424,6 +440,9 @@ struct Engine {
                      (wtype == EK_WINDOW_HOPPING && plan.is_event_time && plan.late_tolerance_ms > 0) ||
                      wtype == EK_WINDOW_STATE || sort_aggs || has_first ||
                      (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
+        if (plan.sliding_send_twice && wtype == EK_WINDOW_SLIDING && plan.delay > 0 && plan.is_event_time)
+            return fail(EK_ERR_UNSUPPORTED, "enableSlidingWindowSendTwice is built for processing-time sliding windows "
+                                            "(window_op.go:355-373); event-time send-twice is not");
         if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
             return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
         need_rel = (wtype == EK_WINDOW_SLIDING && !proc) || (inc && wtype == EK_WINDOW_COUNT) ||
@@ -634,6 +653,7 @@ struct Engine {
         chunk = env_int("EKGPU_CHUNK", 8192);
         sorted_chunk = env_int("EKGPU_SORTED_CHUNK", kTile);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
+        sw_grid = std::max(1, env_int("EKGPU_SW_GRID", 4096));
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
@@ -657,10 +677,28 @@ struct Engine {
         own_stream = true;
         hipEventCreate(&ev0);
         hipEventCreate(&ev1);
-        if (proc_pushdown) {
+        // the pre-window filter plan (d_plan_where: its where_prog is the program of the FilterOp in front of the window):
+        // processing time — WHERE AND FILTER pushed below TUMBLING / HOPPING / SESSION, FILTER alone before SLIDING,
+        // COUNT and STATE windows (rows compacted at delivery, proc_prefilter); event time — FILTER alone, applied to
+        // the rows WatermarkOp accepted (filter_accept)
+        pre_filter = proc_pushdown || plan.n_filter > 0;
+        if (pre_filter) {
+            const bool push_where = proc && wtype != EK_WINDOW_SLIDING && plan.n_where > 0;
+            std::vector<ek_instr> prog;
+            if (push_where) prog.insert(prog.end(), plan.where_prog, plan.where_prog + plan.n_where);
+            if (plan.n_filter > 0) {
+                prog.insert(prog.end(), plan.filter_prog, plan.filter_prog + plan.n_filter);
+                if (push_where) { ek_instr a{}; a.op = EK_OP_AND; prog.push_back(a); }   // combine(where, filter)
+            }
+            if ((int)prog.size() > EK_MAX_PROG || !prog_depth_ok(prog.data(), (int)prog.size()))
+                return fail(EK_ERR_UNSUPPORTED, "WHERE AND FILTER pushed below the window: the combined condition is longer "
+                                                "than %d instructions or nests deeper than %d operands", EK_MAX_PROG, kEvalDepth);
+            DPlan pre = dp;
+            pre.n_where = (int)prog.size();
+            memcpy(pre.where_prog, prog.data(), prog.size() * sizeof(ek_instr));
             if (hipMalloc((void**)&d_plan_where, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
-            if (hipMemcpy(d_plan_where, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
-            dp.n_where = 0;   // the pre-filter already dropped every row whose WHERE is not true
+            if (hipMemcpy(d_plan_where, &pre, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+            if (push_where) dp.n_where = 0;   // the pre-filter already dropped every row whose WHERE is not true
         }
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
         if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
@@ -1685,11 +1723,13 @@ struct Engine {
     bool hop_discard_pending = false;   // fire_windows applies the hopping empty-window discard to this set
 
     // Resolve the ranges of `pw` on the device, register the windows, launch their aggregation.
-    // k_small_win over nb windows (one wave each; see ek_range.h), specialised by value columns, WHERE and rows per lane
+    // k_small_win over nb windows (persistent waves, one window at a time each; see ek_range.h), specialised by value
+    // columns, WHERE and rows per lane
+    int sw_grid = 4096;   // EKGPU_SW_GRID: waves of a k_small_win launch
     void small_win_launch(int nb, const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot,
                           const int64_t* ob, int max_n, SwArith ar) {
-        ek::launch_small_win(std::max(1, dp.n_vc), dp.n_where > 0, max_n <= 16 * kSwLanes ? 16 : kSwRows, nb, sw_lds_bytes(max_n),
-                         stream, d_plan, src, ab, wl, slot, ob, results_view(), max_n, ar);
+        ek::launch_small_win(std::max(1, dp.n_vc), dp.n_where > 0, max_n <= 16 * kSwLanes ? 16 : kSwRows, std::min(nb, sw_grid), nb,
+                             sw_lds_bytes(max_n), stream, d_plan, src, ab, wl, slot, ob, results_view(), ar);
     }
 
     int fire_windows(std::vector<PendWin>& pw) {
@@ -2743,7 +2783,7 @@ struct Engine {
         clock_ms = t0;
         if (wtype == EK_WINDOW_TUMBLING || wtype == EK_WINDOW_HOPPING) {
             e1_known = true;
-            first_ts = 0;   // triggerTime is zero until the first scan: window_start falls back to end - length
+            first_ts = t0;  // Exec sets triggerTime = now in processing time (window_op.go:149-151): the first windowStart
             E1 = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
             grid.tumbling = wtype == EK_WINDOW_TUMBLING;
             grid.origin = grid.tumbling ? E1 : E1 - L;
@@ -2785,7 +2825,7 @@ struct Engine {
 
     // WHERE pushed below the window: the rows whose WHERE is true, compacted (stable), with their arrival indices as
     // the batch's row arrivals (g_row_arr). A row whose WHERE errors is dropped and counted (FilterOp forwards its error).
-    DevBuf pf_cols[EK_MAX_COLUMNS], pf_valid[EK_MAX_COLUMNS], pf_arr;
+    DevBuf pf_cols[EK_MAX_COLUMNS], pf_valid[EK_MAX_COLUMNS], pf_arr, filt_d;
     int proc_prefilter(DBatch& db, int64_t arrival_base) {
         const int64_t n = db.n;
         if (int rc = ensure(flags_d, (size_t)n)) return rc;
@@ -2891,7 +2931,7 @@ struct Engine {
     // arrived before it (its gcInputs dropped the rows with ts + length <= ts).
     int proc_slide_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
         const int64_t n_new = eb_rel - rel_prev;
-        if (n_new <= 0) return 0;
+        if (n_new <= 0) return slide_delay > 0 ? proc_slide_delayed(rel_prev, {}, {}, pw) : 0;
         if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
         if (int rc = ensure(trig_d, (size_t)n_new * 8)) return rc;
         const int nb = (int)((n_new + kCompactTile - 1) / kCompactTile);
@@ -2915,6 +2955,7 @@ struct Engine {
             hipMemcpyAsync(tts.data(), g_ts, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+        if (slide_delay > 0) return proc_slide_delayed(rel_prev, pos, tts, pw);
         // the latest non-matching row before each trigger (its ts decides the gcInputs edge): the row just before the
         // trigger unless that row is a trigger too (then the same as that trigger's); rows before this batch: carried
         std::vector<int64_t> qpos;            // batch rows whose ts is needed (non-matching predecessors, the last row)
@@ -2954,10 +2995,115 @@ struct Engine {
         }
         return 0;
     }
-    // rows older than clock - length can no longer be in a window (every later trigger is at or after the clock)
+    // Delayed SLIDINGWINDOW(unit, L, D) in processing time (window_op.go:355-373,325-337): a trigger row at t arms a
+    // timer due at t + D; when the clock reaches it (before any row stamped t + D) the window scans [t - L, t + D).
+    // With enableSlidingWindowSendTwice the trigger first scans (t - L, t] over the rows delivered up to it and the
+    // timer (t, t + D]; handleInputsForSlidingWindow (window_op.go:576-603) then keeps only the EXPIRED prefix of the
+    // inputs (ts < windowEnd - L - D) whenever some input expired: restated on the host over the mirror of the
+    // delivered timestamps as an inert expired set sw2_e (its rows are never in a later window) and the index sw2_cut
+    // from which delivered rows are live. Windows are fired in clock order, a timer before a trigger at the same ms.
+    int64_t slide_delay = 0;            // SLIDINGWINDOW delay (ms); > 0: proc_dq holds the armed timers (trigger ts)
+    bool send_twice = false;
+    std::vector<int64_t> proc_dq;
+    size_t proc_dq_head = 0;
+    std::vector<int64_t> sw2_e;         // send-twice: ts of the expired inputs the reference keeps
+    int64_t sw2_cut = 0;                // send-twice: absolute buffer index of the first live input
+    int proc_slide_delayed(int64_t rel_prev, const std::vector<int64_t>& pos, const std::vector<int64_t>& tts,
+                           std::vector<PendWin>& pw) {
+        const int64_t D = slide_delay;
+        if (!send_twice) {
+            for (int64_t t : tts) proc_dq.push_back(t);
+            while (proc_dq_head < proc_dq.size() && proc_dq[proc_dq_head] + D <= W) {
+                const int64_t t = proc_dq[proc_dq_head++];
+                PendWin p{};
+                p.q.kind = RB_LB;
+                p.q.lo_ts = t - L;
+                p.q.hi_ts = t + D;
+                p.q.floor = eb_floor;
+                p.start = t - L;   // scan(t + D, length + delay): windowStart = windowEnd - (L + D)
+                p.end = t + D;
+                pw.push_back(p);
+            }
+        } else {
+            // host mirror of the delivered timestamps [h_rts_base, ...)
+            const int64_t n_new = eb_rel - rel_prev;
+            if (h_rts.empty()) h_rts_base = eb_base + rel_prev;
+            if (n_new > 0) {
+                const size_t o = h_rts.size();
+                h_rts.resize(o + n_new);
+                hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8,
+                               hipMemcpyDeviceToHost, stream);
+                if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "timestamp mirror copy failed");
+            }
+            if (sw2_cut < h_rts_base) sw2_cut = h_rts_base;
+            auto ts_at = [&](int64_t abs) { return h_rts[abs - h_rts_base]; };
+            auto first_gt = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts > x
+                return h_rts_base + (std::upper_bound(h_rts.begin() + (lo - h_rts_base), h_rts.begin() + (hi - h_rts_base), x) - h_rts.begin());
+            };
+            auto first_ge = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts >= x
+                return h_rts_base + (std::lower_bound(h_rts.begin() + (lo - h_rts_base), h_rts.begin() + (hi - h_rts_base), x) - h_rts.begin());
+            };
+            // one scan over the inputs delivered up to `delivered`: content (ws, we], then the expired-prefix rule
+            auto scan2 = [&](int64_t ws, int64_t we, int64_t delivered) {
+                const int64_t a = std::max(sw2_cut, first_gt(sw2_cut, delivered, ws));
+                const int64_t b = std::max(a, first_gt(a, delivered, we));
+                PendWin p{};
+                p.q.kind = RB_FIXED;
+                p.q.pos = a - eb_base;
+                p.q.rstep = b - eb_base;
+                p.start = ws;
+                p.end = we;
+                pw.push_back(p);
+                const int64_t dl = we - (L + D);
+                const int64_t ne = std::lower_bound(sw2_e.begin(), sw2_e.end(), dl) - sw2_e.begin();
+                const int64_t nl = first_ge(sw2_cut, delivered, dl) - sw2_cut;
+                const int64_t present = (int64_t)sw2_e.size() + (delivered - sw2_cut);
+                if (ne + nl == 0) return;
+                if (ne + nl == present) {
+                    sw2_e.clear();
+                } else {
+                    sw2_e.resize((size_t)ne);
+                    for (int64_t k = 0; k < nl; ++k) sw2_e.push_back(ts_at(sw2_cut + k));
+                }
+                sw2_cut = delivered;
+            };
+            const int64_t end_abs = eb_base + eb_rel;
+            size_t k = 0;
+            for (;;) {
+                const int64_t due = proc_dq_head < proc_dq.size() ? proc_dq[proc_dq_head] + D : INT64_MAX;
+                const int64_t tn = k < tts.size() ? tts[k] : INT64_MAX;
+                if (due <= tn && due <= W) {
+                    // the second part (t, t + D] over the rows delivered before the timer (ts < t + D)
+                    const int64_t t = proc_dq[proc_dq_head++];
+                    scan2(t, t + D, first_ge(sw2_cut, end_abs, t + D));
+                } else if (tn != INT64_MAX) {
+                    // the first part (t - L, t] over the rows delivered up to the trigger
+                    scan2(tn - L, tn, eb_base + pos[k] + 1);
+                    proc_dq.push_back(tn);
+                    ++k;
+                } else {
+                    break;
+                }
+            }
+            eb_floor = std::max(eb_floor, sw2_cut - eb_base);
+            const int64_t drop = sw2_cut - h_rts_base;
+            if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
+                h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+                h_rts_base = sw2_cut;
+            }
+        }
+        if (proc_dq_head > 4096 && proc_dq_head * 2 > proc_dq.size()) {
+            proc_dq.erase(proc_dq.begin(), proc_dq.begin() + (int64_t)proc_dq_head);
+            proc_dq_head = 0;
+        }
+        return 0;
+    }
+
+    // rows older than clock - length - delay can no longer be in a window (every later trigger is at or after the
+    // clock; a pending delayed window of trigger t > clock - delay starts at t - length)
     int proc_slide_floor() {
         if (eb_rel <= eb_floor) return 0;
-        const int64_t bound = W - L;
+        const int64_t bound = W - L - slide_delay;
         if (int rc = ensure(bounds_val, 8)) return rc;
         if (int rc = ensure(bounds_idx, 8)) return rc;
         hipMemcpyAsync(bounds_val.p, &bound, 8, hipMemcpyHostToDevice, stream);
@@ -3197,7 +3343,7 @@ struct Engine {
     // unfinished window are appended. Windows, arrivals and membership are those of the buffered path.
     bool count_direct_ok(const DBatch& db) const {
         const int64_t len = plan.length;
-        return count_direct && plan.interval <= 0 && !inc && !need_rel && !gmode && rowpos_col < 0 && dp.n_sagg == 0 &&
+        return count_direct && plan.interval <= 0 && !inc && !need_rel && !gmode && !g_row_arr && rowpos_col < 0 && dp.n_sagg == 0 &&
                small_win_on && len >= 1 && len <= kSmallWin && db.n >= 2 * len;
     }
     int push_count_direct(const DBatch& db) {
@@ -3327,17 +3473,26 @@ struct Engine {
             const int rc = push_filter(db);
             return rc ? rc : record_time();
         }
+        if (!plan.is_event_time && (wtype == EK_WINDOW_COUNT || wtype == EK_WINDOW_STATE) && pre_filter) {
+            // the window FILTER op in front of the count / state window: only the rows it keeps reach the window (they
+            // keep their source arrival indices for the membership check)
+            if (int rc = proc_prefilter(db, stats.records_in - n)) { g_row_arr = nullptr; return rc; }
+        }
         if (wtype == EK_WINDOW_COUNT && !plan.is_event_time) {
             const int rc = push_count(db);
+            g_row_arr = nullptr;
             return rc ? rc : record_time();
         }
         if (wtype == EK_WINDOW_STATE && !plan.is_event_time) {
             // processing time: the rows reach StateWindowOp in arrival order
-            if (int rc = eb_append(db, 0, n, arrivals)) return rc;
-            arrivals += n;
+            const int64_t m = db.n;
+            int rc = eb_append(db, 0, m, arrivals);
+            g_row_arr = nullptr;
+            if (rc) return rc;
+            arrivals += m;
             const int64_t lo = eb_rel;
             eb_rel = eb.n;
-            const int rc = state_scan(lo, eb_rel);
+            rc = state_scan(lo, eb_rel);
             return rc ? rc : record_time();
         }
         if (proc) {
@@ -3400,6 +3555,26 @@ struct Engine {
             d_acc = (const uint8_t*)acc.p;
         }
         stats.records_late += n - n_acc;
+        // ---- 2b. the window's FILTER (WHERE ...) op between WatermarkOp and the window (planner.go:388-392): a row it
+        // drops never reaches the window (no member, no trigger, not the first window's anchor) but moved the watermark
+        bool filt_dropped = false;
+        if (plan.n_filter > 0 && n_acc > 0) {
+            if (int rc = ensure(filt_d, (size_t)n)) return rc;
+            BatchStats* bs = (BatchStats*)bstats.p;
+            hipMemsetAsync(&bs->n_accepted, 0, 8, stream);
+            hipMemsetAsync(&bs->n_dropped, 0, 8, stream);
+            const int64_t big = INT64_MAX;
+            hipMemcpyAsync(&bs->min_accepted, &big, 8, hipMemcpyHostToDevice, stream);
+            hipLaunchKernelGGL(k_filter_mask, dim3((int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                               d_plan_where, db, d_acc, start, (uint8_t*)filt_d.p, bs);
+            hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window filter kernel failed");
+            stats.records_filter_error += h_stats->n_dropped;
+            filt_dropped = h_stats->n_accepted < n_acc;
+            n_acc = h_stats->n_accepted;
+            if (n_acc > 0) min_acc = h_stats->min_accepted;   // none left: the batch only moves the watermark
+            d_acc = (const uint8_t*)filt_d.p;
+        }
         int64_t arrival_base = arrivals;
         arrivals += n;
         h_wdesc_used = 0;   // the stats sync above drained every earlier descriptor upload
@@ -3442,8 +3617,9 @@ struct Engine {
             const int rc = push_range(db, sorted, start, d_acc, n_acc, min_acc, s.max_ts, arrival_base, M_prev, had_M, s.min_ts);
             return rc ? rc : record_time();
         }
-        // a batch whose every accepted event was discarded still advanced the watermark: its windows close below
-        if (n_acc == 0 && !(hop_dropped && e1_known)) return record_time();
+        // a batch whose every accepted event was discarded (or filtered) still advanced the watermark: its windows close
+        // below
+        if (n_acc == 0 && !((hop_dropped || filt_dropped) && e1_known)) return record_time();
 
         // ---- 4. first window alignment once the first event is released
         if (!e1_known) {
@@ -3524,8 +3700,10 @@ struct Engine {
                 return fail(EK_ERR_UNSUPPORTED, "shard mode: delayed sliding windows are not built");
             if (wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms != 0)
                 return fail(EK_ERR_UNSUPPORTED, "shard mode: the hopping empty-window discard is built for lateTolerance 0");
-        } else if (wtype != EK_WINDOW_COUNT || inc) {
-            return fail(EK_ERR_UNSUPPORTED, "shard mode: processing time is built for COUNTWINDOW");
+            if (plan.n_filter > 0)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: a window FILTER is not built (the router would drop the rows)");
+        } else if (wtype != EK_WINDOW_COUNT || inc || plan.n_filter > 0) {
+            return fail(EK_ERR_UNSUPPORTED, "shard mode: processing time is built for COUNTWINDOW (without FILTER)");
         }
         return 0;
     }

@@ -8,6 +8,8 @@
 // (sliding, session, count, and tumbling/hopping when an aggregate needs the raw values) are
 // aggregated by the same partition/aggregate kernels as "virtual panes" (k_part MODE 2 + k_agg).
 #pragma once
+#include <algorithm>
+
 #include "ek_kernels.h"
 
 namespace ek {
@@ -286,6 +288,39 @@ __global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* _
 }
 #endif
 
+// The window's FILTER (WHERE ...) op between WatermarkOp and the window (planner.go:388-392), event time: acc_out[i] =
+// the row was accepted (acc_in[i], or i >= start when acc_in is null) and its condition (the pre plan's where_prog) is
+// true; nil / false drop it, an error drops it and is counted (filter_operator.go:41-57). st: n_accepted and
+// min_accepted of the kept rows, n_dropped = the evaluation errors (all three reset by the caller).
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kBlock) void k_filter_mask(DPlan* __restrict__ pp, DBatch b, const uint8_t* __restrict__ acc_in,
+                                                        int64_t start, uint8_t* __restrict__ acc_out, BatchStats* st) {
+    const DPlan& p = *pp;
+    const int64_t* ts = (const int64_t*)b.col[p.ts_col];
+    unsigned long long c = 0, e = 0;
+    int64_t m = INT64_MAX;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += (int64_t)gridDim.x * blockDim.x) {
+        bool keep = acc_in ? acc_in[i] != 0 : i >= start;
+        if (keep) {
+            const int w = where_decide_slow(p, b, i);
+            e += w < 0;
+            keep = w > 0;
+        }
+        acc_out[i] = keep ? 1 : 0;
+        if (keep) { c++; m = min(m, ts[i]); }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, 64);
+        e += __shfl_xor(e, o, 64);
+        m = min(m, (int64_t)__shfl_xor(m, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c) { atomicAdd((unsigned long long*)&st->n_accepted, c); atomicMin((long long*)&st->min_accepted, (long long)m); }
+        if (e) atomicAdd((unsigned long long*)&st->n_dropped, e);
+    }
+}
+#endif
+
 // Per-block counts of set flags (stable compaction, pass 1)
 constexpr int kCompactTile = 4096;
 #ifndef EK_NO_PLAIN_KERNELS
@@ -505,20 +540,28 @@ __global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* _
 // ---------------------------------------------------------------- small range windows: one wave64 per window
 // For a window of at most kSmallWin rows (COUNTWINDOW(1000), state windows, short sliding windows) the pane/bucket
 // partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here ONE WAVE
-// owns the whole window (a 64-thread workgroup, so its barriers are a wave's own LDS waits): it loads the window's
-// rows [a, a + n) (every key load of a lane issued before the first use), applies WHERE (an error replaces the
-// window's output, filter_operator.go:63-77), groups the rows by key through an LDS hash table (linear probing, 2n..4n
-// slots, 16-bit row counts packed two per word), scans the slot counts into group offsets (slots whose group HAVING
-// over count(*) drops are skipped before any row is placed), places the kept rows by slot, and one lane per group
-// folds the group's rows in window order (aggregate_operator.go:34-82; exact two-pass M2), applies HAVING and emits
-// (wave ballot compaction, the window's row count stored once: no atomics on the result counter).
-// LDS per window: 6 B per slot + 2 B per row (14 KB for n = 1000), so ~11 windows are in flight per CU, each
-// progressing on its own instead of four waves waiting on each other's barriers.
+// owns a whole window at a time (a 64-thread workgroup: its barriers are the wave's own LDS waits) and persistent
+// waves walk the launch's windows, loading the next window's keys while grouping the current one. Per window:
+//   WHERE (an error replaces the window's output, filter_operator.go:63-77);
+//   a duplicate filter: every row sets its key's hash bit in an LDS bitmap of >= 32 bits per row and marks the bit
+//     in a second map when it was already set — a row whose bit no other row set is a group of its own (count 1),
+//     emitted straight from its lane (HAVING count(*) > 1 drops it without a fold);
+//   the other rows (candidates: real duplicates plus the few hash collisions) are grouped exactly through an LDS hash
+//     table sized by their count, with a slot scan (groups HAVING over count(*) drops are never placed) and one
+//     lane per group;
+//   every group folds its rows in window order (aggregate_operator.go:34-82; exact two-pass M2), applies HAVING and
+//   is emitted by wave ballot compaction; the window's row count is stored once (no atomics on the counter).
+// LDS per wave: the larger of the two bitmaps (8 KB for n = 1000) and the candidates' hash table (6 B per slot,
+// 2n..4n slots, + 2 B per row + 4 B per group), sized by the launch's largest window.
 constexpr int kSmallWin = 2048;
 constexpr int kSwLanes = 64;                    // threads per k_small_win workgroup (one wave)
 constexpr int kSwRows = kSmallWin / kSwLanes;   // rows per lane, at most (RM: 16 for windows up to 1024 rows, else 32)
 __host__ __device__ inline int sw_slots(int n) { int h = 128; while (h < 2 * n) h <<= 1; return h; }
-inline size_t sw_lds_bytes(int max_n) { return (size_t)sw_slots(max_n) * 6 + (((size_t)max_n * 2 + 15) & ~(size_t)15); }
+__host__ __device__ inline int sw_bits(int n) { int b = 2048; while (b < 32 * n) b <<= 1; return b; }
+inline size_t sw_lds_bytes(int max_n) {
+    const size_t tab = (size_t)sw_slots(max_n) * 6 + (((size_t)max_n * 2 + 3) & ~(size_t)3) + (size_t)max_n * 4;
+    return std::max(tab, (size_t)sw_bits(max_n) / 4);
+}
 
 // a window group's rows (indices into the window, distinct) into ascending order, so the group folds its values in
 // the window's row order: the f64 sums are the reference's sequential ones, whatever order the LDS atomics of the
@@ -583,41 +626,17 @@ __device__ __forceinline__ int having_star_decide(const DPlan& p, int c, int h1,
     return having_decide(p, cp);
 }
 
+// One small window per call: rows [a, a + n) of b, keys already in key[] (lane + 64 j), result region out, slot widx.
+// Returns the rows emitted (-1: a WHERE error replaced the window's output).
 template <int NVC, bool WHERE, int RM>
-__global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
-                                                       const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
-                                                       const int64_t* __restrict__ obase, Results res, int max_n, SwArith ar) {
-    const DPlan& p = *pp;
+__device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, const uint32_t* kcol, int64_t a, int n,
+                                             int32_t widx, int64_t out, const uint32_t (&key)[RM], Results& res,
+                                             uint32_t* s_dyn, int h1, int h2) {
     const int lane = threadIdx.x;
-    const int w = wlist ? wlist[blockIdx.x] : (int)blockIdx.x;
-    const int64_t a = wlist ? ab[2 * w] : ar.a0 + (int64_t)w * ar.len;
-    const int n = wlist ? (int)(ab[2 * w + 1] - a) : ar.len;   // 1 <= n <= kSmallWin (host-checked)
-    const int32_t widx = wlist ? slots[w] : ar.slot0 + w;
-    const int64_t out = wlist ? obase[w] : ar.ob0 + (int64_t)w * ar.rowcap;
-    // dynamic LDS sized by the launch's largest window (sw_lds_bytes): Hmax = the power of two >= 2 max_n
-    extern __shared__ uint32_t s_dyn[];
-    const int Hmax = sw_slots(max_n);
-    uint32_t* s_key = s_dyn;                           // [Hmax] slot -> key (~0u: free); then group g -> off << 16 | rows
-    uint32_t* s_cnt = s_key + Hmax;                    // [Hmax / 2] two u16 per word: slot rows, then slot cursor
-    uint16_t* s_row = (uint16_t*)(s_cnt + Hmax / 2);   // [max_n] kept window rows grouped by slot
-    const int H = sw_slots(n);
-    for (int k = lane; k < H; k += kSwLanes) s_key[k] = ~0u;
-    for (int k = lane; k < H / 2; k += kSwLanes) s_cnt[k] = 0u;
-    const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
-    const int nj = (n + kSwLanes - 1) / kSwLanes;
-    // every key load of the lane in flight at once; sl[j] = the key, then its slot (-1: not a member / WHERE false)
-    int sl[RM];
+    uint32_t live = 0;   // bit j: row lane + 64 j is in the window (and its WHERE is true)
 #pragma unroll
-    for (int j = 0; j < RM; ++j) {
-        const int k = lane + j * kSwLanes;
-        sl[j] = (j < nj && k < n) ? (int)(kcol ? kcol[a + k] : 0u) : -1;
-    }
-    uint32_t live = 0;   // bit j: row lane + 64 j is a member of a group
-#pragma unroll
-    for (int j = 0; j < RM; ++j) {
-        const int k = lane + j * kSwLanes;
-        if (j < nj && k < n) live |= 1u << j;
-    }
+    for (int j = 0; j < RM; ++j)
+        if (lane + j * kSwLanes < n) live |= 1u << j;
     if (WHERE) {
         bool err = false;
 #pragma unroll
@@ -629,35 +648,232 @@ __global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, 
         }
         if (__any(err)) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
             if (lane == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
-            return;
+            return -1;
         }
     }
+    // ---- duplicate filter: two bitmaps over HB hash bits. A row whose bit no other row of the window set is a
+    // group of its own (no other row shares its hash, so none shares its key); the others are candidates.
+    const int HB = sw_bits(n);
+    uint32_t* s_seen = s_dyn;
+    uint32_t* s_dupb = s_dyn + HB / 32;
+    for (int k = lane; k < HB / 64; k += kSwLanes) ((uint4*)s_dyn)[k] = make_uint4(0u, 0u, 0u, 0u);   // both maps
     __syncthreads();
-    // insertion: one probe of every pending row per round (their CAS round trips overlap), then the row counts
-    {
-        uint32_t pend = live;
-        int h[RM];
 #pragma unroll
-        for (int j = 0; j < RM; ++j) h[j] = (int)(sw_hash((uint32_t)sl[j]) & (uint32_t)(H - 1));
-        while (__any(pend != 0u)) {
+    for (int j = 0; j < RM; ++j) {
+        if (!((live >> j) & 1u)) continue;
+        const uint32_t h = sw_hash(key[j]) & (uint32_t)(HB - 1), bit = 1u << (h & 31u);
+        if (atomicOr(&s_seen[h >> 5], bit) & bit) atomicOr(&s_dupb[h >> 5], bit);
+    }
+    __syncthreads();
+    uint32_t cand = 0;
 #pragma unroll
-            for (int j = 0; j < RM; ++j) {
-                if (!((pend >> j) & 1u)) continue;
-                const uint32_t key = (uint32_t)sl[j];
-                const uint32_t old = atomicCAS(&s_key[h[j]], ~0u, key);
-                if (old == ~0u || old == key) pend &= ~(1u << j);
-                else h[j] = (h[j] + 1) & (H - 1);
+    for (int j = 0; j < RM; ++j) {
+        if (!((live >> j) & 1u)) continue;
+        const uint32_t h = sw_hash(key[j]) & (uint32_t)(HB - 1);
+        if ((s_dupb[h >> 5] >> (h & 31u)) & 1u) cand |= 1u << j;
+    }
+    __syncthreads();   // the bitmaps are dead: their LDS is reused below
+    const uint32_t single = live & ~cand;
+    int fl[NVC], col[NVC];
+    bool isf[NVC];
+#pragma unroll
+    for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; col[v] = v < p.n_vc ? p.vc_col[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
+    int64_t emitted = 0;
+    bool herr = false;
+    auto emit = [&](bool present, const Part<NVC>& s, uint32_t k) {
+        const unsigned long long m = __ballot(present);
+        if (present) {
+            const int64_t pos = out + emitted + __popcll(m & ((1ull << lane) - 1ull));
+            res.key[pos] = k;
+#pragma unroll
+            for (int q = 0; q < EK_MAX_AGGS; ++q) {
+                if (q >= p.n_aggs) break;
+                const Val v = agg_value(p, s, q);
+                res.tag[q][pos] = v.tag == V_NULL ? EK_TAG_NULL : (v.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+                res.val[q][pos] = v.tag == V_F64 ? __double_as_longlong(v.f) : v.i;
+            }
+        }
+        emitted += __popcll(m);
+    };
+    // fold of a group given its rows in window order (row(u) for u in [0, c)): count, sums, min / max, centred M2
+    auto fold = [&](Part<NVC>& s, int c, auto row) {
+        int64_t vc[NVC], is[NVC];
+        double fs[NVC], m2[NVC];
+        uint64_t mn[NVC], mx[NVC];
+#pragma unroll
+        for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
+        for (int u = 0; u < c; ++u) {
+            const int64_t r = a + row(u);
+#pragma unroll
+            for (int v = 0; v < NVC; ++v) {
+                if (!fl[v] || !col_valid(b, col[v], r)) continue;
+                const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
+                const double xv = isf[v] ? __longlong_as_double(raw) : (double)raw;
+                const uint64_t o = isf[v] ? f64_to_ord(xv) : i64_to_ord(raw);
+                vc[v]++;
+                is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
+                fs[v] = __dadd_rn(fs[v], xv);
+                mn[v] = o < mn[v] ? o : mn[v];
+                mx[v] = o > mx[v] ? o : mx[v];
             }
         }
 #pragma unroll
+        for (int v = 0; v < NVC; ++v) {   // centred second pass (stats._variance shape)
+            if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;
+            const double mean = __ddiv_rn(fs[v], (double)vc[v]);
+            for (int u = 0; u < c; ++u) {
+                const int64_t r = a + row(u);
+                if (!col_valid(b, col[v], r)) continue;
+                const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
+                const double d = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
+                m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
+            }
+        }
+        part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+    };
+    // keep decision of a folded group: HAVING over count(*) alone from its row count, any other HAVING on the partial
+    auto keep = [&](const Part<NVC>& s, int c) -> bool {
+        if (p.having_star) {
+            const int d = having_star_decide<NVC>(p, c, h1, h2);
+            herr |= d < 0;
+            return d > 0;
+        }
+        return having_keep(p, s, &res.win_err[widx]);
+    };
+    // ---- one-row groups, straight from their lanes (coalesced value loads; a rolled loop: one copy of the fold)
+    if (__any(single != 0u) && !(p.having_star && h1 == 0)) {
         for (int j = 0; j < RM; ++j) {
-            sl[j] = ((live >> j) & 1u) ? h[j] : -1;
-            if (sl[j] >= 0) atomicAdd(&s_cnt[sl[j] >> 1], 1u << ((sl[j] & 1) * 16));
+            const bool mine = (single >> j) & 1u;
+            if (!__any(mine)) continue;
+            Part<NVC> s{};
+            bool present = false;
+            if (mine) {
+                fold(s, 1, [&](int) { return lane + j * kSwLanes; });
+                present = keep(s, 1);
+            }
+            emit(present, s, sel(key, j));
         }
     }
-    __syncthreads();
-    // slot scan: kept rows and kept groups before each lane's slots; a slot whose group HAVING drops gets the cursor
-    // 0x8000 (its rows are then skipped by the placement below)
+    int nc = __popc(cand);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, kSwLanes);
+    if (nc > 0) {
+        // ---- the candidates (real duplicates + hash collisions): an LDS hash table over them sized by their count
+        // (linear probing, 16-bit counts packed two per word), a slot scan into group offsets (groups HAVING over
+        // count(*) drops get cursor 0x8000: their rows are never placed), the rows placed by slot, one lane per group
+        const int H = sw_slots(nc);
+        uint32_t* s_key = s_dyn;                        // [H] slot -> key; then group g -> off << 16 | rows
+        uint32_t* s_cnt = s_key + H;                    // [H / 2] slot rows, then slot cursors
+        uint16_t* s_row = (uint16_t*)(s_cnt + H / 2);   // [nc] candidate rows grouped by slot
+        for (int k = lane; k < H; k += kSwLanes) s_key[k] = ~0u;
+        for (int k = lane; k < H / 2; k += kSwLanes) s_cnt[k] = 0u;
+        __syncthreads();
+        for (int j = 0; j < RM; ++j) {
+            bool pend = (cand >> j) & 1u;
+            if (!__any(pend)) continue;
+            const uint32_t kj = sel(key, j);
+            int h = (int)(sw_hash(kj) & (uint32_t)(H - 1));
+            while (__any(pend)) {
+                if (pend) {
+                    const uint32_t old = atomicCAS(&s_key[h], ~0u, kj);
+                    if (old == ~0u || old == kj) pend = false;
+                    else h = (h + 1) & (H - 1);
+                }
+            }
+            if ((cand >> j) & 1u) atomicAdd(&s_cnt[h >> 1], 1u << ((h & 1) * 16));
+        }
+        __syncthreads();
+        const int per = H / kSwLanes;   // slots per lane (even)
+        const int s0 = lane * per;
+        uint32_t x = 0;                 // kept groups << 16 | kept rows of this lane's slots
+        for (int q = 0; q < per; q += 2) {
+            const uint32_t wd = s_cnt[(s0 + q) >> 1];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
+                if (c == 0) continue;
+                int d = 1;
+                if (p.having_star) {
+                    d = having_star_decide<NVC>(p, c, h1, h2);
+                    herr |= d < 0;
+                }
+                if (d > 0) x += 0x10000u + (uint32_t)c;
+            }
+        }
+        uint32_t inc = x;
+#pragma unroll
+        for (int o = 1; o < kSwLanes; o <<= 1) { const uint32_t y = __shfl_up(inc, o, kSwLanes); if (lane >= o) inc += y; }
+        const int ng = (int)(__shfl(inc, kSwLanes - 1, kSwLanes) >> 16);
+        if (ng > 0) {
+            // the key table is still needed below to find each row's slot: the group table goes after the rows
+            uint32_t* s_grp = (uint32_t*)(s_row + ((nc + 1) & ~1));
+            uint32_t run = inc - x;
+            for (int q = 0; q < per; q += 2) {
+                const uint32_t wd = s_cnt[(s0 + q) >> 1];
+                uint32_t cur = 0;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
+                    int d = c > 0 ? 1 : 0;
+                    if (c > 0 && p.having_star) d = having_star_decide<NVC>(p, c, h1, h2);
+                    if (d > 0) {
+                        s_grp[run >> 16] = ((run & 0xFFFFu) << 16) | (uint32_t)c;
+                        cur |= (run & 0xFFFFu) << (16 * hh);
+                        run += 0x10000u + (uint32_t)c;
+                    } else {
+                        cur |= 0x8000u << (16 * hh);
+                    }
+                }
+                s_cnt[(s0 + q) >> 1] = cur;
+            }
+            __syncthreads();
+            for (int j = 0; j < RM; ++j) {
+                const bool mine = (cand >> j) & 1u;
+                if (!__any(mine)) continue;
+                if (mine) {
+                    const uint32_t kj = sel(key, j);
+                    int h = (int)(sw_hash(kj) & (uint32_t)(H - 1));
+                    while (s_key[h] != kj) h = (h + 1) & (H - 1);   // the row's slot (its key is in the table)
+                    const uint32_t sh = (uint32_t)(h & 1) * 16;
+                    const uint32_t pos = (atomicAdd(&s_cnt[h >> 1], 1u << sh) >> sh) & 0xFFFFu;
+                    if (pos < 0x8000u) s_row[pos] = (uint16_t)(lane + j * kSwLanes);
+                }
+            }
+            __syncthreads();
+            for (int gbase = 0; gbase < ng; gbase += kSwLanes) {
+                const int gi = gbase + lane;
+                Part<NVC> s{};
+                bool present = false;
+                uint32_t k = 0;
+                if (gi < ng) {
+                    const uint32_t gw = s_grp[gi];
+                    const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu);
+                    sw_sort_rows(s_row + g0, c);   // the placement's atomics put them in no fixed order
+                    k = kcol ? kcol[a + s_row[g0]] : 0u;
+                    fold(s, c, [&](int u) { return (int)s_row[g0 + u]; });
+                    // HAVING over count(*) alone was decided by the slot scan
+                    present = p.having_star ? true : having_keep(p, s, &res.win_err[widx]);
+                }
+                emit(present, s, k);
+            }
+        }
+    }
+    if (__any(herr) && lane == 0) atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
+    __syncthreads();   // the next window reuses the LDS
+    return emitted;
+}
+
+// Persistent waves over the launch's windows (grid-stride): the next window's keys are loaded while this one is
+// grouped, so a wave never waits for its keys after the first window.
+template <int NVC, bool WHERE, int RM>
+__global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
+                                                       const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
+                                                       const int64_t* __restrict__ obase, Results res, int nwin, SwArith ar) {
+    const DPlan& p = *pp;
+    const int lane = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
+    // HAVING over count(*) alone: the decisions for one- and two-row groups, once per wave
     int h1 = 1, h2 = 1;
     if (p.having_star) {
         Part<NVC> cp{};
@@ -666,130 +882,30 @@ __global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, 
         cp.cnt = 2;
         h2 = having_decide(p, cp);
     }
-    const int per = H / kSwLanes;   // slots per lane (even)
-    const int s0 = lane * per;
-    uint32_t x = 0;                 // kept groups << 16 | kept rows of this lane's slots
-    bool herr = false;
-    for (int q = 0; q < per; q += 2) {
-        const uint32_t wd = s_cnt[(s0 + q) >> 1];
+    auto window_a = [&](int i) { return wlist ? ab[2 * wlist[i]] : ar.a0 + (int64_t)i * ar.len; };
+    auto window_n = [&](int i) { return wlist ? (int)(ab[2 * wlist[i] + 1] - ab[2 * wlist[i]]) : ar.len; };   // 1..kSmallWin
+    uint32_t key[RM];
+    auto load_keys = [&](int i, uint32_t (&k)[RM]) {
+        const int64_t a = window_a(i);
+        const int n = window_n(i);
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
-            if (c == 0) continue;
-            int d = 1;
-            if (p.having_star) {
-                d = having_star_decide<NVC>(p, c, h1, h2);
-                herr |= d < 0;
-            }
-            if (d > 0) x += 0x10000u + (uint32_t)c;
-        }
+        for (int j = 0; j < RM; ++j) k[j] = (kcol && lane + j * kSwLanes < n) ? kcol[a + lane + j * kSwLanes] : 0u;
+    };
+    int i = blockIdx.x;
+    if (i < nwin) load_keys(i, key);
+    for (; i < nwin; i += gridDim.x) {
+        const int w = wlist ? wlist[i] : i;
+        const int64_t a = window_a(i);
+        const int n = window_n(i);
+        const int32_t widx = wlist ? slots[w] : ar.slot0 + i;
+        const int64_t out = wlist ? obase[w] : ar.ob0 + (int64_t)i * ar.rowcap;
+        uint32_t nkey[RM] = {};
+        if (i + (int)gridDim.x < nwin) load_keys(i + gridDim.x, nkey);
+        const int64_t e = sw_window<NVC, WHERE, RM>(p, b, kcol, a, n, widx, out, key, res, s_dyn, h1, h2);
+        if (e >= 0 && lane == 0) res.win_cnt[widx] = e;
+#pragma unroll
+        for (int j = 0; j < RM; ++j) key[j] = nkey[j];
     }
-    if (__any(herr) && lane == 0) atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < kSwLanes; o <<= 1) { const uint32_t y = __shfl_up(inc, o, kSwLanes); if (lane >= o) inc += y; }
-    const uint32_t tot = __shfl(inc, kSwLanes - 1, kSwLanes);
-    const int ng = (int)(tot >> 16);
-    if (ng == 0) {   // nothing kept (C4b: most windows hold no key twice)
-        if (lane == 0) res.win_cnt[widx] = 0;
-        return;
-    }
-    {
-        uint32_t run = inc - x;
-        for (int q = 0; q < per; q += 2) {
-            const uint32_t wd = s_cnt[(s0 + q) >> 1];
-            uint32_t cur = 0;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
-                int d = c > 0 ? 1 : 0;
-                if (c > 0 && p.having_star) d = having_star_decide<NVC>(p, c, h1, h2);
-                if (d > 0) {
-                    s_key[run >> 16] = ((run & 0xFFFFu) << 16) | (uint32_t)c;
-                    cur |= (run & 0xFFFFu) << (16 * hh);
-                    run += 0x10000u + (uint32_t)c;
-                } else {
-                    cur |= 0x8000u << (16 * hh);
-                }
-            }
-            s_cnt[(s0 + q) >> 1] = cur;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RM; ++j) {
-        if (sl[j] < 0) continue;
-        const uint32_t sh = (uint32_t)(sl[j] & 1) * 16;
-        const uint32_t pos = (atomicAdd(&s_cnt[sl[j] >> 1], 1u << sh) >> sh) & 0xFFFFu;
-        if (pos < 0x8000u) s_row[pos] = (uint16_t)(lane + j * kSwLanes);
-    }
-    __syncthreads();
-    int fl[NVC], col[NVC];
-    bool isf[NVC];
-#pragma unroll
-    for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; col[v] = v < p.n_vc ? p.vc_col[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
-    int64_t emitted = 0;
-    for (int base = 0; base < ng; base += kSwLanes) {
-        const int gi = base + lane;
-        Part<NVC> s{};
-        bool present = false;
-        uint32_t key = 0;
-        if (gi < ng) {
-            const uint32_t gw = s_key[gi];
-            const int g0 = (int)(gw >> 16), c = (int)(gw & 0xFFFFu), g1 = g0 + c;
-            sw_sort_rows(s_row + g0, c);   // the placement's atomics put them in no fixed order
-            key = kcol ? kcol[a + s_row[g0]] : 0u;
-            int64_t vc[NVC], is[NVC];
-            double fs[NVC], m2[NVC];
-            uint64_t mn[NVC], mx[NVC];
-#pragma unroll
-            for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
-            for (int u = g0; u < g1; ++u) {
-                const int64_t r = a + s_row[u];
-#pragma unroll
-                for (int v = 0; v < NVC; ++v) {
-                    if (!fl[v] || !col_valid(b, col[v], r)) continue;
-                    const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
-                    const double xv = isf[v] ? __longlong_as_double(raw) : (double)raw;
-                    const uint64_t o = isf[v] ? f64_to_ord(xv) : i64_to_ord(raw);
-                    vc[v]++;
-                    is[v] = (int64_t)((uint64_t)is[v] + (uint64_t)raw);
-                    fs[v] = __dadd_rn(fs[v], xv);
-                    mn[v] = o < mn[v] ? o : mn[v];
-                    mx[v] = o > mx[v] ? o : mx[v];
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < NVC; ++v) {   // centred second pass (stats._variance shape)
-                if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;
-                const double mean = __ddiv_rn(fs[v], (double)vc[v]);
-                for (int u = g0; u < g1; ++u) {
-                    const int64_t r = a + s_row[u];
-                    if (!col_valid(b, col[v], r)) continue;
-                    const int64_t raw = ((const int64_t*)b.col[col[v]])[r];
-                    const double d = __dsub_rn(isf[v] ? __longlong_as_double(raw) : (double)raw, mean);
-                    m2[v] = __dadd_rn(m2[v], __dmul_rn(d, d));
-                }
-            }
-            part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-            // HAVING over count(*) alone was decided by the slot scan; any other HAVING here
-            present = p.having_star ? true : having_keep(p, s, &res.win_err[widx]);
-        }
-        const unsigned long long m = __ballot(present);
-        if (present) {
-            const int64_t pos = out + emitted + __popcll(m & ((1ull << lane) - 1ull));
-            res.key[pos] = key;
-#pragma unroll
-            for (int k = 0; k < EK_MAX_AGGS; ++k) {
-                if (k >= p.n_aggs) break;
-                const Val v = agg_value(p, s, k);
-                res.tag[k][pos] = v.tag == V_NULL ? EK_TAG_NULL : (v.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
-                res.val[k][pos] = v.tag == V_F64 ? __double_as_longlong(v.f) : v.i;
-            }
-        }
-        emitted += __popcll(m);
-    }
-    if (lane == 0) res.win_cnt[widx] = emitted;
 }
 
 }  // namespace ek

@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 7
+EKGPU_ABI_VERSION = 8
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -87,6 +87,9 @@ class ek_plan(C.Structure):
         ("derived_type", C.c_int32 * EK_MAX_DERIVED),
         ("n_derived_prog", C.c_int32 * EK_MAX_DERIVED),
         ("derived_prog", (ek_instr * EK_MAX_PROG) * EK_MAX_DERIVED),
+        ("n_filter", C.c_int32),
+        ("filter_prog", ek_instr * EK_MAX_PROG),
+        ("sliding_send_twice", C.c_int32),
     ]
 
 

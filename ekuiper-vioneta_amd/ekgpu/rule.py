@@ -10,7 +10,7 @@ Supported subset (everything the BASELINE configs and the reference's window tes
   SELECT <key | agg(col | arithmetic over columns) | count(*) | window_start() | window_end()> [AS alias], ...
   FROM <stream> [WHERE <expr>]
   GROUP BY [<key>,] TUMBLINGWINDOW|HOPPINGWINDOW|SLIDINGWINDOW|SESSIONWINDOW|COUNTWINDOW(...)
-           [OVER (WHEN <expr>)]
+           [FILTER (WHERE <expr>)] [OVER (WHEN <expr>)]
   [HAVING <expr>]
 Expressions: comparisons, AND/OR, + - * / %, numeric literals, column refs, aggregate calls (HAVING).
 GROUP BY dimensions: one dictionary-encoded key column (type "key") goes to the engine as is; any other set of
@@ -333,15 +333,18 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                  window_version: str = "", sliding_send_twice: bool = False) -> CompiledRule:
     """schema: ordered {column: "bigint" | "float" | "key" | "string"}; the TIMESTAMP column must be bigint (epoch
     ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring).
-    sliding_send_twice: the rule option enableSlidingWindowSendTwice (a delayed sliding window also emits its first
-    part at the trigger, event_window_trigger.go:156-161) only changes a SLIDINGWINDOW with a delay: that case is not
-    implemented and is rejected; for every other window the option has no effect and is ignored."""
+    sliding_send_twice: the rule option planOptimizeStrategy.windowOption.enableSendSlidingWindowTwice
+    (def/rule.go:104-112): a delayed SLIDINGWINDOW emits its first part at the trigger and its second part when the
+    delay expires (window_op.go:98,355-373, event_window_trigger.go:156-161); no effect on other windows."""
     rule = _compile_rule(sql, schema, is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms,
                          timestamp=timestamp, num_keys=num_keys, tz_offset_s=tz_offset_s,
                          debug_membership=debug_membership, nullable=nullable, incremental=incremental,
                          window_version=window_version)
-    if sliding_send_twice and rule.plan.window_type == A.EK_WINDOW_SLIDING and rule.plan.delay > 0:
-        raise RuleError("enableSlidingWindowSendTwice with a delayed SLIDINGWINDOW is not supported by the GPU path")
+    # window_op.go:98: the option only holds for a sliding window with a delay
+    rule.plan.sliding_send_twice = 1 if (sliding_send_twice and rule.plan.window_type == A.EK_WINDOW_SLIDING and
+                                         rule.plan.delay > 0) else 0
+    rule.options.setdefault("planOptimizeStrategy", {}).setdefault("windowOption", {})[
+        "enableSendSlidingWindowTwice"] = bool(sliding_send_twice)
     return rule
 
 
@@ -433,6 +436,7 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
     key_col = -1
     dims: List[str] = []
     trigger = []
+    wfilter = []
     begin, emit = [], []
     wtype = A.EK_WINDOW_NONE
     if p.kw("group"):
@@ -472,6 +476,12 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
                         nums.append(int(p.peek()))
                         p.i += 1
                 p.expect(")")
+                if p.kw("filter"):
+                    # the window's FILTER (WHERE <cond>) clause (parser.go: WindowPlan.condition, planner.go:388-392)
+                    p.expect("(")
+                    p.expect("where")
+                    wfilter = p.expr(False)
+                    p.expect(")")
                 plan.length = nums[0] if nums else 0
                 if wtype in (A.EK_WINDOW_HOPPING, A.EK_WINDOW_SESSION, A.EK_WINDOW_COUNT):
                     plan.interval = nums[1] if len(nums) > 1 else 0
@@ -547,7 +557,7 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
     if strings:
         free = (A.EK_AGG_FIRST, A.EK_AGG_COUNT, A.EK_AGG_MIN, A.EK_AGG_MAX)
         used = {p.columns[c] for (fn, c, _) in p.aggs if c >= 0 and c < len(p.columns) and fn not in free}
-        for prog in [where, having, trigger, begin, emit] + [list(pr) for pr, _ in p.derived]:
+        for prog in [where, having, trigger, wfilter, begin, emit] + [list(pr) for pr, _ in p.derived]:
             used |= {p.columns[ins[1]] for ins in prog if ins[0] == A.EK_OP_COL and ins[1] < len(p.columns)}
         if used & strings:
             raise RuleError(f"string column(s) {sorted(used & strings)} may only be GROUP BY dimensions, min / max / count arguments or first-row fields")
@@ -563,6 +573,7 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
     plan.n_where = _fill_prog(plan.where_prog, where)
     plan.n_having = _fill_prog(plan.having_prog, having)
     plan.n_trigger = _fill_prog(plan.trigger_prog, trigger)
+    plan.n_filter = _fill_prog(plan.filter_prog, wfilter)
     plan.n_begin = _fill_prog(plan.begin_prog, begin)
     plan.n_emit = _fill_prog(plan.emit_prog, emit)
     if key_col >= 0 and num_keys <= 0:

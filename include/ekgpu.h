@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 7
+#define EKGPU_ABI_VERSION 8
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -162,6 +162,19 @@ typedef struct {
     int32_t derived_type[EK_MAX_DERIVED];
     int32_t n_derived_prog[EK_MAX_DERIVED];
     ek_instr derived_prog[EK_MAX_DERIVED][EK_MAX_PROG];
+    /* ABI v8. The window's FILTER (WHERE <cond>) clause (WindowPlan.condition, planner.go:388-392,639-641): a FilterOp
+     * planned between the WatermarkOp and the window, so a row whose condition is not true never reaches the window —
+     * it is no member, no OVER (WHEN) trigger and no gcInputs edge — while it still moved the watermark (event time).
+     * An evaluation error drops the row and is counted in ek_stats.records_filter_error (the reference forwards that
+     * row's error, filter_operator.go:41-57). In processing time under TUMBLING / HOPPING / SESSION the planner combines
+     * it with WHERE and pushes both below the window (windowPlan.go:82-99: WHERE AND FILTER). */
+    int32_t n_filter;
+    ek_instr filter_prog[EK_MAX_PROG];
+    /* ABI v8. def.RuleOption.PlanOptimizeStrategy.WindowOption.EnableSendSlidingWindowTwice (def/rule.go:104-112,
+     * window_op.go:98): a SLIDINGWINDOW with a delay D emits the rows (t - length, t] when its trigger t fires and the
+     * rows (t, t + D] when the delay expires (handleInputsForSlidingWindow, window_op.go:576-603; the second part's
+     * WindowRange is [t, t + D]). Ignored for every other window. */
+    int32_t sliding_send_twice;
 } ek_plan;
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };
@@ -330,7 +343,7 @@ typedef struct {
 } ek_global_ctx;
 
 /* ---------------------------------------------------------------- processing-time clock
- * Processing-time TUMBLING / HOPPING / SLIDING (no delay) / SESSION windows (WindowOperator.execProcessingWindow,
+ * Processing-time TUMBLING / HOPPING / SLIDING / SESSION windows (WindowOperator.execProcessingWindow,
  * window_op.go:235-470) run under the caller's clock, the way the reference's tests drive them with its mock clock
  * (pkg/timex/time.go:31-100): every row carries its arrival time in the plan's ts_column (non-decreasing); the clock
  * reaches a row's timestamp before the row is delivered, so every ticker / timeout due at or before it fires first.

@@ -787,6 +787,7 @@ typedef struct {
     int64_t next_end, prev_end; /* prev_end ZERO_MS = IsZero */
     vec64 trigger_ts, delay_ts;
     int last_ticked;
+    int send_twice;            /* enableSlidingWindowSendTwice (window_op.go:98): delayed sliding windows only */
     int64_t* ts;
     vec64 content;
     /* shard model (eko_run_shard): the window op of one key-hash shard fed the global WatermarkTuples */
@@ -842,8 +843,33 @@ static void handle_inputs(winop* o, int64_t right, int64_t* keep_from) {
     *keep_from = nextleft < 0 ? o->inputs.n : nextleft;
 }
 
+/* window_op.go:576-603 handleInputsForSlidingWindow (enableSlidingWindowSendTwice): content = the inputs with
+ * windowStart < ts <= windowEnd; an input with ts < discardedLeft = windowEnd - (length + delay) (- calDelta: 0 once
+ * triggerTime is set, MaxInt16 ns before, invisible at ms resolution) is expired and nextleft = the LAST expired index;
+ * the inputs kept are inputs[:nextleft+1] — the expired prefix: the reference keeps those and drops the rest —
+ * unless no input expired (unchanged) or every one did (none). */
+static void handle_inputs_sliding(winop* o, int64_t ws, int64_t we) {
+    const int64_t dl = we - (o->L + o->D);
+    int64_t nextleft = -1;
+    o->content.n = 0;
+    for (int64_t i = 0; i < o->inputs.n; ++i) {
+        const int64_t t = ev_ts(o, o->inputs.a[i]);
+        if (t < dl) { nextleft = i; continue; }
+        if (t > ws && t <= we) v_push(&o->content, o->inputs.a[i]);
+    }
+    if (nextleft < 0) return;
+    o->inputs.n = nextleft == o->inputs.n - 1 ? 0 : nextleft + 1;
+}
+
 /* window_op.go:675-721 scan */
 static void scan(winop* o, int64_t t, int64_t length, int is_first_part) {
+    if (o->send_twice && o->wtype == EK_WINDOW_SLIDING) {
+        handle_inputs_sliding(o, t - length, t);
+        /* WindowRange: [t - length, t] for both parts (the second part's third field is its trigger, t - delay) */
+        emit_window(o->d, o->ob, t - length, t, o->content.a, o->content.n);
+        o->trigger_time = t; o->has_trigger = 1;
+        return;
+    }
     int64_t keep_from;
     handle_inputs(o, t, &keep_from);
     int64_t tt = o->has_trigger ? o->trigger_time : ZERO_MS;
@@ -981,8 +1007,12 @@ static void win_on_watermark(winop* o, int64_t wm) {
         }
         if (o->wtype == EK_WINDOW_SLIDING) {
             while (o->trigger_ts.n > 0 && o->trigger_ts.a[0] <= wm) {
-                if (o->D > 0) v_push(&o->delay_ts, o->trigger_ts.a[0] + o->D);
-                else scan(o, o->trigger_ts.a[0], o->L + o->D, 1);
+                if (o->D > 0) {
+                    v_push(&o->delay_ts, o->trigger_ts.a[0] + o->D);
+                    if (o->send_twice) scan(o, o->trigger_ts.a[0], o->L, 1);   /* the first part, at the trigger */
+                } else {
+                    scan(o, o->trigger_ts.a[0], o->L + o->D, 1);
+                }
                 v_erase_front(&o->trigger_ts, 1);
             }
         } else {
@@ -1103,6 +1133,17 @@ static void finish_output(const ek_plan* p, outbuf* ob, eko_output* out) {
     out->win_error = ob->werr ? ob->werr : (char*)calloc(1, 128);
 }
 
+/* FilterOp.Apply of the window's FILTER (WHERE ...) clause on one row (filter_operator.go:41-57): true keeps it;
+ * nil / false drop it; an evaluation error or a non-bool drops it and is counted (the reference forwards that error) */
+static int filter_pass(const dataset* d, int64_t row, int64_t* n_err) {
+    const ek_plan* p = d->p;
+    if (p->n_filter <= 0) return 1;
+    val_t r = eval_prog(p->filter_prog, p->n_filter, d, row, NULL);
+    if (r.tag == V_BOOL) return r.i != 0;
+    if (r.tag != V_NULL && n_err) (*n_err)++;
+    return 0;
+}
+
 int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity, eko_output* out) {
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
@@ -1167,6 +1208,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         o.raw_interval = (p->window_type == EK_WINDOW_HOPPING) ? p->interval : p->length; /* planner.go:394-400 */
         o.unit = p->time_unit; o.tz = p->tz_offset_s;
         o.next_end = MAXT_MS; o.prev_end = ZERO_MS;
+        o.send_twice = p->sliding_send_twice && p->window_type == EK_WINDOW_SLIDING && o.D > 0;
 
         /* WatermarkOp (single stream) watermark_op.go:54-67,144-225 */
         int64_t lateTol = p->late_tolerance_ms;
@@ -1189,6 +1231,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                     int64_t c = buf.n;
                     for (int64_t k = 0; k < buf.n; ++k) if (ts[buf.a[k]] > wm) { c = k; break; }
                     for (int64_t k = 0; k < c; ++k) {
+                        /* the window's FILTER (WHERE ...) op between WatermarkOp and the window (planner.go:388-392) */
+                        if (!filter_pass(&d, buf.a[k], &out->records_filter_error)) continue;
                         if (p->window_type == EK_WINDOW_STATE) state_on_row(&so, buf.a[k]);
                         else if (inc_slide) incslide_on_event(&isl, buf.a[k]);
                         else if (inc_count) inccount_on_event(&icn, buf.a[k]);
@@ -1221,7 +1265,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
     } else if (p->window_type == EK_WINDOW_STATE) {
-        for (int64_t i = 0; i < n; ++i) state_on_row(&so, i);
+        for (int64_t i = 0; i < n; ++i)
+            if (filter_pass(&d, i, &out->records_filter_error)) state_on_row(&so, i);
     } else {
         if (p->window_type == EK_WINDOW_NONE) {
             /* window-less rule: FilterOp.Apply per event (filter_operator.go:36-90) + SELECT * projection.
@@ -1260,6 +1305,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         vec64 inputs; memset(&inputs, 0, sizeof inputs);
         int64_t msg = 0;
         for (int64_t i = 0; i < n; ++i) {
+            if (!filter_pass(&d, i, &out->records_filter_error)) continue;   /* window FILTER before the window */
             v_push(&inputs, i);
             msg++;
             if (msg % itv != 0) continue;
@@ -1281,25 +1327,38 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
 }
 
 /* ------------------------------------------------------------------ processing time (deterministic clock)
- * WindowOperator.execProcessingWindow (window_op.go:235-470) for TUMBLING / HOPPING / SLIDING (no delay) / SESSION,
- * driven by a clock the way the reference's own tests drive it (pkg/timex/time.go:31-100 mock clock;
- * topotest/mock_topo.go:208-235,263-268): the rule opens at start_ms; before row i is delivered the clock is set to
- * its timestamp ts_i (the row's arrival time) and every timer due at or before ts_i fires first, in due order (a
- * ticker before a session timeout due at the same instant); after the last row the clock moves to end_ms.
+ * WindowOperator.execProcessingWindow (window_op.go:235-470) for TUMBLING / HOPPING / SLIDING / SESSION, driven by a
+ * clock the way the reference's own tests drive it (pkg/timex/time.go:31-100 mock clock; topotest/mock_topo.go:208-235,
+ * 263-268): the rule opens at start_ms (Exec sets triggerTime = now, window_op.go:149-151); before row i is delivered
+ * the clock is set to its timestamp ts_i (the row's arrival time) and every timer due at or before ts_i fires first,
+ * in due order (a ticker before a session timeout due at the same instant); after the last row the clock moves to
+ * end_ms.
  *   tickers (getFirstTimer + setupTicker, window_op.go:228-233,250-260,471-481): the first tick at
  *     getAlignedWindowEndTime(start_ms, rawInterval) (rawInterval = length for tumbling / session, interval for
  *     hopping, planner.go:394-400), then every length (tumbling, session) or interval (hopping);
  *   tick (window_op.go:483-499): scan(tick); a session window scans only when it has inputs and the first one is at
  *     least `length` before the tick;
  *   rows (window_op.go:343-419): appended to the inputs; SLIDING: a row matching OVER (WHEN) scans at its own
- *     timestamp, any other row garbage-collects the inputs that expired (gcInputs, window_op.go:657-673: ts + length
- *     <= t); SESSION: the timeout timer is (re)armed at ts + timeout, the first row of a session sets triggerTime;
+ *     timestamp, or with a delay D arms a timer due at ts + D (window_op.go:355-373) that scans [ts - length, ts + D)
+ *     — with enableSlidingWindowSendTwice the row first scans its first part (ts - length, ts] and the timer the second
+ *     part (ts, ts + D]; any other row garbage-collects the inputs that expired (gcInputs, window_op.go:657-673:
+ *     ts + length + delay <= t); SESSION: the timeout timer is (re)armed at ts + timeout, the first row of a session
+ *     sets triggerTime;
  *   session timeout (window_op.go:448-461): scan(now) over the whole inputs, then every input is dropped.
- * WHERE: windowPlan.PushDownPredicate (windowPlan.go:82-99) moves it below a processing-time TUMBLING / HOPPING /
- * SESSION window: a row whose WHERE is not true never reaches the window (an evaluation error drops the row; the
- * reference forwards that error by itself, not as a window result). Rows must arrive with non-decreasing ts. */
-int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
-                 int64_t start_ms, int64_t end_ms, eko_output* out) {
+ * WHERE / FILTER: windowPlan.PushDownPredicate (windowPlan.go:82-99) moves WHERE AND the window's FILTER below a
+ * processing-time TUMBLING / HOPPING / SESSION window: a row whose combined condition is not true never reaches the
+ * window (an evaluation error drops the row; the reference forwards that error by itself, not as a window result).
+ * Under SLIDING the FILTER op alone sits before the window (planner.go:388-392) and WHERE stays above it.
+ * Restart (rs != NULL, rs->split >= 0): rows [0, split) are delivered, the clock moves to rs->export_ms and the rule
+ * is checkpointed — inputs, triggerTime once a scan or a session's first row stored it (TriggerTimeKey) — then it
+ * restarts at rs->restart_ms: the timers are gone (a session's timeout is re-armed by its next row), the tickers are
+ * re-aligned to the restart, triggerTime is the restored one or the restart time, and the restored inputs are
+ * replayed (window_op.go:268-325): TUMBLING / HOPPING scan at triggerTime + k * interval while <= restart + interval;
+ * SESSION scans at the next session end computed over the inputs while <= restart + timeout (the reference panics on
+ * inputs[0] once a replay emptied the inputs and re-scans the same end forever when none is found: both stop the
+ * replay here). Rows must arrive with non-decreasing ts. */
+int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
+                         int64_t start_ms, int64_t end_ms, const eko_restart* rs, eko_output* out) {
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
     const int wt = p->window_type;
@@ -1307,14 +1366,18 @@ int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const 
         set_status(out, EK_ERR_UNSUPPORTED, "processing-time clock runs are for TUMBLING / HOPPING / SLIDING / SESSION"); return out->status;
     }
     if (p->incremental || p->window_version == 2) { set_status(out, EK_ERR_UNSUPPORTED, "incremental / v2 windows are not restated in processing time"); return out->status; }
-    if (wt == EK_WINDOW_SLIDING && p->delay != 0) { set_status(out, EK_ERR_UNSUPPORTED, "delayed processing-time sliding windows are not restated"); return out->status; }
     if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "processing-time rows need their arrival timestamp column"); return out->status; }
+    const int64_t split = rs && rs->split >= 0 ? (rs->split < n ? rs->split : n) : -1;
+    if (split >= 0 && (rs->export_ms < start_ms || rs->restart_ms < rs->export_ms)) {
+        set_status(out, EK_ERR_INVALID, "restart: start <= export <= restart"); return out->status;
+    }
     dataset d = { p, n, columns, validity, NULL };
     outbuf ob; memset(&ob, 0, sizeof ob);
     int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
     for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
     for (int64_t i = 0; i < n; ++i)
-        if ((i > 0 && ts[i] < ts[i - 1]) || ts[i] < start_ms) {
+        if ((i > 0 && ts[i] < ts[i - 1]) || ts[i] < start_ms || (split >= 0 && i < split && ts[i] > rs->export_ms) ||
+            (split >= 0 && i >= split && ts[i] < rs->restart_ms)) {
             free(ts); set_status(out, EK_ERR_INVALID, "processing-time rows must arrive with non-decreasing timestamps after the start"); return out->status;
         }
     winop o; memset(&o, 0, sizeof o);
@@ -1323,53 +1386,123 @@ int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const 
     o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = (int64_t)p->delay * u;
     o.raw_interval = wt == EK_WINDOW_HOPPING ? p->interval : p->length;
     o.unit = p->time_unit; o.tz = p->tz_offset_s;
-    const int pushdown = p->n_where > 0 && wt != EK_WINDOW_SLIDING;
+    o.send_twice = p->sliding_send_twice && wt == EK_WINDOW_SLIDING && o.D > 0;
+    /* Exec: triggerTime = now in processing time (window_op.go:149-151) */
+    o.has_trigger = 1; o.trigger_time = start_ms;
+    int trig_saved = 0;   /* TriggerTimeKey was put (a tick / timeout scan, a session's first row) */
+    const int pushdown = wt != EK_WINDOW_SLIDING;
     const int has_tick = wt != EK_WINDOW_SLIDING;
     int64_t tick = has_tick ? eko_aligned_window_end(start_ms, o.raw_interval, o.unit, o.tz) : MAXT_MS;
     const int64_t period = wt == EK_WINDOW_HOPPING ? o.I : o.L;
     int to_exists = 0, to_armed = 0;
     int64_t to_due = 0;
-    /* every timer due at or before `now`, in due order (ticker first on a tie) */
+    vec64 dq; memset(&dq, 0, sizeof dq);   /* delayed sliding timers: due times, in order */
+    int64_t dq_head = 0;
+    /* every timer due at or before `now`, in due order (ticker first on a tie; delay timers are sliding-only) */
 #define EKO_ADVANCE(now)                                                                                        \
     for (;;) {                                                                                                  \
         const int tk = has_tick && tick <= (now);                                                               \
         const int tm = wt == EK_WINDOW_SESSION && to_armed && to_due <= (now) && (!tk || to_due < tick);        \
+        const int dl = dq_head < dq.n && dq.a[dq_head] <= (now);                                                \
         if (tm) {                                                                                               \
             to_armed = 0;                                                                                       \
-            if (o.inputs.n > 0) { scan(&o, to_due, o.L + o.D, 1); o.inputs.n = 0; to_exists = 0; }              \
+            if (o.inputs.n > 0) { scan(&o, to_due, o.L + o.D, 1); o.inputs.n = 0; to_exists = 0; trig_saved = 1; } \
         } else if (tk) {                                                                                        \
-            if (wt != EK_WINDOW_SESSION || (o.inputs.n > 0 && tick - ts[o.inputs.a[0]] >= o.L))                 \
-                scan(&o, tick, o.L + o.D, 1);                                                                   \
+            if (wt != EK_WINDOW_SESSION || (o.inputs.n > 0 && tick - ts[o.inputs.a[0]] >= o.L)) {               \
+                scan(&o, tick, o.L + o.D, 1); trig_saved = 1;                                                   \
+            }                                                                                                   \
             tick += period;                                                                                     \
+        } else if (dl) {                                                                                        \
+            const int64_t due = dq.a[dq_head++];                                                                \
+            if (o.send_twice) scan(&o, due, o.D, 0);   /* the last part (t, t + D] */                           \
+            else scan(&o, due, o.L + o.D, 1);                                                                   \
         } else break;                                                                                           \
     }
-    for (int64_t i = 0; i < n; ++i) {
+    for (int64_t i = 0; i <= n; ++i) {
+        if (i == split) {
+            EKO_ADVANCE(rs->export_ms)
+            /* checkpoint at export_ms, restart at restart_ms: timers gone, tickers re-aligned, inputs replayed */
+            to_armed = 0; to_exists = 0; dq_head = dq.n;
+            if (!trig_saved) { o.trigger_time = rs->restart_ms; o.has_trigger = 1; }
+            const int64_t R = rs->restart_ms;
+            if (o.inputs.n > 0 && (wt == EK_WINDOW_TUMBLING || wt == EK_WINDOW_HOPPING)) {
+                const int64_t itv = wt == EK_WINDOW_HOPPING ? o.I : o.L, next_tick = R + itv;
+                for (int64_t next = o.trigger_time + itv; next <= next_tick; next += itv) scan(&o, next, o.L + o.D, 1);
+            } else if (o.inputs.n > 0 && wt == EK_WINDOW_SESSION) {
+                const int64_t timeout = o.I, duration = o.L, next_tick = R + o.I;
+                while (o.inputs.n > 0) {
+                    const int64_t et = ts[o.inputs.a[0]];
+                    const int64_t dd = et % duration;
+                    int64_t tk2 = dd == 0 ? et : et + duration - dd;
+                    int64_t pp = ZERO_MS, next = MAXT_MS;
+                    for (int64_t k = 0; k < o.inputs.n; ++k) {
+                        const int64_t tt = ts[o.inputs.a[k]];
+                        int64_t r = MAXT_MS;
+                        if (pp != ZERO_MS && tt - pp > timeout) r = pp + timeout;
+                        if (tt > tk2) {
+                            if (tk2 - et > duration && tk2 < r) r = tk2;
+                            tk2 += duration;
+                        }
+                        if (r < MAXT_MS) { next = r; break; }
+                        pp = tt;
+                    }
+                    if (next == MAXT_MS || next > next_tick) break;
+                    scan(&o, next, o.L + o.D, 1);
+                }
+            }
+            if (has_tick) tick = eko_aligned_window_end(R, o.raw_interval, o.unit, o.tz);
+        }
+        if (i == n) break;
         EKO_ADVANCE(ts[i])
         if (pushdown) {
-            val_t r = eval_prog(p->where_prog, p->n_where, &d, i, NULL);
-            if (!(r.tag == V_BOOL && r.i)) continue;
+            /* WHERE AND FILTER below the window: combine(where, filter) (windowPlan.go:82-99) evaluated as the binary
+             * AND of valuer.go:574-660 (a false / error lhs decides; nil AND x -> false unless x errors) */
+            if (p->n_where > 0 || p->n_filter > 0) {
+                val_t r = mk_bool(1);
+                if (p->n_where > 0) r = eval_prog(p->where_prog, p->n_where, &d, i, NULL);
+                if (p->n_filter > 0 && r.tag != V_ERR && !(r.tag == V_BOOL && !r.i)) {
+                    const val_t rf = eval_prog(p->filter_prog, p->n_filter, &d, i, NULL);
+                    r = p->n_where > 0 ? (rf.tag == V_ERR ? rf : simple_eval(r, rf, EK_OP_AND)) : rf;
+                }
+                if (!(r.tag == V_BOOL && r.i)) {
+                    if (r.tag != V_BOOL && r.tag != V_NULL) out->records_filter_error++;
+                    continue;
+                }
+            }
+        } else if (!filter_pass(&d, i, &out->records_filter_error)) {
+            continue;   /* the window's FILTER op before a sliding window */
         }
         v_push(&o.inputs, i);
         if (wt == EK_WINDOW_SESSION) {
-            if (!to_exists) { to_exists = 1; o.trigger_time = ts[i]; o.has_trigger = 1; }
+            if (!to_exists) { to_exists = 1; o.trigger_time = ts[i]; o.has_trigger = 1; trig_saved = 1; }
             to_armed = 1;
             to_due = ts[i] + o.I;
         } else if (wt == EK_WINDOW_SLIDING) {
             if (match_trigger(&o, i)) {
-                scan(&o, ts[i], o.L + o.D, 1);
+                if (o.D > 0) {
+                    if (o.send_twice) scan(&o, ts[i], o.L, 1);   /* the first part (t - length, t] */
+                    v_push(&dq, ts[i] + o.D);
+                } else {
+                    scan(&o, ts[i], o.L + o.D, 1);
+                }
             } else {
-                int64_t g = 0;   /* gcInputs(inputs, ts + 1ns): drop the prefix with ts_k + length <= ts */
-                while (g < o.inputs.n && ts[o.inputs.a[g]] + o.L <= ts[i]) g++;
+                int64_t g = 0;   /* gcInputs(inputs, ts + 1ns): drop the prefix with ts_k + length + delay <= ts */
+                while (g < o.inputs.n && ts[o.inputs.a[g]] + o.L + o.D <= ts[i]) g++;
                 v_erase_front(&o.inputs, g);
             }
         }
     }
     EKO_ADVANCE(end_ms)
 #undef EKO_ADVANCE
-    free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
+    free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a); free(dq.a);
     free(ts);
     finish_output(p, &ob, out);
     return 0;
+}
+
+int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
+                 int64_t start_ms, int64_t end_ms, eko_output* out) {
+    return eko_run_proc_restart(p, n, columns, validity, start_ms, end_ms, NULL, out);
 }
 
 /* ------------------------------------------------------------------ shard model (multi-GPU protocol)

@@ -31,6 +31,7 @@ typedef struct {
     int64_t* members;
     /* per window error text (only for win_status != 0), 128 bytes each */
     char* win_error;
+    int64_t records_filter_error;   /* rows a pushed-down WHERE / the window FILTER dropped with an evaluation error */
 } eko_output;
 
 /* Run the whole stream (arrival order) through the reference operator chain. */
@@ -43,6 +44,12 @@ void eko_free(eko_output* out);
  * (its arrival time), and the clock finally moves to end_ms. */
 int eko_run_proc(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,
                  int64_t start_ms, int64_t end_ms, eko_output* out);
+/* The same with a checkpoint / restart (window_op.go:131-168,268-325): rows [0, split) delivered, the clock at
+ * export_ms, the rule restarted at restart_ms (timers gone, tickers re-aligned, the restored inputs replayed), then
+ * rows [split, n). split < 0: no restart. */
+typedef struct { int64_t split, export_ms, restart_ms; } eko_restart;
+int eko_run_proc_restart(const ek_plan* plan, int64_t n_rows, const void* const* columns, const uint8_t* const* validity,
+                         int64_t start_ms, int64_t end_ms, const eko_restart* rs, eko_output* out);
 
 /* Shard model of the multi-GPU protocol: one key-hash shard's rows (global arrivals g->row_arrival) with the
  * global WatermarkTuples / window anchor / sliding triggers of the whole stream (g: host memory). */

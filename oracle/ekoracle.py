@@ -29,7 +29,12 @@ class eko_output(C.Structure):
         ("member_offset", C.POINTER(C.c_int64)),
         ("members", C.POINTER(C.c_int64)),
         ("win_error", C.c_void_p),
+        ("records_filter_error", C.c_int64),
     ]
+
+
+class eko_restart(C.Structure):
+    _fields_ = [("split", C.c_int64), ("export_ms", C.c_int64), ("restart_ms", C.c_int64)]
 
 
 _lib = None
@@ -60,6 +65,10 @@ def lib():
         _lib.eko_run_proc.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                       C.c_int64, C.c_int64, C.POINTER(eko_output)]
         _lib.eko_run_proc.restype = C.c_int
+        _lib.eko_run_proc_restart.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p),
+                                              C.POINTER(C.c_void_p), C.c_int64, C.c_int64, C.POINTER(eko_restart),
+                                              C.POINTER(eko_output)]
+        _lib.eko_run_proc_restart.restype = C.c_int
         _lib.eko_shard_triggers.argtypes = [C.POINTER(A.ek_plan), C.c_int64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                             C.POINTER(A.ek_global_ctx), C.c_void_p, C.c_void_p]
         _lib.eko_shard_triggers.restype = C.c_int64
@@ -67,11 +76,13 @@ def lib():
 
 
 class OracleRun:
-    def __init__(self, windows, members: List[np.ndarray], records_late: int, errors: List[str]):
+    def __init__(self, windows, members: List[np.ndarray], records_late: int, errors: List[str],
+                 records_filter_error: int = 0):
         self.windows = windows
         self.members = members
         self.records_late = records_late
         self.errors = errors
+        self.records_filter_error = records_filter_error
 
 
 def _col_arrays(plan: A.ek_plan, columns: List[np.ndarray]):
@@ -106,7 +117,7 @@ def _collect(L, out) -> OracleRun:
         members = [mem[moff[w]:moff[w + 1]] for w in range(nw)]
         raw = C.string_at(out.win_error, 128 * max(nw, 1))
         errors = [raw[128 * w:128 * (w + 1)].split(b"\0")[0].decode() for w in range(nw)]
-        return OracleRun(wins, members, int(out.records_late), errors)
+        return OracleRun(wins, members, int(out.records_late), errors, int(out.records_filter_error))
     finally:
         L.eko_free(C.byref(out))
 
@@ -130,6 +141,22 @@ def run_proc(plan: A.ek_plan, columns: List[np.ndarray], start_ms: int, end_ms: 
     n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
     out = eko_output()
     rc = L.eko_run_proc(C.byref(plan), n, cptr, vptr, int(start_ms), int(end_ms), C.byref(out))
+    if rc != 0:
+        msg = out.error.decode()
+        raise RuntimeError(f"oracle error {rc}: {msg}")
+    return _collect(L, out)
+
+
+def run_proc_restart(plan: A.ek_plan, columns: List[np.ndarray], start_ms: int, end_ms: int, split: int,
+                     export_ms: int, restart_ms: int,
+                     validity: Optional[List[Optional[np.ndarray]]] = None) -> OracleRun:
+    """run_proc with a checkpoint after row `split` at clock export_ms and the rule restarted at restart_ms
+    (eko_run_proc_restart: timers dropped, tickers re-aligned, restored inputs replayed, window_op.go:268-325)."""
+    L = lib()
+    n, cptr, vptr, _keep = _ptrs(plan, columns, validity)
+    out = eko_output()
+    rs = eko_restart(int(split), int(export_ms), int(restart_ms))
+    rc = L.eko_run_proc_restart(C.byref(plan), n, cptr, vptr, int(start_ms), int(end_ms), C.byref(rs), C.byref(out))
     if rc != 0:
         msg = out.error.decode()
         raise RuntimeError(f"oracle error {rc}: {msg}")

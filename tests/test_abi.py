@@ -138,15 +138,25 @@ def test_oracle_expression_argument_is_per_row(oracle):
         assert np.allclose(a, b * 1.8 + 32, rtol=1e-12, atol=1e-9)
 
 
-def test_sliding_send_twice_rejected():
-    """enableSlidingWindowSendTwice (event_window_trigger.go:156-161) is not modelled: the lowering refuses it."""
-    from ekgpu.rule import RuleError, compile_rule
+def test_sliding_send_twice_plan():
+    """enableSlidingWindowSendTwice (def/rule.go:104-112) lowers to ek_plan.sliding_send_twice for a delayed
+    SLIDINGWINDOW only (window_op.go:98); every other window ignores it."""
+    from ekgpu.rule import compile_rule
     sql = "SELECT count(*) FROM s GROUP BY SLIDINGWINDOW(ss, 10, 2)"
-    compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1)
-    with pytest.raises(RuleError):
-        compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1, sliding_send_twice=True)
-    # the option only changes a delayed sliding window: without a delay, and for other windows, it is ignored
+    assert compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1).plan.sliding_send_twice == 0
+    r = compile_rule(sql, {"a": "bigint", "ts": "bigint"}, num_keys=1, sliding_send_twice=True)
+    assert r.plan.sliding_send_twice == 1 and r.plan.delay == 2
     for other in ("SLIDINGWINDOW(ss, 10)", "TUMBLINGWINDOW(ss, 10)", "HOPPINGWINDOW(ss, 10, 5)"):
         r = compile_rule(f"SELECT count(*) FROM s GROUP BY {other}", {"a": "bigint", "ts": "bigint"}, num_keys=1,
                          sliding_send_twice=True)
-        assert r.plan.delay == 0
+        assert r.plan.delay == 0 and r.plan.sliding_send_twice == 0
+
+
+def test_window_filter_lowering():
+    """GROUP BY <window> FILTER (WHERE <cond>) (planner.go:388-392) lowers to ek_plan.filter_prog; WHERE stays."""
+    from ekgpu import abi as A
+    from ekgpu.rule import compile_rule
+    r = compile_rule("SELECT count(*) FROM s WHERE a > 1 GROUP BY SLIDINGWINDOW(ss, 5) FILTER (WHERE a < 9) OVER (WHEN a = 3)",
+                     {"a": "bigint", "ts": "bigint"}, num_keys=1)
+    assert r.plan.n_where == 3 and r.plan.n_filter == 3 and r.plan.n_trigger == 3
+    assert [r.plan.filter_prog[k].op for k in range(3)] == [A.EK_OP_COL, A.EK_OP_CONST_I64, A.EK_OP_LT]

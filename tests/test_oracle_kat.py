@@ -115,9 +115,9 @@ def test_processing_window_kat(oracle, case):
     row's second, rows arrive at their timestamps, the run ends at the last row (eko_run_proc)."""
     g = _load("kat_window_proc.json")
     cols = _stream_cols(g["streams"][case["stream"]])
-    rule = compile_rule(case["sql"], SCHEMA, is_event_time=False, num_keys=4)
-    start = int(cols[0][0]) // 1000 * 1000
-    run = oracle.run_proc(rule.plan, cols, start, int(cols[0][-1]))
+    rule = compile_rule(case["sql"], SCHEMA, is_event_time=False, num_keys=4, **case.get("options", {}))
+    start = case.get("start_ms", int(cols[0][0]) // 1000 * 1000)
+    run = oracle.run_proc(rule.plan, cols, start, case.get("end_ms", int(cols[0][-1])))
     assert len(run.windows) == case["windows_out"]
     for w, members, exp in zip(run.windows, run.members, case["windows"]):
         assert sorted(int(m) for m in members) == exp["members"]

@@ -46,8 +46,10 @@ def test_processing_kat_engine(oracle, engine_mod, case):
     rows = np.array(g["streams"][case["stream"]]["rows"], dtype=object)
     cols = [np.array(rows[:, 0], np.int64), np.array(rows[:, 1], np.int64), np.array(rows[:, 2], np.uint32),
             np.array(rows[:, 3], np.float64)]
-    rule = compile_rule(case["sql"], KAT_SCHEMA, is_event_time=False, num_keys=4, debug_membership=True)
-    start, end = int(cols[0][0]) // 1000 * 1000, int(cols[0][-1])
+    rule = compile_rule(case["sql"], KAT_SCHEMA, is_event_time=False, num_keys=4, debug_membership=True,
+                        **case.get("options", {}))
+    start = case.get("start_ms", int(cols[0][0]) // 1000 * 1000)
+    end = case.get("end_ms", int(cols[0][-1]))
     exp = oracle.run_proc(rule.plan, cols, start, end)
     assert len(exp.windows) == case["windows_out"]
     n = len(cols[0])
@@ -76,6 +78,20 @@ CASES = [
     ("session", "SELECT k, count(*), avg(x) FROM s GROUP BY k, SESSIONWINDOW(ss, 5, 1)"),
     ("session_where", "SELECT k, count(*), sum(y) FROM s WHERE x < 60 GROUP BY k, SESSIONWINDOW(ss, 4, 1)"),
     ("ungrouped_tumbling", "SELECT count(*), avg(x) FROM s GROUP BY TUMBLINGWINDOW(ss, 1)"),
+    # the window FILTER (WHERE ...) op (planner.go:388-392): combined with WHERE below tumbling / hopping / session,
+    # alone before sliding windows
+    ("tumbling_filter", "SELECT k, sum(x), count(*) FROM s WHERE y > 20 GROUP BY k, TUMBLINGWINDOW(ss, 1) FILTER (WHERE x < 70)"),
+    ("hopping_filter", "SELECT k, max(x), count(*) FROM s GROUP BY k, HOPPINGWINDOW(ss, 2, 1) FILTER (WHERE y > 40)"),
+    ("session_filter", "SELECT k, count(*), avg(y) FROM s GROUP BY k, SESSIONWINDOW(ss, 4, 1) FILTER (WHERE x > 10)"),
+    ("sliding_filter", "SELECT k, count(*), min(x) FROM s WHERE y < 80 GROUP BY k, SLIDINGWINDOW(ms, 400) FILTER (WHERE x > 30) OVER (WHEN x > 97)"),
+    # delayed sliding windows (window_op.go:355-373): a timer per trigger, the window [t - length, t + delay)
+    ("sliding_delay", "SELECT k, count(*), stddev(x) FROM s GROUP BY k, SLIDINGWINDOW(ms, 500, 300) OVER (WHEN x > 98)"),
+    ("sliding_delay_where", "SELECT k, count(*), sum(y) FROM s WHERE y > 25 GROUP BY k, SLIDINGWINDOW(ss, 1, 2) OVER (WHEN x > 99)"),
+]
+# enableSlidingWindowSendTwice (window_op.go:98): first part at the trigger, second part when the delay expires
+SEND_TWICE = [
+    ("send_twice", "SELECT k, count(*), max(x) FROM s GROUP BY k, SLIDINGWINDOW(ms, 500, 300) OVER (WHEN x > 98)"),
+    ("send_twice_long_delay", "SELECT count(*), avg(y) FROM s GROUP BY SLIDINGWINDOW(ms, 200, 2000) OVER (WHEN x > 99)"),
 ]
 
 
@@ -87,6 +103,22 @@ def test_processing_windows_parity(oracle, engine_mod, name, sql, batches):
     rule = compile_rule(sql, SCHEMA, is_event_time=False, num_keys=keys, debug_membership=True)
     start = int(cols[1][0]) - 1234
     end = int(cols[1][-1]) + 12_000
+    exp = oracle.run_proc(rule.plan, cols, start, end)
+    assert len(exp.windows) >= 3
+    cuts = np.linspace(0, len(cols[0]), batches + 1).astype(np.int64).tolist()
+    got = run_engine(engine_mod, rule, cols, start, end, cuts)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("name,sql", SEND_TWICE, ids=[c[0] for c in SEND_TWICE])
+@pytest.mark.parametrize("batches", [1, 7])
+def test_processing_send_twice_parity(oracle, engine_mod, name, sql, batches):
+    keys = 40
+    cols = _stream(30_000, keys, seed=len(name) * 17 + batches, gap_ms=6, burst=batches == 7)
+    rule = compile_rule(sql, SCHEMA, is_event_time=False, num_keys=keys, debug_membership=True, sliding_send_twice=True)
+    assert rule.plan.sliding_send_twice == 1
+    start = int(cols[1][0]) - 500
+    end = int(cols[1][-1]) + 5_000
     exp = oracle.run_proc(rule.plan, cols, start, end)
     assert len(exp.windows) >= 3
     cuts = np.linspace(0, len(cols[0]), batches + 1).astype(np.int64).tolist()
