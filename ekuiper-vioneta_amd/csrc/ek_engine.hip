@@ -830,6 +830,13 @@ struct Engine {
         ps_to_due = 0;
         ps_next_abs = 0;
         ps_last_nonmatch = INT64_MIN;
+        proc_dq.clear();
+        proc_dq_head = 0;
+        sw2_e.clear();
+        sw2_cut = 0;
+        sw2_gcb = INT64_MIN;
+        sw2_gcx = 0;
+        h_rtrig.clear();
         g_wa = g_wt = nullptr;
         g_nwm = 0;
         g_trig.clear();
@@ -980,12 +987,43 @@ struct Engine {
     WinInfo& win_info(int64_t j) { return wins[(size_t)(j - wins.front().j)]; }
     int64_t Krows() const { return dp.pseudo_keys ? 1 : (int64_t)K; }   // result rows a window can hold
 
-    // Emit every window j >= next_win with E_j <= W whose panes are complete (last pane <= q_done).
+    // Emit every window j >= next_win with E_j <= W whose panes are complete (last pane <= q_done). A window none of
+    // whose panes a row touched is empty: it is reported with no rows and takes neither result rows nor pane slots,
+    // and the windows before it are merged first, so an idle stretch of N windows (a clock jump, an event-time gap)
+    // costs O(N) host work and no memory (the reference fires one scan per tick, window_op.go:483-499).
     int finalize_ready(int64_t q_done) {
         if (!e1_known || !has_W) return 0;
-        int64_t j0 = next_win, j1 = next_win;
+        int64_t j1 = next_win;
         while (win_end(j1) <= W && win_last_pane(j1) <= q_done) j1++;
-        if (j1 == j0) return 0;
+        int64_t seg = next_win;
+        for (int64_t j = next_win; j < j1; ++j) {
+            if (j < reg_win || pane_touched(j)) continue;
+            if (int rc = finalize_range(seg, j)) return rc;
+            if (int rc = ensure_results(0, 1)) return rc;
+            WinInfo wi{};
+            wi.j = j;
+            wi.end = win_end(j);
+            wi.start = window_start(j);
+            wi.out_base = r_rows_used;
+            wi.slot = (int32_t)wins.size();
+            wi.direct = true;
+            wins.push_back(wi);
+            reg_win = j + 1;
+            next_win = j + 1;
+            stats.windows_out++;
+            seg = j + 1;
+        }
+        return finalize_range(seg, j1);
+    }
+    // a row reached one of window j's panes (its pane is bound to a ring slot)
+    bool pane_touched(int64_t j) const {
+        for (int64_t q = std::max<int64_t>(0, win_first_pane(j)); q <= win_last_pane(j); ++q)
+            if (slot_pane[(size_t)(q % ring)] == q) return true;
+        return false;
+    }
+    // Merge and emit windows [j0, j1) (all registered or registrable, none empty-skipped).
+    int finalize_range(int64_t j0, int64_t j1) {
+        if (j1 <= j0) return 0;
         int64_t n = j1 - j0;
         if (int rc = register_until(j1 - 1)) return rc;
         // panes no group touched hold no events: bind and zero them so the merge reads empty partials
@@ -1044,10 +1082,12 @@ struct Engine {
     int process(const DBatch& db, bool sorted, int64_t start, const uint8_t* d_acc, int64_t min_acc, int64_t max_ts,
                 const int64_t* d_arrival) {
         int64_t n = db.n;
-        // size the result store once for every window this batch will close
+        // size the result store once for the windows this batch will close that can hold rows (the windows of an
+        // event-time gap before the batch are empty: no result rows)
         if (W >= win_end(next_win)) {
-            int64_t nclose = (W - win_end(next_win)) / H + 1;
-            if (int rc = ensure_results(nclose * Krows(), nclose)) return rc;
+            const int64_t nclose = (W - win_end(next_win)) / H + 1;
+            const int64_t nrows = std::min<int64_t>(nclose, (max_ts - min_acc) / H + 2 * ppw + 2);
+            if (int rc = ensure_results(nrows * Krows(), nclose)) return rc;
         }
         int64_t q_lo = std::max<int64_t>(0, pane_host(min_acc));
         int64_t q_hi = pane_host(max_ts);
@@ -2898,9 +2938,7 @@ struct Engine {
     // pane mode, no rows: every window whose tick is due fires (its panes can no longer receive rows)
     int proc_close() {
         if (!e1_known || W < win_end(next_win)) return 0;
-        const int64_t nclose = (W - win_end(next_win)) / H + 1;
-        if (int rc = ensure_results(nclose * Krows(), nclose)) return rc;
-        return finalize_ready(INT64_MAX);
+        return finalize_ready(INT64_MAX);   // windows no row reached are reported empty, without result rows
     }
 
     int advance_time(int64_t now) {
@@ -2955,6 +2993,12 @@ struct Engine {
             hipMemcpyAsync(tts.data(), g_ts, (size_t)nt * 8, hipMemcpyDeviceToHost, stream);
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
+        if (slide_delay > 0 && send_twice) {
+            // send-twice keeps a host mirror of which delivered rows matched OVER (WHEN) (the others gcInputs)
+            const size_t o = h_rtrig.size();
+            h_rtrig.resize(o + n_new);
+            hipMemcpyAsync(h_rtrig.data() + o, flags_d.p, (size_t)n_new, hipMemcpyDeviceToHost, stream);
+        }
         if (slide_delay > 0) return proc_slide_delayed(rel_prev, pos, tts, pw);
         // the latest non-matching row before each trigger (its ts decides the gcInputs edge): the row just before the
         // trigger unless that row is a trigger too (then the same as that trigger's); rows before this batch: carried
@@ -3008,6 +3052,9 @@ struct Engine {
     size_t proc_dq_head = 0;
     std::vector<int64_t> sw2_e;         // send-twice: ts of the expired inputs the reference keeps
     int64_t sw2_cut = 0;                // send-twice: absolute buffer index of the first live input
+    int64_t sw2_gcb = INT64_MIN;        // send-twice: the gcInputs bound so far (inputs with ts <= it are gone)
+    int64_t sw2_gcx = 0;                // send-twice: absolute index up to which sw2_gcb accounts for the rows
+    std::vector<uint8_t> h_rtrig;       // send-twice: OVER (WHEN) flag of each mirrored row (h_rts)
     int proc_slide_delayed(int64_t rel_prev, const std::vector<int64_t>& pos, const std::vector<int64_t>& tts,
                            std::vector<PendWin>& pw) {
         const int64_t D = slide_delay;
@@ -3025,7 +3072,8 @@ struct Engine {
                 pw.push_back(p);
             }
         } else {
-            // host mirror of the delivered timestamps [h_rts_base, ...)
+            // host mirror of the delivered timestamps [h_rts_base, ...) (h_rtrig: their OVER (WHEN) flags, copied by
+            // proc_slide_triggers)
             const int64_t n_new = eb_rel - rel_prev;
             if (h_rts.empty()) h_rts_base = eb_base + rel_prev;
             if (n_new > 0) {
@@ -3035,6 +3083,7 @@ struct Engine {
                                hipMemcpyDeviceToHost, stream);
                 if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "timestamp mirror copy failed");
             }
+            if (h_rtrig.size() < h_rts.size()) h_rtrig.resize(h_rts.size(), 0);
             if (sw2_cut < h_rts_base) sw2_cut = h_rts_base;
             auto ts_at = [&](int64_t abs) { return h_rts[abs - h_rts_base]; };
             auto first_gt = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts > x
@@ -3043,9 +3092,21 @@ struct Engine {
             auto first_ge = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts >= x
                 return h_rts_base + (std::lower_bound(h_rts.begin() + (lo - h_rts_base), h_rts.begin() + (hi - h_rts_base), x) - h_rts.begin());
             };
-            // one scan over the inputs delivered up to `delivered`: content (ws, we], then the expired-prefix rule
+            // gcInputs of every non-matching row delivered before index x (window_op.go:376-378): it drops the inputs
+            // with ts + L + D <= its ts; the bound only grows, so applied lazily as "ts > gc bound"
+            auto gc_bound = [&](int64_t x) {   // (rows before sw2_gcx are in sw2_gcb already: each row is walked once)
+                for (int64_t k = x - 1; k >= std::max(sw2_gcx, h_rts_base); --k)
+                    if (!h_rtrig[k - h_rts_base]) return std::max(sw2_gcb, ts_at(k) - L - D);
+                return sw2_gcb;
+            };
+            // one scan over the inputs delivered before index `delivered`: content (ws, we], then the expired-prefix
+            // rule of handleInputsForSlidingWindow
             auto scan2 = [&](int64_t ws, int64_t we, int64_t delivered) {
-                const int64_t a = std::max(sw2_cut, first_gt(sw2_cut, delivered, ws));
+                const int64_t gcb = gc_bound(delivered);
+                sw2_gcb = gcb;
+                sw2_gcx = std::max(sw2_gcx, delivered);
+                const int64_t live0 = std::max(sw2_cut, first_gt(sw2_cut, delivered, gcb));
+                const int64_t a = std::max(live0, first_gt(live0, delivered, ws));
                 const int64_t b = std::max(a, first_gt(a, delivered, we));
                 PendWin p{};
                 p.q.kind = RB_FIXED;
@@ -3055,15 +3116,17 @@ struct Engine {
                 p.end = we;
                 pw.push_back(p);
                 const int64_t dl = we - (L + D);
-                const int64_t ne = std::lower_bound(sw2_e.begin(), sw2_e.end(), dl) - sw2_e.begin();
-                const int64_t nl = first_ge(sw2_cut, delivered, dl) - sw2_cut;
-                const int64_t present = (int64_t)sw2_e.size() + (delivered - sw2_cut);
+                const size_t e0 = std::upper_bound(sw2_e.begin(), sw2_e.end(), gcb) - sw2_e.begin();   // gc'd expired rows
+                const int64_t ne = std::max<int64_t>(0, (std::lower_bound(sw2_e.begin(), sw2_e.end(), dl) - sw2_e.begin()) - (int64_t)e0);
+                const int64_t nl = first_ge(live0, delivered, dl) - live0;
+                const int64_t present = (int64_t)(sw2_e.size() - e0) + (delivered - live0);
                 if (ne + nl == 0) return;
                 if (ne + nl == present) {
                     sw2_e.clear();
                 } else {
+                    sw2_e.erase(sw2_e.begin(), sw2_e.begin() + (int64_t)e0);
                     sw2_e.resize((size_t)ne);
-                    for (int64_t k = 0; k < nl; ++k) sw2_e.push_back(ts_at(sw2_cut + k));
+                    for (int64_t k = 0; k < nl; ++k) sw2_e.push_back(ts_at(live0 + k));
                 }
                 sw2_cut = delivered;
             };
@@ -3085,10 +3148,13 @@ struct Engine {
                     break;
                 }
             }
+            sw2_gcb = gc_bound(end_abs);
+            sw2_gcx = end_abs;
             eb_floor = std::max(eb_floor, sw2_cut - eb_base);
             const int64_t drop = sw2_cut - h_rts_base;
             if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
                 h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+                h_rtrig.erase(h_rtrig.begin(), h_rtrig.begin() + drop);
                 h_rts_base = sw2_cut;
             }
         }
@@ -4131,7 +4197,7 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 2;
+    static constexpr int64_t kStateVersion = 3;   // 3: the processing-time clock and timers
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -4236,6 +4302,15 @@ struct Engine {
             if (pend_has_valid[c]) s.put(pend_vhost[c].data(), pend_vhost[c].size());
         }
         s.put(pend_arr.data(), pend_arr.size() * 8);
+        // processing time: the caller's clock and the timers armed by it (tickers, session timeout, delayed sliding
+        // triggers, the send-twice inputs state) — the import resumes the rule exactly where the export left it
+        for (int64_t v : {(int64_t)clock_started, clock_ms, ps_tick, (int64_t)ps_to_exists, (int64_t)ps_to_armed, ps_to_due,
+                          ps_next_abs, ps_last_nonmatch, sw2_cut, sw2_gcb, sw2_gcx})
+            s.i64(v);
+        s.i64((int64_t)(proc_dq.size() - proc_dq_head));
+        s.put(proc_dq.data() + proc_dq_head, (proc_dq.size() - proc_dq_head) * 8);
+        s.i64((int64_t)sw2_e.size());
+        s.put(sw2_e.data(), sw2_e.size() * 8);
         if (wtype != EK_WINDOW_NONE && !range_mode) {
             // partials of every open pane: field-major SoA, field f of slot x at ((f * ring) + x) * Kpad
             const int nf = n_state_fields();
@@ -4281,6 +4356,8 @@ struct Engine {
             s.i64(h_rts_base);                                                // session: released timestamps
             s.i64((int64_t)h_rts.size());
             s.put(h_rts.data(), h_rts.size() * 8);
+            s.i64((int64_t)h_rtrig.size());                                   // send-twice: OVER (WHEN) flags
+            s.put(h_rtrig.data(), h_rtrig.size());
             s.i64(inc_has_T ? 1 : 0);                                         // incremental windows: T + open windows
             s.i64(inc_T);
             s.i64((int64_t)inc_pend.size());
@@ -4333,6 +4410,20 @@ struct Engine {
         }
         pend_arr.resize((size_t)pend_n);
         r.read(pend_arr.data(), pend_n * 8);
+        clock_started = r.i64() != 0; clock_ms = r.i64(); ps_tick = r.i64();
+        ps_to_exists = r.i64() != 0; ps_to_armed = r.i64() != 0; ps_to_due = r.i64();
+        ps_next_abs = r.i64(); ps_last_nonmatch = r.i64(); sw2_cut = r.i64(); sw2_gcb = r.i64(); sw2_gcx = r.i64();
+        {
+            const int64_t nq = r.i64();
+            if (!r.ok || nq < 0 || nq > size) return fail(EK_ERR_INVALID, "bad timer queue in state blob");
+            proc_dq.resize((size_t)nq);
+            proc_dq_head = 0;
+            r.read(proc_dq.data(), nq * 8);
+            const int64_t ne = r.i64();
+            if (!r.ok || ne < 0 || ne > size) return fail(EK_ERR_INVALID, "bad send-twice state in state blob");
+            sw2_e.resize((size_t)ne);
+            r.read(sw2_e.data(), ne * 8);
+        }
         if (!r.ok) return fail(EK_ERR_INVALID, "state blob truncated");
         if (wtype != EK_WINDOW_NONE && !range_mode) {
             const int64_t kp = r.i64(), nf = r.i64(), R = r.i64(), nl = r.i64();
@@ -4389,6 +4480,10 @@ struct Engine {
             if (!r.ok || nr < 0 || nr > size) return fail(EK_ERR_INVALID, "bad session mirror in state blob");
             h_rts.resize((size_t)nr);
             r.read(h_rts.data(), nr * 8);
+            const int64_t nf = r.i64();
+            if (!r.ok || nf < 0 || nf > size) return fail(EK_ERR_INVALID, "bad trigger mirror in state blob");
+            h_rtrig.resize((size_t)nf);
+            r.read(h_rtrig.data(), nf);
             inc_has_T = r.i64() != 0;
             inc_T = r.i64();
             const int64_t ni = r.i64();

@@ -163,3 +163,71 @@ def test_export_requires_polled_results_and_matching_plan(engine_mod):
     assert len(fresh.poll()) >= 1
     fresh.close()
     eng.close()
+
+
+# ------------------------------------------------------------------ processing time (the caller's clock)
+PROC_CASES = [
+    ("proc_tumbling", "SELECT k, avg(x), count(*) FROM s GROUP BY k, TUMBLINGWINDOW(ss, 1)", {}),
+    ("proc_hopping_filter", "SELECT k, max(x), count(*) FROM s GROUP BY k, HOPPINGWINDOW(ss, 2, 1) FILTER (WHERE y > 30)", {}),
+    ("proc_sliding", "SELECT k, count(*), min(y) FROM s GROUP BY k, SLIDINGWINDOW(ms, 400) OVER (WHEN x > 97)", {}),
+    ("proc_sliding_delay", "SELECT k, count(*), sum(y) FROM s GROUP BY k, SLIDINGWINDOW(ms, 300, 500) OVER (WHEN x > 98)", {}),
+    ("proc_send_twice", "SELECT k, count(*), max(y) FROM s GROUP BY k, SLIDINGWINDOW(ms, 300, 500) OVER (WHEN x > 98)",
+     dict(sliding_send_twice=True)),
+    ("proc_session", "SELECT k, count(*), avg(x) FROM s WHERE y < 70 GROUP BY k, SESSIONWINDOW(ss, 3, 1)", {}),
+]
+
+
+@pytest.mark.parametrize("name,sql,kw", PROC_CASES, ids=[c[0] for c in PROC_CASES])
+def test_state_processing_time_split(oracle, engine_mod, name, sql, kw):
+    """Processing-time rules checkpointed mid-stream: the clock, the next tick, an armed session timeout, pending
+    delay timers and the send-twice inputs state travel in the blob (state version 3), so the restored handle goes on
+    exactly where the exported one stopped (the same windows as the uncut run under the same clock)."""
+    from test_processing_gpu import SCHEMA as PSCHEMA, _stream
+    cols = _stream(40_000, 30, seed=len(name) * 7 + 3, gap_ms=6, burst=True)
+    rule = compile_rule(sql, PSCHEMA, is_event_time=False, num_keys=30, debug_membership=True, **kw)
+    start, end = int(cols[1][0]) - 777, int(cols[1][-1]) + 6_000
+    exp = oracle.run_proc(rule.plan, cols, start, end)
+    n = len(cols[0])
+    cut = int(n * 0.47)
+    clock = int(cols[1][cut - 1]) + 3       # the clock when the checkpoint is taken (no row at or after it yet)
+    a = engine_mod.Engine(rule.plan)
+    a.advance_time(start)
+    for lo, hi in ((0, cut // 2), (cut // 2, cut)):
+        a.advance_time(int(cols[1][lo]))
+        a.push_host([c[lo:hi] for c in cols])
+    if clock <= int(cols[1][cut]):
+        a.advance_time(clock)
+    got = list(a.poll())
+    blob = a.export_state()
+    a.close()
+    b = engine_mod.Engine(rule.plan)
+    b.import_state(blob)
+    for lo, hi in ((cut, (cut + n) // 2), ((cut + n) // 2, n)):
+        b.advance_time(int(cols[1][lo]))
+        b.push_host([c[lo:hi] for c in cols])
+    b.advance_time(end)
+    got += list(b.poll())
+    b.close()
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_state_processing_idle_gap(oracle, engine_mod):
+    """A clock jump over thousands of empty tumbling windows (pane mode): they are reported empty without pane slots
+    or result rows (an idle day of 1 s windows used to allocate 86,400 x keys partials)."""
+    from test_processing_gpu import SCHEMA as PSCHEMA
+    rule = compile_rule("SELECT k, count(*), sum(x) FROM s GROUP BY k, TUMBLINGWINDOW(ss, 1)", PSCHEMA, is_event_time=False,
+                        num_keys=65536, debug_membership=True)
+    t0 = 1541152480000
+    ts = np.array([t0 + 10, t0 + 20, t0 + 20 + 86_400_000, t0 + 86_400_500], np.int64)
+    cols = [np.array([1, 2, 3, 1], np.uint32), ts, np.array([1.0, 2.0, 3.0, 4.0]), np.zeros(4)]
+    exp = oracle.run_proc(rule.plan, cols, t0, int(ts[-1]) + 3_000)
+    assert len(exp.windows) > 86_000
+    eng = engine_mod.Engine(rule.plan)
+    eng.advance_time(t0)
+    eng.push_host([c[:2] for c in cols])
+    eng.advance_time(int(ts[2]))
+    eng.push_host([c[2:] for c in cols])
+    eng.advance_time(int(ts[-1]) + 3_000)
+    got = eng.poll()
+    eng.close()
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
