@@ -51,7 +51,7 @@ CONFIGS = {
     "C4b": dict(sql="SELECT deviceId, stddev(temperature), var(temperature) FROM demo "
                     "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1",
                 n=100_000_000, keys=1_000_000, epm=100, seed=93, t0=T0, in_cols=("key", "temperature"),
-                out_bytes=4 + 8 + 8, processing_time=True),
+                out_bytes=4 + 8 + 8, processing_time=True, having_star_window=1000, having_star_col="temperature"),
     "C5": dict(sql="SELECT deviceId, median(temperature), percentile_cont(temperature, 0.9) FROM demo "
                    "GROUP BY deviceId, TUMBLINGWINDOW(ss, 60)",
                n=125_000_000, keys=12_500_000, epm=2084, seed=94, t0=1541152440000, in_cols=("key", "ts", "temperature"),
@@ -178,55 +178,6 @@ def global_tuples(cfg, world, n_glob):
 
 
 CPU_SAMPLE = {"C2": 100_000_000, "C3": 15_000_000, "C4a": 1_000_000, "C4b": 50_000_000, "C5": 30_000_000}
-
-
-def device_router(ts, arr, tol, dist, want_list):
-    """The rule's WatermarkOp over the WHOLE global stream (ekgpu.shard.GlobalWatermark, watermark_op.go:144-225),
-    computed by the ranks from their own rows, inside the timed step: F[v] = first global arrival with ts == v
-    (scatter-min on each rank, one all_reduce MIN over the stream's ts range); the running max advances exactly at
-    the arrivals F[v] < min_{u > v} F[u] (no earlier arrival reached v), which are the WatermarkTuples (wm = v - tol);
-    each rank checks its rows against the tuple before them (accepted iff ts >= mark - tol) and one all_reduce MIN
-    gives all_accepted. Returns the tuple dict make_ctx takes: the full tuple list when `want_list` (range-mode
-    windows) or when some row is late, else only the batch's last tuple with the all_accepted / max_wm_step hints
-    (a pane-mode shard needs nothing else, include/ekgpu.h ek_global_ctx)."""
-    import numpy as np
-    import torch
-    i64max = torch.iinfo(torch.int64).max
-    dev = ts.device
-    mm = torch.stack([-ts.min(), ts.max()]) if ts.numel() else torch.tensor([-i64max, -i64max], device=dev)
-    dist.all_reduce(mm, op=dist.ReduceOp.MAX)
-    lo, hi = -int(mm[0]), int(mm[1])
-    F = torch.full((hi - lo + 1,), i64max, dtype=torch.int64, device=dev)
-    if ts.numel():
-        F.scatter_reduce_(0, ts - lo, arr, reduce="amin", include_self=True)
-    dist.all_reduce(F, op=dist.ReduceOp.MIN)
-    S = torch.flip(torch.cummin(torch.flip(F, [0]), 0).values, [0])
-    nxt = torch.cat([S[1:], torch.tensor([i64max], dtype=torch.int64, device=dev)])
-    tv = torch.nonzero(F < nxt).squeeze(1)
-    t_arr = F[tv].contiguous()
-    t_mark = tv + lo
-    k = torch.searchsorted(t_arr, arr) - 1
-    zero_mark = -62135596800000 + tol          # the stream mark before the first event (watermark_op.go:55-58)
-    mb = torch.where(k >= 0, t_mark[k.clamp(min=0)], torch.full_like(k, zero_mark))
-    acc = torch.tensor([int(bool((ts >= mb - tol).all())) if ts.numel() else 1], dtype=torch.int64, device=dev)
-    dist.all_reduce(acc, op=dist.ReduceOp.MIN)
-    wm_ts = t_mark - tol
-    steps = wm_ts[1:] - wm_ts[:-1]
-    j = torch.searchsorted(wm_ts, torch.tensor([lo], dtype=torch.int64, device=dev))
-    jj = int(j.clamp(max=len(wm_ts) - 1))
-    head = torch.stack([acc[0], steps.max() if steps.numel() else torch.tensor(0, device=dev), t_arr[jj], F[0],
-                        t_arr[-1], wm_ts[-1]]).cpu().tolist()
-    all_acc, max_step, o_arr, first_lo = bool(head[0]), int(head[1]), int(head[2]), int(head[3])
-    out = {"arrivals_end": None, "all_accepted": all_acc, "max_wm_step": max_step,
-           # the first window's anchor: the earliest event (ts = lo) is released at the first tuple reaching it
-           "origin_known": all_acc and first_lo <= o_arr, "origin_ts": lo, "origin_arrival": o_arr}
-    if want_list or not all_acc:
-        out["wm_arrival"] = t_arr.cpu().numpy()
-        out["wm_ts"] = wm_ts.cpu().numpy()
-    else:
-        out["wm_arrival"] = np.array([int(head[4])], np.int64)
-        out["wm_ts"] = np.array([int(head[5])], np.int64)
-    return out
 
 
 def cpu_model():
@@ -521,7 +472,7 @@ def main():
 
     from ekgpu.engine import Engine
     from ekgpu.rule import compile_rule
-    from ekgpu.shard import make_ctx
+    from ekgpu.shard import device_watermark, make_ctx
 
     cfg = dict(CONFIGS[args.config])
     if args.events:
@@ -592,6 +543,12 @@ def main():
             if sent_ptrs:
                 cnt_eng.push_global(None, sent_ctx)
 
+    last_global = None
+    count_pp = None
+    if cnt_eng is not None:
+        from ekgpu.dist import global_windows, make_partial_plan
+        count_pp = make_partial_plan(crule)
+
     def step():
         nonlocal ctx, tup
         eng.reset()
@@ -605,7 +562,7 @@ def main():
         else:
             if iet and dist is not None:
                 # the router (global WatermarkOp) runs inside the timed step, on the ranks' own rows
-                tup = device_router(ts_dev, arr, args.disorder, dist, want_list)
+                tup = device_watermark(ts_dev, arr, args.disorder, dist, want_list)
                 tup["arrivals_end"] = n_glob
                 ctx = make_ctx(tup, np.zeros(0, np.int64))
                 ctx.row_arrival = arr.data_ptr()
@@ -625,6 +582,11 @@ def main():
                 eng.push_global(None, sent_ctx)
         if fut is not None:
             fut.result()   # both rules' pushes are inside the step
+            if dist is not None and not blocks:
+                # the reference's final result gather of the global (un-grouped) count(*): every rank's per-window
+                # partial, one all_gather over RCCL, merged (ekgpu.dist.global_windows) — inside the timed step
+                nonlocal last_global
+                last_global = global_windows(count_pp, cnt_eng.poll())
 
     for _ in range(args.warmup):
         step()
@@ -635,12 +597,10 @@ def main():
     eng.release(r)
     global_count = None
     if cnt_eng is not None:
-        from ekgpu.dist import global_windows, make_partial_plan
-        cw = cnt_eng.poll()
-        if dist:
-            gw = global_windows(make_partial_plan(crule), cw)
-            global_count = [w.values for w in gw]
+        if dist and not blocks:
+            global_count = [w.values for w in last_global]
         else:
+            cw = cnt_eng.poll()
             global_count = [int(w.values[0][0]) for w in cw if len(w.keys)]
 
     if dist:
@@ -671,6 +631,25 @@ def main():
     value = n_glob * args.steps / dt
     in_bytes_per_event = sum(COL_BYTES[c] for c in cfg["in_cols"])
     alg_bytes = n * in_bytes_per_event + rows * cfg["out_bytes"]
+    formula_bytes = alg_bytes
+    required = None
+    if cfg.get("having_star_window"):
+        # HAVING count(*) > 1 decides a group from its row count alone: the value column is only
+        # needed for the rows of kept groups. The line counts what the step must move: every key + those values +
+        # the result rows (the §8(d) formula, every referenced column of every event, is reported beside it)
+        wl = cfg["having_star_window"]
+        nwf = n // wl
+        kk = cols[0][: nwf * wl].view(nwf, wl).to(torch.int64).sort(dim=1).values
+        eq = kk[:, 1:] == kk[:, :-1]
+        kept = torch.zeros_like(kk, dtype=torch.bool)
+        kept[:, 1:] |= eq
+        kept[:, :-1] |= eq
+        kept_rows = int(kept.sum())
+        del kk, eq, kept
+        alg_bytes = n * COL_BYTES["key"] + kept_rows * COL_BYTES[cfg["having_star_col"]] + rows * cfg["out_bytes"]
+        required = {"bytes_per_step": alg_bytes, "kept_group_rows": kept_rows,
+                    "what": "every key (4 B) + the value column of the rows of groups HAVING count(*) > 1 keeps (8 B) "
+                            "+ result rows; the rows of dropped one-row groups never need their value"}
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
     kernels = {}
     for k, ph in enumerate(PHASES):
@@ -690,12 +669,16 @@ def main():
                                         "achieved_gbs": kb_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None}
     dominant = max(kernels.items(), key=lambda kv: kv[1]["launch_ms"] * kv[1]["launches_per_step"])[0] if kernels else None
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", f"r03_pmc_{args.config}.json")
-    if os.path.exists(pmc):
+    sim = f"_sim{world}" if args.sim_world > 1 else ""
+    for rnd in ("r04", "r03"):
+        pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.config}{sim}.json")
+        if not os.path.exists(pmc):
+            continue
         pm = json.load(open(pmc))
-        if pm.get("events_per_gpu") == n and world == 1:
+        if pm.get("events_per_gpu") == n and (world == 1 or sim):
             traffic = pm.get("hbm_bytes_per_step")
             traffic_src = os.path.relpath(pmc, ROOT)
+            break
     out = {
         "metric": "events/sec (whole node) for windowed GROUP BY at 1/2/4/8 GPUs; % HBM peak",
         "value": value,
@@ -719,9 +702,13 @@ def main():
                                                                   + ")" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "what": f"whole step: {in_bytes_per_event} B/event in + {cfg['out_bytes']} B/result row out "
-                             f"(SURVEY.md §8(d)) over ms_per_step (driver clock)",
+                     "what": (f"whole step: {in_bytes_per_event} B/event in + {cfg['out_bytes']} B/result row out "
+                              f"(SURVEY.md §8(d)) over ms_per_step (driver clock)") if required is None else
+                             "whole step: the bytes the step must move (required_bytes) over ms_per_step (driver clock)",
                      "algorithmic_bytes_per_step": alg_bytes, "device_ms_per_step": dev_ms / args.steps,
+                     "formula_bytes_per_step": formula_bytes,
+                     "formula_frac": formula_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "required_bytes": required,
                      "dominant_kernel": dominant, "kernels": kernels},
     }
     if global_count is not None:

@@ -31,6 +31,7 @@
 #include "ek_global.h"
 #include "ek_keymajor.h"
 #include "ek_launch.h"
+#include "ek_errmsg.h"
 
 using namespace ek;
 
@@ -126,6 +127,34 @@ int prog_depth_ok(const ek_instr* prog, int n) {
     return n == 0 || sp == 1;
 }
 
+// Whether a (depth-checked) condition can fail at run time — an error or a non-bool result (filter_operator.go:45-58,
+// having_operator.go:45-55) — by the static types of its operands: numbers (columns, constants, aggregates) and bools
+// (comparisons, AND / OR). Division / modulo by a possible zero, bool-number mixes, AND / OR over numbers, a non-bool
+// root and order statistics (their "Input is outside of range") can; a plan whose conditions cannot fail records no
+// error witnesses.
+bool prog_can_fail(const ek_instr* prog, int n, const int32_t* agg_fn) {
+    bool st[EK_MAX_PROG + 1];   // true: bool-typed
+    int sp = 0;
+    bool f = false;
+    for (int k = 0; k < n; ++k) {
+        const int op = prog[k].op;
+        if (op == EK_OP_COL || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) { st[sp++] = false; continue; }
+        if (op == EK_OP_AGG) {
+            const int fn = agg_fn[prog[k].arg];
+            f |= fn == EK_AGG_PERCENTILE_CONT || fn == EK_AGG_PERCENTILE_DISC;
+            st[sp++] = false;
+            continue;
+        }
+        const bool r = st[--sp], l = st[--sp];
+        if (op == EK_OP_EQ || op == EK_OP_NEQ) f |= l != r;
+        else if (op >= EK_OP_LT && op <= EK_OP_GTE) f |= l || r;
+        else if (op == EK_OP_AND || op == EK_OP_OR) f |= !l || !r;
+        else f |= l || r || op == EK_OP_DIV || op == EK_OP_MOD;
+        st[sp++] = op <= EK_OP_OR;
+    }
+    return f || sp != 1 || !st[0];
+}
+
 }  // namespace
 
 struct Engine {
@@ -201,6 +230,13 @@ struct Engine {
 
     // ---- device memory
     DevBuf state_buf, pane_err, pane_mcnt, pane_mhash;
+    // error witnesses (ek_window_error): allocated only for plans whose WHERE / HAVING / order statistics can fail
+    bool where_can_fail = false, having_can_fail = false, agg_can_fail = false;
+    DevBuf pane_wit;                   // [ring] WitRec: each pane slot's first failed WHERE row
+    DevBuf r_wwit, r_aslot;
+    DevBuf vp_wit;                     // range mode: the launch's window witnesses (its virtual panes)            // [2 per window] WitRec (WHERE, HAVING), [window] failed order statistic
+    int64_t wit_seq = 0;               // launch counter: the release-order tie-break of pane witnesses
+    std::vector<std::string> poll_msgs;   // the last poll's window error texts
     DState dstate{};
     DevBuf bstats, bstats_part;        // BatchStats, per-block partials of k_stats
     BatchStats* h_stats = nullptr;     // pinned
@@ -700,6 +736,10 @@ struct Engine {
             if (hipMemcpy(d_plan_where, &pre, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
             if (push_where) dp.n_where = 0;   // the pre-filter already dropped every row whose WHERE is not true
         }
+        where_can_fail = dp.n_where > 0 && prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
+        having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+        for (int k = 0; k < dp.n_aggs; ++k)
+            agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC;
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
         if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
         if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
@@ -741,6 +781,10 @@ struct Engine {
         if (int rc = ensure(pane_err, (size_t)ring * 4)) return rc;
         if (int rc = ensure(pane_mcnt, (size_t)ring * 8)) return rc;
         if (int rc = ensure(pane_mhash, (size_t)ring * 8)) return rc;
+        if (where_can_fail) {
+            if (int rc = ensure(pane_wit, (size_t)ring * sizeof(WitRec))) return rc;
+            hipMemsetAsync(pane_wit.p, 0, (size_t)ring * sizeof(WitRec), stream);
+        }
         return 0;
     }
     // Grow the pane ring to at least `need` slots, moving the partials of live panes.
@@ -749,13 +793,18 @@ struct Engine {
         int R = (int)std::max<int64_t>(need, (int64_t)ring * 2);
         hipStreamSynchronize(stream);
         const int nf = n_state_fields();
-        DevBuf nsb, npe, npm, nph;
+        DevBuf nsb, npe, npm, nph, npw;
         if (hipMalloc(&nsb.p, (size_t)R * Kpad * 8 * nf) != hipSuccess) return fail(EK_ERR_NOMEM, "pane state alloc (%d slots)", R);
         nsb.bytes = (size_t)R * Kpad * 8 * nf;
         if (hipMalloc(&npe.p, (size_t)R * 4) != hipSuccess || hipMalloc(&npm.p, (size_t)R * 8) != hipSuccess ||
             hipMalloc(&nph.p, (size_t)R * 8) != hipSuccess)
             return fail(EK_ERR_NOMEM, "pane scalar alloc");
         npe.bytes = (size_t)R * 4; npm.bytes = nph.bytes = (size_t)R * 8;
+        if (where_can_fail) {
+            if (hipMalloc(&npw.p, (size_t)R * sizeof(WitRec)) != hipSuccess) return fail(EK_ERR_NOMEM, "pane witness alloc");
+            npw.bytes = (size_t)R * sizeof(WitRec);
+            hipMemsetAsync(npw.p, 0, npw.bytes, stream);
+        }
         DState nd = carve_state(nsb.p, R);
         std::vector<int64_t> nslot(R, INT64_MIN);
         const int64_t first_live = win_first_pane(next_win);
@@ -778,10 +827,13 @@ struct Engine {
             hipMemcpyAsync((char*)npe.p + sn * 4, (char*)pane_err.p + so * 4, 4, hipMemcpyDeviceToDevice, stream);
             hipMemcpyAsync((char*)npm.p + sn * 8, (char*)pane_mcnt.p + so * 8, 8, hipMemcpyDeviceToDevice, stream);
             hipMemcpyAsync((char*)nph.p + sn * 8, (char*)pane_mhash.p + so * 8, 8, hipMemcpyDeviceToDevice, stream);
+            if (npw.p)
+                hipMemcpyAsync((char*)npw.p + sn * sizeof(WitRec), (char*)pane_wit.p + so * sizeof(WitRec), sizeof(WitRec),
+                               hipMemcpyDeviceToDevice, stream);
         }
         hipStreamSynchronize(stream);
-        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash);
-        state_buf = nsb; pane_err = npe; pane_mcnt = npm; pane_mhash = nph;
+        release(state_buf); release(pane_err); release(pane_mcnt); release(pane_mhash); release(pane_wit);
+        state_buf = nsb; pane_err = npe; pane_mcnt = npm; pane_mhash = nph; pane_wit = npw;
         dstate = nd;
         slot_pane = nslot;
         ring = R;
@@ -879,6 +931,7 @@ struct Engine {
             hipMemsetAsync((char*)pane_err.p + s * 4, 0, 4, stream);
             hipMemsetAsync((char*)pane_mcnt.p + s * 8, 0, 8, stream);
             hipMemsetAsync((char*)pane_mhash.p + s * 8, 0, 8, stream);
+            if (pane_wit.p) hipMemsetAsync((char*)pane_wit.p + s * sizeof(WitRec), 0, sizeof(WitRec), stream);
         }
         return 0;
     }
@@ -943,6 +996,10 @@ struct Engine {
             if (int rc = growz(r_werr, 4)) return rc;
             if (int rc = growz(r_wmc, 8)) return rc;
             if (int rc = growz(r_wmh, 8)) return rc;
+            if (where_can_fail || having_can_fail)
+                if (int rc = growz(r_wwit, 2 * sizeof(WitRec))) return rc;
+            if (agg_can_fail)
+                if (int rc = growz(r_aslot, 4)) return rc;
             r_win_cap = cap;
         }
         return 0;
@@ -954,6 +1011,9 @@ struct Engine {
         for (int k = 0; k < n_out; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
         r.win_cnt = (int64_t*)r_wcnt.p;
         r.win_err = (int32_t*)r_werr.p;
+        r.wwit = (WitRec*)r_wwit.p;
+        r.pwit = (const WitRec*)pane_wit.p;
+        r.aslot = (int32_t*)r_aslot.p;
         return r;
     }
 
@@ -1225,7 +1285,9 @@ struct Engine {
         gd.has_accept = d_acc != nullptr;
         gd.sorted = pbnd_host != nullptr;
         gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
-
+        gd.pwit = (WitRec*)pane_wit.p;   // pane witnesses in release order: (ts, this launch, row)
+        gd.wit_ts = 1;
+        gd.wit_o2 = (wit_seq++) << 36;
 
         for (int k = 0; k <= npn; ++k) h_pbnd[k] = pbnd_host ? pbnd_host[k] : 0;
         for (int r = 0; r < npn; ++r) { h_dbase[r] = -1; h_didx[r] = -1; }
@@ -1319,6 +1381,7 @@ struct Engine {
         {
             const int nvc = std::max(1, dp.n_vc);
             Results rv = results_view();
+            rv.pwit = gd.pwit;   // the group's pane (range mode: window) witnesses
             dim3 ga(gd.np);
             const uint32_t* ct = (const uint32_t*)chist.p;
             const int ph = phase_begin(EK_PHASE_AGGREGATE);
@@ -1787,6 +1850,13 @@ struct Engine {
         h_ab.resize((size_t)nq * 2);
         hipMemcpyAsync(h_ab.data(), ab_d.p, (size_t)nq * 16, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "window range kernel failed");
+        // every aggregation kernel below reads rows [a, b) of the buffer: check the ranges on the host first
+        for (int w = 0; w < nq; ++w)
+            if (h_ab[2 * w] < 0 || h_ab[2 * w] > h_ab[2 * w + 1] || h_ab[2 * w + 1] > eb.n)
+                return fail(EK_ERR_STATE, "internal: window %d of %d has rows [%lld, %lld) outside the buffer [0, %lld) "
+                                          "(kind %d, pos %lld, rstep %lld)", w, nq, (long long)h_ab[2 * w],
+                            (long long)h_ab[2 * w + 1], (long long)eb.n, (int)pw[w].q.kind, (long long)pw[w].q.pos,
+                            (long long)pw[w].q.rstep);
         if (hop_discard_pending) {
             hop_discard_pending = false;
             if (int rc = hopping_discard(pw)) return rc;
@@ -1875,9 +1945,11 @@ struct Engine {
         }
         if (dp.n_first > 0)
             if (int rc = first_fetch(slots, obase)) return rc;
-        // windows never start below the last fired one's start (overlapping) or end (disjoint)
+        // windows never start below the last fired one's start (overlapping) or end (disjoint); send-twice windows do
+        // not fire in start order (a timer's (t, t + D] precedes the next trigger's (t' - L, t']): proc_slide_delayed
+        // and proc_slide_floor keep their floor
         const bool overlap = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_COUNT;
-        eb_floor = std::max(eb_floor, overlap ? h_ab[2 * (nq - 1)] : h_ab[2 * (nq - 1) + 1]);
+        if (!send_twice) eb_floor = std::max(eb_floor, overlap ? h_ab[2 * (nq - 1)] : h_ab[2 * (nq - 1) + 1]);
         if (hop_floor >= 0) { eb_floor = std::max(eb_floor, hop_floor); hop_floor = -1; }
         return 0;
     }
@@ -2263,6 +2335,10 @@ struct Engine {
         if (int rc = ensure(vp_err, (size_t)npn * 4)) return rc;
         if (int rc = ensure(vp_mc, (size_t)npn * 8)) return rc;
         if (int rc = ensure(vp_mh, (size_t)npn * 8)) return rc;
+        if (where_can_fail) {   // window witnesses in buffer order (k_group_prep zeroes them: every pane is fresh)
+            if (int rc = ensure(vp_wit, (size_t)npn * sizeof(WitRec))) return rc;
+            gd.pwit = (WitRec*)vp_wit.p;
+        }
         return launch_part_agg(buffer_view(), gd, 2, nullptr, (int32_t*)vp_err.p, (int64_t*)vp_mc.p,
                                (unsigned long long*)vp_mh.p, lp_stride, true);
     }
@@ -4118,6 +4194,7 @@ struct Engine {
             }
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "poll sync failed");
+        if (int rc = window_messages(we)) return rc;
         h_ws.assign(nw, 0); h_we.assign(nw, 0); h_off.assign(nw, 0); h_cnt.assign(nw, 0); h_st.assign(nw, 0);
         h_mc.assign(nw, 0); h_mh.assign(nw, 0);
         int64_t total = 0;
@@ -4172,12 +4249,93 @@ struct Engine {
         return 0;
     }
 
+    // The error text of each failed window of this poll (ek_window_error): the operator's message re-evaluated on the
+    // host over the window's witness (ek_errmsg.h). Precedence follows the reference's operator order: FilterOp, then
+    // HavingOp, then ProjectOp (planner.go:387-446) — a window the WHERE failed never reaches HAVING.
+    static const char* order_stat_error(int fn) {   // funcs_agg.go:321-326,357-362 over stats v0.7.1 ErrBounds
+        return fn == EK_AGG_PERCENTILE_DISC ? "PopulationVariance exec with error: Input is outside of range."
+                                            : "percentile exec with error: Input is outside of range.";
+    }
+    HVal wit_value(const WitRec& r, int k, bool agg) const {
+        HVal v;
+        switch (r.tag[k]) {
+        case V_BOOL: v.tag = HVal::BOOL; v.i = r.v[k]; break;
+        case V_I64: v.tag = HVal::I64; v.i = r.v[k]; break;
+        case V_F64: v.tag = HVal::F64; memcpy(&v.f, &r.v[k], 8); break;
+        case V_ERR: v = hv_err(agg ? order_stat_error(dp.agg_fn[k]) : "invalid value"); break;
+        default: break;
+        }
+        return v;
+    }
+    int window_messages(const std::vector<int32_t>& we) {
+        const int64_t nw = (int64_t)we.size();
+        poll_msgs.assign((size_t)nw, std::string());
+        bool any = false;
+        for (int32_t e : we) any |= e != 0;
+        if (!any) return 0;
+        std::vector<WitRec> wit;
+        std::vector<int32_t> as;
+        if (r_wwit.p) {
+            wit.resize((size_t)nw * 2);
+            hipMemcpyAsync(wit.data(), r_wwit.p, (size_t)nw * 2 * sizeof(WitRec), hipMemcpyDeviceToHost, stream);
+        }
+        if (r_aslot.p) {
+            as.resize((size_t)nw);
+            hipMemcpyAsync(as.data(), r_aslot.p, (size_t)nw * 4, hipMemcpyDeviceToHost, stream);
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "error witness copy failed");
+        for (int64_t w = 0; w < nw; ++w) {
+            const int32_t st = we[w];
+            if (!st) continue;
+            std::string m;
+            if (st == EK_WIN_WHERE_ERROR) {
+                if (!wit.empty() && wit[2 * w].set) {
+                    const WitRec& r = wit[2 * w];
+                    const HVal v = h_eval_prog(dp.where_prog, dp.n_where, [&](int c) { return wit_value(r, c, false); },
+                                               [&](int) { return HVal{}; });
+                    m = condition_error("run Where error: ", v, true);
+                }
+                if (m.empty()) m = "run Where error: (no witness row recorded)";
+            } else if (!wit.empty() && wit[2 * w + 1].set) {
+                const WitRec& r = wit[2 * w + 1];
+                const HVal v = h_eval_prog(dp.having_prog, dp.n_having, [&](int) { return HVal{}; },
+                                           [&](int k) { return wit_value(r, k, true); });
+                m = condition_error("run Having error: ", v, false);
+            }
+            if (m.empty() && !as.empty() && as[w] > 0) {
+                // the first failed order statistic: HavingOp meets it first when HAVING reads it, ProjectOp otherwise
+                const int a = kMaxSortAggs - as[w];
+                const int slot = dp.sagg_agg[a];
+                bool in_having = false;
+                for (int k = 0; k < dp.n_having; ++k)
+                    in_having |= dp.having_prog[k].op == EK_OP_AGG && dp.having_prog[k].arg == slot;
+                m = std::string(in_having ? "run Having error: " : "run Select error: ") + order_stat_error(dp.agg_fn[slot]);
+            }
+            if (m.empty()) m = st == EK_WIN_HAVING_ERROR ? "run Having error: (no witness group recorded)" : "run Select error";
+            poll_msgs[(size_t)w] = std::move(m);
+        }
+        return 0;
+    }
+    int window_error(int64_t w, char* buf, int64_t cap, int64_t* len) {
+        if (w < 0 || w >= (int64_t)poll_msgs.size()) return fail(EK_ERR_INVALID, "window %lld not in the last poll", (long long)w);
+        const std::string& m = poll_msgs[(size_t)w];
+        if (len) *len = (int64_t)m.size();
+        if (buf && cap > 0) {
+            const size_t n = std::min<size_t>(m.size(), (size_t)cap - 1);
+            memcpy(buf, m.data(), n);
+            buf[n] = 0;
+        }
+        return 0;
+    }
+
     int release_results() {
         // windows handed out are dropped; device regions are recycled
         int64_t nw = (int64_t)wins.size();
         if (nw && r_wcnt.p)
             hipLaunchKernelGGL(k_zero_wins, dim3((unsigned)std::min<int64_t>(1024, (nw + 255) / 256)), dim3(256), 0, stream, nw,
                                (int64_t*)r_wcnt.p, (int32_t*)r_werr.p, (int64_t*)r_wmc.p, (int64_t*)r_wmh.p);
+        if (nw && r_wwit.p) hipMemsetAsync(r_wwit.p, 0, (size_t)nw * 2 * sizeof(WitRec), stream);
+        if (nw && r_aslot.p) hipMemsetAsync(r_aslot.p, 0, (size_t)nw * 4, stream);
         wins.clear();
         r_rows_used = 0;
         return 0;
@@ -4506,6 +4664,7 @@ struct Engine {
         for (int c = 0; c < EK_MAX_COLUMNS; ++c) { release(in_cols[c]); release(in_valid[c]); release(pend_cols[c]); release(pend_valid[c]); }
         release(pend_arr_d);
         release(wdesc); release(r_key); release(r_wcnt); release(r_werr); release(r_wmc); release(r_wmh);
+        release(pane_wit); release(r_wwit); release(r_aslot); release(vp_wit);
         for (int k = 0; k < EK_MAX_AGGS; ++k) { release(r_val[k]); release(r_tag[k]); }
         if (d_plan) hipFree(d_plan);
         if (d_plan_where) hipFree(d_plan_where);
@@ -4585,6 +4744,11 @@ int ek_poll_results(void* h, int32_t memory, ek_result* out) {
     if (!h || !out) return EK_ERR_INVALID;
     DeviceGuard dg(h);
     return ((Engine*)h)->poll(memory, out);
+}
+
+int ek_window_error(void* h, int64_t w, char* buf, int64_t cap, int64_t* len) {
+    if (!h) return EK_ERR_INVALID;
+    return ((Engine*)h)->window_error(w, buf, cap, len);
 }
 
 int ek_release_results(void* h, ek_result* res) {

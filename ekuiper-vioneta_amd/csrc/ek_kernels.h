@@ -377,6 +377,71 @@ __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_
 }
 #endif
 
+// ---------------------------------------------------------------- error witnesses
+// Error witness (ek_window_error, ek_errmsg.h): the earliest offender of one window / pane — a row whose WHERE failed
+// (v / tag: the columns the program reads, by column id) or a group whose HAVING did (the aggregate slots it reads,
+// by slot) — in (o1, o2) order. Offers serialise on a per-record lock, so the record is the minimum whatever the
+// order of the offers; zeroed = empty. Tags are Val tags (V_NULL .. V_ERR).
+struct WitRec {
+    unsigned long long o1, o2;
+    int32_t lock, set;
+    int64_t v[EK_MAX_AGGS];
+    uint8_t tag[EK_MAX_AGGS];
+};
+static_assert(EK_MAX_AGGS >= EK_MAX_COLUMNS, "witness slots cover the columns");
+
+// One lane at a time offers (o1, o2) to r; fill(r) writes the values under the lock when the offer is the new minimum.
+// Divergent callers are fine: the active lanes take turns (a lane spinning on the lock never waits on its own wave).
+template <typename F>
+__device__ __forceinline__ void wit_offer(WitRec* r, unsigned long long o1, unsigned long long o2, F fill) {
+    unsigned long long m = __ballot(1);
+    const int lane = (int)__lane_id();
+    while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        if (lane == l) {
+            while (atomicCAS(&r->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+            __threadfence();
+            const int set = __hip_atomic_load(&r->set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long a1 = __hip_atomic_load(&r->o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long a2 = __hip_atomic_load(&r->o2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!set || o1 < a1 || (o1 == a1 && o2 < a2)) {
+                fill(r);
+                r->o1 = o1;
+                r->o2 = o2;
+                r->set = 1;
+            }
+            __threadfence();
+            atomicExch(&r->lock, 0);
+        }
+        m &= m - 1;
+    }
+}
+__device__ __forceinline__ void wit_put(WitRec* r, int k, const Val& v) {
+    r->tag[k] = (uint8_t)v.tag;
+    r->v[k] = v.tag == V_F64 ? (int64_t)__double_as_longlong(v.f) : v.i;
+}
+// a failed WHERE row: the columns its program reads
+__device__ inline void wit_where_row(WitRec* r, unsigned long long o1, unsigned long long o2, const DPlan& p,
+                                     const DBatch& b, int64_t row) {
+    wit_offer(r, o1, o2, [&](WitRec* w) {
+        for (int k = 0; k < p.n_where; ++k) {
+            if (p.where_prog[k].op != EK_OP_COL) continue;
+            const int c = p.where_prog[k].arg;
+            Val v{V_NULL, 0, 0.0};
+            if (col_valid(b, c, row)) v = p.col_type[c] == EK_COL_F64 ? Val{V_F64, 0, col_f64(b, c, row)} : Val{V_I64, col_i64(p, b, c, row), 0.0};
+            wit_put(w, c, v);
+        }
+    });
+}
+// copy a set record (one thread)
+__device__ inline void wit_copy(WitRec* dst, const WitRec* src) {
+    if (!src->set) return;
+    dst->o1 = src->o1;
+    dst->o2 = src->o2;
+    for (int k = 0; k < EK_MAX_AGGS; ++k) { dst->v[k] = src->v[k]; dst->tag[k] = src->tag[k]; }
+    dst->set = 1;
+}
+
 // ---------------------------------------------------------------- partition pass
 struct GroupDesc {
     int64_t lo, hi;        // event index range in the batch
@@ -403,6 +468,12 @@ struct GroupDesc {
     const uint8_t* fresh;  // 1: pane r was claimed for this group (its partials are written, not merged)
     const int64_t* voff;   // range mode (virtual panes): physical row of virtual row v in pane r = v + voff[r]
     int32_t* cpa;          // first pane (group-relative) of every chunk, written by k_part for k_agg
+    // WHERE error witnesses (nullptr: the plan's WHERE cannot fail): per pane slot like pane_err, ordered by
+    // (ts, wit_o2 + row) in pane mode (release order), by buffer row in range mode (wit_ts = 0)
+    WitRec* pwit;
+    int64_t wit_o2;
+    int32_t wit_ts;
+    int32_t pad2;
 };
 
 constexpr int kMaxGroupPanes = 64;
@@ -467,7 +538,13 @@ __device__ __forceinline__ int local_part(const DPlan& p, const DBatch& b, const
     if (WHERE) {
         int w = where_decide_slow(p, b, i);
         if (w < 0) {
-            if (check_where) atomicOr(&pane_err[(gd.q_lo + rel) % gd.ring], EK_WIN_WHERE_ERROR);
+            if (check_where) {
+                const int64_t slot = (gd.q_lo + rel) % gd.ring;
+                atomicOr(&pane_err[slot], EK_WIN_WHERE_ERROR);
+                if (gd.pwit)
+                    wit_where_row(&gd.pwit[slot], gd.wit_ts ? i64_to_ord(((const int64_t*)b.col[gd.ts_col])[i]) : 0ull,
+                                  (unsigned long long)(gd.wit_o2 + i), p, b, i);
+            }
             return -1;
         }
         if (w == 0) return -1;
@@ -738,6 +815,7 @@ __global__ void k_group_prep(GroupDesc gd, int32_t* pane_err, int64_t* pane_mcnt
         pane_err[s] = 0;
         pane_mcnt[s] = 0;
         pane_mhash[s] = 0;
+        if (gd.pwit) { gd.pwit[s].set = 0; gd.pwit[s].lock = 0; }
     }
 }
 #endif
@@ -769,6 +847,12 @@ struct Results {
     uint8_t* tag[EK_MAX_AGGS];
     int64_t* win_cnt;      // rows per window
     int32_t* win_err;      // EK_WIN_* per window
+    // error witnesses (nullptr when the plan cannot fail): wwit[2 w] the window's WHERE offender, wwit[2 w + 1] its
+    // HAVING offender (smallest key), aslot[w] the smallest order-statistic index whose value failed; pwit: the pane
+    // slots' WHERE offenders (GroupDesc::pwit), read when a window takes its panes' errors
+    WitRec* wwit;
+    const WitRec* pwit;
+    int32_t* aslot;
 };
 
 // Merged partial aggregate of one (window, key), kept in registers (all indices compile-time).
@@ -869,11 +953,26 @@ __device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int
 
 // HAVING (having_operator.go:41-56): true keeps the group, false drops it, anything else is an error.
 // Aggregate slots are evaluated on demand from the group's partial (no per-lane array).
+// A failed HAVING group becomes the window's HAVING witness when its key is the smallest failed one (the reference's
+// groups come out of a Go map, aggregate_operator.go:44-72, so any failed group's error is one it can report).
+template <typename AGGF>
+__device__ __noinline__ void wit_having(WitRec* r, uint32_t key, const DPlan& p, AGGF aggf) {
+    wit_offer(r, key, 0ull, [&](WitRec* w) {
+        for (int k = 0; k < p.n_having; ++k)
+            if (p.having_prog[k].op == EK_OP_AGG) wit_put(w, p.having_prog[k].arg, aggf(p.having_prog[k].arg));
+    });
+}
 template <int NVC>
-__device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, int32_t* win_err, const SortRes* sr = nullptr) {
+__device__ __forceinline__ bool having_keep(const DPlan& p, const Part<NVC>& s, const Results& res, int32_t widx, uint32_t key,
+                                            const SortRes* sr = nullptr) {
     if (p.n_having <= 0) return true;
-    const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, [&](int k) { return agg_value(p, s, k, sr); });
-    if (h.tag != V_BOOL) { atomicOr(win_err, EK_WIN_HAVING_ERROR); return false; }
+    auto aggf = [&](int k) { return agg_value(p, s, k, sr); };
+    const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, aggf);
+    if (h.tag != V_BOOL) {
+        atomicOr(&res.win_err[widx], EK_WIN_HAVING_ERROR);
+        if (res.wwit) wit_having(&res.wwit[2 * widx + 1], key, p, aggf);
+        return false;
+    }
     return h.i != 0;
 }
 
@@ -1073,7 +1172,10 @@ __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Sta
     const int32_t widx = gd.didx[rel];
     const int32_t perr = pane_err[slot];
     if (perr) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
-        if (t == 0 && bucket == 0) atomicOr(&res.win_err[widx], perr);
+        if (t == 0 && bucket == 0) {
+            atomicOr(&res.win_err[widx], perr);
+            if (res.wwit) wit_copy(&res.wwit[2 * widx], &res.pwit[slot]);
+        }
         return;
     }
     Part<NVC> s{};
@@ -1118,7 +1220,7 @@ __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Sta
                 }
             }
             part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-            present = having_keep(p, s, &res.win_err[widx]);
+            present = having_keep(p, s, res, widx, (uint32_t)((int64_t)bucket * kk + kl));
         }
     }
     __shared__ uint32_t esh[20];
@@ -1173,7 +1275,15 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         __syncthreads();
     }
     const uint32_t total = nruns > 0 ? r_pre[nruns] : 0u;
-    if (total == 0 && (!fresh || dbase >= 0)) return;   // nothing to merge / no rows to emit
+    if (total == 0 && (!fresh || dbase >= 0)) {   // nothing to merge / no rows to emit
+        // a directly emitted pane whose every row failed WHERE still carries the window's error
+        if (dbase >= 0 && bucket == 0 && threadIdx.x == 0 && pane_err[slot]) {
+            const int32_t widx = gd.didx[rel];
+            atomicOr(&res.win_err[widx], pane_err[slot]);
+            if (res.wwit) wit_copy(&res.wwit[2 * widx], &res.pwit[slot]);
+        }
+        return;
+    }
     if (!SORT && dbase >= 0 && total <= (uint32_t)kSparseRows) {
         agg_sparse<NVC>(p, gd, st, lds, r_start, r_pre, nruns, total, bucket, kk, slot, rel, dbase, pane_err, res);
         return;
@@ -1387,7 +1497,10 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         const int32_t widx = gd.didx[rel];
         const int32_t perr = pane_err[slot];
         if (perr) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
-            if (threadIdx.x == 0 && bucket == 0) atomicOr(&res.win_err[widx], perr);
+            if (threadIdx.x == 0 && bucket == 0) {
+                atomicOr(&res.win_err[widx], perr);
+                if (res.wwit) wit_copy(&res.wwit[2 * widx], &res.pwit[slot]);
+            }
             return;
         }
         const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
@@ -1403,14 +1516,18 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                 lds_part(kl, c, vc, is, fs, m2, mn, mx);
                 if (c > 0) {
                     part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-                    bool err = false;
+                    int ea = -1;   // the first order statistic that failed
                     if constexpr (SORT) {
-                        for (int a = 0; a < p.n_sagg; ++a) err |= ((uint8_t*)(lds + lay.off_stag))[a * kk + kl] == kTagErr;
+                        for (int a = p.n_sagg - 1; a >= 0; --a) if (((uint8_t*)(lds + lay.off_stag))[a * kk + kl] == kTagErr) ea = a;
                     }
-                    if (err) atomicOr(&res.win_err[widx], EK_WIN_AGG_ERROR);   // "run Select error: ..." replaces the window
+                    const bool err = ea >= 0;
+                    if (err) {   // "run Select error: ..." replaces the window
+                        atomicOr(&res.win_err[widx], EK_WIN_AGG_ERROR);
+                        if (res.aslot) atomicMax(&res.aslot[widx], kMaxSortAggs - ea);
+                    }
                     else {
                         const SortRes sr{(const uint64_t*)(lds + lay.off_sres), (const uint8_t*)(lds + lay.off_stag), kl, kk};
-                        present = having_keep(p, s, &res.win_err[widx], SORT ? &sr : nullptr);
+                        present = having_keep(p, s, res, widx, (uint32_t)key, SORT ? &sr : nullptr);
                     }
                 }
             }
@@ -1491,7 +1608,12 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
     int32_t werr = 0;
     for (int64_t q = w.q_first; q <= w.q_last; ++q) werr |= pane_err[q % ring];
     if (werr) {
-        if (key == 0) atomicOr(&res.win_err[w.idx], werr);
+        if (key == 0) {
+            atomicOr(&res.win_err[w.idx], werr);
+            if (res.wwit)   // the first pane with an error holds the window's first failed row
+                for (int64_t q = w.q_first; q <= w.q_last; ++q)
+                    if (pane_err[q % ring]) { wit_copy(&res.wwit[2 * w.idx], &res.pwit[q % ring]); break; }
+        }
         return;
     }
     const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
@@ -1518,7 +1640,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
             }
             part_merge(p, s, c, vc, is, fs, m2, mn, mx);
         }
-        present = s.cnt > 0 && having_keep(p, s, &res.win_err[w.idx]);
+        present = s.cnt > 0 && having_keep(p, s, res, w.idx, (uint32_t)key);
     }
     __shared__ uint32_t esh[20];
     emit_rows(p, present, s, key, w.out_base, w.idx, res, esh);
@@ -1535,7 +1657,12 @@ __global__ __launch_bounds__(kBlock) void k_finalize_merge(DPlan* __restrict__ p
     int32_t werr = 0;
     for (int64_t q = w.q_first; q <= w.q_last; ++q) werr |= pane_err[q % ring];
     if (werr) {
-        if (threadIdx.x == 0) atomicOr(&res.win_err[w.idx], werr);
+        if (threadIdx.x == 0) {
+            atomicOr(&res.win_err[w.idx], werr);
+            if (res.wwit)   // the first pane with an error holds the window's first failed row
+                for (int64_t q = w.q_first; q <= w.q_last; ++q)
+                    if (pane_err[q % ring]) { wit_copy(&res.wwit[2 * w.idx], &res.pwit[q % ring]); break; }
+        }
         return;
     }
     Part<NVC> s{};
@@ -1588,7 +1715,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize_merge(DPlan* __restrict__ p
         __syncthreads();
     }
     bool present = false;
-    if (t == 0) present = s.cnt > 0 && having_keep(p, s, &res.win_err[w.idx]);
+    if (t == 0) present = s.cnt > 0 && having_keep(p, s, res, w.idx, 0u);
     __shared__ uint32_t esh[20];
     emit_rows(p, present, s, 0, w.out_base, w.idx, res, esh);
 }
@@ -1641,7 +1768,7 @@ __global__ void k_ung_zero(GroupDesc gd, DState ds) {
 #endif
 
 template <int NVC, bool WHERE>
-__global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, DBatch b, GroupDesc gd,
+__global__ __launch_bounds__(kUngBlock) __attribute__((amdgpu_waves_per_eu(NVC <= 2 ? 4 : 3))) void k_ung_tile(DPlan* __restrict__ pp, DBatch b, GroupDesc gd,
                                                         const uint8_t* __restrict__ acc, DState ds, int64_t tile,
                                                         int32_t* __restrict__ pane_err) {
     const DPlan& p = *pp;
@@ -1674,7 +1801,7 @@ __global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, 
                 if (gd.has_accept && !acc[i]) continue;
                 if (WHERE) {
                     const int w = where_decide_slow(p, b, i);
-                    if (w < 0) werr = true;
+                    werr |= w < 0;
                     if (w <= 0) continue;
                 }
                 c++;
@@ -1691,7 +1818,17 @@ __global__ __launch_bounds__(kUngBlock) void k_ung_tile(DPlan* __restrict__ pp, 
                     mx[v] = o > mx[v] ? o : mx[v];
                 }
             }
-            if (werr) atomicOr(&pane_err[(gd.q_lo + r) % gd.ring], EK_WIN_WHERE_ERROR);
+            if (werr) {
+                const int64_t slot = (gd.q_lo + r) % gd.ring;
+                atomicOr(&pane_err[slot], EK_WIN_WHERE_ERROR);
+                if (gd.pwit)   // this thread's first failed row (found again: no register holds it in the loop)
+                    for (int64_t i = s0 + threadIdx.x; i < s1; i += kUngBlock) {
+                        if ((gd.has_accept && !acc[i]) || where_decide_slow(p, b, i) >= 0) continue;
+                        wit_where_row(&gd.pwit[slot], gd.wit_ts ? i64_to_ord(((const int64_t*)b.col[gd.ts_col])[i]) : 0ull,
+                                      (unsigned long long)(gd.wit_o2 + i), p, b, i);
+                        break;
+                    }
+            }
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {   // centred second pass over the thread's own rows (L1/L2-warm)
                 if (!(fl[v] & NEED_M2) || vc[v] == 0) continue;

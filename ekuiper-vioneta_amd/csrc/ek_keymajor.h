@@ -321,7 +321,11 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 cp.cnt = j1 - j0;
                 const int hc = km_having(p, cp, nullptr);
                 if (hc <= 0) {
-                    if (WRITE && hc < 0) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
+                    if (WRITE && hc < 0)
+                        for (int kk = k; kk < kend; ++kk) {
+                            atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
+                            if (res.wwit) wit_having(&res.wwit[2 * d.widx[kk] + 1], (uint32_t)g, p, [&](int q) { return agg_value(p, cp, q); });
+                        }
                     k = kend;
                     continue;
                 }
@@ -337,10 +341,22 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
             const bool agg_err = km_fold<NVC, SORT>(p, d, j0, j1, fl, isf, s_seg, part, sres, stag);
             const SortRes sr{sres, stag, 0, 1};
             if (agg_err) {   // "run Select error" replaces each of these windows' output
-                if (WRITE) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_AGG_ERROR);
+                int ea = 0;   // the first order statistic that failed
+                for (int a = p.n_sagg - 1; a >= 0; --a) if (sel(stag, a) == kTagErr) ea = a;
+                if (WRITE)
+                    for (int kk = k; kk < kend; ++kk) {
+                        atomicOr(&res.win_err[d.widx[kk]], EK_WIN_AGG_ERROR);
+                        if (res.aslot) atomicMax(&res.aslot[d.widx[kk]], kMaxSortAggs - ea);
+                    }
             } else {
                 const int hv = km_having(p, part, SORT ? &sr : nullptr);
-                if (WRITE && hv < 0) for (int kk = k; kk < kend; ++kk) atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
+                if (WRITE && hv < 0)
+                    for (int kk = k; kk < kend; ++kk) {
+                        atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
+                        if (res.wwit)
+                            wit_having(&res.wwit[2 * d.widx[kk] + 1], (uint32_t)g, p,
+                                       [&](int q) { return agg_value(p, part, q, SORT ? &sr : nullptr); });
+                    }
                 if (hv > 0) {
                     if constexpr (ONE) {
                         one_present = true;
@@ -693,9 +709,17 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                 const SortRes sr{sres, stag, 0, 1};
                 if (agg_err) {
                     atomicOr(&res.win_err[g.widx], EK_WIN_AGG_ERROR);
+                    int ea = 0;   // the first order statistic that failed
+                    for (int a = p.n_sagg - 1; a >= 0; --a) if (sel(stag, a) == kTagErr) ea = a;
+                    if (res.aslot) atomicMax(&res.aslot[g.widx], kMaxSortAggs - ea);
                 } else {
                     const int hv = km_having(p, part, SORT ? &sr : nullptr);
-                    if (hv < 0) atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
+                    if (hv < 0) {
+                        atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
+                        if (res.wwit)
+                            wit_having(&res.wwit[2 * g.widx + 1], kbase | (uint32_t)lk, p,
+                                       [&](int q) { return agg_value(p, part, q, SORT ? &sr : nullptr); });
+                    }
                     present = hv > 0;
                 }
             }

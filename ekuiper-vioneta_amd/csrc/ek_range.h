@@ -639,14 +639,20 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
         if (lane + j * kSwLanes < n) live |= 1u << j;
     if (WHERE) {
         bool err = false;
+        int64_t erow = INT64_MAX;   // this lane's first failed row
 #pragma unroll
         for (int j = 0; j < RM; ++j) {
             if (!((live >> j) & 1u)) continue;
             const int wd = where_decide_slow(p, b, a + lane + j * kSwLanes);
+            if (wd < 0 && !err) erow = a + lane + j * kSwLanes;
             err |= wd < 0;
             if (wd <= 0) live &= ~(1u << j);
         }
         if (__any(err)) {   // a WHERE error replaces the window's output (filter_operator.go:63-77)
+            if (res.wwit) {   // the window's first failed row (buffer order = the window's order)
+                for (int o = 32; o > 0; o >>= 1) erow = min(erow, (int64_t)__shfl_xor(erow, o, kSwLanes));
+                if (lane == 0) wit_where_row(&res.wwit[2 * widx], 0ull, (unsigned long long)erow, p, b, erow);
+            }
             if (lane == 0) atomicOr(&res.win_err[widx], EK_WIN_WHERE_ERROR);
             return -1;
         }
@@ -732,13 +738,20 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
         part_merge(p, s, c, vc, is, fs, m2, mn, mx);
     };
     // keep decision of a folded group: HAVING over count(*) alone from its row count, any other HAVING on the partial
-    auto keep = [&](const Part<NVC>& s, int c) -> bool {
+    // a group HAVING over count(*) alone failed on: its witness (the count is its only aggregate input)
+    auto star_wit = [&](int c, uint32_t k) {
+        if (!res.wwit) return;
+        Part<NVC> cp{};
+        cp.cnt = c;
+        wit_having(&res.wwit[2 * widx + 1], k, p, [&](int q) { return agg_value(p, cp, q); });
+    };
+    auto keep = [&](const Part<NVC>& s, int c, uint32_t k) -> bool {
         if (p.having_star) {
             const int d = having_star_decide<NVC>(p, c, h1, h2);
-            herr |= d < 0;
+            if (d < 0) { herr = true; star_wit(c, k); }
             return d > 0;
         }
-        return having_keep(p, s, &res.win_err[widx]);
+        return having_keep(p, s, res, widx, k);
     };
     // ---- one-row groups, straight from their lanes (coalesced value loads; a rolled loop: one copy of the fold)
     if (__any(single != 0u) && !(p.having_star && h1 == 0)) {
@@ -749,7 +762,7 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
             bool present = false;
             if (mine) {
                 fold(s, 1, [&](int) { return lane + j * kSwLanes; });
-                present = keep(s, 1);
+                present = keep(s, 1, sel(key, j));
             }
             emit(present, s, sel(key, j));
         }
@@ -795,7 +808,7 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
                 int d = 1;
                 if (p.having_star) {
                     d = having_star_decide<NVC>(p, c, h1, h2);
-                    herr |= d < 0;
+                    if (d < 0) { herr = true; star_wit(c, s_key[s0 + q + hh]); }
                 }
                 if (d > 0) x += 0x10000u + (uint32_t)c;
             }
@@ -852,7 +865,7 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
                     k = kcol ? kcol[a + s_row[g0]] : 0u;
                     fold(s, c, [&](int u) { return (int)s_row[g0 + u]; });
                     // HAVING over count(*) alone was decided by the slot scan
-                    present = p.having_star ? true : having_keep(p, s, &res.win_err[widx]);
+                    present = p.having_star ? true : having_keep(p, s, res, widx, k);
                 }
                 emit(present, s, k);
             }

@@ -40,6 +40,8 @@ def lib():
         L.ek_poll_results.restype = C.c_int
         L.ek_release_results.argtypes = [C.c_void_p, C.POINTER(A.ek_result)]
         L.ek_release_results.restype = C.c_int
+        L.ek_window_error.argtypes = [C.c_void_p, C.c_int64, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.ek_window_error.restype = C.c_int
         L.ek_reset.argtypes = [C.c_void_p]
         L.ek_reset.restype = C.c_int
         L.ek_sync.argtypes = [C.c_void_p]
@@ -88,7 +90,8 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_release_results", "ek_reset", "ek_sync", "ek_set_stream", "ek_get_stats", "ek_last_error",
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
-                    "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time"]
+                    "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
+                    "ek_window_error"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -214,9 +217,21 @@ class Engine:
         r = A.ek_result()
         self._check(lib().ek_poll_results(self.h, A.EK_MEM_HOST, C.byref(r)))
         try:
-            return result_to_python(r)
+            out = result_to_python(r)
+            for w, wr in enumerate(out):
+                if wr.status != A.EK_WIN_OK:
+                    wr.error = self.window_error(w)
+            return out
         finally:
             self._check(lib().ek_release_results(self.h, C.byref(r)))
+
+    def window_error(self, w: int) -> str:
+        """The error text of window w of the last poll (ek_window_error): "run Where error: ..." etc., "" if none."""
+        n = C.c_int64()
+        self._check(lib().ek_window_error(self.h, w, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value + 1)
+        self._check(lib().ek_window_error(self.h, w, buf, n.value + 1, C.byref(n)))
+        return buf.value.decode()
 
     def poll_device(self) -> A.ek_result:
         r = A.ek_result()

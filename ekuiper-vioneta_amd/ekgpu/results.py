@@ -22,6 +22,7 @@ class WindowResult:
     keys: np.ndarray            # uint32 [rows]
     values: List[np.ndarray]    # per agg: int64 bit patterns [rows]
     tags: List[np.ndarray]      # per agg: uint8 tags [rows]
+    error: str = ""             # status != EK_WIN_OK: the reference's error text (ek_window_error)
 
     def value(self, a: int, r: int):
         t = int(self.tags[a][r])

@@ -265,3 +265,88 @@ def merge_triggers(parts):
     t = np.concatenate([np.asarray(p[1], np.int64) for p in parts])
     o = np.argsort(a, kind="stable")
     return a[o], t[o]
+
+
+def device_watermark(ts, arr, tol: int, dist, want_list: bool, dense_limit: int = 1 << 24) -> dict:
+    """The rule's WatermarkOp over the WHOLE stream (GlobalWatermark.track, watermark_op.go:144-225) computed by the
+    ranks from their own rows (torch tensors: this rank's ts and global arrival indices, on any device) with
+    collectives of `dist` (RCCL on GPUs, gloo on CPUs): F[v] = first global arrival with ts == v; the running max
+    advances exactly at the arrivals F[v] < min over u > v of F[u] (no earlier arrival reached v) — those are the
+    WatermarkTuples (watermark = v - tol); each rank checks its rows against the tuple before them (accepted iff
+    ts >= mark - tol) and one all_reduce MIN gives all_accepted.
+    F is a dense array over the batch's ts range combined by one all_reduce(MIN) when the range holds at most
+    `dense_limit` ms, otherwise the ranks' distinct timestamps (with their first arrival) are all-gathered and merged:
+    memory O(distinct ts) instead of O(ts range) (a batch spanning a day at ms resolution is 86.4 M entries).
+    Returns the tuple dict make_ctx takes: the full tuple list when `want_list` (range-mode windows) or when some row
+    is late, else only the batch's last tuple with the all_accepted / max_wm_step hints (a pane-mode shard needs
+    nothing else, include/ekgpu.h ek_global_ctx)."""
+    import torch
+    i64max = torch.iinfo(torch.int64).max
+    dev = ts.device
+    mm = torch.stack([-ts.min(), ts.max()]) if ts.numel() else torch.tensor([-i64max, -i64max], device=dev)
+    dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+    lo, hi = -int(mm[0]), int(mm[1])
+    if hi - lo + 1 <= dense_limit:
+        F = torch.full((hi - lo + 1,), i64max, dtype=torch.int64, device=dev)
+        if ts.numel():
+            F.scatter_reduce_(0, ts - lo, arr, reduce="amin", include_self=True)
+        dist.all_reduce(F, op=dist.ReduceOp.MIN)
+        S = torch.flip(torch.cummin(torch.flip(F, [0]), 0).values, [0])
+        nxt = torch.cat([S[1:], torch.tensor([i64max], dtype=torch.int64, device=dev)])
+        tv = torch.nonzero(F < nxt).squeeze(1)
+        t_arr = F[tv].contiguous()
+        t_mark = tv + lo
+        first_lo = F[0]
+    else:
+        # sparse: this rank's distinct ts with their first arrival, all-gathered (padded to the longest list)
+        u, inv = torch.unique(ts, return_inverse=True)
+        fa = torch.full((u.numel(),), i64max, dtype=torch.int64, device=dev)
+        if ts.numel():
+            fa.scatter_reduce_(0, inv, arr, reduce="amin", include_self=True)
+        world = dist.get_world_size()
+        cnt = torch.tensor([u.numel()], dtype=torch.int64, device=dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        m = int(max(int(c) for c in cnts))
+        pad_t = torch.full((m,), i64max, dtype=torch.int64, device=dev)
+        pad_a = torch.full((m,), i64max, dtype=torch.int64, device=dev)
+        pad_t[:u.numel()] = u
+        pad_a[:u.numel()] = fa
+        gt = [torch.empty_like(pad_t) for _ in range(world)]
+        ga = [torch.empty_like(pad_a) for _ in range(world)]
+        dist.all_gather(gt, pad_t)
+        dist.all_gather(ga, pad_a)
+        allt, alla = torch.cat(gt), torch.cat(ga)
+        keep = allt != i64max
+        allt, alla = allt[keep], alla[keep]
+        vt, vinv = torch.unique(allt, return_inverse=True)   # sorted distinct ts of the stream
+        F = torch.full((vt.numel(),), i64max, dtype=torch.int64, device=dev)
+        F.scatter_reduce_(0, vinv, alla, reduce="amin", include_self=True)
+        S = torch.flip(torch.cummin(torch.flip(F, [0]), 0).values, [0])
+        nxt = torch.cat([S[1:], torch.tensor([i64max], dtype=torch.int64, device=dev)])
+        k = torch.nonzero(F < nxt).squeeze(1)
+        t_arr = F[k].contiguous()
+        t_mark = vt[k].contiguous()
+        first_lo = F[0]
+    k = torch.searchsorted(t_arr, arr) - 1
+    zero_mark = ZERO_MS + tol          # the stream mark before the first event (watermark_op.go:55-58)
+    mb = torch.where(k >= 0, t_mark[k.clamp(min=0)], torch.full_like(k, zero_mark))
+    acc = torch.tensor([int(bool((ts >= mb - tol).all())) if ts.numel() else 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(acc, op=dist.ReduceOp.MIN)
+    wm_ts = t_mark - tol
+    steps = wm_ts[1:] - wm_ts[:-1]
+    j = torch.searchsorted(wm_ts, torch.tensor([lo], dtype=torch.int64, device=dev))
+    jj = int(j.clamp(max=len(wm_ts) - 1))
+    head = torch.stack([acc[0], steps.max() if steps.numel() else torch.tensor(0, device=dev), t_arr[jj], first_lo,
+                        t_arr[-1], wm_ts[-1]]).cpu().tolist()
+    all_acc, max_step, o_arr, first_lo = bool(head[0]), int(head[1]), int(head[2]), int(head[3])
+    out = {"arrivals_end": None, "all_accepted": all_acc, "max_wm_step": max_step,
+           # the first window's anchor: the earliest event (ts = lo) is released at the first tuple reaching it
+           "origin_known": all_acc and first_lo <= o_arr, "origin_ts": lo, "origin_arrival": o_arr}
+    if want_list or not all_acc:
+        out["wm_arrival"] = t_arr.cpu().numpy()
+        out["wm_ts"] = wm_ts.cpu().numpy()
+    else:
+        out["wm_arrival"] = np.array([int(head[4])], np.int64)
+        out["wm_ts"] = np.array([int(head[5])], np.int64)
+    return out

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 8
+#define EKGPU_ABI_VERSION 9
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -265,6 +265,17 @@ int ek_push_batch(void* h, const ek_batch* batch);
  * the engine; EK_MEM_DEVICE hands out device pointers. Valid until ek_release_results. */
 int ek_poll_results(void* h, int32_t memory, ek_result* out);
 int ek_release_results(void* h, ek_result* res);
+
+/* The error text of window w (0 <= w < n_windows) of the last ek_poll_results: what the reference's operator chain
+ * broadcasts in place of a failed window's rows (node/operations.go:108-113) — FilterOp "run Where error: ..."
+ * (filter_operator.go:45-58), HavingOp "run Having error: ..." (having_operator.go:45-55), ProjectOp
+ * "run Select error: ..." (project_operator.go:79-102), e.g. "run Where error: divided by zero" or
+ * "run Having error: invalid condition that returns non-bool value int64(3)"; "" when win_status is EK_WIN_OK.
+ * The text comes from the window's first failed row in window order (WHERE) or its failed group with the smallest
+ * key (HAVING: the reference's groups come out of a Go map, any failed group's text is one it can print).
+ * *len = the text's length; buf (cap bytes) receives it NUL-terminated, truncated to cap - 1 (buf NULL: length only).
+ * Valid until the next ek_poll_results. (ABI v9) */
+int ek_window_error(void* h, int64_t w, char* buf, int64_t cap, int64_t* len);
 
 /* Forget all stream state (watermark, open windows, unpolled results) but keep the device
  * allocations, so that a new stream can be pushed without re-creating the handle. */

@@ -131,8 +131,84 @@ static val_t col_val(const dataset* d, int c, int64_t row) {
 }
 
 static val_t mk_bool(int b) { val_t v; v.tag = V_BOOL; v.i = b ? 1 : 0; v.f = 0; return v; }
-static val_t mk_err(void) { val_t v; v.tag = V_ERR; v.i = 0; v.f = 0; return v; }
 static val_t mk_null(void) { val_t v; v.tag = V_NULL; v.i = 0; v.f = 0; return v; }
+
+/* ------------------------------------------------------------------ error texts
+ * An error value carries its text (v.i indexes a ring of texts, enough for one program's evaluation): valuer.go's
+ * "divided by zero" (:897-979) and invalidOpError "invalid operation %T(%v) %s %T(%v)" (:1243-1245) with the
+ * ast.Tokens spellings (pkg/ast/token.go:135-193). Go's %v of a float64 is strconv.FormatFloat(f, 'g', -1, 64):
+ * the shortest round-trip digits, exponent form when the decimal exponent is below -4 or at least 6
+ * (strconv/ftoa.go %g with the shortest precision), e.g. 2.5, 123456, 1.234567e+06, 1e-05. */
+static char eko_errtab[64][160];
+static unsigned eko_errn;
+static val_t mk_err_text(const char* fmt, ...) {
+    const unsigned k = (eko_errn++) & 63u;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(eko_errtab[k], sizeof eko_errtab[k], fmt, ap);
+    va_end(ap);
+    val_t v; v.tag = V_ERR; v.i = (int64_t)k; v.f = 0;
+    return v;
+}
+static const char* err_text(val_t v) { return eko_errtab[v.i & 63]; }
+static void go_float_v(char* out, size_t cap, double x) {
+    if (x != x) { snprintf(out, cap, "NaN"); return; }
+    if (isinf(x)) { snprintf(out, cap, x > 0 ? "+Inf" : "-Inf"); return; }
+    if (x == 0) { snprintf(out, cap, signbit(x) ? "-0" : "0"); return; }
+    char e[48];
+    for (int prec = 0; prec < 17; ++prec) {   /* shortest %.{prec}e that reads back as x */
+        snprintf(e, sizeof e, "%.*e", prec, x);
+        if (strtod(e, NULL) == x) break;
+    }
+    /* e = [-]D[.DDD]e(+|-)XX: digits without the point, decimal exponent */
+    char dig[32];
+    int nd = 0, neg = e[0] == '-';
+    const char* q = e + neg;
+    for (; *q && *q != 'e'; ++q) if (*q != '.') dig[nd++] = *q;
+    while (nd > 1 && dig[nd - 1] == '0') --nd;
+    dig[nd] = 0;
+    const int x10 = atoi(q + 1);
+    char* o = out;
+    size_t left = cap;
+#define EKO_PUT(...) do { int m_ = snprintf(o, left, __VA_ARGS__); if (m_ < 0 || (size_t)m_ >= left) return; o += m_; left -= (size_t)m_; } while (0)
+    if (neg) EKO_PUT("-");
+    if (x10 < -4 || x10 >= 6) {
+        EKO_PUT("%c", dig[0]);
+        if (nd > 1) EKO_PUT(".%s", dig + 1);
+        EKO_PUT("e%c%02d", x10 < 0 ? '-' : '+', x10 < 0 ? -x10 : x10);
+    } else if (x10 < 0) {
+        EKO_PUT("0.");
+        for (int k = 0; k < -x10 - 1; ++k) EKO_PUT("0");
+        EKO_PUT("%s", dig);
+    } else {
+        for (int k = 0; k <= x10 || k < nd; ++k) {
+            if (k == x10 + 1) EKO_PUT(".");
+            EKO_PUT("%c", k < nd ? dig[k] : '0');
+        }
+    }
+#undef EKO_PUT
+}
+/* %T(%v) of a value */
+static void go_typed(char* out, size_t cap, val_t v) {
+    char f[48];
+    switch (v.tag) {
+    case V_BOOL: snprintf(out, cap, "bool(%s)", v.i ? "true" : "false"); break;
+    case V_I64: snprintf(out, cap, "int64(%lld)", (long long)v.i); break;
+    case V_F64: go_float_v(f, sizeof f, v.f); snprintf(out, cap, "float64(%s)", f); break;
+    default: snprintf(out, cap, "<nil>(<nil>)"); break;
+    }
+}
+static const char* go_token(int op) {
+    static const char* t[] = {"", "", "", "", "", "=", "!=", "<", "<=", ">", ">=", "AND", "OR", "+", "-", "*", "/", "%"};
+    return op >= 0 && op <= EK_OP_MOD ? t[op] : "?";
+}
+static val_t invalid_op(val_t l, int op, val_t r) {
+    char a[64], b[64];
+    go_typed(a, sizeof a, l);
+    go_typed(b, sizeof b, r);
+    return mk_err_text("invalid operation %s %s %s", a, go_token(op), b);
+}
+static val_t div_zero(void) { return mk_err_text("divided by zero"); }
 
 /* valuer.go:823-1000 SimpleDataEval for the op subset of the plan ISA */
 static val_t simple_eval(val_t l, val_t r, int op) {
@@ -146,16 +222,16 @@ static val_t simple_eval(val_t l, val_t r, int op) {
         }
     }
     if (l.tag == V_BOOL) {
-        if (r.tag != V_BOOL) return mk_err();
+        if (r.tag != V_BOOL) return invalid_op(l, op, r);
         switch (op) {
         case EK_OP_AND: return mk_bool(l.i && r.i);
         case EK_OP_OR: return mk_bool(l.i || r.i);
         case EK_OP_EQ: return mk_bool(l.i == r.i);
         case EK_OP_NEQ: return mk_bool(l.i != r.i);
-        default: return mk_err();
+        default: return invalid_op(l, op, r);
         }
     }
-    if (r.tag == V_BOOL) return mk_err();
+    if (r.tag == V_BOOL) return invalid_op(l, op, r);
     if (l.tag == V_F64 || r.tag == V_F64) {
         double a = l.tag == V_F64 ? l.f : (double)l.i;
         double b = r.tag == V_F64 ? r.f : (double)r.i;
@@ -170,9 +246,9 @@ static val_t simple_eval(val_t l, val_t r, int op) {
         case EK_OP_ADD: v.f = a + b; return v;
         case EK_OP_SUB: v.f = a - b; return v;
         case EK_OP_MUL: v.f = a * b; return v;
-        case EK_OP_DIV: if (b == 0) return mk_err(); v.f = a / b; return v;
-        case EK_OP_MOD: if (b == 0) return mk_err(); v.f = fmod(a, b); return v;
-        default: return mk_err();
+        case EK_OP_DIV: if (b == 0) return div_zero(); v.f = a / b; return v;
+        case EK_OP_MOD: if (b == 0) return div_zero(); v.f = fmod(a, b); return v;
+        default: { val_t lf = v, rf = v; lf.f = a; rf.f = b; return invalid_op(lf, op, rf); }
         }
     }
     {
@@ -188,9 +264,9 @@ static val_t simple_eval(val_t l, val_t r, int op) {
         case EK_OP_ADD: v.i = (int64_t)((uint64_t)a + (uint64_t)b); return v;
         case EK_OP_SUB: v.i = (int64_t)((uint64_t)a - (uint64_t)b); return v;
         case EK_OP_MUL: v.i = (int64_t)((uint64_t)a * (uint64_t)b); return v;
-        case EK_OP_DIV: if (b == 0) return mk_err(); v.i = (a == INT64_MIN && b == -1) ? a : a / b; return v;
-        case EK_OP_MOD: if (b == 0) return mk_err(); v.i = (b == -1) ? 0 : a % b; return v;
-        default: return mk_err();
+        case EK_OP_DIV: if (b == 0) return div_zero(); v.i = (a == INT64_MIN && b == -1) ? a : a / b; return v;
+        case EK_OP_MOD: if (b == 0) return div_zero(); v.i = (b == -1) ? 0 : a % b; return v;
+        default: return invalid_op(l, op, r);
         }
     }
 }
@@ -208,7 +284,7 @@ static val_t eval_prog(const ek_instr* prog, int n, const dataset* d, int64_t ro
         case EK_OP_CONST_I64: { val_t v; v.tag = V_I64; v.i = in->i64; v.f = 0; st[sp++] = v; } break;
         case EK_OP_CONST_F64: { val_t v; v.tag = V_F64; v.i = 0; v.f = in->f64; st[sp++] = v; } break;
         default: {
-            if (sp < 2) return mk_err();
+            if (sp < 2) return mk_err_text("malformed program");
             val_t r = st[--sp], l = st[--sp], res;
             if (l.tag == V_ERR) res = l;
             else if (in->op == EK_OP_AND && l.tag == V_BOOL && !l.i) res = mk_bool(0);
@@ -428,9 +504,16 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
     for (int64_t k = 0; k < nc; ++k) {
         if (p->n_where <= 0) { sel[ns++] = content[k]; continue; }
         val_t r = eval_prog(p->where_prog, p->n_where, d, content[k], NULL);
-        if (r.tag == V_ERR) { status = EK_WIN_WHERE_ERROR; snprintf(ob->werr + w * 128, 128, "run Where error: evaluation error"); break; }
+        /* FilterOp over the window's rows in order: the first failure is the window's error (filter_operator.go:60-81) */
+        if (r.tag == V_ERR) { status = EK_WIN_WHERE_ERROR; snprintf(ob->werr + w * 128, 128, "run Where error: %s", err_text(r)); break; }
         if (r.tag == V_BOOL) { if (r.i) sel[ns++] = content[k]; }
-        else if (r.tag != V_NULL) { status = EK_WIN_WHERE_ERROR; snprintf(ob->werr + w * 128, 128, "run Where error: invalid condition that returns non-bool value"); break; }
+        else if (r.tag != V_NULL) {
+            char tv[80];
+            go_typed(tv, sizeof tv, r);
+            status = EK_WIN_WHERE_ERROR;
+            snprintf(ob->werr + w * 128, 128, "run Where error: invalid condition that returns non-bool value %s", tv);
+            break;
+        }
     }
     int64_t rows_before = ob->key.n;
     if (status == EK_WIN_OK && ns > 0) {
@@ -470,9 +553,14 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
         uint8_t* nul = (uint8_t*)malloc((size_t)ns);
         val_t aggv[EK_MAX_AGGS];
         agg_out ao[EK_MAX_AGGS];
-        for (int64_t g = 0; g < ng && status == EK_WIN_OK; ++g) {
+        /* every group is aggregated: HavingOp's error (any failed group: the reference ranges a Go map, the engine
+         * reports the smallest failed key) wins over ProjectOp's (the first failed aggregate slot over the groups) */
+        int64_t hkey = INT64_MAX, aslot = EK_MAX_AGGS;
+        char htext[128] = "", atext[160] = "";
+        for (int64_t g = 0; g < ng; ++g) {
             int64_t gn = goff[g + 1] - goff[g];
             const int64_t* rows = grows + goff[g];
+            int gfail = 0;
             for (int a = 0; a < p->n_aggs; ++a) {
                 const ek_agg_spec* as = &p->aggs[a];
                 int c = as->column;
@@ -486,21 +574,29 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
                 }
                 agg_eval(as->fn, is_float, gn, iv, fv, nul, as->param, &ao[a]);
                 if (ao[a].err) {
-                    status = EK_WIN_AGG_ERROR;
-                    snprintf(ob->werr + w * 128, 128, "run Select error: %s", ao[a].msg);
+                    status |= EK_WIN_AGG_ERROR;
+                    if (a < aslot) { aslot = a; snprintf(atext, sizeof atext, "%s", ao[a].msg); }
+                    gfail = 1;
                     break;
                 }
                 aggv[a].tag = ao[a].tag == EK_TAG_NULL ? V_NULL : (ao[a].tag == EK_TAG_I64 ? V_I64 : V_F64);
                 aggv[a].i = ao[a].i; aggv[a].f = ao[a].f;
             }
-            if (status != EK_WIN_OK) break;
+            if (gfail) continue;   /* a failed aggregate: no HAVING, no row for this group */
             if (p->n_having > 0) {
                 val_t r = eval_prog(p->having_prog, p->n_having, d, rows[0], aggv);
                 if (r.tag != V_BOOL) {
-                    status = EK_WIN_HAVING_ERROR;
-                    snprintf(ob->werr + w * 128, 128, r.tag == V_ERR ? "run Having error: evaluation error"
-                                                                      : "run Having error: invalid condition that returns non-bool value");
-                    break;
+                    status |= EK_WIN_HAVING_ERROR;
+                    if (gkey[g] < hkey) {
+                        hkey = gkey[g];
+                        if (r.tag == V_ERR) snprintf(htext, sizeof htext, "run Having error: %s", err_text(r));
+                        else {
+                            char tv[80];
+                            go_typed(tv, sizeof tv, r);
+                            snprintf(htext, sizeof htext, "run Having error: invalid condition that returns non-bool value %s", tv);
+                        }
+                    }
+                    continue;
                 }
                 if (!r.i) continue;
             }
@@ -511,6 +607,13 @@ static void emit_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t we
                 v_push(&ob->aval[a], bits);
                 v_push(&ob->atag[a], ao[a].tag);
             }
+        }
+        if (htext[0]) snprintf(ob->werr + w * 128, 128, "%s", htext);
+        else if (atext[0]) {
+            /* HavingOp meets a failed aggregate it reads before ProjectOp does */
+            int in_having = 0;
+            for (int k = 0; k < p->n_having; ++k) in_having |= p->having_prog[k].op == EK_OP_AGG && p->having_prog[k].arg == aslot;
+            snprintf(ob->werr + w * 128, 128, "%s%s", in_having ? "run Having error: " : "run Select error: ", atext);
         }
         free(gstart); free(gkey); free(gcount); free(rowg); free(goff); free(fill); free(grows);
         free(iv); free(fv); free(nul);
@@ -637,8 +740,12 @@ static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_
             val_t r = eval_prog(p->having_prog, p->n_having, d, glast[g], aggv);
             if (r.tag != V_BOOL) {
                 status = EK_WIN_HAVING_ERROR;
-                snprintf(ob->werr + w * 128, 128, r.tag == V_ERR ? "run Having error: evaluation error"
-                                                                  : "run Having error: invalid condition that returns non-bool value");
+                if (r.tag == V_ERR) snprintf(ob->werr + w * 128, 128, "run Having error: %s", err_text(r));
+                else {
+                    char tv[80];
+                    go_typed(tv, sizeof tv, r);
+                    snprintf(ob->werr + w * 128, 128, "run Having error: invalid condition that returns non-bool value %s", tv);
+                }
                 break;
             }
             if (!r.i) continue;

@@ -1,5 +1,6 @@
-"""bench.py's distributed router (device_router: the global WatermarkOp computed by the ranks from their own rows,
-one all_reduce MIN over the ts range) against the host router ekgpu.shard.GlobalWatermark.track over the whole
+"""The distributed router (ekgpu.shard.device_watermark: the global WatermarkOp computed by the ranks from their own
+rows — one all_reduce MIN over the ts range, or the ranks' distinct timestamps all-gathered when the range is wider
+than dense_limit) against the host router ekgpu.shard.GlobalWatermark.track over the whole
 stream (watermark_op.go:144-225): the same WatermarkTuples, all_accepted and first-window anchor, on gloo with
 world 2 and 4, for a sorted stream, an out-of-order stream inside the tolerance and one with late events."""
 import os
@@ -31,36 +32,36 @@ def _stream(kind, n=20_000):
 TOL = {"sorted": 0, "disorder": 30, "late": 20}
 
 
-def _worker(rank, world, port, kind, q):
+def _worker(rank, world, port, kind, q, dense_limit):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch
     import torch.distributed as dist
-    import bench
-    from ekgpu.shard import shard_of
+    from ekgpu.shard import device_watermark, shard_of
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         key, ts = _stream(kind)
         own = np.nonzero(shard_of(key, world) == rank)[0]
-        tup = bench.device_router(torch.from_numpy(ts[own].copy()), torch.from_numpy(own.astype(np.int64)), TOL[kind],
-                                  dist, want_list=True)
+        tup = device_watermark(torch.from_numpy(ts[own].copy()), torch.from_numpy(own.astype(np.int64)), TOL[kind],
+                               dist, want_list=True, dense_limit=dense_limit)
         if rank == 0:
             q.put({k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in tup.items()})
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("dense_limit", [1 << 24, 0], ids=["dense", "sparse"])
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("kind", ["sorted", "disorder", "late"])
-def test_device_router_matches_global_watermark(kind, world):
+def test_device_router_matches_global_watermark(kind, world, dense_limit):
     import torch.multiprocessing as mp
     from ekgpu.shard import GlobalWatermark
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q, dense_limit)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=180)
