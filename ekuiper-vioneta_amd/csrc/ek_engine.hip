@@ -4355,7 +4355,7 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 3;   // 3: the processing-time clock and timers
+    static constexpr int64_t kStateVersion = 4;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -4488,6 +4488,8 @@ struct Engine {
                 if (int rc = dev_append(s, (char*)pane_err.p + (size_t)x * 4, 4)) return rc;
                 if (int rc = dev_append(s, (char*)pane_mcnt.p + (size_t)x * 8, 8)) return rc;
                 if (int rc = dev_append(s, (char*)pane_mhash.p + (size_t)x * 8, 8)) return rc;
+                if (pane_wit.p)   // the pane's WHERE witness (a plan whose WHERE can fail: the same plan on import)
+                    if (int rc = dev_append(s, (char*)pane_wit.p + (size_t)x * sizeof(WitRec), sizeof(WitRec))) return rc;
             }
         }
         if (range_mode) {
@@ -4599,6 +4601,8 @@ struct Engine {
                 if (int rc = dev_restore(r, (char*)pane_err.p + (size_t)x * 4, 4)) return rc;
                 if (int rc = dev_restore(r, (char*)pane_mcnt.p + (size_t)x * 8, 8)) return rc;
                 if (int rc = dev_restore(r, (char*)pane_mhash.p + (size_t)x * 8, 8)) return rc;
+                if (pane_wit.p)
+                    if (int rc = dev_restore(r, (char*)pane_wit.p + (size_t)x * sizeof(WitRec), sizeof(WitRec))) return rc;
             }
         }
         if (range_mode) {

@@ -118,3 +118,25 @@ def test_window_error_abi(engine_mod):
     assert lib().ek_window_error(eng.h, int(r.n_windows), buf, 8, C.byref(n)) == A.EK_ERR_INVALID
     lib().ek_release_results(eng.h, C.byref(r))
     eng.close()
+
+
+def test_window_error_texts_across_restore(oracle, engine_mod):
+    """A checkpoint taken while panes hold failed rows carries their witnesses (state v4): the restored handle
+    prints the same texts as one uninterrupted run."""
+    sql = "SELECT count(*) FROM demo WHERE temp * 1.5 GROUP BY color, HOPPINGWINDOW(ss, 2, 1)"
+    rule = compile_rule(sql, SCHEMA, num_keys=37)
+    cols = _stream(20_000, 37, seed=5)
+    exp = oracle.run(rule.plan, cols)
+    half = 10_037
+    a = engine_mod.Engine(rule.plan)
+    a.push_host([c[:half] for c in cols])
+    got = a.poll()
+    blob = a.export_state()
+    a.close()
+    b = engine_mod.Engine(rule.plan)
+    b.import_state(blob)
+    b.push_host([c[half:] for c in cols])
+    got += b.poll()
+    b.close()
+    assert any(exp.errors)
+    _assert_errors(got, exp)
