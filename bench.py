@@ -661,6 +661,10 @@ def main():
             kb = n * 8 if iet else 0
         elif ph == "partition":
             kb = n * sum(COL_BYTES[c] for c in cfg["in_cols"] if c != "ts")
+        elif ph_n[PHASES.index("partition")] == 0:
+            # no partition pass (range windows: k_small_win / the key-major walks read the event columns
+            # themselves): the aggregate kernels move the step's bytes less what the stats pass read
+            kb = alg_bytes - (n * 8 if iet and ph_n[PHASES.index("stats")] else 0)
         else:
             kb = rows * cfg["out_bytes"]
         kb_launch = kb / per_step
