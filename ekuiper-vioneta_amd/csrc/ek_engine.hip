@@ -891,6 +891,7 @@ struct Engine {
         h_rtrig.clear();
         g_wa = g_wt = nullptr;
         g_nwm = 0;
+        g_sess_last_end = INT64_MIN;
         g_trig.clear();
         wins.clear();
         r_rows_used = 0;
@@ -3832,6 +3833,7 @@ struct Engine {
     std::vector<GTrig> g_trig;          // accepted global sliding triggers not released yet (arrival order)
     struct GSess { int64_t start, end; };
     std::vector<GSess> g_sess;          // sessions the router closed in this push (ek_global_ctx sess_*), in order
+    int64_t g_sess_last_end = INT64_MIN;   // the last session end delivered (ends advance across pushes)
 
     int global_check() {
         if (plan.is_event_time) {
@@ -3882,10 +3884,13 @@ struct Engine {
             return fail(EK_ERR_INVALID, "missing session list");
         g_sess.clear();
         if (wtype == EK_WINDOW_SESSION)
-            for (int64_t k = 0; k < g->n_sess; ++k) {
-                if (g->sess_end[k] <= (k ? g->sess_end[k - 1] : INT64_MIN)) return fail(EK_ERR_INVALID, "session ends must advance");
+            for (int64_t k = 0; k < g->n_sess; ++k) {   // ends advance within the list and across pushes
+                if (g->sess_end[k] <= (k ? g->sess_end[k - 1] : g_sess_last_end))
+                    return fail(EK_ERR_INVALID, "session ends must advance (session %lld ends at %lld, after %lld)",
+                                (long long)k, (long long)g->sess_end[k], (long long)(k ? g->sess_end[k - 1] : g_sess_last_end));
                 g_sess.push_back(GSess{g->sess_start[k], g->sess_end[k]});
             }
+        if (!g_sess.empty()) g_sess_last_end = g_sess.back().end;
         g_wa = g->wm_arrival;
         g_wt = g->wm_ts;
         g_nwm = g->n_wm;
@@ -4713,6 +4718,10 @@ int ek_device_count(void) {
 int ek_create(const ek_plan* plan, int device, void** out_handle) {
     if (!plan || !out_handle) return EK_ERR_INVALID;
     *out_handle = nullptr;
+    // init selects `device`: give the calling thread its current device back
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    struct Restore { int d; ~Restore() { if (d >= 0) hipSetDevice(d); } } restore{prev};
     Engine* e = new (std::nothrow) Engine();
     if (!e) return EK_ERR_NOMEM;
     int rc = e->init(plan, device);
@@ -4823,6 +4832,9 @@ int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end) {
     if (!h) return EK_ERR_INVALID;
     DeviceGuard dg(h);
     Engine* e = (Engine*)h;
+    if (e->wtype == EK_WINDOW_SESSION)   // the sessions a tuple closes travel in ek_global_ctx.sess_* only
+        return e->fail(EK_ERR_INVALID, "a SESSIONWINDOW shard takes watermark advances through ek_push_batch_global "
+                                       "(with the router's session list), not ek_advance_watermark");
     const int64_t a = std::max<int64_t>(0, arrivals_end - 1);
     ek_global_ctx g{};
     g.arrivals_end = arrivals_end;

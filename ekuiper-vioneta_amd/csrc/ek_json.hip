@@ -480,6 +480,7 @@ struct Buf {
 };
 
 struct JsonDecoder {
+    int dev = 0;
     JSchema sch{};
     JSchema* d_sch = nullptr;
     hipStream_t stream = nullptr;
@@ -532,6 +533,7 @@ struct JsonDecoder {
             sch.hash[c] = h;
         }
         if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
+        dev = device;
         if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(EK_ERR_DEVICE, "stream");
         if (hipMalloc((void**)&d_sch, sizeof(JSchema)) != hipSuccess) return fail(EK_ERR_NOMEM, "schema alloc");
         if (hipMemcpy(d_sch, &sch, sizeof(JSchema), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "schema copy");
@@ -629,6 +631,18 @@ struct JsonDecoder {
 
 thread_local std::string g_json_create_error;
 
+// Every entry point runs on the decoder's device and gives the calling thread its current device back (a Go node
+// may call from any OS thread), like ek_engine.hip's DeviceGuard.
+struct JsonDeviceGuard {
+    int prev = -1;
+    explicit JsonDeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) { prev = -1; return; }
+        if (dev >= 0 && prev != dev) hipSetDevice(dev);
+        else if (dev >= 0) prev = -1;
+    }
+    ~JsonDeviceGuard() { if (prev >= 0) hipSetDevice(prev); }
+};
+
 }  // namespace
 
 extern "C" {
@@ -636,6 +650,7 @@ extern "C" {
 int ek_json_create(const ek_json_schema* schema, int device, void** out) {
     if (!out) return EK_ERR_INVALID;
     *out = nullptr;
+    JsonDeviceGuard dg(-1);   // init selects `device`: the guard restores the caller's
     JsonDecoder* d = new (std::nothrow) JsonDecoder();
     if (!d) return EK_ERR_NOMEM;
     if (int rc = d->init(schema, device)) {
@@ -650,11 +665,13 @@ int ek_json_create(const ek_json_schema* schema, int device, void** out) {
 int ek_json_decode(void* h, const char* bytes, int64_t n_bytes, const int64_t* offsets, int64_t n_msgs, int32_t memory,
                    ek_batch* out) {
     if (!h) return EK_ERR_INVALID;
+    JsonDeviceGuard dg(((JsonDecoder*)h)->dev);
     return ((JsonDecoder*)h)->decode(bytes, n_bytes, offsets, n_msgs, memory, out);
 }
 
 int ek_json_errors(void* h, int64_t* msg_index, uint8_t* code, int64_t cap, int64_t* n_errors) {
     if (!h || !n_errors) return EK_ERR_INVALID;
+    JsonDeviceGuard dg(((JsonDecoder*)h)->dev);
     return ((JsonDecoder*)h)->errors(msg_index, code, cap, n_errors);
 }
 
@@ -667,6 +684,8 @@ int ek_json_get_stats(void* h, ek_json_stats* out) {
 const char* ek_json_last_error(void* h) { return h ? ((JsonDecoder*)h)->err.c_str() : g_json_create_error.c_str(); }
 
 int ek_json_destroy(void* h) {
+    if (!h) return 0;
+    JsonDeviceGuard dg(((JsonDecoder*)h)->dev);
     delete (JsonDecoder*)h;
     return 0;
 }

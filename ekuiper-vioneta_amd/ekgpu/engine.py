@@ -194,8 +194,27 @@ class Engine:
                 return oa[:k], ot[:k]
             cap = k
 
-    def advance_watermark(self, wm_ms: int, arrivals_end: int):
-        self._check(lib().ek_advance_watermark(self.h, int(wm_ms), int(arrivals_end)))
+    def advance_watermark(self, wm_ms: int, arrivals_end: int, sessions=None):
+        """A global WatermarkTuple with no rows for this shard. sessions: the (start, end) pairs the router's session
+        logic closed at it (SESSIONWINDOW shards, which ek_advance_watermark refuses): sent through
+        ek_push_batch_global with an empty batch."""
+        if sessions is None:
+            self._check(lib().ek_advance_watermark(self.h, int(wm_ms), int(arrivals_end)))
+            return
+        a = np.array([max(0, int(arrivals_end) - 1)], np.int64)
+        t = np.array([int(wm_ms)], np.int64)
+        ss = np.array([s for s, _ in sessions] or [0], np.int64)
+        se = np.array([e for _, e in sessions] or [0], np.int64)
+        ctx = A.ek_global_ctx()
+        ctx.arrivals_end = int(arrivals_end)
+        ctx.wm_arrival = a.ctypes.data
+        ctx.wm_ts = t.ctypes.data
+        ctx.n_wm = 1
+        ctx.sess_start = ss.ctypes.data
+        ctx.sess_end = se.ctypes.data
+        ctx.n_sess = len(sessions)
+        ctx.memory = A.EK_MEM_HOST
+        self.push_global(None, ctx)
 
     def advance_time(self, now_ms: int):
         """Processing-time windows: move the handle's clock to now_ms (the first call, before any row, is the rule's

@@ -66,11 +66,31 @@ def group_key_string(values: Sequence) -> str:
     return "".join(go_v(v) + "," for v in values)
 
 
+def _factorize_dense(a):
+    """(codes, uniques) of a nil-free array, uniques in first-seen order: pandas.factorize when pandas is importable
+    (hashing in C), numpy otherwise (a sort: np.unique, then the first-seen order restored)."""
+    try:
+        import pandas as pd
+    except ImportError:
+        pd = None
+    if pd is not None:
+        codes, uniques = pd.factorize(a, use_na_sentinel=False)
+        return np.asarray(codes, np.int64), np.asarray(uniques, dtype=object)
+    if len(a) == 0:
+        return np.zeros(0, np.int64), np.zeros(0, dtype=object)
+    uniq, first, inv = np.unique(a, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")
+    rank = np.empty(len(order), np.int64)
+    rank[order] = np.arange(len(order))
+    return rank[np.asarray(inv).reshape(-1)], np.asarray(uniq[order], dtype=object)
+
+
 def _factorize(col, valid=None):
-    """(codes, uniques) of a column, hashed in C (pandas.factorize): uniques in first-seen order over the non-nil
-    rows, codes[i] = -1 for nil rows (None, or validity 0). The dictionaries below loop over the distinct values
-    only, not over the rows."""
-    import pandas as pd
+    """(codes, uniques) of a column: uniques in first-seen order over the non-nil rows, codes[i] = -1 for nil rows
+    (None, or validity 0). The dictionaries below loop over the distinct values only, not over the rows.
+    An object column holding values of several Python types is keyed by their Go %v strings (the reference's group
+    key, aggregate_operator.go:49-56): Python-equal values of different types (True == 1 == 1.0) are one key only
+    where Go prints them alike (1 and 1.0 both print "1", true does not)."""
     a = col if isinstance(col, np.ndarray) and col.dtype.kind in "iuf" else np.asarray(col, dtype=object)
     n = len(a)
     keep = None
@@ -79,15 +99,16 @@ def _factorize(col, valid=None):
     if a.dtype == object:
         nn = np.not_equal(a, None)
         keep = nn if keep is None else keep & nn
+        live = a if keep.all() else a[keep]
+        if len({type(x) for x in live}) > 1:
+            a = np.array([None if x is None else go_v(x) for x in a], dtype=object)
     if keep is None or keep.all():
-        codes, uniques = pd.factorize(a, use_na_sentinel=False)
-        codes = np.asarray(codes, np.int64)
-    else:
-        idx = np.nonzero(keep)[0]
-        sub, uniques = pd.factorize(a[idx], use_na_sentinel=False)
-        codes = np.full(n, -1, np.int64)
-        codes[idx] = sub
-    return codes, np.asarray(uniques, dtype=object)
+        return _factorize_dense(a)
+    idx = np.nonzero(keep)[0]
+    sub, uniques = _factorize_dense(a[idx])
+    codes = np.full(n, -1, np.int64)
+    codes[idx] = sub
+    return codes, uniques
 
 
 def _first_rows(codes: np.ndarray) -> np.ndarray:

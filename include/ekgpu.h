@@ -366,7 +366,9 @@ int ek_advance_time(void* h, int64_t now_ms);
 /* One micro-batch of a shard: the rows owned by this handle plus the global context above. */
 int ek_push_batch_global(void* h, const ek_batch* batch, const ek_global_ctx* g);
 /* A WatermarkTuple with no new rows (event_window_trigger.go:126-146): the global watermark reached wm_ms after
- * `arrivals_end` global arrivals. Equivalent to ek_push_batch_global with an empty batch and one tuple. */
+ * `arrivals_end` global arrivals. Equivalent to ek_push_batch_global with an empty batch and one tuple.
+ * A SESSIONWINDOW shard is refused (EK_ERR_INVALID): the sessions such a tuple closes only travel in
+ * ek_global_ctx.sess_*, so it takes ek_push_batch_global with an empty batch instead. */
 int ek_advance_watermark(void* h, int64_t wm_ms, int64_t arrivals_end);
 /* The rows of `batch` (global arrivals g->row_arrival) that are accepted by the global watermark and match
  * SLIDINGWINDOW ... OVER (WHEN ...) (every accepted row when there is no OVER): their global arrival and ts,

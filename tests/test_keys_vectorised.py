@@ -57,3 +57,35 @@ def test_string_dicts_match_per_row():
     ss = sorted(seen)
     codes = [od.code[s] for s in ss]
     assert codes == sorted(codes)
+
+
+def _per_row_ids(cols, valids):
+    ids, out = {}, []
+    for i in range(len(cols[0])):
+        row = tuple(None if (m is not None and not m[i]) else c[i] for c, m in zip(cols, valids))
+        out.append(ids.setdefault(group_key_string(row), len(ids)))
+    return out
+
+
+def test_mixed_type_object_dimension_keys_by_go_strings():
+    """True == 1 == 1.0 in Python, but the reference's group key is the %v string: 1 and 1.0 print "1" (one group),
+    true prints "true" (the group of the string "true", not of 1)."""
+    col = np.array([True, 1, 1.0, "1", "true", None, 2.5, False, 0, "x"] * 3, dtype=object)
+    d = GroupKeyDict(["v"], ["string"], capacity=64)
+    got = list(d.encode([col], [None]))
+    assert got == _per_row_ids([col], [None])
+    assert got[0] == got[4] and got[1] == got[2] == got[3] and got[0] != got[1] and got[7] != got[8]
+
+
+def test_factorize_without_pandas(monkeypatch):
+    """pandas is optional: the numpy fallback gives the same first-seen codes."""
+    import sys
+    from ekgpu import keys
+    rng = np.random.default_rng(11)
+    cols, valids = _rows(2000, rng)
+    with_pd = [keys._factorize(c, v) for c, v in zip(cols, valids)]
+    monkeypatch.setitem(sys.modules, "pandas", None)
+    without = [keys._factorize(c, v) for c, v in zip(cols, valids)]
+    for (c1, u1), (c2, u2) in zip(with_pd, without):
+        assert np.array_equal(c1, c2)
+        assert [group_key_string([x]) for x in u1] == [group_key_string([x]) for x in u2]

@@ -116,3 +116,19 @@ def test_shard_mode_rejections(engine_mod):
         eng.push_global(cols, make_ctx(wm, np.arange(100)))
     assert ei.value.code == A.EK_ERR_STATE
     eng.close()
+
+
+def test_session_shard_watermark_takes_session_list(engine_mod):
+    """A SESSIONWINDOW shard: ek_advance_watermark (no session list) is refused rather than losing the sessions the
+    tuple closes; Engine.advance_watermark(..., sessions=) delivers them through ek_push_batch_global; session ends
+    must advance across pushes."""
+    rule = compile_rule(H.CASES["session_gaps"][0], H.SCHEMA, num_keys=4)
+    eng = engine_mod.Engine(rule.plan)
+    with pytest.raises(engine_mod.EngineError) as ei:
+        eng.advance_watermark(1541152480000, 1)
+    assert ei.value.code == A.EK_ERR_INVALID
+    eng.advance_watermark(1541152490000, 1, sessions=[(1541152480000, 1541152485000)])
+    with pytest.raises(engine_mod.EngineError) as ei:
+        eng.advance_watermark(1541152500000, 1, sessions=[(1541152481000, 1541152484000)])
+    assert ei.value.code == A.EK_ERR_INVALID
+    eng.close()
