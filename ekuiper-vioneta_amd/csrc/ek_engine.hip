@@ -690,6 +690,8 @@ struct Engine {
         sorted_chunk = env_int("EKGPU_SORTED_CHUNK", kTile);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
         sw_grid = std::max(1, env_int("EKGPU_SW_GRID", 4096));
+        fin_ring = env_int("EKGPU_FIN_RING", 1) != 0;
+        fin_ring_chunks = env_int("EKGPU_FIN_RING_CHUNKS", 0);
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
@@ -1121,12 +1123,38 @@ struct Engine {
         if (nf || plan.debug_membership)
             hipMemcpyAsync(wdesc.p, hd, (size_t)n * sizeof(WinDesc), hipMemcpyHostToDevice, stream);
         if (nf) {
-            dim3 grid_f((unsigned)((K + kBlock - 1) / kBlock), (unsigned)nf);
             const int nvc = std::max(1, dp.n_vc);
             Results rv = results_view();
             const WinDesc* wd = (const WinDesc*)wdesc.p;
             const int ph = phase_begin(EK_PHASE_FINALIZE);
-            ek::launch_fin(nvc, dp.pseudo_keys != 0, grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv);
+            // consecutive hopping windows over one count / sum / min / max column: the register-ring walk reads each
+            // pane once (k_finalize_ring); anything else merges per (window, key block) (k_finalize)
+            int64_t span = 0;
+            bool ordered = true;
+            for (int64_t i = 0; i < nf; ++i) {
+                span = std::max(span, hd[i].q_last - hd[i].q_first + 1);
+                if (i && (hd[i].q_first < hd[i - 1].q_first || hd[i].q_last <= hd[i - 1].q_last)) ordered = false;
+            }
+            bool ring_ok = fin_ring && nf >= 2 && ordered && span <= 16 && !dp.pseudo_keys && dp.n_vc == 1 &&
+                           dp.n_sagg == 0 && (dp.vc_flags[0] & ~(NEED_CNT | NEED_SUM | NEED_MIN | NEED_MAX)) == 0;
+            for (int k = 0; k < dp.n_aggs && ring_ok; ++k)   // the ring's own emission: count / sum / avg / min / max
+                ring_ok = dp.agg_fn[k] == EK_AGG_COUNT_STAR ||
+                          (dp.agg_vc[k] == 0 && (dp.agg_fn[k] == EK_AGG_COUNT || dp.agg_fn[k] == EK_AGG_SUM ||
+                                                 dp.agg_fn[k] == EK_AGG_AVG || dp.agg_fn[k] == EK_AGG_MIN ||
+                                                 dp.agg_fn[k] == EK_AGG_MAX));
+            if (ring_ok) {
+                const int64_t kb = (K + kBlock - 1) / kBlock;
+                int64_t chunks = fin_ring_chunks > 0 ? fin_ring_chunks
+                                                     : std::max<int64_t>(1, std::min<int64_t>(nf / (4 * span), (1024 + kb - 1) / kb));
+                chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, nf));
+                const int64_t cw = (nf + chunks - 1) / chunks;
+                dim3 grid_r((unsigned)kb, (unsigned)((nf + cw - 1) / cw));
+                ek::launch_fin_ring((int)span, (dp.vc_flags[0] & NEED_CNT) != 0, dp.n_having > 0, grid_r, stream, d_plan, wd, (int32_t)nf,
+                                    (int32_t)cw, dstate, ring, (const int32_t*)pane_err.p, rv);
+            } else {
+                dim3 grid_f((unsigned)((K + kBlock - 1) / kBlock), (unsigned)nf);
+                ek::launch_fin(nvc, dp.pseudo_keys != 0, grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv);
+            }
             phase_end(ph);
         }
         if (plan.debug_membership) {
@@ -1830,6 +1858,8 @@ struct Engine {
     // k_small_win over nb windows (persistent waves, one window at a time each; see ek_range.h), specialised by value
     // columns, WHERE and rows per lane
     int sw_grid = 4096;   // EKGPU_SW_GRID: waves of a k_small_win launch
+    bool fin_ring = true;       // EKGPU_FIN_RING=0: hopping windows always through k_finalize
+    int fin_ring_chunks = 0;    // EKGPU_FIN_RING_CHUNKS: window chunks of a k_finalize_ring launch (0: by the key blocks)
     void small_win_launch(int nb, const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot,
                           const int64_t* ob, int max_n, SwArith ar) {
         ek::launch_small_win(std::max(1, dp.n_vc), dp.n_where > 0, max_n <= 16 * kSwLanes ? 16 : kSwRows, std::min(nb, sw_grid), nb,

@@ -956,7 +956,7 @@ __device__ __forceinline__ Val agg_value(const DPlan& p, const Part<NVC>& s, int
 // A failed HAVING group becomes the window's HAVING witness when its key is the smallest failed one (the reference's
 // groups come out of a Go map, aggregate_operator.go:44-72, so any failed group's error is one it can report).
 template <typename AGGF>
-__device__ __noinline__ void wit_having(WitRec* r, uint32_t key, const DPlan& p, AGGF aggf) {
+__device__ inline void wit_having(WitRec* r, uint32_t key, const DPlan& p, AGGF aggf) {
     wit_offer(r, key, 0ull, [&](WitRec* w) {
         for (int k = 0; k < p.n_having; ++k)
             if (p.having_prog[k].op == EK_OP_AGG) wit_put(w, p.having_prog[k].arg, aggf(p.having_prog[k].arg));
@@ -1644,6 +1644,176 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
     }
     __shared__ uint32_t esh[20];
     emit_rows(p, present, s, key, w.out_base, w.idx, res, esh);
+}
+
+// Hopping finalize with a register ring (one value column whose fields are count / sum / min / max; VC: its non-nil
+// count): one thread per key walks the launch's consecutive windows [c0, c1) pane by pane. Each pane's partial is
+// loaded once — coalesced over the block's keys — into a ring of R register slots that shifts by one per pane, so
+// every slot index is static (no scratch). When a window's last pane arrives it is merged from the ring's last
+// panes in pane order (the same merge order as k_finalize: the same f64 sums). k_finalize re-reads a pane once per
+// window that spans it (ppw times); here a block chunk of cw windows reads cw + ppw - 1 panes.
+#ifndef EK_RING_WPE
+#define EK_RING_WPE 1
+#endif
+#ifndef EK_RING_AHEAD
+#define EK_RING_AHEAD 3
+#endif
+constexpr int kRingAhead = EK_RING_AHEAD;   // k_finalize_ring: panes loaded ahead of the one being merged
+template <int R, bool VC, bool HV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_WPE))) void k_finalize_ring(DPlan* __restrict__ pp, const WinDesc* __restrict__ wins,
+                                                          int32_t nwin, int32_t cw, DState ds, int32_t ring,
+                                                          const int32_t* __restrict__ pane_err, Results res) {
+    const DPlan& p = *pp;
+    const int c0 = (int)blockIdx.y * cw, c1 = min(nwin, c0 + cw);
+    if (c0 >= c1) return;   // uniform over the block
+    const int64_t key = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
+    const bool live = key < (int64_t)K;
+    const int f = p.vc_flags[0];
+    const bool isf = p.vc_is_float[0] != 0;
+    const bool fsum_out = isf || p.inc;   // sum / avg as float64 (funcs_agg.go; inc_* aggregates)
+    // the ring, newest pane in slot R - 1 (a shift per pane keeps every index static): a pane's count (< 2^31 rows of
+    // a key), non-nil count, sum bits, ordered min / max
+    int32_t rc[R], rv[R], re[R];   // re: the pane's WHERE error flag (uniform)
+    int64_t rs[R];
+    uint64_t rmn[R], rmx[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) { rc[t] = rv[t] = re[t] = 0; rs[t] = 0; rmn[t] = rmx[t] = 0; }
+    // block-compacted emission, one window behind: window w's rows are stored while window w + 1 is merged, so the
+    // returning atomic on w's row counter is off the critical path. esh[8 par + wave]: row counts -> offsets of the
+    // two windows in flight, esh[16 + par]: the block's base in the window's region
+    __shared__ uint32_t esh[20];
+    int par = 0;
+    bool pd_has = false, pd_present = false;
+    int32_t pd_idx = 0;
+    int64_t pd_out = 0;
+    unsigned long long pd_mask = 0;
+    int64_t pd_cnt = 0, pd_vcn = 0, pd_isum = 0;
+    double pd_fsum = 0.0;
+    uint64_t pd_omn = 0, pd_omx = 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto store_pending = [&]() {   // window pd's rows: esh[8 (1 - par) + wave] + esh[16 + (1 - par)] are final
+        if (!pd_has || !pd_present) return;
+        const int pp_ = par ^ 1;
+        const int64_t pos = pd_out + (int64_t)esh[16 + pp_] + esh[8 * pp_ + wv] + __popcll(pd_mask & ((1ull << lane) - 1ull));
+        res.key[pos] = (uint32_t)key;
+        for (int k = 0; k < p.n_aggs; ++k) {
+            const int fn = p.agg_fn[k];
+            int64_t v = 0;
+            uint8_t tg = EK_TAG_I64;
+            if (fn == EK_AGG_COUNT_STAR) v = pd_cnt;
+            else if (fn == EK_AGG_COUNT) v = pd_vcn;
+            else if (pd_vcn == 0) tg = EK_TAG_NULL;
+            else if (fn == EK_AGG_SUM) { if (fsum_out) { tg = EK_TAG_F64; v = __double_as_longlong(pd_fsum); } else v = pd_isum; }
+            else if (fn == EK_AGG_AVG) {
+                if (fsum_out) { tg = EK_TAG_F64; v = __double_as_longlong(__ddiv_rn(pd_fsum, (double)pd_vcn)); }
+                else v = pd_isum / pd_vcn;
+            } else {
+                const uint64_t o = fn == EK_AGG_MIN ? pd_omn : pd_omx;
+                if (isf) { tg = EK_TAG_F64; v = __double_as_longlong(ord_to_f64(o)); }
+                else v = ord_to_i64(o);
+            }
+            res.tag[k][pos] = tg;
+            res.val[k][pos] = v;
+        }
+    };
+    const int64_t P0 = wins[c0].q_first, P1 = wins[c1 - 1].q_last;
+    int w = c0;
+    int64_t wl = wins[c0].q_last;   // the last pane of window w
+    int32_t sq = (int32_t)(P0 % ring);
+    // pane loads run kRingAhead panes ahead (a queue shifted like the ring): enough bytes in flight per wave to
+    // cover the HBM latency at the two waves per SIMD the ring's registers leave
+    constexpr int D = kRingAhead;
+    int32_t pc[D], pv[D], pe[D];
+    int64_t ps[D];
+    uint64_t pmn[D], pmx[D];
+    auto load = [&](int d, int32_t slot, bool ok) {
+        const int64_t e = (int64_t)slot * ds.K + key;
+        const bool l = live && ok;
+        pe[d] = ok ? pane_err[slot] : 0;
+        pc[d] = l ? (int32_t)ds.cnt[e] : 0;
+        pv[d] = (VC && l) ? (int32_t)ds.vcnt[0][e] : 0;
+        ps[d] = (l && (f & NEED_SUM)) ? ds.sum[0][e] : 0;
+        pmn[d] = (l && (f & NEED_MIN)) ? (uint64_t)ds.mn[0][e] : 0ull;
+        pmx[d] = (l && (f & NEED_MAX)) ? (uint64_t)ds.mx[0][e] : 0ull;
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        load(d, sq, P0 + d <= P1);
+        sq = sq + 1 == ring ? 0 : sq + 1;
+    }
+    for (int64_t q = P0; q <= P1; ++q) {
+#pragma unroll
+        for (int t = 0; t + 1 < R; ++t) {
+            rc[t] = rc[t + 1]; rv[t] = rv[t + 1]; re[t] = re[t + 1]; rs[t] = rs[t + 1]; rmn[t] = rmn[t + 1]; rmx[t] = rmx[t + 1];
+        }
+        rc[R - 1] = pc[0]; rv[R - 1] = pv[0]; re[R - 1] = pe[0]; rs[R - 1] = ps[0]; rmn[R - 1] = pmn[0]; rmx[R - 1] = pmx[0];
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d) { pc[d] = pc[d + 1]; pv[d] = pv[d + 1]; pe[d] = pe[d + 1]; ps[d] = ps[d + 1]; pmn[d] = pmn[d + 1]; pmx[d] = pmx[d + 1]; }
+        load(D - 1, sq, q + D <= P1);
+        sq = sq + 1 == ring ? 0 : sq + 1;
+        while (w < c1 && wl == q) {   // window w closes with pane q (uniform): its panes are the ring's last `span`
+            const WinDesc wd = wins[w];
+            const int span = (int)(q - wd.q_first + 1);   // <= R (host-checked)
+            int32_t werr = 0;
+#pragma unroll
+            for (int t = 0; t < R; ++t) werr |= t >= R - span ? re[t] : 0;
+            if (werr) {
+                if (blockIdx.x == 0 && threadIdx.x == 0) {
+                    atomicOr(&res.win_err[wd.idx], werr);
+                    if (res.wwit)   // the first pane with an error holds the window's first failed row
+                        for (int64_t qq = wd.q_first; qq <= q; ++qq)
+                            if (pane_err[qq % ring]) { wit_copy(&res.wwit[2 * wd.idx], &res.pwit[qq % ring]); break; }
+                }
+            } else {
+                // part_merge restricted to count / sum / min / max, the same operations in the same pane order
+                int64_t cnt = 0, vcn = 0, isum = 0;
+                double fsum = 0.0;
+                uint64_t omn = 0, omx = 0;
+#pragma unroll
+                for (int t = 0; t < R; ++t) {   // the window's panes in pane order
+                    if (t < R - span || rc[t] == 0) continue;
+                    cnt += rc[t];
+                    const int64_t nb = VC ? (int64_t)rv[t] : (int64_t)rc[t];
+                    if (nb == 0) continue;
+                    const bool first = vcn == 0;
+                    vcn += nb;
+                    isum = (int64_t)((uint64_t)isum + (uint64_t)(isf ? 0 : rs[t]));
+                    const double fs = isf ? __longlong_as_double(rs[t]) : 0.0;
+                    fsum = first ? fs : __dadd_rn(fsum, fs);
+                    omn = (first || rmn[t] < omn) ? rmn[t] : omn;
+                    omx = (first || rmx[t] > omx) ? rmx[t] : omx;
+                }
+                bool present = live && cnt > 0;
+                if (HV && present) {
+                    Part<1> s{};
+                    s.cnt = cnt; s.vcnt[0] = vcn; s.isum[0] = isum; s.fsum[0] = fsum; s.omn[0] = omn; s.omx[0] = omx;
+                    present = having_keep(p, s, res, wd.idx, (uint32_t)key);
+                }
+                // rows of count / sum / avg / min / max (funcs_agg.go:56-113): counted now, stored one window later
+                const unsigned long long mask = __ballot(present);
+                if (lane == 0) esh[8 * par + wv] = (uint32_t)__popcll(mask);
+                __syncthreads();   // this window's counts are in; the previous window's base (thread 0) too
+                store_pending();
+                if (threadIdx.x == 0) {
+                    uint32_t run = 0;
+                    for (int x = 0; x < kBlock / 64; ++x) { const uint32_t c = esh[8 * par + x]; esh[8 * par + x] = run; run += c; }
+                    esh[16 + par] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[wd.idx], (unsigned long long)run) : 0u;
+                }
+                pd_has = true;
+                pd_present = present;
+                pd_idx = wd.idx;
+                pd_out = wd.out_base;
+                pd_mask = mask;
+                pd_cnt = cnt; pd_vcn = vcn; pd_isum = isum; pd_fsum = fsum; pd_omn = omn; pd_omx = omx;
+                par ^= 1;
+            }
+            ++w;
+            wl = w < c1 ? wins[w].q_last : INT64_MAX;
+        }
+    }
+    __syncthreads();   // the last window's base
+    store_pending();
 }
 
 // Un-grouped rule (pseudo keys): one workgroup per window merges every (pane, partial slot) entry of the window into

@@ -24,6 +24,16 @@ void launch_fin(int nvc, bool merge, dim3 grid, hipStream_t s, DPlan* p, const W
 #undef EK_FIN
 }
 
+void launch_fin_ring(int r, bool vc, bool hv, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, int32_t nwin,
+                     int32_t cw, const DState& ds, int32_t ring, const int32_t* pane_err, const Results& res) {
+#define EK_FR(R, V, H) hipLaunchKernelGGL((k_finalize_ring<R, V, H>), grid, dim3(kBlock), 0, s, p, w, nwin, cw, ds, ring, pane_err, res)
+#define EK_FR_R(V, H) if (r <= 4) EK_FR(4, V, H); else if (r <= 8) EK_FR(8, V, H); else if (r <= 12) EK_FR(12, V, H); else EK_FR(16, V, H)
+    if (vc) { if (hv) { EK_FR_R(true, true); } else { EK_FR_R(true, false); } }
+    else { if (hv) { EK_FR_R(false, true); } else { EK_FR_R(false, false); } }
+#undef EK_FR_R
+#undef EK_FR
+}
+
 void launch_ung(int nvc, bool where, dim3 grid, hipStream_t s, DPlan* p, const DBatch& db, const GroupDesc& gd,
                 const uint8_t* acc, const DState& ds, int64_t tile, int32_t* pane_err) {
 #define EK_UNG(N, W) hipLaunchKernelGGL((k_ung_tile<N, W>), grid, dim3(kUngBlock), 0, s, p, db, gd, acc, ds, tile, pane_err)
