@@ -857,6 +857,8 @@ struct Engine {
         slot_pane.assign(ring, INT64_MIN);
         // range mode
         eb.n = 0;
+        eb_arr_impl = true;
+        eb_arr0 = 0;
         eb_base = 0;
         eb_rel = 0;
         eb_floor = 0;
@@ -1619,6 +1621,21 @@ struct Engine {
     bool need_rel = false;             // sliding windows: per-event release step (closed right boundary)
     int64_t eb_rel = 0;                // released prefix (buffer index)
     int64_t eb_floor = 0;              // smallest buffer index a future window can start at
+    // The arrival column is implicit (arrival(i) = eb_arr0 + i, nothing stored) while the buffer is filled only by
+    // in-order appends of consecutive arrivals; an out-of-order merge, shard mode or a state restore materialises it.
+    bool eb_arr_impl = true;
+    int64_t eb_arr0 = 0;
+    const int64_t* arr_ptr() const { return eb_arr_impl ? nullptr : (const int64_t*)eb.arr.p; }
+    int arr_materialize() {
+        if (!eb_arr_impl) return 0;
+        if (int rc = ensure(eb.arr, (size_t)std::max<int64_t>(eb.cap, 1) * 8)) return rc;
+        if (eb.n > 0) {
+            const int g = (int)std::min<int64_t>(4096, (eb.n + 255) / 256);
+            hipLaunchKernelGGL(k_iota64, dim3(g), dim3(256), 0, stream, (int64_t*)eb.arr.p, eb_arr0, eb.n);
+        }
+        eb_arr_impl = false;
+        return 0;
+    }
     int64_t sW = -1;                   // arrival index at which the watermark reached W
     int64_t range_wins = 0;            // windows triggered so far
     // sliding windows with delay: queued triggers (event_window_trigger.go:129-135,156-161)
@@ -1683,9 +1700,10 @@ struct Engine {
             if (int rc = mv(eb_alt.col[c], eb.col[c], col_es(c))) return rc;
             if (eb_valid_on[c]) if (int rc = mv(eb_alt.valid[c], eb.valid[c], 1)) return rc;
         }
-        if (int rc = mv(eb_alt.arr, eb.arr, 8)) return rc;
+        if (!eb_arr_impl) if (int rc = mv(eb_alt.arr, eb.arr, 8)) return rc;
         if (need_rel) if (int rc = mv(eb_alt.rel, eb.rel, 8)) return rc;
         std::swap(eb, eb_alt);
+        if (eb_arr_impl) eb_arr0 += d;
         eb.cap = cap;
         eb.n = live;
         eb_alt.n = 0;
@@ -1723,8 +1741,12 @@ struct Engine {
             }
         }
         if (g_row_arr) {   // shard mode: the rows' global arrival indices
+            if (int rc = arr_materialize()) return rc;
             if (cnt > 0) hipMemcpyAsync((int64_t*)eb.arr.p + eb.n, g_row_arr + start, (size_t)cnt * 8, hipMemcpyDeviceToDevice, stream);
+        } else if (eb_arr_impl && (eb.n == 0 || arr_base + start == eb_arr0 + eb.n)) {
+            if (eb.n == 0) eb_arr0 = arr_base + start;   // consecutive arrivals: the column stays implicit
         } else {
+            if (int rc = arr_materialize()) return rc;
             const int g = (int)std::min<int64_t>(4096, (cnt + 255) / 256);
             hipLaunchKernelGGL(k_iota64, dim3(std::max(g, 1)), dim3(256), 0, stream, (int64_t*)eb.arr.p + eb.n, arr_base + start, cnt);
         }
@@ -1743,6 +1765,7 @@ struct Engine {
         for (int c = 0; c < plan.n_columns; ++c)
             if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
         if (int rc = eb_reserve(n_acc)) return rc;
+        if (int rc = arr_materialize()) return rc;
         // accepted row indices of the batch, in arrival order
         if (int rc = ensure(mrg_bidx, (size_t)std::max<int64_t>(n, 1) * 8)) return rc;
         int64_t* bidx = (int64_t*)mrg_bidx.p;
@@ -1876,7 +1899,7 @@ struct Engine {
         for (int w = 0; w < nq; ++w) hq[w] = pw[w].q;
         hipMemcpyAsync(rq_d.p, hq.data(), (size_t)nq * sizeof(RangeQ), hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(k_window_ranges, dim3((nq + 255) / 256), dim3(256), 0, stream, (const int64_t*)eb.col[std::max(0, dp.ts_col)].p,
-                           need_rel ? (const int64_t*)eb.rel.p : nullptr, (const int64_t*)eb.arr.p, eb_rel, (const RangeQ*)rq_d.p, nq,
+                           need_rel ? (const int64_t*)eb.rel.p : nullptr, arr_ptr(), eb_arr0, eb_rel, (const RangeQ*)rq_d.p, nq,
                            (int64_t*)ab_d.p);
         h_ab.resize((size_t)nq * 2);
         hipMemcpyAsync(h_ab.data(), ab_d.p, (size_t)nq * 16, hipMemcpyDeviceToHost, stream);
@@ -1918,9 +1941,9 @@ struct Engine {
         if (plan.debug_membership) {
             if (int rc = ensure(slot_d, (size_t)nq * 4)) return rc;
             hipMemcpyAsync(slot_d.p, slots.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream);
-            hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)eb.arr.p,
+            hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, arr_ptr(),
                                (const int64_t*)ab_d.p, (const int32_t*)slot_d.p, (int64_t*)r_wmc.p,
-                               (unsigned long long*)r_wmh.p, (int64_t)0);
+                               (unsigned long long*)r_wmh.p, eb_arr_impl ? eb_arr0 : (int64_t)0);
             hipStreamSynchronize(stream);   // slots/ab host vectors are reused
         }
         // small windows: one workgroup each (k_small_win); no order statistics on that path
@@ -1996,7 +2019,7 @@ struct Engine {
         int64_t* d_ends = (int64_t*)mrg_col.p;
         hipMemcpyAsync(d_ends, ends.data(), (size_t)nq * 8, hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(k_fire_prefix, dim3((nq + 255) / 256), dim3(256), 0, stream, runmax_p, cur_nb,
-                           cur_arr_base, plan.late_tolerance_ms, (const int64_t*)eb.col[dp.ts_col].p, (const int64_t*)eb.arr.p,
+                           cur_arr_base, plan.late_tolerance_ms, (const int64_t*)eb.col[dp.ts_col].p, arr_ptr(), eb_arr0,
                            eb.n, d_ends, nq, d_ends + nq);
         hipMemcpyAsync(pre.data(), d_ends + nq, (size_t)nq * 8, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "fire prefix kernel failed");
@@ -3376,13 +3399,13 @@ struct Engine {
         if (eb.n > 0) {
             if (int rc = ensure(bounds_idx, 8)) return rc;
             hipLaunchKernelGGL(k_rel_end, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                               (const int64_t*)eb.arr.p, eb.n, W, sW, (int64_t*)bounds_idx.p);
+                               arr_ptr(), eb_arr0, eb.n, W, sW, (int64_t*)bounds_idx.p);
             eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
         }
         if (need_rel && eb_rel > rel_prev) {
             const int g = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
             hipLaunchKernelGGL(k_release_step, dim3(g), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                               (const int64_t*)eb.arr.p, rel_prev, eb_rel, runmax_p, n, arrival_base,
+                               arr_ptr(), eb_arr0, rel_prev, eb_rel, runmax_p, n, arrival_base,
                                had_M ? M_prev : INT64_MIN, plan.late_tolerance_ms, (int64_t*)eb.rel.p);
         }
         const int rc = range_triggers(rel_prev);
@@ -4075,11 +4098,12 @@ struct Engine {
             if (has_W && eb.n > 0) {
                 if (int rc = ensure(bounds_idx, 8)) return rc;
                 hipLaunchKernelGGL(k_rel_end, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                                   (const int64_t*)eb.arr.p, eb.n, W, sW, (int64_t*)bounds_idx.p);
+                                   arr_ptr(), eb_arr0, eb.n, W, sW, (int64_t*)bounds_idx.p);
                 eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
             }
             if (need_rel && eb_rel > rel_prev) {
                 if (int rc = wm_to_device()) return rc;
+                if (int rc = arr_materialize()) return rc;
                 const int gg = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);
                 hipLaunchKernelGGL(k_release_step_global, dim3(gg), dim3(256), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
                                    (const int64_t*)eb.arr.p, rel_prev, eb_rel, wm_list(W_carry), (int64_t*)eb.rel.p);
@@ -4542,6 +4566,7 @@ struct Engine {
                     if (eb_valid_on[c])
                         if (int rc = dev_append(s, (uint8_t*)eb.valid[c].p + drop, (size_t)live)) return rc;
                 }
+                if (int rc = arr_materialize()) return rc;
                 if (int rc = dev_append(s, (int64_t*)eb.arr.p + drop, (size_t)live * 8)) return rc;
                 if (need_rel) if (int rc = dev_append(s, (int64_t*)eb.rel.p + drop, (size_t)live * 8)) return rc;
             }
@@ -4655,6 +4680,7 @@ struct Engine {
                 if ((vmask >> c) & 1) { if (int rc = dev_restore(r, eb.valid[c].p, (size_t)live)) return rc; }
                 else if (eb_valid_on[c]) fill_valid_ones(c, 0, live);
             }
+            if (int rc = arr_materialize()) return rc;   // eb.n == 0 here: allocates the column
             if (int rc = dev_restore(r, eb.arr.p, (size_t)live * 8)) return rc;
             if (need_rel) if (int rc = dev_restore(r, eb.rel.p, (size_t)live * 8)) return rc;
             eb.n = live;

@@ -64,6 +64,18 @@ __device__ __forceinline__ int64_t ub_i64(const int64_t* a, int64_t lo, int64_t 
     return lo;
 }
 
+// Searches over a buffer's arrival column; barr == nullptr: the column is implicit, arrival(i) = arr0 + i (a buffer
+// filled only by in-order appends keeps no arrival column at all)
+__device__ __forceinline__ int64_t arr_at(const int64_t* barr, int64_t arr0, int64_t i) { return barr ? barr[i] : arr0 + i; }
+__device__ __forceinline__ int64_t arr_lb(const int64_t* barr, int64_t arr0, int64_t lo, int64_t hi, int64_t x) {
+    if (barr) return lb_i64(barr, lo, hi, x);
+    return lo < hi ? min(hi, max(lo, x - arr0)) : lo;
+}
+__device__ __forceinline__ int64_t arr_ub(const int64_t* barr, int64_t arr0, int64_t lo, int64_t hi, int64_t x) {
+    if (barr) return ub_i64(barr, lo, hi, x);
+    return lo < hi ? min(hi, max(lo, x - arr0 + 1)) : lo;
+}
+
 // Galloping searches from lo (the answer is usually a few rows away: a ts-sorted batch releases an event at its own
 // arrival or at the end of its equal-ts run): O(log distance) probes near lo instead of a binary search over the
 // whole remaining batch (whose first probes miss every cache). Same results as lb_i64 / ub_i64.
@@ -85,12 +97,12 @@ __device__ __forceinline__ int64_t gallop_ub(const int64_t* a, int64_t lo, int64
 // W_j >= ts). runmax[0..nb) = batch running max (arrival arr_base + j), prevmax = stream max before the
 // batch (INT64_MIN if none), W_j = runmax[j] - late_tol. Events not released in this batch get INT64_MAX.
 #ifndef EK_NO_PLAIN_KERNELS
-__global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t i0,
+__global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t arr0, int64_t i0,
                                int64_t i1, const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base,
                                int64_t prevmax, int64_t late_tol, int64_t* __restrict__ brel) {
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < i1; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t x = bts[i] + late_tol;
-        const int64_t ls = max((int64_t)0, barr[i] - arr_base);
+        const int64_t ls = max((int64_t)0, arr_at(barr, arr0, i) - arr_base);
         int64_t r = INT64_MAX;
         if (ls < nb) {
             const int64_t j0 = gallop_lb(runmax, ls, nb, x);
@@ -111,12 +123,12 @@ __global__ void k_release_step(const int64_t* __restrict__ bts, const int64_t* _
 // Released prefix of the buffer after a batch (single thread): events with ts < W, plus those with
 // ts == W that arrived no later than the step sW at which the watermark reached W.
 #ifndef EK_NO_PLAIN_KERNELS
-__global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n, int64_t W,
-                          int64_t sW, int64_t* out) {
+__global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t arr0, int64_t n,
+                          int64_t W, int64_t sW, int64_t* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const int64_t p = lb_i64(bts, 0, n, W);
     const int64_t q = ub_i64(bts, p, n, W);
-    out[0] = ub_i64(barr, p, q, sW);   // arrivals are increasing inside one ts run
+    out[0] = arr_ub(barr, arr0, p, q, sW);   // arrivals are increasing inside one ts run
 }
 #endif
 
@@ -133,7 +145,7 @@ __global__ void k_first_ge(const int64_t* __restrict__ a, int64_t n, int64_t x, 
 // handleInputs (window_op.go:605-655) drops every input present at that tuple when the window finds no member.
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, int64_t arr_base, int64_t late_tol,
-                              const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t n,
+                              const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t arr0, int64_t n,
                               const int64_t* __restrict__ ends, int nq, int64_t* __restrict__ out) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nq) return;
@@ -142,7 +154,7 @@ __global__ void k_fire_prefix(const int64_t* __restrict__ runmax, int64_t nb, in
     const int64_t W = runmax[j] - late_tol;
     const int64_t p = lb_i64(bts, 0, n, W);
     const int64_t q = ub_i64(bts, p, n, W);
-    out[w] = ub_i64(barr, p, q, arr_base + j);
+    out[w] = arr_ub(barr, arr0, p, q, arr_base + j);
 }
 #endif
 
@@ -398,15 +410,15 @@ struct RangeQ {
 
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_window_ranges(const int64_t* __restrict__ bts, const int64_t* __restrict__ brel,
-                                const int64_t* __restrict__ barr, int64_t n_rel, const RangeQ* __restrict__ q, int nq,
-                                int64_t* __restrict__ ab) {
+                                const int64_t* __restrict__ barr, int64_t arr0, int64_t n_rel, const RangeQ* __restrict__ q,
+                                int nq, int64_t* __restrict__ ab) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nq) return;
     const RangeQ d = q[w];
     int64_t a, b;
     if (d.kind == RB_ARR) {
-        a = max(d.floor, lb_i64(barr, d.floor, n_rel, d.lo_ts));
-        b = lb_i64(barr, a, n_rel, d.hi_ts);
+        a = max(d.floor, arr_lb(barr, arr0, d.floor, n_rel, d.lo_ts));
+        b = arr_lb(barr, arr0, a, n_rel, d.hi_ts);
     } else if (d.kind == RB_FIXED) {
         a = d.pos;
         b = d.rstep;
