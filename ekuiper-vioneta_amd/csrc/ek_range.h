@@ -615,6 +615,7 @@ __device__ __forceinline__ uint32_t sw_hash(uint32_t k) {
 
 // Windows laid out arithmetically (consecutive COUNTWINDOW blocks of one batch): window w = rows [a0 + w len, + len),
 // result slot slot0 + w, result region ob0 + w rowcap — no per-window lists to upload.
+constexpr int kSwFoldRegs = 4;   // k_small_win: groups of up to this many rows fold from registers
 struct SwArith {
     int64_t a0, ob0, rowcap;
     int32_t len, slot0;
@@ -720,6 +721,42 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
         uint64_t mn[NVC], mx[NVC];
 #pragma unroll
         for (int v = 0; v < NVC; ++v) { vc[v] = 0; is[v] = 0; fs[v] = 0.0; m2[v] = 0.0; mn[v] = ~0ull; mx[v] = 0ull; }
+        if constexpr (NVC == 1) {
+            if (c <= kSwFoldRegs) {
+                // a short group: its values are loaded together (one memory latency instead of one per row and pass)
+                // and both passes run from registers, in the same row order as below (the same f64 operations)
+                int64_t rv[kSwFoldRegs];
+                bool ok[kSwFoldRegs];
+#pragma unroll
+                for (int u = 0; u < kSwFoldRegs; ++u) {
+                    const int64_t r = a + row(u < c ? u : 0);
+                    ok[u] = u < c && fl[0] && col_valid(b, col[0], r);
+                    rv[u] = ok[u] ? ((const int64_t*)b.col[col[0]])[r] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kSwFoldRegs; ++u) {
+                    if (!ok[u]) continue;
+                    const double xv = isf[0] ? __longlong_as_double(rv[u]) : (double)rv[u];
+                    const uint64_t o = isf[0] ? f64_to_ord(xv) : i64_to_ord(rv[u]);
+                    vc[0]++;
+                    is[0] = (int64_t)((uint64_t)is[0] + (uint64_t)rv[u]);
+                    fs[0] = __dadd_rn(fs[0], xv);
+                    mn[0] = o < mn[0] ? o : mn[0];
+                    mx[0] = o > mx[0] ? o : mx[0];
+                }
+                if ((fl[0] & NEED_M2) && vc[0] > 0) {
+                    const double mean = __ddiv_rn(fs[0], (double)vc[0]);
+#pragma unroll
+                    for (int u = 0; u < kSwFoldRegs; ++u) {
+                        if (!ok[u]) continue;
+                        const double d = __dsub_rn(isf[0] ? __longlong_as_double(rv[u]) : (double)rv[u], mean);
+                        m2[0] = __dadd_rn(m2[0], __dmul_rn(d, d));
+                    }
+                }
+                part_merge(p, s, c, vc, is, fs, m2, mn, mx);
+                return;
+            }
+        }
         for (int u = 0; u < c; ++u) {
             const int64_t r = a + row(u);
 #pragma unroll
