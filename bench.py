@@ -435,6 +435,8 @@ def main():
                     help="events of the CPU baseline sample (default: CPU_SAMPLE of the config, ~10 s single-threaded)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-shared-stats", action="store_true",
+                    help="C5: each rule scans the source's timestamps itself (no ek_batch_ts_stats sharing)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="one process plays rank 0 of an N-GPU run in shard mode (no collective; a single-GPU check of "
                          "the shard path: C4a then sees only its own triggers)")
@@ -532,10 +534,15 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=1)
 
+    # the two rules read one source batch: its timestamp statistics are computed once (ek_batch_ts_stats) and shared by
+    # both pushes, as eKuiper's shared source feeds every subscribed rule (subtopo.go)
+    share_stats = cnt_eng is not None and iet and not args.no_shared_stats
+    shared = None
+
     def count_rule(c):
         cnt_eng.reset()
         if world == 1 or blocks:
-            cnt_eng.push_device(n, ptrs)
+            cnt_eng.push_device(n, ptrs, ts_stats=shared)
             if sent_ptrs:
                 cnt_eng.push_device(1, sent_ptrs)
         else:
@@ -550,13 +557,15 @@ def main():
         count_pp = make_partial_plan(crule)
 
     def step():
-        nonlocal ctx, tup
+        nonlocal ctx, tup, shared
         eng.reset()
         fut = None
         if world == 1 or blocks:
+            if share_stats:
+                shared = eng.batch_ts_stats(n, ptrs)   # inside the timed step
             if pool is not None:
                 fut = pool.submit(count_rule, None)
-            eng.push_device(n, ptrs)
+            eng.push_device(n, ptrs, ts_stats=shared)
             if sent_ptrs:
                 eng.push_device(1, sent_ptrs)
         else:
@@ -717,6 +726,7 @@ def main():
     }
     if global_count is not None:
         out["config"]["global_count"] = str(global_count)[:200]
+        out["config"]["shared_ts_stats"] = bool(share_stats)
     if args.disorder > 0 and iet:
         out["config"]["disorder_ms"] = args.disorder
         out["config"]["late_tolerance_ms"] = args.disorder

@@ -2963,19 +2963,99 @@ struct Engine {
         }
     }
 
-    int push_proc(DBatch db) {
-        const int64_t n = db.n;
-        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+    // ---- batch statistics: one pass over ts (k_stats), or the shared ek_ts_stats the pushed batch carries (ABI v10:
+    // computed once by ek_batch_ts_stats for every rule over the same source). GAP (hopping, lateTolerance 0): also the
+    // widest arrival gap, seeded with the carried stream maximum.
+    const ek_ts_stats* ts_hint = nullptr;   // set by push / push_global for the batch being pushed
+
+    struct HintScope {   // the hint points into the caller's batch: valid for one push only
+        const ek_ts_stats*& h;
+        ~HintScope() { h = nullptr; }
+    };
+
+    void set_ts_hint(const ek_batch* b) {
+        const ek_ts_stats* t = b ? b->ts_stats : nullptr;
+        ts_hint = t && t->n_rows == b->n_rows && t->ts_column == dp.ts_col && dp.ts_col < user_cols ? t : nullptr;
+    }
+
+    int batch_stats(const int64_t* ts, int64_t n, bool gap, int64_t seed, BatchStats* out) {
+        if (ts_hint && ts_hint->n_rows == n) {
+            BatchStats s{};
+            s.min_ts = ts_hint->ts_min;
+            s.max_ts = ts_hint->ts_max;
+            s.unsorted = ts_hint->unsorted != 0;
+            s.min_accepted = INT64_MAX;
+            s.max_gap = INT64_MIN;
+            if (gap) {
+                s.max_gap = ts_hint->max_step;
+                if (seed != INT64_MIN && n > 0) s.max_gap = std::max(s.max_gap, ts_hint->ts_first - seed);
+            }
+            *out = s;
+            // the callers rely on the stats sync having drained the stream (pinned descriptor buffers are reused)
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream sync failed");
+            return 0;
+        }
         const int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
         if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
         const int ph_s = phase_begin(EK_PHASE_STATS);
-        hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN, (BatchStats*)bstats_part.p);
+        if (gap)
+            hipLaunchKernelGGL(k_stats<true>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, seed, (BatchStats*)bstats_part.p);
+        else
+            hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN, (BatchStats*)bstats_part.p);
         hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
                            (BatchStats*)bstats.p);
         phase_end(ph_s);
         hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
-        const BatchStats s = *h_stats;
+        *out = *h_stats;
+        return 0;
+    }
+
+    // ek_batch_ts_stats: the shareable form of the statistics above
+    int ts_stats_of(const ek_batch* b, ek_ts_stats* out) {
+        if (!b || !out) return fail(EK_ERR_INVALID, "null batch / output");
+        if (dp.ts_col < 0 || dp.ts_col >= user_cols) return fail(EK_ERR_STATE, "the rule has no timestamp column");
+        const int64_t n = b->n_rows;
+        if (n < 0 || !b->columns[dp.ts_col]) return fail(EK_ERR_INVALID, "bad batch");
+        ek_ts_stats t{};
+        t.n_rows = n;
+        t.ts_column = dp.ts_col;
+        t.ts_min = INT64_MAX;
+        t.ts_max = INT64_MIN;
+        t.max_step = INT64_MIN;
+        if (n > 0 && b->memory == EK_MEM_HOST) {
+            const int64_t* ts = (const int64_t*)b->columns[dp.ts_col];
+            t.ts_first = ts[0];
+            for (int64_t i = 0; i < n; ++i) {
+                t.ts_min = std::min(t.ts_min, ts[i]);
+                t.ts_max = std::max(t.ts_max, ts[i]);
+                if (i > 0) { t.unsorted |= ts[i] < ts[i - 1]; t.max_step = std::max(t.max_step, ts[i] - ts[i - 1]); }
+            }
+        } else if (n > 0) {
+            const int64_t* ts = (const int64_t*)b->columns[dp.ts_col];
+            const ek_ts_stats* keep = ts_hint;
+            ts_hint = nullptr;
+            BatchStats s;
+            const int rc = batch_stats(ts, n, true, INT64_MIN, &s);
+            ts_hint = keep;
+            if (rc) return rc;
+            hipMemcpyAsync(h_stats, ts, 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "ts copy failed");
+            t.ts_first = h_stats->min_ts;   // the pinned stats block doubles as the 8-byte landing slot
+            t.ts_min = s.min_ts;
+            t.ts_max = s.max_ts;
+            t.unsorted = s.unsorted != 0;
+            t.max_step = s.max_gap;
+        }
+        *out = t;
+        return 0;
+    }
+
+    int push_proc(DBatch db) {
+        const int64_t n = db.n;
+        const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+        BatchStats s;
+        if (int rc = batch_stats(ts, n, false, INT64_MIN, &s)) return rc;
         if (s.unsorted) return fail(EK_ERR_INVALID, "processing-time rows must arrive in timestamp order (their arrival times)");
         if (!clock_started) start_clock(s.min_ts);
         else if (s.min_ts < clock_ms)
@@ -3665,6 +3745,8 @@ struct Engine {
         DBatch db{};
         if (int rc = stage_batch(b, db)) return rc;
         stats.records_in += n;
+        set_ts_hint(b);
+        const HintScope hint_scope{ts_hint};
         if (wtype == EK_WINDOW_NONE) {
             const int rc = push_filter(db);
             return rc ? rc : record_time();
@@ -3697,22 +3779,10 @@ struct Engine {
         }
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
 
-        // ---- 1. batch statistics (one pass over ts)
-        int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
-        if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
-        const int ph_s = phase_begin(EK_PHASE_STATS);
-        if (wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms == 0)
-            hipLaunchKernelGGL(k_stats<true>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, has_M ? M : INT64_MIN,
-                               (BatchStats*)bstats_part.p);
-        else
-            hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN,
-                               (BatchStats*)bstats_part.p);
-        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
-                           (BatchStats*)bstats.p);
-        phase_end(ph_s);
-        hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
-        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
-        BatchStats s = *h_stats;
+        // ---- 1. batch statistics (one pass over ts, or the batch's shared ek_ts_stats)
+        BatchStats s;
+        const bool gap = wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms == 0;
+        if (int rc = batch_stats(ts, n, gap, gap && has_M ? M : INT64_MIN, &s)) return rc;
         const int64_t T = plan.late_tolerance_ms;
 
         // ---- 2. late-event drop (watermark_op.go:144-155)
@@ -4026,6 +4096,8 @@ struct Engine {
             if (int rc = stage_batch(b, db)) return rc;
         }
         stats.records_in += n;
+        set_ts_hint(b);
+        const HintScope hint_scope{ts_hint};
         int rc = 0;
         if (!plan.is_event_time) rc = push_count_global(db, g);
         else rc = push_global_event(db, g);
@@ -4045,16 +4117,7 @@ struct Engine {
         s.max_ts = INT64_MIN;
         if (n > 0) {
             const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
-            const int sblocks = (int)std::min<int64_t>(stats_blocks, std::max<int64_t>(1, (n / 2 + kBlock - 1) / kBlock));
-            if (int rc = ensure(bstats_part, (size_t)sblocks * sizeof(BatchStats))) return rc;
-            const int ph_s = phase_begin(EK_PHASE_STATS);
-            hipLaunchKernelGGL(k_stats<false>, dim3(sblocks), dim3(kBlock), 0, stream, ts, n, INT64_MIN, (BatchStats*)bstats_part.p);
-            hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, (const BatchStats*)bstats_part.p, sblocks,
-                               (BatchStats*)bstats.p);
-            phase_end(ph_s);
-            hipMemcpyAsync(h_stats, bstats.p, sizeof(BatchStats), hipMemcpyDeviceToHost, stream);
-            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stats kernel failed");
-            s = *h_stats;
+            if (int rc = batch_stats(ts, n, false, INT64_MIN, &s)) return rc;
         }
         // the first window's anchor: the global earliest released event (getEarliestEventTs at that tuple)
         const bool origin_now = !e1_known && g->origin_known;
@@ -4807,6 +4870,12 @@ int ek_push_batch(void* h, const ek_batch* batch) {
     if (!h) return EK_ERR_INVALID;
     DeviceGuard dg(h);
     return ((Engine*)h)->push(batch);
+}
+
+int ek_batch_ts_stats(void* h, const ek_batch* batch, ek_ts_stats* out) {
+    if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
+    return ((Engine*)h)->ts_stats_of(batch, out);
 }
 
 int ek_poll_results(void* h, int32_t memory, ek_result* out) {

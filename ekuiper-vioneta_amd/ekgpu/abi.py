@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 9
+EKGPU_ABI_VERSION = 10
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -93,12 +93,25 @@ class ek_plan(C.Structure):
     ]
 
 
+class ek_ts_stats(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("ts_column", C.c_int32),
+        ("unsorted", C.c_int32),
+        ("ts_min", C.c_int64),
+        ("ts_max", C.c_int64),
+        ("ts_first", C.c_int64),
+        ("max_step", C.c_int64),
+    ]
+
+
 class ek_batch(C.Structure):
     _fields_ = [
         ("n_rows", C.c_int64),
         ("columns", C.c_void_p * EK_MAX_COLUMNS),
         ("validity", C.c_void_p * EK_MAX_COLUMNS),
         ("memory", C.c_int32),
+        ("ts_stats", C.POINTER(ek_ts_stats)),
     ]
 
 

@@ -42,6 +42,8 @@ def lib():
         L.ek_release_results.restype = C.c_int
         L.ek_window_error.argtypes = [C.c_void_p, C.c_int64, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
         L.ek_window_error.restype = C.c_int
+        L.ek_batch_ts_stats.argtypes = [C.c_void_p, C.POINTER(A.ek_batch), C.POINTER(A.ek_ts_stats)]
+        L.ek_batch_ts_stats.restype = C.c_int
         L.ek_reset.argtypes = [C.c_void_p]
         L.ek_reset.restype = C.c_int
         L.ek_sync.argtypes = [C.c_void_p]
@@ -91,7 +93,7 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
                     "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
-                    "ek_window_error"]
+                    "ek_window_error", "ek_batch_ts_stats"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
 
@@ -129,7 +131,8 @@ class Engine:
         b.memory = A.EK_MEM_HOST
         self._check(lib().ek_push_batch(self.h, C.byref(b)))
 
-    def push_device(self, n_rows: int, col_ptrs: Sequence[int], valid_ptrs: Optional[Sequence[int]] = None):
+    @staticmethod
+    def _device_batch(n_rows, col_ptrs, valid_ptrs=None, ts_stats=None):
         b = A.ek_batch()
         b.n_rows = n_rows
         b.memory = A.EK_MEM_DEVICE
@@ -139,7 +142,23 @@ class Engine:
             for k, p in enumerate(valid_ptrs):
                 if p:
                     b.validity[k] = p
+        if ts_stats is not None:
+            b.ts_stats = C.pointer(ts_stats)
+        return b
+
+    def push_device(self, n_rows: int, col_ptrs: Sequence[int], valid_ptrs: Optional[Sequence[int]] = None,
+                    ts_stats: Optional[A.ek_ts_stats] = None):
+        """ts_stats: the batch's shared timestamp statistics (batch_ts_stats), e.g. from another rule over the same
+        source; the push then skips its own pass over the timestamp column."""
+        b = self._device_batch(n_rows, col_ptrs, valid_ptrs, ts_stats)
         self._check(lib().ek_push_batch(self.h, C.byref(b)))
+
+    def batch_ts_stats(self, n_rows: int, col_ptrs: Sequence[int]) -> A.ek_ts_stats:
+        """ek_batch_ts_stats over a device batch: computed once, handed to every rule that pushes the batch."""
+        b = self._device_batch(n_rows, col_ptrs)
+        out = A.ek_ts_stats()
+        self._check(lib().ek_batch_ts_stats(self.h, C.byref(b), C.byref(out)))
+        return out
 
     def push_batch(self, batch: A.ek_batch):
         """Push an ek_batch as is (e.g. the device columns returned by JsonDecoder.decode)."""

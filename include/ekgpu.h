@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 9
+#define EKGPU_ABI_VERSION 10
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -179,12 +179,26 @@ typedef struct {
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };
 
+/* ABI v10. Statistics of a batch's timestamp column, computed once by ek_batch_ts_stats and shared by every rule that
+ * reads the same batch: eKuiper fans one source out to all the rules subscribed to it (internal/topo/subtopo.go:
+ * SrcSubTopo.AddOutput / the shared source node), and each rule's WatermarkOp then scans the same timestamps again
+ * (watermark_op.go:118-155). A push whose batch carries matching statistics skips its own pass over the column. */
+typedef struct {
+    int64_t n_rows;      /* rows they describe (a push with another n_rows ignores them)             */
+    int32_t ts_column;   /* the column they were computed over (a rule with another ts column ignores them) */
+    int32_t unsorted;    /* 1 when some ts[i] < ts[i - 1]                                             */
+    int64_t ts_min, ts_max;
+    int64_t ts_first;    /* ts[0]                                                                     */
+    int64_t max_step;    /* max over i >= 1 of ts[i] - ts[i - 1] (INT64_MIN for one row)              */
+} ek_ts_stats;
+
 /* One columnar micro-batch in arrival order. */
 typedef struct {
     int64_t n_rows;
     const void* columns[EK_MAX_COLUMNS];
     const uint8_t* validity[EK_MAX_COLUMNS]; /* 1 byte per row, 1 = valid; NULL = all valid */
     int32_t memory;                          /* EK_MEM_HOST or EK_MEM_DEVICE                */
+    const ek_ts_stats* ts_stats;             /* ABI v10: host memory; NULL = none            */
 } ek_batch;
 
 /* Per-row value tags of aggregate outputs (Go dynamic type of the reference's result). */
@@ -260,6 +274,11 @@ int ek_create(const ek_plan* plan, int device, void** out_handle);
  * window_op.go:339-419). Windows whose end passes the new watermark are triggered and their
  * GROUP BY results become available to ek_poll_results. */
 int ek_push_batch(void* h, const ek_batch* batch);
+
+/* Compute `out` for `batch` over the handle's timestamp column, on the handle's stream (one pass over the column,
+ * synchronous). Set batch->ts_stats = out before pushing the batch into this and every other event-time rule over the
+ * same source. EK_ERR_STATE for a rule without a timestamp column. (ABI v10) */
+int ek_batch_ts_stats(void* h, const ek_batch* batch, ek_ts_stats* out);
 
 /* Take the results produced so far. memory = EK_MEM_HOST copies them to host memory owned by
  * the engine; EK_MEM_DEVICE hands out device pointers. Valid until ek_release_results. */

@@ -50,6 +50,8 @@ size_t off_aggs(void){return offsetof(ek_plan,aggs);} size_t off_having(void){re
 size_t size_plan(void){return sizeof(ek_plan);} size_t size_result(void){return sizeof(ek_result);}
 size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){return sizeof(ek_batch);}
 size_t size_stats(void){return sizeof(ek_stats);} size_t off_kmaj(void){return offsetof(ek_stats,windows_keymajor);}
+size_t off_bts(void){return offsetof(ek_batch,ts_stats);} size_t size_tss(void){return sizeof(ek_ts_stats);}
+size_t off_tss_step(void){return offsetof(ek_ts_stats,max_step);}
 '''
     d = tempfile.mkdtemp()
     with open(os.path.join(d, "p.c"), "w") as f:
@@ -57,7 +59,8 @@ size_t size_stats(void){return sizeof(ek_stats);} size_t off_kmaj(void){return o
     so = os.path.join(d, "p.so")
     subprocess.check_call(["gcc", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(d, "p.c")])
     P = C.CDLL(so)
-    for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch", "size_stats", "off_kmaj"):
+    for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch", "size_stats", "off_kmaj",
+               "off_bts", "size_tss", "off_tss_step"):
         getattr(P, fn).restype = C.c_size_t
     assert P.off_aggs() == A.ek_plan.aggs.offset
     assert P.off_having() == A.ek_plan.having_prog.offset
@@ -67,6 +70,9 @@ size_t size_stats(void){return sizeof(ek_stats);} size_t off_kmaj(void){return o
     assert P.size_batch() == C.sizeof(A.ek_batch)
     assert P.size_stats() == C.sizeof(A.ek_stats)
     assert P.off_kmaj() == A.ek_stats.windows_keymajor.offset
+    assert P.off_bts() == A.ek_batch.ts_stats.offset
+    assert P.size_tss() == C.sizeof(A.ek_ts_stats)
+    assert P.off_tss_step() == A.ek_ts_stats.max_step.offset
 
 
 def test_compile_baseline_configs():
