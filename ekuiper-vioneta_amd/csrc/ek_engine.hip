@@ -696,6 +696,7 @@ struct Engine {
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
         km_packed = env_int("EKGPU_KM_PACKED", 1);
+        km_states = env_int("EKGPU_KM_STATES", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
@@ -2072,7 +2073,8 @@ struct Engine {
     int km_one = 1;   // EKGPU_KM_ONE=0: one-window launches take the count + scan + write passes too
     int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
-    DevBuf km_rbase, km_rec;
+    int km_states = 1;   // EKGPU_KM_STATES=0: multi-window launches emit one record per (state, window) (k_km_unpack)
+    DevBuf km_rbase, km_rec, km_skend;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
     std::vector<unsigned int> grp_h;
@@ -2302,6 +2304,22 @@ struct Engine {
             *handled = true;
             return 0;
         }
+        // state emission: each kept membership state stored once and fanned out to its windows by k_km_expand
+        const bool states = km_packed && km_states && dp.n_aggs <= kKmRecAggs && nw > 1 && nw <= 65535;
+        int R = 0;
+        if (states) {
+            // R = the most windows one buffer position belongs to (attained at some window start; a, b monotone)
+            for (int i = 0; i < nw; ++i) {
+                const int64_t x = h_rab[2 * i];
+                int lo_j = 0, hi_j = i;   // first j <= i with b_j > x
+                while (lo_j < hi_j) { const int mid = (lo_j + hi_j) >> 1; if (h_rab[2 * mid + 1] > x) hi_j = mid; else lo_j = mid + 1; }
+                int a_lo = i + 1, a_hi = nw;   // first j > i with a_j > x
+                while (a_lo < a_hi) { const int mid = (a_lo + a_hi) >> 1; if (h_rab[2 * mid] > x) a_hi = mid; else a_lo = mid + 1; }
+                R = std::max(R, a_lo - lo_j);
+            }
+            if (int rc = ensure(km_skend, 64)) return rc;
+            d.skend = (uint16_t*)km_skend.p;   // the count pass only tests it
+        }
         walk(false);
         if (sort) {
             hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
@@ -2319,9 +2337,16 @@ struct Engine {
             if (int rc = ensure(km_rec, (size_t)std::max<int64_t>(nrec, 1) * 32)) return rc;
             d.rbase = (const int64_t*)km_rbase.p;
             d.rec = (uint4*)km_rec.p;
+            if (states) {
+                if (int rc = ensure(km_skend, (size_t)std::max<int64_t>(nrec, 32) * 2)) return rc;
+                d.skend = (uint16_t*)km_skend.p;
+            }
         }
         walk(true);
-        if (packed && nrec > 0) {
+        if (states) {
+            if (nrec > 0)
+                hipLaunchKernelGGL(k_km_expand, dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(1024), 0, stream, d, dp.n_aggs, R, rv);
+        } else if (packed && nrec > 0) {
             const int64_t per = (nrec + nw - 1) / nw;
             const dim3 gu((unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (per + kBlock - 1) / kBlock)), (unsigned)nw);
             hipLaunchKernelGGL(k_km_unpack, gu, dim3(kBlock), 0, stream, d, dp.n_aggs, rv);
@@ -2991,7 +3016,11 @@ struct Engine {
                 if (seed != INT64_MIN && n > 0) s.max_gap = std::max(s.max_gap, ts_hint->ts_first - seed);
             }
             *out = s;
-            // the callers rely on the stats sync having drained the stream (pinned descriptor buffers are reused)
+            // the device copy too, as k_stats_reduce leaves it: later passes accumulate into it (k_hop_drop's
+            // n_dropped); and the callers rely on the stats sync having drained the stream (pinned buffers are reused)
+            if (int rc = ensure(bstats, sizeof(BatchStats))) return rc;
+            *h_stats = s;
+            hipMemcpyAsync(bstats.p, h_stats, sizeof(BatchStats), hipMemcpyHostToDevice, stream);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream sync failed");
             return 0;
         }

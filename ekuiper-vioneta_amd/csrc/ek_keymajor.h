@@ -47,6 +47,10 @@ struct KmDesc {
     // left 5-7 partial lines per row, 10.9x write amplification on C4a)
     const int64_t* rbase;          // [nw + 1] exclusive prefix of the windows' kept rows
     uint4* rec;                    // nullptr: store the result columns directly
+    // state emission (skend != nullptr): a kept membership state [k, kend) is counted and stored ONCE, in bucket k
+    // (its first window), with skend = kend; k_km_expand copies it into every window of its run. rbase / bcnt then
+    // count states per bucket instead of rows per window.
+    uint16_t* skend;
 };
 constexpr int kKmRecAggs = 3;      // record: key u32 | 4 tag bytes | 3 x 8-byte values
 
@@ -330,7 +334,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                     continue;
                 }
                 if (!WRITE && !ONE) {   // the count pass needs only the decision
-                    for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
+                    if (d.skend) atomicAdd(&s_h[k], 1u);
+                    else for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
                     k = kend;
                     continue;
                 }
@@ -362,7 +367,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                         one_present = true;
                         km_row(p, part, SORT ? &sr : nullptr, one_v, one_t);
                     } else if constexpr (!WRITE) {
-                        for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
+                        if (d.skend) atomicAdd(&s_h[k], 1u);
+                        else for (int kk = k; kk < kend; ++kk) atomicAdd(&s_h[kk], 1u);
                     } else {
                         int64_t ov[EK_MAX_AGGS];
                         uint8_t ot[EK_MAX_AGGS];
@@ -372,11 +378,17 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                             const uint4 r0 = make_uint4((uint32_t)g, tg, (uint32_t)ov[0], (uint32_t)((uint64_t)ov[0] >> 32));
                             const uint4 r1 = make_uint4((uint32_t)ov[1], (uint32_t)((uint64_t)ov[1] >> 32), (uint32_t)ov[2],
                                                         (uint32_t)((uint64_t)ov[2] >> 32));
-                            for (int kk = k; kk < kend; ++kk) {
-                                const int64_t ri = d.rbase[kk] + (int64_t)atomicAdd(&s_h[kk], 1u);
+                            if (d.skend) {   // the state once, in bucket k (k_km_expand fans it out)
+                                const int64_t ri = d.rbase[k] + (int64_t)atomicAdd(&s_h[k], 1u);
                                 d.rec[2 * ri] = r0;
                                 d.rec[2 * ri + 1] = r1;
-                            }
+                                d.skend[ri] = (uint16_t)kend;
+                            } else
+                                for (int kk = k; kk < kend; ++kk) {
+                                    const int64_t ri = d.rbase[kk] + (int64_t)atomicAdd(&s_h[kk], 1u);
+                                    d.rec[2 * ri] = r0;
+                                    d.rec[2 * ri + 1] = r1;
+                                }
                         } else {
                             for (int kk = k; kk < kend; ++kk) {
                                 const int64_t pos = d.obase[kk] + (int64_t)atomicAdd(&s_h[kk], 1u);
@@ -474,6 +486,53 @@ __global__ __launch_bounds__(kBlock) void k_km_unpack(KmDesc d, int n_aggs, Resu
             }
         }
     }
+}
+#endif
+
+// states -> result rows. Window w's rows are the states of buckets k in [w - R + 1, w] whose run reaches it
+// (kend > w; R = the most windows any one buffer position belongs to bounds every run). One workgroup per window;
+// the grid is laid out so that XCD x takes a contiguous range of windows (workgroup b runs on XCD b % 8): neighbouring
+// windows share most of their candidate states, which then come from that XCD's L2. Each 1024-state tile is compacted
+// with a ballot + LDS scan and its rows stored on consecutive rows of the window's region.
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(1024) void k_km_expand(KmDesc d, int n_aggs, int R, Results res) {
+    const int per = (d.nw + 7) >> 3;
+    const int w = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+    if (w >= d.nw) return;   // uniform per workgroup
+    __shared__ uint32_t s_w[16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t c0 = d.rbase[max(0, w - R + 1)], c1 = d.rbase[w + 1];
+    const int64_t ob = d.obase[w];
+    uint32_t cur = 0;
+    for (int64_t t = c0; t < c1; t += 1024) {
+        const int64_t i = t + threadIdx.x;
+        const bool sel = i < c1 && (int)d.skend[i] > w;
+        const unsigned long long m = __ballot(sel);
+        if (lane == 0) s_w[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) { const uint32_t c = s_w[q]; wb += q < wv ? c : 0u; tot += c; }
+        if (sel) {
+            const int64_t pos = ob + cur + wb + __popcll(m & ((1ull << lane) - 1ull));
+            const uint4 r0 = d.rec[2 * i];
+            res.key[pos] = r0.x;
+            res.tag[0][pos] = (uint8_t)r0.y;
+            res.val[0][pos] = (int64_t)(((uint64_t)r0.w << 32) | r0.z);
+            if (n_aggs > 1) {
+                const uint4 r1 = d.rec[2 * i + 1];
+                res.tag[1][pos] = (uint8_t)(r0.y >> 8);
+                res.val[1][pos] = (int64_t)(((uint64_t)r1.y << 32) | r1.x);
+                if (n_aggs > 2) {
+                    res.tag[2][pos] = (uint8_t)(r0.y >> 16);
+                    res.val[2][pos] = (int64_t)(((uint64_t)r1.w << 32) | r1.z);
+                }
+            }
+        }
+        cur += tot;
+        __syncthreads();   // s_w is rewritten by the next tile
+    }
+    if (threadIdx.x == 0 && cur) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[w]], (unsigned long long)cur);
 }
 #endif
 
@@ -784,7 +843,7 @@ __global__ __launch_bounds__(1024) void k_km_scan(KmDesc d, Results res) {
     }
     if (threadIdx.x == 0) {
         c[d.nblk] = s_carry;
-        if (s_carry) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
+        if (s_carry && !d.skend) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[k]], (unsigned long long)s_carry);
     }
 }
 #endif

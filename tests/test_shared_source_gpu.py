@@ -39,14 +39,21 @@ def _stream(name, n=60_000, keys=97):
     return [key, ts.astype(np.int64), temp, hum]
 
 
-def _push_all(engine_mod, rule, dcols, cuts, share_from=None):
+def _push_all(engine_mod, rule, dcols, cuts, share_from=None, clock=None):
     """Push the batches [cuts[b], cuts[b+1]); with share_from (another rule's handle), each batch carries the
-    statistics that handle computed for it."""
+    statistics that handle computed for it. clock = (start, end, ts): processing time, the clock advanced to start,
+    to each batch's first arrival and to end (tests/test_processing_gpu.py::run_engine)."""
     eng = engine_mod.Engine(rule.plan)
+    if clock:
+        eng.advance_time(clock[0])
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         ptrs = [c[lo:hi].data_ptr() for c in dcols]
         st = share_from.batch_ts_stats(int(hi - lo), ptrs) if share_from is not None else None
+        if clock:
+            eng.advance_time(int(clock[2][lo]))
         eng.push_device(int(hi - lo), ptrs, ts_stats=st)
+    if clock:
+        eng.advance_time(clock[1])
     got = eng.poll()
     s = eng.stats()
     eng.close()
@@ -62,11 +69,16 @@ def test_shared_ts_stats_parity(oracle, engine_mod, name, sql, kw):
                          is_event_time=kw.get("is_event_time", True))
     cols = _stream(name)
     dcols = [torch.from_numpy(c).cuda() for c in cols]
-    exp = oracle.run(rule.plan, cols)
+    clock = None
+    if kw.get("is_event_time", True):
+        exp = oracle.run(rule.plan, cols)
+    else:
+        clock = (int(cols[1][0]) - 1234, int(cols[1][-1]) + 5_000, cols[1])
+        exp = oracle.run_proc(rule.plan, cols, clock[0], clock[1])
     cuts = np.linspace(0, len(cols[0]), 5).astype(np.int64)
     sharer = engine_mod.Engine(other.plan)
-    got_plain, st_plain = _push_all(engine_mod, rule, dcols, cuts)
-    got_shared, st_shared = _push_all(engine_mod, rule, dcols, cuts, share_from=sharer)
+    got_plain, st_plain = _push_all(engine_mod, rule, dcols, cuts, clock=clock)
+    got_shared, st_shared = _push_all(engine_mod, rule, dcols, cuts, share_from=sharer, clock=clock)
     sharer.close()
     assert_windows_equal(rule.plan, got_plain, exp.windows, check_members=True)
     assert_windows_equal(rule.plan, got_shared, exp.windows, check_members=True)
