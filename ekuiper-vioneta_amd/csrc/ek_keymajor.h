@@ -285,6 +285,14 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     int32_t* s_b = s_a + nw;                        // [nw] window ends
     uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
+    __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
+    if (!SORT && threadIdx.x == 0 && p.having_star) {
+        Part<NVC> cp{};
+        cp.cnt = 1;
+        s_hc[0] = km_having(p, cp, nullptr);
+        cp.cnt = 2;
+        s_hc[1] = km_having(p, cp, nullptr);
+    }
     for (int k = threadIdx.x; k < nw; k += kKmBlock) {
         // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
         s_h[k] = (WRITE && !ONE) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 // a state it drops (most (key, window) states hold one row) reads no value at all
                 Part<NVC> cp{};
                 cp.cnt = j1 - j0;
-                const int hc = km_having(p, cp, nullptr);
+                const int hc = cp.cnt <= 2 ? s_hc[cp.cnt - 1] : km_having(p, cp, nullptr);
                 if (hc <= 0) {
                     if (WRITE && hc < 0)
                         for (int kk = k; kk < kend; ++kk) {
@@ -354,7 +362,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                         if (res.aslot) atomicMax(&res.aslot[d.widx[kk]], kMaxSortAggs - ea);
                     }
             } else {
-                const int hv = km_having(p, part, SORT ? &sr : nullptr);
+                // (HAVING over count(*) alone already kept this state above)
+                const int hv = (!SORT && p.having_star) ? 1 : km_having(p, part, SORT ? &sr : nullptr);
                 if (WRITE && hv < 0)
                     for (int kk = k; kk < kend; ++kk) {
                         atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);
@@ -772,7 +781,8 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                     for (int a = p.n_sagg - 1; a >= 0; --a) if (sel(stag, a) == kTagErr) ea = a;
                     if (res.aslot) atomicMax(&res.aslot[g.widx], kMaxSortAggs - ea);
                 } else {
-                    const int hv = km_having(p, part, SORT ? &sr : nullptr);
+                    // (HAVING over count(*) alone already kept this state above)
+                const int hv = (!SORT && p.having_star) ? 1 : km_having(p, part, SORT ? &sr : nullptr);
                     if (hv < 0) {
                         atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
                         if (res.wwit)

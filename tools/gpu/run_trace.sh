@@ -1,7 +1,13 @@
 #!/bin/bash
-# rocprofv3 kernel trace (+ stats) of the default C2 bench: per-kernel durations and inter-kernel gaps
-cd "$(dirname "$0")/../.."; mkdir -p gpurun_out/prof
+# kernel-trace stats only, per CONFIGS (ENV applied to the bench)
+cd "$(dirname "$0")/../.."; mkdir -p gpurun_out/tr
 export TMPDIR=/tmp
-rm -rf gpurun_out/prof/*
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu > gpurun_out/prof.log 2>&1 || exit $?
-tail -1 gpurun_out/prof.log | cut -c1-300
+for c in ${CONFIGS:-C4a}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tr/$c -o run -- python3 bench.py --config $c --steps 5 --warmup 1 --no-cpu --no-ingest > gpurun_out/tr/$c.log 2>&1 || { echo "$c trace failed"; tail -3 gpurun_out/tr/$c.log; exit 1; }
+  f=$(ls gpurun_out/tr/$c/*kernel_stats.csv 2>/dev/null | head -1); [ -z "$f" ] && f=$(find gpurun_out/tr/$c -name '*kernel_stats.csv' | head -1)
+  python3 -c "
+import csv,sys
+r=list(csv.DictReader(open('$f')))
+for x in r[:14]: print('$c', x['Name'][:70], x['Calls'], round(float(x['AverageNs'])/1e3,1), 'us', x['Percentage'])
+"
+done
