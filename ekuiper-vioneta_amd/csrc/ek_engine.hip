@@ -697,6 +697,7 @@ struct Engine {
         km_one = env_int("EKGPU_KM_ONE", 1);
         km_packed = env_int("EKGPU_KM_PACKED", 1);
         km_states = env_int("EKGPU_KM_STATES", 1);
+        km_single = env_int("EKGPU_KM_SINGLE", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
@@ -2074,7 +2075,8 @@ struct Engine {
     int km_packed = 1;   // EKGPU_KM_PACKED=0: the write pass stores the result columns directly
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
     int km_states = 1;   // EKGPU_KM_STATES=0: multi-window launches emit one record per (state, window) (k_km_unpack)
-    DevBuf km_rbase, km_rec, km_skend;
+    int km_single = 1;   // EKGPU_KM_SINGLE=0: state emission keeps the count pass (states sorted as they are stored)
+    DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
     std::vector<unsigned int> grp_h;
@@ -2320,6 +2322,41 @@ struct Engine {
             if (int rc = ensure(km_skend, 64)) return rc;
             d.skend = (uint16_t*)km_skend.p;   // the count pass only tests it
         }
+        // single pass (no order statistics, so nothing can send the launch back to the window-major path after the
+        // walk): the walk stores its states unsorted per block and counts them, k_km_sscatter sorts them by bucket
+        const bool single = states && !sort && km_single && (double)n * 2.0 * 36.0 <= 8e9;
+        if (single) {
+            if (int rc = ensure(km_urec, (size_t)n * 2 * 32)) return rc;
+            if (int rc = ensure(km_ukend, (size_t)n * 2 * 2 * 2)) return rc;
+            if (int rc = ensure(km_scount, (size_t)nblk * 4)) return rc;
+            KmDesc du = d;
+            du.rec = (uint4*)km_urec.p;
+            du.skend = (uint16_t*)km_ukend.p;
+            du.sk = du.skend + (size_t)n * 2;
+            du.scount = (uint32_t*)km_scount.p;
+            ek::launch_km_walk(nvc, sort, true, false, nblk, lds, stream, d_plan, du, rv);
+            hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);
+            if (int rc = ensure(km_rbase, (size_t)(nw + 1) * 8)) return rc;
+            hipLaunchKernelGGL(k_km_rbase, dim3(1), dim3(1024), 0, stream, d, (int64_t*)km_rbase.p);
+            const int64_t nrec = fetch_i64((int64_t*)km_rbase.p + nw);
+            if (nrec > 0) {
+                if (int rc = ensure(km_rec, (size_t)nrec * 32)) return rc;
+                if (int rc = ensure(km_skend, (size_t)std::max<int64_t>(nrec, 32) * 2)) return rc;
+                d.rbase = (const int64_t*)km_rbase.p;
+                d.rec = (uint4*)km_rec.p;
+                d.skend = (uint16_t*)km_skend.p;
+                d.scount = du.scount;
+                hipLaunchKernelGGL(k_km_sscatter, dim3((unsigned)nblk), dim3(kKmBlock), (size_t)nw * 4, stream, d,
+                                   (const uint4*)du.rec, (const uint16_t*)du.skend, (const uint16_t*)du.sk);
+                hipLaunchKernelGGL(k_km_expand, dim3((unsigned)(8 * ((nw + 7) / 8) * kKmExpChunks)), dim3(kKmExpBlock), 0, stream, d,
+                                   dp.n_aggs, R, rv);
+            }
+            phase_end(ph2);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major aggregation failed");
+            stats.windows_keymajor += nw;
+            *handled = true;
+            return 0;
+        }
         walk(false);
         if (sort) {
             hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
@@ -2345,7 +2382,8 @@ struct Engine {
         walk(true);
         if (states) {
             if (nrec > 0)
-                hipLaunchKernelGGL(k_km_expand, dim3((unsigned)(8 * ((nw + 7) / 8))), dim3(1024), 0, stream, d, dp.n_aggs, R, rv);
+                hipLaunchKernelGGL(k_km_expand, dim3((unsigned)(8 * ((nw + 7) / 8) * kKmExpChunks)), dim3(kKmExpBlock), 0, stream, d,
+                                   dp.n_aggs, R, rv);
         } else if (packed && nrec > 0) {
             const int64_t per = (nrec + nw - 1) / nw;
             const dim3 gu((unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (per + kBlock - 1) / kBlock)), (unsigned)nw);

@@ -51,6 +51,12 @@ struct KmDesc {
     // (its first window), with skend = kend; k_km_expand copies it into every window of its run. rbase / bcnt then
     // count states per bucket instead of rows per window.
     uint16_t* skend;
+    // single-pass state emission (sk != nullptr, !SORT write pass, no count pass): the walk stores its kept states
+    // unsorted in its block's region [2 kstart[b * kKmBlock], ...) (a key of r rows has at most 2r membership states),
+    // with their bucket in sk, counts them per (bucket, block) into bcnt and per block into scount; k_km_sscatter then
+    // moves them into bucket order
+    uint16_t* sk;
+    uint32_t* scount;
 };
 constexpr int kKmRecAggs = 3;      // record: key u32 | 4 tag bytes | 3 x 8-byte values
 
@@ -276,6 +282,8 @@ template <int NVC, bool SORT, bool WRITE, bool ONE = false>
 __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, KmDesc d, Results res) {
     extern __shared__ uint32_t s_dyn[];
     __shared__ uint32_t s_wc[kKmBlock / 64 + 1];
+    __shared__ uint32_t s_n;   // single-pass state emission: states stored by this block
+    if (threadIdx.x == 0) s_n = 0;
     bool one_present = false;
     int64_t one_v[EK_MAX_AGGS];
     uint8_t one_t[EK_MAX_AGGS];
@@ -295,7 +303,7 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     }
     for (int k = threadIdx.x; k < nw; k += kKmBlock) {
         // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
-        s_h[k] = (WRITE && !ONE) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
+        s_h[k] = (WRITE && !ONE && !d.sk) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
         s_a[k] = (int32_t)d.ab[2 * k];
         s_b[k] = (int32_t)d.ab[2 * k + 1];
     }
@@ -387,7 +395,14 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                             const uint4 r0 = make_uint4((uint32_t)g, tg, (uint32_t)ov[0], (uint32_t)((uint64_t)ov[0] >> 32));
                             const uint4 r1 = make_uint4((uint32_t)ov[1], (uint32_t)((uint64_t)ov[1] >> 32), (uint32_t)ov[2],
                                                         (uint32_t)((uint64_t)ov[2] >> 32));
-                            if (d.skend) {   // the state once, in bucket k (k_km_expand fans it out)
+                            if (d.sk) {   // single pass: unsorted in the block's region, counted per bucket
+                                const int64_t ri = 2 * (int64_t)d.kstart[(int64_t)blockIdx.x * kKmBlock] + (int64_t)atomicAdd(&s_n, 1u);
+                                atomicAdd(&s_h[k], 1u);
+                                d.rec[2 * ri] = r0;
+                                d.rec[2 * ri + 1] = r1;
+                                d.skend[ri] = (uint16_t)kend;
+                                d.sk[ri] = (uint16_t)k;
+                            } else if (d.skend) {   // the state once, in bucket k (k_km_expand fans it out)
                                 const int64_t ri = d.rbase[k] + (int64_t)atomicAdd(&s_h[k], 1u);
                                 d.rec[2 * ri] = r0;
                                 d.rec[2 * ri + 1] = r1;
@@ -438,11 +453,35 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
             }
         }
     }
-    if constexpr (!WRITE) {
+    if (!WRITE || (!ONE && d.sk)) {
         __syncthreads();
         for (int k = threadIdx.x; k < nw; k += kKmBlock) d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] = s_h[k];
+        if (WRITE && threadIdx.x == 0) d.scount[blockIdx.x] = s_n;
     }
 }
+
+// single-pass state emission: block b's unsorted states (k_km_walk) -> bucket order. State q of the block lands at
+// rbase[k] + bcnt[k][b] (the block's exclusive offset in bucket k after k_km_scan) + an LDS cursor per bucket.
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(kKmBlock) void k_km_sscatter(KmDesc d, const uint4* __restrict__ urec,
+                                                         const uint16_t* __restrict__ ukend, const uint16_t* __restrict__ uk) {
+    extern __shared__ uint32_t s_c[];   // [nw] cursors
+    for (int k = threadIdx.x; k < d.nw; k += kKmBlock) s_c[k] = 0;
+    __syncthreads();
+    const int b = blockIdx.x;
+    const int64_t base = 2 * (int64_t)d.kstart[(int64_t)b * kKmBlock];
+    const uint32_t cnt = d.scount[b];
+    for (uint32_t q = threadIdx.x; q < cnt; q += kKmBlock) {
+        const int64_t i = base + q;
+        const int k = uk[i];
+        const int64_t ri = d.rbase[k] + (int64_t)d.bcnt[(int64_t)k * (d.nblk + 1) + b] + (int64_t)atomicAdd(&s_c[k], 1u);
+        const uint4 r0 = urec[2 * i], r1 = urec[2 * i + 1];
+        d.rec[2 * ri] = r0;
+        d.rec[2 * ri + 1] = r1;
+        d.skend[ri] = ukend[i];
+    }
+}
+#endif
 
 // rbase[k] = exclusive prefix over the launch's windows of their kept rows (bcnt[k][nblk] after k_km_scan);
 // rbase[nw] = the total (one workgroup)
@@ -499,31 +538,54 @@ __global__ __launch_bounds__(kBlock) void k_km_unpack(KmDesc d, int n_aggs, Resu
 #endif
 
 // states -> result rows. Window w's rows are the states of buckets k in [w - R + 1, w] whose run reaches it
-// (kend > w; R = the most windows any one buffer position belongs to bounds every run). One workgroup per window;
-// the grid is laid out so that XCD x takes a contiguous range of windows (workgroup b runs on XCD b % 8): neighbouring
-// windows share most of their candidate states, which then come from that XCD's L2. Each 1024-state tile is compacted
-// with a ballot + LDS scan and its rows stored on consecutive rows of the window's region.
+// (kend > w; R = the most windows any one buffer position belongs to bounds every run). kKmExpChunks workgroups per
+// window each take every kKmExpChunks-th tile of kKmExpTile candidates (4 per thread: independent loads in flight);
+// a tile's rows are compacted per (candidate slot, wave) with ballots, reserved with one atomic on the window's row
+// counter and stored on consecutive rows (each wave's store instructions cover consecutive addresses). Grid layout:
+// XCD x (workgroup b runs on XCD b % 8) takes a contiguous range of windows, all chunks of each: neighbouring windows
+// share most of their candidate states, which then come from that XCD's L2.
+constexpr int kKmExpBlock = 256, kKmExpU = 4, kKmExpTile = kKmExpBlock * kKmExpU, kKmExpChunks = 8;
 #ifndef EK_NO_PLAIN_KERNELS
-__global__ __launch_bounds__(1024) void k_km_expand(KmDesc d, int n_aggs, int R, Results res) {
-    const int per = (d.nw + 7) >> 3;
-    const int w = (int)(blockIdx.x & 7u) * per + (int)(blockIdx.x >> 3);
+__global__ __launch_bounds__(kKmExpBlock) void k_km_expand(KmDesc d, int n_aggs, int R, Results res) {
+    const int per = (d.nw + 7) >> 3;   // windows per XCD
+    const int xcd = (int)(blockIdx.x & 7u), idx = (int)(blockIdx.x >> 3);
+    const int w = xcd * per + idx / kKmExpChunks, chunk = idx % kKmExpChunks;
     if (w >= d.nw) return;   // uniform per workgroup
-    __shared__ uint32_t s_w[16];
+    constexpr int NW = kKmExpBlock / 64;
+    __shared__ uint32_t s_off[kKmExpU * NW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t c0 = d.rbase[max(0, w - R + 1)], c1 = d.rbase[w + 1];
     const int64_t ob = d.obase[w];
-    uint32_t cur = 0;
-    for (int64_t t = c0; t < c1; t += 1024) {
-        const int64_t i = t + threadIdx.x;
-        const bool sel = i < c1 && (int)d.skend[i] > w;
-        const unsigned long long m = __ballot(sel);
-        if (lane == 0) s_w[wv] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t wb = 0, tot = 0;
+    unsigned long long* cnt = (unsigned long long*)&res.win_cnt[d.widx[w]];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int64_t t = c0 + (int64_t)chunk * kKmExpTile; t < c1; t += (int64_t)kKmExpChunks * kKmExpTile) {
+        bool sel[kKmExpU];
+        unsigned long long m[kKmExpU];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) { const uint32_t c = s_w[q]; wb += q < wv ? c : 0u; tot += c; }
-        if (sel) {
-            const int64_t pos = ob + cur + wb + __popcll(m & ((1ull << lane) - 1ull));
+        for (int u = 0; u < kKmExpU; ++u) {
+            const int64_t i = t + u * kKmExpBlock + threadIdx.x;
+            sel[u] = i < c1 && (int)d.skend[i] > w;
+        }
+#pragma unroll
+        for (int u = 0; u < kKmExpU; ++u) {
+            m[u] = __ballot(sel[u]);
+            if (lane == 0) s_off[u * NW + wv] = (uint32_t)__popcll(m[u]);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int e = 0; e < kKmExpU * NW; ++e) { const uint32_t c = s_off[e]; s_off[e] = run; run += c; }
+            const uint32_t base = run ? (uint32_t)atomicAdd(cnt, (unsigned long long)run) : 0u;
+#pragma unroll
+            for (int e = 0; e < kKmExpU * NW; ++e) s_off[e] += base;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kKmExpU; ++u) {
+            if (!sel[u]) continue;
+            const int64_t i = t + u * kKmExpBlock + threadIdx.x;
+            const int64_t pos = ob + (int64_t)s_off[u * NW + wv] + __popcll(m[u] & lt);
             const uint4 r0 = d.rec[2 * i];
             res.key[pos] = r0.x;
             res.tag[0][pos] = (uint8_t)r0.y;
@@ -538,10 +600,8 @@ __global__ __launch_bounds__(1024) void k_km_expand(KmDesc d, int n_aggs, int R,
                 }
             }
         }
-        cur += tot;
-        __syncthreads();   // s_w is rewritten by the next tile
+        __syncthreads();   // s_off is rewritten by the next tile
     }
-    if (threadIdx.x == 0 && cur) atomicAdd((unsigned long long*)&res.win_cnt[d.widx[w]], (unsigned long long)cur);
 }
 #endif
 

@@ -5,7 +5,7 @@ TESTS="${TESTS:-tests/test_keymajor_gpu.py tests/test_range_gpu.py tests/test_sh
 timeout -k 10 900 python -u -m pytest $TESTS "tests/test_fullsize_parity_gpu.py::test_c4a_sliding_full_parity" \
   -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4_km_tests.log 2>&1
 rc=$?; tail -6 gpurun_out/r4_km_tests.log; [ $rc -eq 0 ] || exit $rc
-CONFIGS="C4a" ENVS="EKGPU_KM_STATES=1 EKGPU_KM_STATES=0" bash tools/gpu/run_r4_quick.sh || exit 1
+CONFIGS="C4a" ENVS="${KM_ENVS:-EKGPU_KM_STATES=1 EKGPU_KM_STATES=0}" bash tools/gpu/run_r4_quick.sh || exit 1
 for flag in "" "--no-shared-stats"; do
   tag="C5${flag:+_noshare}"
   timeout -k 10 300 python bench.py --config C5 --steps 10 --warmup 2 --no-cpu $flag > gpurun_out/s_${tag}.json 2> gpurun_out/s_${tag}.err
