@@ -2076,7 +2076,7 @@ struct Engine {
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
     int km_states = 1;   // EKGPU_KM_STATES=0: multi-window launches emit one record per (state, window) (k_km_unpack)
     int km_single = 1;   // EKGPU_KM_SINGLE=0: state emission keeps the count pass (states sorted as they are stored)
-    DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount;
+    DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount, km_ex;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
     std::vector<unsigned int> grp_h;
@@ -2287,15 +2287,26 @@ struct Engine {
         d.bcnt = (uint32_t*)km_bcnt.p;
         d.flags = (int32_t*)(d_flag + 2);
         const Results rv = results_view();
-        // kept-row counters + window starts / ends (+ the order-statistic lanes)
-        const size_t lds = (size_t)((3 * nw + 1) & ~1) * 4 + (sort ? (size_t)kKmSegMax * kKmBlock * 8 : 0);
+        // kept-row counters / cursors per window (+ the order-statistic lanes)
+        const size_t lds = (size_t)((nw + 1) & ~1) * 4 + (sort ? (size_t)kKmSegMax * kKmBlock * 8 : 0);
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
         const dim3 gg((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
+        size_t glds = 0;
+        if (!one) {   // multi-window walk: each row's first window and first window past it, beside its values
+            if (int rc = ensure(km_ex, (size_t)n * 4)) return rc;
+            cols.E = (uint16_t*)km_ex.p;
+            cols.X = cols.E + n;
+            cols.ab = d_ab;
+            cols.nw = nw;
+            d.sE = cols.E;
+            d.sX = cols.X;
+            glds = (size_t)nw * 8;
+        }
         if (!vsort) switch (nvc) {
-        case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
-        case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
-        case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
-        default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), 0, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
+        default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         }
         auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
         if (one) {

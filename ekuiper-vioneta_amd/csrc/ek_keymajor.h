@@ -57,6 +57,8 @@ struct KmDesc {
     // moves them into bucket order
     uint16_t* sk;
     uint32_t* scount;
+    const uint16_t* sE;            // multi-window launches: KmCols::E / X of the sorted rows
+    const uint16_t* sX;
 };
 constexpr int kKmRecAggs = 3;      // record: key u32 | 4 tag bytes | 3 x 8-byte values
 
@@ -114,9 +116,25 @@ __global__ __launch_bounds__(kBlock) void k_km_maxrun(const uint32_t* __restrict
 }
 #endif
 
+// first window k in [k0, nw) with e[k] > x (e non-decreasing: window starts or ends in LDS), nw if none
+__device__ __forceinline__ int km_first_gt(const int32_t* e, int k0, int nw, int64_t x) {
+    int lo = k0, hi = nw;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)e[mid] > x) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
 struct KmCols {
     int64_t* val[kMaxVC];
     uint8_t* ok[kMaxVC];
+    // multi-window launches: per row in key order, the first window that holds it (E: first k with b_k > pos) and the
+    // first window past it (X: first k with a_k > pos); row i is a member of window k iff E_i <= k < X_i
+    uint16_t* E;
+    uint16_t* X;
+    const int64_t* ab;   // [2 * nw] window ranges relative to the span start
+    int32_t nw;
 };
 
 // value columns (and validity) of the rows that passed WHERE, in key order
@@ -125,9 +143,18 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
                                                       const uint32_t* __restrict__ spos, const uint32_t* __restrict__ kstart,
                                                       KmCols out) {
     const DPlan& p = *pp;
+    extern __shared__ int32_t s_ab[];   // E / X: window starts [nw], ends [nw]
+    if (out.E) {
+        for (int k = threadIdx.x; k < out.nw; k += kBlock) { s_ab[k] = (int32_t)out.ab[2 * k]; s_ab[out.nw + k] = (int32_t)out.ab[2 * k + 1]; }
+        __syncthreads();
+    }
     const int64_t m = kstart[p.num_keys];
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
         const int64_t r = lo + spos[i];
+        if (out.E) {
+            out.E[i] = (uint16_t)km_first_gt(s_ab + out.nw, 0, out.nw, (int64_t)spos[i]);
+            out.X[i] = (uint16_t)km_first_gt(s_ab, 0, out.nw, (int64_t)spos[i]);
+        }
 #pragma unroll
         for (int v = 0; v < NVC; ++v) {
             if (v >= p.n_vc) break;
@@ -138,15 +165,6 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
     }
 }
 
-// first window k in [k0, nw) with e[k] > x (e non-decreasing: window starts or ends in LDS), nw if none
-__device__ __forceinline__ int km_first_gt(const int32_t* e, int k0, int nw, int64_t x) {
-    int lo = k0, hi = nw;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((int64_t)e[mid] > x) hi = mid; else lo = mid + 1;
-    }
-    return lo;
-}
 
 // rank-r value (ordered bits) among the valid values of sub-run [j0, j1) of column v: O(n^2) counting
 __device__ __forceinline__ uint64_t km_select(const int64_t* __restrict__ val, const uint8_t* __restrict__ ok, bool isf,
@@ -289,9 +307,7 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     uint8_t one_t[EK_MAX_AGGS];
     const int nw = d.nw;
     uint32_t* s_h = s_dyn;                          // [nw] kept rows (count pass) / cursors (write pass)
-    int32_t* s_a = (int32_t*)(s_dyn + nw);          // [nw] window starts (relative rows)
-    int32_t* s_b = s_a + nw;                        // [nw] window ends
-    uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
+    uint64_t* s_seg = (uint64_t*)(s_dyn + ((nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
     __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
     if (!SORT && threadIdx.x == 0 && p.having_star) {
@@ -301,12 +317,9 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
         cp.cnt = 2;
         s_hc[1] = km_having(p, cp, nullptr);
     }
-    for (int k = threadIdx.x; k < nw; k += kKmBlock) {
+    for (int k = threadIdx.x; k < nw; k += kKmBlock)
         // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
         s_h[k] = (WRITE && !ONE && !d.sk) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
-        s_a[k] = (int32_t)d.ab[2 * k];
-        s_b[k] = (int32_t)d.ab[2 * k + 1];
-    }
     __syncthreads();
     const int64_t g = (int64_t)blockIdx.x * kKmBlock + threadIdx.x;
     if (g < d.nkeys) {
@@ -316,23 +329,21 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
 #pragma unroll
         for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
         int64_t j0 = s, j1 = s;
-        int k = s < e ? (ONE ? 0 : km_first_gt(s_b, 0, nw, (int64_t)d.spos[s])) : nw;
+        int k = s < e ? (ONE ? 0 : min((int)d.sE[s], (int)d.sX[s])) : nw;
         while (k < nw) {
             int kend = 1;
             if constexpr (ONE) {
                 j0 = s;
                 j1 = e;
             } else {
-                const int64_t wa = s_a[k], wb = s_b[k];
-                while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
+                // window k's members: rows with E <= k (a prefix, up to j1) and X > k (a suffix, from j0); the set
+                // changes at the next row's E or the first member's X: a merge of the two non-decreasing lists
+                while (j1 < e && (int)d.sE[j1] <= k) ++j1;
+                while (j0 < e && (int)d.sX[j0] <= k) ++j0;
                 if (j0 == e) break;
-                if (j1 < j0) j1 = j0;
-                while (j1 < e && (int64_t)d.spos[j1] < wb) ++j1;
-                const int64_t p0 = d.spos[j0];
-                if (j1 == j0) { k = km_first_gt(s_b, k + 1, nw, p0); continue; }
+                kend = min(j1 < e ? (int)d.sE[j1] : nw, (int)d.sX[j0]);
+                if (j1 <= j0) { k = kend; continue; }
                 // windows [k, kend) hold exactly rows [j0, j1) of this key
-                kend = km_first_gt(s_a, k + 1, nw, p0);
-                if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
             }
             if (!SORT && p.having_star) {
                 // HAVING over count(*) alone (C4a: count(*) > 1): decided from the state's row count before any fold;
@@ -841,8 +852,7 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                     for (int a = p.n_sagg - 1; a >= 0; --a) if (sel(stag, a) == kTagErr) ea = a;
                     if (res.aslot) atomicMax(&res.aslot[g.widx], kMaxSortAggs - ea);
                 } else {
-                    // (HAVING over count(*) alone already kept this state above)
-                const int hv = (!SORT && p.having_star) ? 1 : km_having(p, part, SORT ? &sr : nullptr);
+                    const int hv = km_having(p, part, SORT ? &sr : nullptr);
                     if (hv < 0) {
                         atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
                         if (res.wwit)

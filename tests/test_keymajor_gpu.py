@@ -222,6 +222,9 @@ def test_km_write_pass_many_aggregates(oracle, engine_mod):
      "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)", "float"),
     ("SELECT deviceId, median(v), percentile_disc(v, 0.25), avg(v), stddev(v) FROM demo "
      "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 2", "int"),
+    # no order statistic, HAVING over count(*) alone: decided in the grouped walk after its fold
+    ("SELECT deviceId, avg(temperature), max(temperature) FROM demo "
+     "GROUP BY deviceId, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 2", "float"),
 ])
 def test_km_one_window_grouped_huge_keys(oracle, engine_mod, grp, sql, col, monkeypatch):
     """K > 2^16, one window per push, one value column: EKGPU_GRP=1 (default) takes the MSD-partitioned grouping
