@@ -3547,18 +3547,20 @@ struct Engine {
                 if (int rc = eb_merge(db, start, d_acc, n_acc, min_acc, max_acc, arrival_base)) return rc;
             }
         }
-        // the watermark's step: first arrival whose running max reached M (only if M advanced in this batch)
-        if (!had_M || max_ts > M_prev) {
-            if (int rc = ensure(bounds_idx, 8)) return rc;
-            hipLaunchKernelGGL(k_first_ge, dim3(1), dim3(64), 0, stream, runmax_p, n, max_ts, (int64_t*)bounds_idx.p);
-            sW = arrival_base + fetch_i64(bounds_idx.p);
-        }
+        // the watermark's step: first arrival whose running max reached M (only if M advanced in this batch), and the
+        // released end of the buffer at (W, sW): one launch, one round trip
         const int64_t rel_prev = eb_rel;
-        if (eb.n > 0) {
-            if (int rc = ensure(bounds_idx, 8)) return rc;
-            hipLaunchKernelGGL(k_rel_end, dim3(1), dim3(64), 0, stream, (const int64_t*)eb.col[dp.ts_col].p,
-                               arr_ptr(), eb_arr0, eb.n, W, sW, (int64_t*)bounds_idx.p);
-            eb_rel = std::max(eb_rel, fetch_i64(bounds_idx.p));
+        const bool first = !had_M || max_ts > M_prev;
+        if (first || eb.n > 0) {
+            if (int rc = ensure(bounds_idx, 16)) return rc;
+            hipLaunchKernelGGL(k_rel_bounds, dim3(1), dim3(64), 0, stream, runmax_p, n, max_ts, first ? 1 : 0, arrival_base, sW,
+                               eb.n > 0 ? (const int64_t*)eb.col[dp.ts_col].p : (const int64_t*)nullptr, arr_ptr(), eb_arr0,
+                               eb.n, W, (int64_t*)bounds_idx.p);
+            int64_t out2[2] = {0, 0};
+            hipMemcpyAsync(out2, bounds_idx.p, 16, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "release bounds failed");
+            sW = out2[0];
+            if (eb.n > 0) eb_rel = std::max(eb_rel, out2[1]);
         }
         if (need_rel && eb_rel > rel_prev) {
             const int g = (int)std::min<int64_t>(4096, (eb_rel - rel_prev + 255) / 256);

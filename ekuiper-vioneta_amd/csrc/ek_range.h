@@ -132,6 +132,23 @@ __global__ void k_rel_end(const int64_t* __restrict__ bts, const int64_t* __rest
 }
 #endif
 
+// k_first_ge (when the batch moved the max: sW = arrival of that step) and k_rel_end at (W, sW) in one launch, one
+// host round trip: out[0] = sW, out[1] = the released end of the buffer (n_buf == 0: not computed)
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_rel_bounds(const int64_t* __restrict__ runmax, int64_t nb, int64_t max_ts, int first, int64_t arr_base,
+                             int64_t sW, const int64_t* __restrict__ bts, const int64_t* __restrict__ barr, int64_t arr0,
+                             int64_t n_buf, int64_t W, int64_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (first) sW = arr_base + lb_i64(runmax, 0, nb, max_ts);
+    out[0] = sW;
+    if (n_buf > 0) {
+        const int64_t p = lb_i64(bts, 0, n_buf, W);
+        const int64_t q = ub_i64(bts, p, n_buf, W);
+        out[1] = arr_ub(barr, arr0, p, q, sW);
+    }
+}
+#endif
+
 // first j in [0, n) with runmax[j] >= x (n if none) — the step at which the stream max reached x
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_first_ge(const int64_t* __restrict__ a, int64_t n, int64_t x, int64_t* out) {
