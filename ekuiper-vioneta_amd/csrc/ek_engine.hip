@@ -2288,11 +2288,11 @@ struct Engine {
         d.flags = (int32_t*)(d_flag + 2);
         const Results rv = results_view();
         // kept-row counters / cursors per window (+ the order-statistic lanes)
-        const size_t lds = (size_t)((nw + 1) & ~1) * 4 + (sort ? (size_t)kKmSegMax * kKmBlock * 8 : 0);
+        const size_t lds = sort ? (size_t)((3 * nw + 1) & ~1) * 4 + (size_t)kKmSegMax * kKmBlock * 8 : (size_t)nw * 4;
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
         const dim3 gg((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
         size_t glds = 0;
-        if (!one) {   // multi-window walk: each row's first window and first window past it, beside its values
+        if (!one && !sort) {   // multi-window walk by merge: each row's first window and first window past it
             if (int rc = ensure(km_ex, (size_t)n * 4)) return rc;
             cols.E = (uint16_t*)km_ex.p;
             cols.X = cols.E + n;
@@ -2308,6 +2308,7 @@ struct Engine {
         case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         }
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return fail(EK_ERR_DEVICE, "key-major gather launch: %s", hipGetErrorName(e));
         auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
         if (one) {
             ek::launch_km_walk(nvc, sort, true, true, nblk, lds, stream, d_plan, d, rv);
@@ -2369,9 +2370,12 @@ struct Engine {
             return 0;
         }
         walk(false);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess)
+            return fail(EK_ERR_DEVICE, "key-major count pass launch (lds %zu, nw %d): %s", lds, nw, hipGetErrorName(e));
         if (sort) {
             hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
-            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major count pass failed");
+            if (hipError_t e = hipStreamSynchronize(stream); e != hipSuccess)
+                return fail(EK_ERR_DEVICE, "key-major count pass failed: %s", hipGetErrorName(e));
             if (h_kmf[2]) { phase_end(ph2); return 0; }   // a (key, window) run too long for one thread: window-major path
         }
         hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);

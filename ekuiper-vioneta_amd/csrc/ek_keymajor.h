@@ -307,7 +307,10 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     uint8_t one_t[EK_MAX_AGGS];
     const int nw = d.nw;
     uint32_t* s_h = s_dyn;                          // [nw] kept rows (count pass) / cursors (write pass)
-    uint64_t* s_seg = (uint64_t*)(s_dyn + ((nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
+    // SORT launches walk by binary search over the window starts / ends in LDS; the others merge E / X (k_km_gather)
+    int32_t* s_a = (int32_t*)(s_dyn + nw);          // SORT: [nw] window starts (relative rows)
+    int32_t* s_b = s_a + nw;                        // SORT: [nw] window ends
+    uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
     __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
     if (!SORT && threadIdx.x == 0 && p.having_star) {
@@ -317,9 +320,14 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
         cp.cnt = 2;
         s_hc[1] = km_having(p, cp, nullptr);
     }
-    for (int k = threadIdx.x; k < nw; k += kKmBlock)
+    for (int k = threadIdx.x; k < nw; k += kKmBlock) {
         // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
         s_h[k] = (WRITE && !ONE && !d.sk) ? d.bcnt[(int64_t)k * (d.nblk + 1) + blockIdx.x] : 0u;
+        if (SORT && !ONE) {
+            s_a[k] = (int32_t)d.ab[2 * k];
+            s_b[k] = (int32_t)d.ab[2 * k + 1];
+        }
+    }
     __syncthreads();
     const int64_t g = (int64_t)blockIdx.x * kKmBlock + threadIdx.x;
     if (g < d.nkeys) {
@@ -329,12 +337,23 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
 #pragma unroll
         for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
         int64_t j0 = s, j1 = s;
-        int k = s < e ? (ONE ? 0 : min((int)d.sE[s], (int)d.sX[s])) : nw;
+        int k = s < e ? (ONE ? 0 : SORT ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : min((int)d.sE[s], (int)d.sX[s])) : nw;
         while (k < nw) {
             int kend = 1;
             if constexpr (ONE) {
                 j0 = s;
                 j1 = e;
+            } else if constexpr (SORT) {
+                const int64_t wa = s_a[k], wb = s_b[k];
+                while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
+                if (j0 == e) break;
+                if (j1 < j0) j1 = j0;
+                while (j1 < e && (int64_t)d.spos[j1] < wb) ++j1;
+                const int64_t p0 = d.spos[j0];
+                if (j1 == j0) { k = km_first_gt(s_b, k + 1, nw, p0); continue; }
+                // windows [k, kend) hold exactly rows [j0, j1) of this key
+                kend = km_first_gt(s_a, k + 1, nw, p0);
+                if (j1 < e) kend = min(kend, km_first_gt(s_b, k + 1, nw, (int64_t)d.spos[j1]));
             } else {
                 // window k's members: rows with E <= k (a prefix, up to j1) and X > k (a suffix, from j0); the set
                 // changes at the next row's E or the first member's X: a merge of the two non-decreasing lists
