@@ -3053,7 +3053,9 @@ struct Engine {
 
     void set_ts_hint(const ek_batch* b) {
         const ek_ts_stats* t = b ? b->ts_stats : nullptr;
-        ts_hint = t && t->n_rows == b->n_rows && t->ts_column == dp.ts_col && dp.ts_col < user_cols ? t : nullptr;
+        // bound to the exact column: same row count, ts column id AND column pointer (ABI v11)
+        ts_hint = t && t->n_rows == b->n_rows && t->ts_column == dp.ts_col && dp.ts_col < user_cols &&
+                          t->ts_data == b->columns[dp.ts_col] ? t : nullptr;
     }
 
     int batch_stats(const int64_t* ts, int64_t n, bool gap, int64_t seed, BatchStats* out) {
@@ -3105,6 +3107,7 @@ struct Engine {
         t.ts_min = INT64_MAX;
         t.ts_max = INT64_MIN;
         t.max_step = INT64_MIN;
+        t.ts_data = b->columns[dp.ts_col];
         if (n > 0 && b->memory == EK_MEM_HOST) {
             const int64_t* ts = (const int64_t*)b->columns[dp.ts_col];
             t.ts_first = ts[0];
@@ -4592,6 +4595,8 @@ struct Engine {
         prog(plan.where_prog, plan.n_where);
         prog(plan.having_prog, plan.n_having);
         prog(plan.trigger_prog, plan.n_trigger);
+        prog(plan.filter_prog, plan.n_filter);   // FILTER (WHERE ...) decides which rows the panes / buffer hold
+        i32(plan.sliding_send_twice);
         if (wtype == EK_WINDOW_STATE) {
             prog(plan.begin_prog, plan.n_begin);
             prog(plan.emit_prog, plan.n_emit);

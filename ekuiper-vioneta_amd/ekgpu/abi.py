@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 10
+EKGPU_ABI_VERSION = 11
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -102,6 +102,7 @@ class ek_ts_stats(C.Structure):
         ("ts_max", C.c_int64),
         ("ts_first", C.c_int64),
         ("max_step", C.c_int64),
+        ("ts_data", C.c_void_p),
     ]
 
 

@@ -68,7 +68,14 @@ def group_key_string(values: Sequence) -> str:
 
 def _factorize_dense(a):
     """(codes, uniques) of a nil-free array, uniques in first-seen order: pandas.factorize when pandas is importable
-    (hashing in C), numpy otherwise (a sort: np.unique, then the first-seen order restored)."""
+    (hashing in C), numpy otherwise (a sort: np.unique, then the first-seen order restored).
+    A float array is keyed by its bit patterns: -0.0 and 0.0 are two keys, as their %v strings "-0" and "0" are in the
+    reference's group key, while every NaN is one ("NaN")."""
+    if isinstance(a, np.ndarray) and a.dtype.kind == "f":
+        bits = np.ascontiguousarray(a, dtype=np.float64).view(np.int64).copy()
+        bits[np.isnan(a)] = np.array([np.nan], np.float64).view(np.int64)[0]
+        codes, ub = _factorize_dense(bits)
+        return codes, np.asarray(np.asarray(ub, np.int64).view(np.float64), dtype=object)
     try:
         import pandas as pd
     except ImportError:
@@ -100,8 +107,11 @@ def _factorize(col, valid=None):
         nn = np.not_equal(a, None)
         keep = nn if keep is None else keep & nn
         live = a if keep.all() else a[keep]
-        if len({type(x) for x in live}) > 1:
+        types = {type(x) for x in live}
+        if len(types) > 1:
             a = np.array([None if x is None else go_v(x) for x in a], dtype=object)
+        elif types and issubclass(next(iter(types)), (float, np.floating)):
+            a = np.array([np.nan if x is None else x for x in a], dtype=np.float64)   # bit-pattern keys (-0 vs 0)
     if keep is None or keep.all():
         return _factorize_dense(a)
     idx = np.nonzero(keep)[0]

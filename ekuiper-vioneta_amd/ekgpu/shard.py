@@ -286,6 +286,11 @@ def device_watermark(ts, arr, tol: int, dist, want_list: bool, dense_limit: int 
     mm = torch.stack([-ts.min(), ts.max()]) if ts.numel() else torch.tensor([-i64max, -i64max], device=dev)
     dist.all_reduce(mm, op=dist.ReduceOp.MAX)
     lo, hi = -int(mm[0]), int(mm[1])
+    if hi == -i64max:
+        # no rank holds a row (a watermark-only step): no tuple, nothing late; every rank takes this branch together
+        empty = np.zeros(0, np.int64)
+        return {"arrivals_end": None, "all_accepted": True, "max_wm_step": 0, "origin_known": False, "origin_ts": 0,
+                "origin_arrival": 0, "wm_arrival": empty, "wm_ts": empty}
     if hi - lo + 1 <= dense_limit:
         F = torch.full((hi - lo + 1,), i64max, dtype=torch.int64, device=dev)
         if ts.numel():

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 10
+#define EKGPU_ABI_VERSION 11
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -190,6 +190,9 @@ typedef struct {
     int64_t ts_min, ts_max;
     int64_t ts_first;    /* ts[0]                                                                     */
     int64_t max_step;    /* max over i >= 1 of ts[i] - ts[i - 1] (INT64_MIN for one row)              */
+    const void* ts_data; /* ABI v11: the timestamp column they describe (batch->columns[ts_column] when computed);
+                          * a push whose timestamp column is another pointer ignores them, so statistics left over from
+                          * the previous micro-batch of the same size are never trusted                           */
 } ek_ts_stats;
 
 /* One columnar micro-batch in arrival order. */

@@ -51,7 +51,7 @@ size_t size_plan(void){return sizeof(ek_plan);} size_t size_result(void){return 
 size_t off_rkey(void){return offsetof(ek_result,key);} size_t size_batch(void){return sizeof(ek_batch);}
 size_t size_stats(void){return sizeof(ek_stats);} size_t off_kmaj(void){return offsetof(ek_stats,windows_keymajor);}
 size_t off_bts(void){return offsetof(ek_batch,ts_stats);} size_t size_tss(void){return sizeof(ek_ts_stats);}
-size_t off_tss_step(void){return offsetof(ek_ts_stats,max_step);}
+size_t off_tss_step(void){return offsetof(ek_ts_stats,max_step);} size_t off_tss_data(void){return offsetof(ek_ts_stats,ts_data);}
 '''
     d = tempfile.mkdtemp()
     with open(os.path.join(d, "p.c"), "w") as f:
@@ -60,7 +60,7 @@ size_t off_tss_step(void){return offsetof(ek_ts_stats,max_step);}
     subprocess.check_call(["gcc", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", so, os.path.join(d, "p.c")])
     P = C.CDLL(so)
     for fn in ("off_aggs", "off_having", "size_plan", "size_result", "off_rkey", "size_batch", "size_stats", "off_kmaj",
-               "off_bts", "size_tss", "off_tss_step"):
+               "off_bts", "size_tss", "off_tss_step", "off_tss_data"):
         getattr(P, fn).restype = C.c_size_t
     assert P.off_aggs() == A.ek_plan.aggs.offset
     assert P.off_having() == A.ek_plan.having_prog.offset
@@ -73,6 +73,7 @@ size_t off_tss_step(void){return offsetof(ek_ts_stats,max_step);}
     assert P.off_bts() == A.ek_batch.ts_stats.offset
     assert P.size_tss() == C.sizeof(A.ek_ts_stats)
     assert P.off_tss_step() == A.ek_ts_stats.max_step.offset
+    assert P.off_tss_data() == A.ek_ts_stats.ts_data.offset
 
 
 def test_compile_baseline_configs():

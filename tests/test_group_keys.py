@@ -68,6 +68,21 @@ def test_dictionary_numeric_path_matches_key_strings():
         assert group_key_string(r) == group_key_string(rows[i])
 
 
+@pytest.mark.parametrize("as_object", [False, True])
+def test_single_float_dimension_signed_zero(as_object):
+    """fmt %v prints -0.0 as "-0" and 0.0 as "0": two groups in the reference (aggregate_operator.go:49-56); every NaN
+    prints "NaN": one group. A single float dimension (numpy or object column) keeps that split."""
+    f = np.array([0.0, -0.0, 1.5, np.nan, -0.0, 0.0, np.nan, 1.5])
+    col = np.array(list(f), dtype=object) if as_object else f
+    d = GroupKeyDict(["f"], ["float"], 100)
+    got = d.encode([col], [None])
+    rows = [(float(x),) for x in f]
+    assert _same_partition(got, _naive_ids(rows))
+    assert len(set(got.tolist())) == 4
+    for i in range(len(f)):
+        assert group_key_string(d.decode([got[i]])[0]) == group_key_string(rows[i])
+
+
 def test_dictionary_string_path_collisions():
     d = GroupKeyDict(["s", "t"], ["string", "string"], 100)
     ids = d.encode([np.array(["a,b", "a", "x", "a,b"], object), np.array(["c", "b,c", "y", "c"], object)])

@@ -26,10 +26,12 @@ def _stream(kind, n=20_000):
     elif kind == "late":
         ts = ts - rng.integers(0, 200, n) * (rng.random(n) < 0.05)   # some rows far behind: late at tolerance 20
     key = rng.integers(0, 1000, n).astype(np.uint32)
+    if kind == "empty":                           # a watermark-only step: no rank holds a row
+        return key[:0], ts[:0]
     return key, ts
 
 
-TOL = {"sorted": 0, "disorder": 30, "late": 20}
+TOL = {"sorted": 0, "disorder": 30, "late": 20, "empty": 0}
 
 
 def _worker(rank, world, port, kind, q, dense_limit):
@@ -78,3 +80,20 @@ def test_device_router_matches_global_watermark(kind, world, dense_limit):
         assert exp["origin_known"]
         assert (got["origin_ts"], got["origin_arrival"]) == (exp["origin_ts"], exp["origin_arrival"])
     assert got["origin_known"] == exp["origin_known"] or not got["all_accepted"]
+
+
+def test_device_router_empty_step():
+    """Every rank's batch empty: no tuple, nothing late, on both ranks (gloo world 2)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, "empty", q, 1 << 24)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got["wm_arrival"] == [] and got["wm_ts"] == []
+    assert got["all_accepted"] is True and got["origin_known"] is False

@@ -109,11 +109,36 @@ def test_ts_stats_values_and_mismatch(oracle, engine_mod):
     b, _keep = eng._host_batch(cols)
     h = A.ek_ts_stats()
     assert lib().ek_batch_ts_stats(eng.h, C.byref(b), C.byref(h)) == 0
-    assert bytes(h) == bytes(st)
+    fields = [f for f, _ in A.ek_ts_stats._fields_ if f != "ts_data"]
+    assert [getattr(h, f) for f in fields] == [getattr(st, f) for f in fields]
+    assert (st.ts_data, h.ts_data) == (ptrs[1], b.columns[1])   # bound to the column they were computed over
     one = eng.batch_ts_stats(1, ptrs)
     assert (one.ts_min, one.ts_max, one.unsorted, one.max_step) == (ts[0], ts[0], 0, np.iinfo(np.int64).min)
     # a hint describing a different row count is ignored: the push still finds the late rows itself
     eng.push_device(len(ts), ptrs, ts_stats=one)
+    got = eng.poll()
+    late = eng.stats().records_late
+    eng.close()
+    exp = oracle.run(rule.plan, cols)
+    assert late == exp.records_late > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_ts_stats_of_another_column_ignored(oracle, engine_mod):
+    """Statistics left over from the previous micro-batch of the same size (same n_rows, same ts column id) describe
+    another column pointer (ABI v11 ts_data) and are ignored: the push runs its own pass and finds this batch's late
+    rows (a sorted, late-free previous batch would otherwise take the sorted fast path with the wrong bounds)."""
+    import torch
+    rule = compile_rule(CASES[2][1], IOT_SCHEMA, num_keys=97, late_tolerance_ms=300, debug_membership=True)
+    cols = _stream("late_drop", n=10_001)
+    prev = [c.copy() for c in cols]
+    prev[1] = np.sort(prev[1])                           # a sorted batch of the same size
+    dprev = [torch.from_numpy(c).cuda() for c in prev]
+    dcols = [torch.from_numpy(c).cuda() for c in cols]
+    eng = engine_mod.Engine(rule.plan)
+    stale = eng.batch_ts_stats(len(cols[1]), [c.data_ptr() for c in dprev])
+    assert stale.unsorted == 0
+    eng.push_device(len(cols[1]), [c.data_ptr() for c in dcols], ts_stats=stale)
     got = eng.poll()
     late = eng.stats().records_late
     eng.close()

@@ -152,6 +152,19 @@ def test_export_requires_polled_results_and_matching_plan(engine_mod):
         other.import_state(blob)                 # a different rule
     assert e.value.code == A.EK_ERR_INVALID
     other.close()
+    # the plan hash covers the window FILTER clause and send-twice: a blob of another FILTER is another plan
+    fsql = "SELECT deviceId, count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1) FILTER (WHERE temperature > 20)"
+    fa = engine_mod.Engine(compile_rule(fsql, IOT_SCHEMA, num_keys=20).plan)
+    fa.push_host(cols)
+    fa.poll()
+    fblob = fa.export_state()
+    fa.close()
+    for osql in (fsql.replace("> 20", "> 30"), sql):
+        fo = engine_mod.Engine(compile_rule(osql, IOT_SCHEMA, num_keys=20).plan)
+        with pytest.raises(engine_mod.EngineError) as e:
+            fo.import_state(fblob)
+        assert e.value.code == A.EK_ERR_INVALID
+        fo.close()
     fresh = engine_mod.Engine(rule.plan)
     with pytest.raises(engine_mod.EngineError) as e:
         fresh.import_state(blob[: len(blob) - 9])   # truncated
