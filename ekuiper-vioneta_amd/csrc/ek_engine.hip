@@ -203,6 +203,7 @@ struct Engine {
 
     // ---- processing time (execProcessingWindow under the caller's clock, ek_advance_time)
     bool proc = false;                 // processing-time TUMBLING / HOPPING / SLIDING / SESSION
+    bool proc_inc = false;             // processing-time incremental TUMBLING / HOPPING / SLIDING (proc_inc_triggers)
     bool proc_pushdown = false;        // WHERE / FILTER moved below the window (windowPlan.go:82-99): rows are pre-filtered
     bool pre_filter = false;           // a FilterOp in front of the window (pushed-down WHERE and / or the window FILTER)
     DPlan* d_plan_where = nullptr;     // the plan with WHERE, for the pre-filter (d_plan has n_where = 0 then)
@@ -427,8 +428,8 @@ struct Engine {
             // to the rule's start, rows delivered at their arrival timestamps
             if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING && wtype != EK_WINDOW_SLIDING && wtype != EK_WINDOW_SESSION)
                 return fail(EK_ERR_UNSUPPORTED, "unsupported processing-time window type %d", wtype);
-            if (plan.incremental || plan.window_version == 2)
-                return fail(EK_ERR_UNSUPPORTED, "incremental / v2 processing-time windows are not built");
+            if (plan.window_version == 2)
+                return fail(EK_ERR_UNSUPPORTED, "v2 processing-time windows are not built");
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64 || (plan.nullable_mask & (1u << plan.ts_column)))
                 return fail(EK_ERR_INVALID, "processing-time windows need the rows' arrival timestamps (a non-nullable i64 column)");
             proc = true;
@@ -452,17 +453,22 @@ struct Engine {
                              wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_TUMBLING;
             inc = plan.incremental != 0 && fns && win;
         }
+        if (inc && proc) {
+            // TumblingWindowIncAggOp / HoppingWindowIncAggOp / SlidingWindowIncAggOp (window_inc_agg_op.go:316-790) under
+            // the caller's clock; WHERE stays above the window (IncWindowPlan.PushDownPredicate, incAggPlan.go:76-78): only
+            // the window FILTER op is in front of it (planner.go:360-365)
+            proc_inc = true;
+            proc_pushdown = plan.n_filter > 0;
+            slide_delay = 0;
+            send_twice = false;
+        }
         if (inc) {
-            if (wtype == EK_WINDOW_SLIDING && !plan.is_event_time)
-                return fail(EK_ERR_UNSUPPORTED, "processing-time incremental sliding windows are wall-clock driven (use event time)");
-            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
+            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0 && !proc)
                 return fail(EK_ERR_UNSUPPORTED, "delayed incremental sliding windows (appendDelayIncAggWindowInEvent, "
                                                 "window_inc_agg_event_op.go:275-296: a window per row) are not built");
             if (plan.n_where > 0)
                 return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
                                                 "(FilterPlan above IncWindowPlan): not built");
-            if (plan.n_filter > 0)
-                return fail(EK_ERR_UNSUPPORTED, "a window FILTER with incremental window aggregates is not built");
             if (has_first)
                 return fail(EK_ERR_UNSUPPORTED, "incremental windows emit the group's LAST row (window_inc_agg_op.go:443-457): "
                                                 "first-row select fields are not on that path");
@@ -475,7 +481,7 @@ struct Engine {
         range_mode = wtype == EK_WINDOW_SLIDING || wtype == EK_WINDOW_SESSION || wtype == EK_WINDOW_COUNT ||
                      (wtype == EK_WINDOW_HOPPING && plan.is_event_time && plan.late_tolerance_ms > 0) ||
                      wtype == EK_WINDOW_STATE || sort_aggs || has_first ||
-                     (inc && plan.is_event_time) || env_int("EKGPU_FORCE_RANGE", 0) != 0;
+                     inc || env_int("EKGPU_FORCE_RANGE", 0) != 0;
         if (plan.sliding_send_twice && wtype == EK_WINDOW_SLIDING && plan.delay > 0 && plan.is_event_time)
             return fail(EK_ERR_UNSUPPORTED, "enableSlidingWindowSendTwice is built for processing-time sliding windows "
                                             "(window_op.go:355-373); event-time send-twice is not");
@@ -698,6 +704,7 @@ struct Engine {
         km_packed = env_int("EKGPU_KM_PACKED", 1);
         km_states = env_int("EKGPU_KM_STATES", 1);
         km_single = env_int("EKGPU_KM_SINGLE", 1);
+        km_merge_sort = env_int("EKGPU_KM_MERGE_SORT", 0);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
@@ -723,7 +730,7 @@ struct Engine {
         // the rows WatermarkOp accepted (filter_accept)
         pre_filter = proc_pushdown || plan.n_filter > 0;
         if (pre_filter) {
-            const bool push_where = proc && wtype != EK_WINDOW_SLIDING && plan.n_where > 0;
+            const bool push_where = proc && !proc_inc && wtype != EK_WINDOW_SLIDING && plan.n_where > 0;
             std::vector<ek_instr> prog;
             if (push_where) prog.insert(prog.end(), plan.where_prog, plan.where_prog + plan.n_where);
             if (plan.n_filter > 0) {
@@ -895,6 +902,7 @@ struct Engine {
         sw2_gcb = INT64_MIN;
         sw2_gcx = 0;
         h_rtrig.clear();
+        pi_reset();
         g_wa = g_wt = nullptr;
         g_nwm = 0;
         g_sess_last_end = INT64_MIN;
@@ -1920,8 +1928,9 @@ struct Engine {
         // register in trigger order; rows reserved = min(K, members)
         int64_t rows = 0;
         for (int w = 0; w < nq; ++w) rows += std::min<int64_t>(K, h_ab[2 * w + 1] - h_ab[2 * w]);
-        // incremental windows none of whose rows joined them (opened by a row outside their range) are not reported
-        const auto skip = [&](int w) { return inc && h_ab[2 * w + 1] == h_ab[2 * w]; };
+        // incremental windows none of whose rows joined them (opened by a row outside their range) are not reported; a
+        // processing-time incremental window is broadcast even when no row joined it (emit, window_inc_agg_op.go:443-457)
+        const auto skip = [&](int w) { return inc && !proc_inc && h_ab[2 * w + 1] == h_ab[2 * w]; };
         if (int rc = ensure_results(rows, nq)) return rc;
         std::vector<int32_t> slots(nq);
         std::vector<int64_t> obase(nq);
@@ -2076,6 +2085,7 @@ struct Engine {
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
     int km_states = 1;   // EKGPU_KM_STATES=0: multi-window launches emit one record per (state, window) (k_km_unpack)
     int km_single = 1;   // EKGPU_KM_SINGLE=0: state emission keeps the count pass (states sorted as they are stored)
+    int km_merge_sort = 0;   // EKGPU_KM_MERGE_SORT=1: order-statistic launches walk by the E / X merge too
     DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount, km_ex;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
@@ -2218,10 +2228,10 @@ struct Engine {
             if (int rc = ensure(km_val[0], (size_t)n * 8)) return rc;
         if (int rc = ensure(km_tmp, tb)) return rc;
         if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
-        if (int rc = ensure(km_flag, 16)) return rc;
+        if (int rc = ensure(km_flag, 64)) return rc;   // [0..3] flags, [8..15] EK_KM_CHECK report
         if (!h_kmf && hipHostMalloc((void**)&h_kmf, 16) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
         unsigned int* d_flag = (unsigned int*)km_flag.p;
-        hipMemsetAsync(d_flag, 0, 16, stream);
+        hipMemsetAsync(d_flag, 0, 64, stream);
         const int ph = phase_begin(EK_PHASE_PARTITION);
         hipLaunchKernelGGL(k_km_keys, dim3((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
                            d_plan, bv, lo, n, (uint32_t*)km_k[0].p, vsort ? (uint32_t*)nullptr : (uint32_t*)km_p[0].p, d_flag);
@@ -2286,22 +2296,35 @@ struct Engine {
         for (int v = 0; v < kMaxVC; ++v) { d.sval[v] = cols.val[v]; d.sok[v] = cols.ok[v]; }
         d.bcnt = (uint32_t*)km_bcnt.p;
         d.flags = (int32_t*)(d_flag + 2);
+#ifdef EK_KM_CHECK
+        d.dbg = (int32_t*)(d_flag + 8);
+        cols.dbg = d.dbg;
+        d.dbg_mode = km_merge_sort == 3 ? 1 : 0;
+#endif
+        cols.n = n;
         const Results rv = results_view();
         // kept-row counters / cursors per window (+ the order-statistic lanes)
         const size_t lds = sort ? (size_t)((3 * nw + 1) & ~1) * 4 + (size_t)kKmSegMax * kKmBlock * 8 : (size_t)nw * 4;
         const int ph2 = phase_begin(EK_PHASE_AGGREGATE);
         const dim3 gg((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
         size_t glds = 0;
-        if (!one && !sort) {   // multi-window walk by merge: each row's first window and first window past it
+        if (!one && (!sort || km_merge_sort)) {   // multi-window walk by merge: each row's first window and first window past it
             if (int rc = ensure(km_ex, (size_t)n * 4)) return rc;
             cols.E = (uint16_t*)km_ex.p;
             cols.X = cols.E + n;
             cols.ab = d_ab;
             cols.nw = nw;
-            d.sE = cols.E;
-            d.sX = cols.X;
+            if (!(sort && km_merge_sort == 2)) {   // 2 (diagnostic): E / X computed, the walk binary-searches
+                d.sE = cols.E;
+                d.sX = cols.X;
+            }
             glds = (size_t)nw * 8;
         }
+#ifdef EK_KM_CHECK
+        fprintf(stderr, "KMH n=%lld nw=%d K=%u nvc=%d sort=%d one=%d vsort=%d glds=%zu lds=%zu km_ex=%p/%zu E=%p X=%p eb.n=%lld lo=%lld\n",
+                (long long)n, nw, K, nvc, (int)sort, (int)one, (int)vsort, glds, lds, km_ex.p, km_ex.bytes, (void*)cols.E,
+                (void*)cols.X, (long long)eb.n, (long long)lo);
+#endif
         if (!vsort) switch (nvc) {
         case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
@@ -2309,6 +2332,12 @@ struct Engine {
         default: hipLaunchKernelGGL(k_km_gather<4>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         }
         if (hipError_t e = hipGetLastError(); e != hipSuccess) return fail(EK_ERR_DEVICE, "key-major gather launch: %s", hipGetErrorName(e));
+#ifdef EK_KM_CHECK
+        if (hipError_t e = hipStreamSynchronize(stream); e != hipSuccess)
+            return fail(EK_ERR_DEVICE, "key-major gather failed: %s", hipGetErrorName(e));
+        if (int rc = km_check_report("gather")) return rc;
+        fprintf(stderr, "KMH gather ok\n");
+#endif
         auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
         if (one) {
             ek::launch_km_walk(nvc, sort, true, true, nblk, lds, stream, d_plan, d, rv);
@@ -2365,6 +2394,7 @@ struct Engine {
             }
             phase_end(ph2);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major aggregation failed");
+            if (int rc = km_check_report("single pass")) return rc;
             stats.windows_keymajor += nw;
             *handled = true;
             return 0;
@@ -2376,6 +2406,7 @@ struct Engine {
             hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
             if (hipError_t e = hipStreamSynchronize(stream); e != hipSuccess)
                 return fail(EK_ERR_DEVICE, "key-major count pass failed: %s", hipGetErrorName(e));
+            if (int rc = km_check_report("count pass")) return rc;
             if (h_kmf[2]) { phase_end(ph2); return 0; }   // a (key, window) run too long for one thread: window-major path
         }
         hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);
@@ -2406,8 +2437,22 @@ struct Engine {
         }
         phase_end(ph2);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major aggregation failed");
+        if (int rc = km_check_report("write pass")) return rc;
         stats.windows_keymajor += nw;
         *handled = true;
+        return 0;
+    }
+    // EK_KM_CHECK builds: the first bound a key-major kernel found violated (ek_keymajor.h km_bad)
+    int km_check_report(const char* where) {
+#ifdef EK_KM_CHECK
+        int32_t r[8];
+        if (hipMemcpy(r, (const unsigned int*)km_flag.p + 8, sizeof r, hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(EK_ERR_DEVICE, "check read failed");
+        if (r[0]) return fail(EK_ERR_DEVICE, "key-major bound check %d after the %s: %d %d %d %d (block %d thread %d)", r[0], where,
+                              r[1], r[2], r[3], r[4], r[5], r[6]);
+#else
+        (void)where;
+#endif
         return 0;
     }
 
@@ -2479,6 +2524,7 @@ struct Engine {
     int range_triggers(int64_t rel_prev) {
         std::vector<PendWin> pw;
         const int64_t n_new = eb_rel - rel_prev;
+        if (proc_inc) return proc_inc_triggers(rel_prev);
         if (inc && wtype == EK_WINDOW_SLIDING) return inc_slide_triggers(rel_prev);
         if (inc && wtype == EK_WINDOW_COUNT) return inc_count_triggers(rel_prev);
         if (wtype == EK_WINDOW_SLIDING && gmode) {
@@ -2901,6 +2947,150 @@ struct Engine {
         return rc;
     }
 
+    // ---- processing-time incremental windows (TumblingWindowIncAggOp / HoppingWindowIncAggOp / SlidingWindowIncAggOp,
+    // window_inc_agg_op.go:316-790) under the caller's clock. The rows arrive in the buffer in delivery order, so every
+    // window's content is a contiguous buffer range [first, upto): the host replays the op's timers over a mirror of the
+    // delivered arrival timestamps (h_rts) — every timer due at or before a row fires before it, an emit timer before a
+    // tick at the same instant — and fires each emitted window as a fixed range with WindowRange [StartTime, now]:
+    //   TUMBLING: aligned (default): the window opened at the start is emitted by the FirstTimer at
+    //     getAlignedWindowEndTime(start, length), then each tick (every length) emits the window the first row after the
+    //     previous emit opened (StartTime = that row's ts), if any; unaligned (inc_unaligned): ticks every length from the
+    //     start, no window before the first row;
+    //   HOPPING: each tick (the FirstTimer at getAlignedWindowEndTime(start, interval), then every interval; unaligned:
+    //     the start itself, then every interval) opens a window [T, T + length) emitted at T + length (the aligned
+    //     op's window opened at the start has no emit timer: never emitted);
+    //   SLIDING: a row matching OVER (WHEN) emits the oldest live window, i.e. the rows since the first one with
+    //     ts > t - length (gcIncAggWindow(length + delay)), StartTime = that row's ts; with a delay D a timer at t + D
+    //     emits the rows since the first one with ts > t - length that were delivered before it.
+    struct PiHop { int64_t start, first_abs; };
+    int64_t pi_tick = INT64_MAX;        // next tick (tumbling / hopping)
+    int64_t pi_D = 0;                   // sliding delay (ms)
+    bool pi_cur = false;                // tumbling: a window is open
+    int64_t pi_cur_start = 0, pi_cur_first = 0;   // its StartTime and first row (absolute buffer index; -1: not yet known)
+    std::vector<PiHop> pi_hop;          // hopping: opened, not yet emitted windows (emit due = start + length)
+    size_t pi_hop_head = 0;
+    std::vector<int64_t> pi_dq;         // sliding: delay timers (trigger ts), due order
+    size_t pi_dq_head = 0;
+    int64_t pi_next_abs = 0;            // first mirrored row not yet replayed
+    void pi_reset() {
+        pi_tick = INT64_MAX;
+        pi_cur = false;
+        pi_cur_start = pi_cur_first = 0;
+        pi_hop.clear();
+        pi_hop_head = 0;
+        pi_dq.clear();
+        pi_dq_head = 0;
+        pi_next_abs = 0;
+    }
+    void pi_start(int64_t t0) {
+        const bool aligned = plan.inc_unaligned == 0;
+        pi_D = wtype == EK_WINDOW_SLIDING ? (int64_t)plan.delay * unit_ms(plan.time_unit) : 0;
+        if (wtype == EK_WINDOW_TUMBLING) {
+            if (aligned) { pi_cur = true; pi_cur_start = t0; pi_cur_first = -1; }
+            pi_tick = aligned ? aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s) : t0 + H;
+        } else if (wtype == EK_WINDOW_HOPPING) {
+            if (aligned) pi_tick = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
+            else { pi_hop.push_back(PiHop{t0, -1}); pi_tick = t0 + H; }
+        }
+    }
+    int proc_inc_triggers(int64_t rel_prev) {
+        std::vector<PendWin> pw;
+        const int64_t n_new = eb_rel - rel_prev;
+        if (h_rts.empty()) { h_rts_base = eb_base + rel_prev; if (pi_next_abs < h_rts_base) pi_next_abs = h_rts_base; }
+        if (n_new > 0) {
+            const size_t o = h_rts.size();
+            h_rts.resize(o + n_new);
+            hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            if (wtype == EK_WINDOW_SLIDING) {   // OVER (WHEN) of every delivered row
+                if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
+                const DBatch bv = buffer_view();
+                hipLaunchKernelGGL(k_trigger_flags, dim3((int)std::min<int64_t>(4096, (n_new + 255) / 256)), dim3(256), 0, stream,
+                                   d_plan, bv, rel_prev, eb_rel, (uint8_t*)flags_d.p);
+                h_rtrig.resize(h_rts.size());
+                hipMemcpyAsync(h_rtrig.data() + o, flags_d.p, (size_t)n_new, hipMemcpyDeviceToHost, stream);
+            }
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "incremental window mirror copy failed");
+        }
+        const int64_t L_ = L, D = pi_D;
+        auto ts_at = [&](int64_t abs) { return h_rts[abs - h_rts_base]; };
+        auto first_gt = [&](int64_t hi_abs, int64_t x) {   // first mirrored row before hi_abs with ts > x (ts non-decreasing)
+            return h_rts_base + (std::upper_bound(h_rts.begin(), h_rts.begin() + (hi_abs - h_rts_base), x) - h_rts.begin());
+        };
+        auto emit = [&](int64_t start, int64_t now, int64_t a_abs, int64_t b_abs) {
+            PendWin p{};
+            p.q.kind = RB_FIXED;
+            p.q.pos = a_abs - eb_base;
+            p.q.rstep = b_abs - eb_base;
+            p.start = start;
+            p.end = now;
+            pw.push_back(p);
+        };
+        // every timer due at or before `now`, `upto` rows delivered (emit timers before a tick at the same instant)
+        auto timers = [&](int64_t now, int64_t upto) {
+            for (;;) {
+                const int64_t due_h = pi_hop_head < pi_hop.size() ? pi_hop[pi_hop_head].start + L_ : INT64_MAX;
+                const int64_t due_s = pi_dq_head < pi_dq.size() ? pi_dq[pi_dq_head] + D : INT64_MAX;
+                const int64_t due_e = std::min(due_h, due_s);
+                if (due_e <= now && due_e <= pi_tick) {
+                    if (due_h <= due_s) {
+                        PiHop& hw = pi_hop[pi_hop_head++];
+                        const int64_t a = hw.first_abs < 0 ? upto : hw.first_abs;
+                        emit(hw.start, due_h, a, upto);
+                    } else {
+                        pi_dq_head++;
+                        const int64_t a = first_gt(upto, due_s - L_ - D);
+                        if (a < upto) emit(ts_at(a), due_s, a, upto);
+                    }
+                } else if (pi_tick <= now) {
+                    if (wtype == EK_WINDOW_TUMBLING) {
+                        if (pi_cur) emit(pi_cur_start, pi_tick, pi_cur_first < 0 ? upto : pi_cur_first, upto);
+                        pi_cur = false;
+                    } else {
+                        pi_hop.push_back(PiHop{pi_tick, -1});
+                    }
+                    pi_tick += H;
+                } else {
+                    break;
+                }
+            }
+        };
+        const int64_t end_abs = eb_base + eb_rel;
+        for (int64_t r = pi_next_abs; r < end_abs; ++r) {
+            const int64_t t = ts_at(r);
+            timers(t, r);
+            if (wtype == EK_WINDOW_TUMBLING) {
+                if (!pi_cur) { pi_cur = true; pi_cur_start = t; pi_cur_first = r; }
+                else if (pi_cur_first < 0) pi_cur_first = r;
+            } else if (wtype == EK_WINDOW_HOPPING) {
+                // a window's rows start at the first row delivered after its tick (windows still waiting for one are the
+                // newest; an open window's start + length is past t, or its emit timer would have fired before this row)
+                for (size_t k = pi_hop.size(); k > pi_hop_head && pi_hop[k - 1].first_abs < 0; --k) pi_hop[k - 1].first_abs = r;
+            } else if (h_rtrig[r - h_rts_base]) {
+                if (D > 0) pi_dq.push_back(t);
+                else { const int64_t a = first_gt(r + 1, t - L_); emit(ts_at(a), t, a, r + 1); }
+            }
+        }
+        pi_next_abs = end_abs;
+        timers(W, end_abs);
+        const int rc = fire_windows(pw);
+        // rows a later emission can still hold: the open tumbling / hopping windows' rows, the sliding windows' rows
+        // with ts > clock - length - delay (every later timer or trigger is at or after the clock)
+        int64_t keep = end_abs;
+        if (wtype == EK_WINDOW_TUMBLING && pi_cur && pi_cur_first >= 0) keep = std::min(keep, pi_cur_first);
+        for (size_t k = pi_hop_head; k < pi_hop.size(); ++k) if (pi_hop[k].first_abs >= 0) keep = std::min(keep, pi_hop[k].first_abs);
+        if (wtype == EK_WINDOW_SLIDING) keep = std::min(keep, first_gt(end_abs, W - L_ - D));
+        eb_floor = std::max(eb_floor, keep - eb_base);
+        const int64_t drop = keep - h_rts_base;
+        if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
+            h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+            if (!h_rtrig.empty()) h_rtrig.erase(h_rtrig.begin(), h_rtrig.begin() + drop);
+            h_rts_base = keep;
+        }
+        if (pi_hop_head > 1024 && pi_hop_head * 2 > pi_hop.size()) { pi_hop.erase(pi_hop.begin(), pi_hop.begin() + (int64_t)pi_hop_head); pi_hop_head = 0; }
+        if (pi_dq_head > 4096 && pi_dq_head * 2 > pi_dq.size()) { pi_dq.erase(pi_dq.begin(), pi_dq.begin() + (int64_t)pi_dq_head); pi_dq_head = 0; }
+        return rc;
+    }
+
     // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
     int64_t cur_arr_base = 0, cur_nb = 0, cur_prevmax = INT64_MIN;
     int64_t relstep_w(int64_t r) {
@@ -3039,6 +3229,7 @@ struct Engine {
         } else if (wtype == EK_WINDOW_SESSION) {
             ps_tick = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
         }
+        if (proc_inc) pi_start(t0);
     }
 
     // ---- batch statistics: one pass over ts (k_stats), or the shared ek_ts_stats the pushed batch carries (ABI v10:
@@ -3217,7 +3408,7 @@ struct Engine {
             const int64_t rel_prev = eb_rel;
             eb_rel = eb.n;
             rc = range_triggers(rel_prev);
-            if (!rc && wtype == EK_WINDOW_SLIDING) rc = proc_slide_floor();
+            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc) rc = proc_slide_floor();
         } else if (db.n > 0) {
             const int64_t save = arrivals;
             arrivals = arrival_base;
@@ -3251,7 +3442,7 @@ struct Engine {
         int rc = 0;
         if (range_mode) {
             rc = range_triggers(eb_rel);
-            if (!rc && wtype == EK_WINDOW_SLIDING) rc = proc_slide_floor();
+            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc) rc = proc_slide_floor();
         } else {
             rc = proc_close();
         }
@@ -4564,7 +4755,8 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 4;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses
+    static constexpr int64_t kStateVersion = 5;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
+                                                  // 5: processing-time incremental windows
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -4597,6 +4789,7 @@ struct Engine {
         prog(plan.trigger_prog, plan.n_trigger);
         prog(plan.filter_prog, plan.n_filter);   // FILTER (WHERE ...) decides which rows the panes / buffer hold
         i32(plan.sliding_send_twice);
+        i32(plan.inc_unaligned);
         if (wtype == EK_WINDOW_STATE) {
             prog(plan.begin_prog, plan.n_begin);
             prog(plan.emit_prog, plan.n_emit);
@@ -4736,6 +4929,12 @@ struct Engine {
             s.put(inc_pend.data(), inc_pend.size() * sizeof(IncWin));
             s.i64(st_on ? 1 : 0);                                             // state window: onBegin + its first row
             s.i64(st_start_abs);
+            // processing-time incremental windows (v5): ticker, the open windows, the delay timers
+            for (int64_t v : {pi_tick, pi_D, (int64_t)pi_cur, pi_cur_start, pi_cur_first, pi_next_abs}) s.i64(v);
+            s.i64((int64_t)(pi_hop.size() - pi_hop_head));
+            s.put(pi_hop.data() + pi_hop_head, (pi_hop.size() - pi_hop_head) * sizeof(PiHop));
+            s.i64((int64_t)(pi_dq.size() - pi_dq_head));
+            s.put(pi_dq.data() + pi_dq_head, (pi_dq.size() - pi_dq_head) * 8);
         }
         *size = (int64_t)s.b.size();
         if (!buf) return 0;
@@ -4867,6 +5066,19 @@ struct Engine {
             r.read(inc_pend.data(), ni * (int64_t)sizeof(IncWin));
             st_on = r.i64() != 0;
             st_start_abs = r.i64();
+            pi_tick = r.i64(); pi_D = r.i64(); pi_cur = r.i64() != 0; pi_cur_start = r.i64(); pi_cur_first = r.i64();
+            pi_next_abs = r.i64();
+            const int64_t nh = r.i64();
+            if (!r.ok || nh < 0 || nh > size) return fail(EK_ERR_INVALID, "bad incremental hopping windows in state blob");
+            pi_hop.resize((size_t)nh);
+            pi_hop_head = 0;
+            r.read(pi_hop.data(), nh * (int64_t)sizeof(PiHop));
+            const int64_t nq = r.i64();
+            if (!r.ok || nq < 0 || nq > size) return fail(EK_ERR_INVALID, "bad incremental delay timers in state blob");
+            pi_dq.resize((size_t)nq);
+            pi_dq_head = 0;
+            r.read(pi_dq.data(), nq * 8);
+            if (!r.ok) return fail(EK_ERR_INVALID, "state blob truncated");
         }
         return 0;
     }

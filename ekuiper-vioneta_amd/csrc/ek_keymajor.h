@@ -57,9 +57,26 @@ struct KmDesc {
     // moves them into bucket order
     uint16_t* sk;
     uint32_t* scount;
-    const uint16_t* sE;            // multi-window launches: KmCols::E / X of the sorted rows
-    const uint16_t* sX;
+    const uint16_t* sE;            // multi-window launches: KmCols::E / X of the sorted rows (SORT launches: when set,
+    const uint16_t* sX;            // the walk merges them too; else it binary-searches the window bounds)
+    int32_t* dbg;                  // EK_KM_CHECK builds: the first violated bound [code, values...] (km_bad)
+    int32_t dbg_mode;              // EK_KM_CHECK builds: 1 = the walk skips the fold (states only)
+    int32_t pad2;
 };
+
+// EK_KM_CHECK (debug builds, make EXTRA=-DEK_KM_CHECK): the walk and the gather test their index bounds and record the
+// first violation (a code and four values) instead of touching memory out of range; the host reports it.
+__device__ __forceinline__ void km_bad(int32_t* dbg, int code, int64_t a, int64_t b, int64_t c, int64_t e) {
+    if (dbg && atomicCAS(dbg, 0, code) == 0) {
+        dbg[1] = (int32_t)a; dbg[2] = (int32_t)b; dbg[3] = (int32_t)c; dbg[4] = (int32_t)e;
+        dbg[5] = (int32_t)blockIdx.x; dbg[6] = (int32_t)threadIdx.x;
+    }
+}
+#ifdef EK_KM_CHECK
+#define KM_CHECK(dbg, cond, code, a, b, c, e) if (!(cond)) { km_bad(dbg, code, a, b, c, e); break; }
+#else
+#define KM_CHECK(dbg, cond, code, a, b, c, e)
+#endif
 constexpr int kKmRecAggs = 3;      // record: key u32 | 4 tag bytes | 3 x 8-byte values
 
 // (key, relative position) of every row of the span; rows that fail WHERE (or carry an out-of-range key) get the
@@ -135,6 +152,8 @@ struct KmCols {
     uint16_t* X;
     const int64_t* ab;   // [2 * nw] window ranges relative to the span start
     int32_t nw;
+    int64_t n;           // rows of the span
+    int32_t* dbg;        // EK_KM_CHECK
 };
 
 // value columns (and validity) of the rows that passed WHERE, in key order
@@ -149,8 +168,18 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
         __syncthreads();
     }
     const int64_t m = kstart[p.num_keys];
+#ifdef EK_KM_CHECK
+    if (m > out.n) { if (threadIdx.x == 0) km_bad(out.dbg, 1, m, out.n, p.num_keys, 0); return; }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        printf("KMG m=%lld n=%lld nw=%d K=%u lo=%lld bn=%lld grid=%u E=%p X=%p ab=%p v0=%p v1=%p ok0=%p spos=%p kstart=%p nvc=%d\n",
+               (long long)m, (long long)out.n, out.nw, p.num_keys, (long long)lo, (long long)b.n, gridDim.x, (void*)out.E,
+               (void*)out.X, (const void*)out.ab, (void*)out.val[0], (void*)(NVC > 1 ? out.val[1 < NVC ? 1 : 0] : nullptr),
+               (void*)out.ok[0], (const void*)spos, (const void*)kstart, p.n_vc);
+#endif
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
+        KM_CHECK(out.dbg, (int64_t)spos[i] < out.n, 2, i, spos[i], out.n, m)
         const int64_t r = lo + spos[i];
+        KM_CHECK(out.dbg, r >= 0 && r < b.n, 3, i, r, b.n, lo)
         if (out.E) {
             out.E[i] = (uint16_t)km_first_gt(s_ab + out.nw, 0, out.nw, (int64_t)spos[i]);
             out.X[i] = (uint16_t)km_first_gt(s_ab, 0, out.nw, (int64_t)spos[i]);
@@ -200,6 +229,13 @@ __device__ __forceinline__ bool km_fold(const DPlan& p, const KmDesc& d, int64_t
                                         const bool (&isf)[NVC], uint64_t* s_seg, Part<NVC>& part,
                                         uint64_t (&sres)[kMaxSortAggs], uint8_t (&stag)[kMaxSortAggs]) {
     // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
+#ifdef EK_KM_CHECK
+    if (!(j0 >= 0 && j0 < j1 && j1 <= d.n)) { km_bad(d.dbg, 20, j0, j1, d.n, 0); return true; }
+    for (int v = 0; v < NVC; ++v)
+        if (fl[v] && !d.sval[v]) { km_bad(d.dbg, 21, v, fl[v], 0, 0); return true; }
+    for (int sc = 0; SORT && sc < p.n_scol; ++sc)
+        if (p.scol_vc[sc] < 0 || p.scol_vc[sc] >= NVC || !d.sval[p.scol_vc[sc]]) { km_bad(d.dbg, 22, sc, p.scol_vc[sc], NVC, 0); return true; }
+#endif
     int64_t vc[NVC], is[NVC];
     double fs[NVC], m2[NVC];
     uint64_t mn[NVC], mx[NVC];
@@ -265,7 +301,12 @@ __device__ __forceinline__ bool km_fold(const DPlan& p, const KmDesc& d, int64_t
                 if (a >= p.n_sagg || p.sagg_scol[a] != sc) continue;
                 const int ka = p.sagg_agg[a];
                 order_stat(p.agg_fn[ka], fv, p.agg_p[ka], n,
-                           [&](int64_t r) { return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r); },
+                           [&](int64_t r) {
+#ifdef EK_KM_CHECK
+                               if (r < 0 || r >= n) { km_bad(d.dbg, 23, r, n, j0, j1); return (uint64_t)0; }
+#endif
+                               return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r);
+                           },
                            &sres[a], &stag[a]);
                 agg_err |= stag[a] == kTagErr;
             }
@@ -312,6 +353,9 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     int32_t* s_b = s_a + nw;                        // SORT: [nw] window ends
     uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
+#ifdef EK_KM_CHECK
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) printf("KMW0 wave %d start\n", (int)(threadIdx.x >> 6));
+#endif
     __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
     if (!SORT && threadIdx.x == 0 && p.having_star) {
         Part<NVC> cp{};
@@ -337,13 +381,23 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
 #pragma unroll
         for (int v = 0; v < NVC; ++v) { fl[v] = v < p.n_vc ? p.vc_flags[v] : 0; isf[v] = p.vc_is_float[v] != 0; }
         int64_t j0 = s, j1 = s;
-        int k = s < e ? (ONE ? 0 : SORT ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : min((int)d.sE[s], (int)d.sX[s])) : nw;
+        const bool merge = !SORT || d.sE != nullptr;   // uniform
+#ifdef EK_KM_CHECK
+        if (!(s <= e && e <= d.n)) { km_bad(d.dbg, 10, g, s, e, d.n); return; }
+        if (g == 0)
+            printf("KMW n=%lld nw=%d nblk=%d K=%u grid=%u lds? kstart=%p spos=%p sE=%p v0=%p v1=%p bcnt=%p flags=%p skend=%p rec=%p SORT=%d WRITE=%d ONE=%d\n",
+                   (long long)d.n, d.nw, d.nblk, d.nkeys, gridDim.x, (const void*)d.kstart, (const void*)d.spos,
+                   (const void*)d.sE, (const void*)d.sval[0], (const void*)d.sval[NVC > 1 ? 1 : 0], (void*)d.bcnt, (void*)d.flags,
+                   (void*)d.skend, (void*)d.rec, (int)SORT, (int)WRITE, (int)ONE);
+#endif
+        int k = s < e ? (ONE ? 0 : !merge ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : min((int)d.sE[s], (int)d.sX[s])) : nw;
         while (k < nw) {
             int kend = 1;
+            KM_CHECK(d.dbg, k >= 0, 11, g, k, nw, 0)
             if constexpr (ONE) {
                 j0 = s;
                 j1 = e;
-            } else if constexpr (SORT) {
+            } else if (!merge) {
                 const int64_t wa = s_a[k], wb = s_b[k];
                 while (j0 < e && (int64_t)d.spos[j0] < wa) ++j0;
                 if (j0 == e) break;
@@ -361,9 +415,11 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 while (j0 < e && (int)d.sX[j0] <= k) ++j0;
                 if (j0 == e) break;
                 kend = min(j1 < e ? (int)d.sE[j1] : nw, (int)d.sX[j0]);
+                KM_CHECK(d.dbg, kend > k && kend <= nw, 12, g, k, kend, j0)
                 if (j1 <= j0) { k = kend; continue; }
                 // windows [k, kend) hold exactly rows [j0, j1) of this key
             }
+            KM_CHECK(d.dbg, s <= j0 && j0 < j1 && j1 <= e && kend > k && kend <= nw, 13, j0 - s, j1 - s, k, kend)
             if (!SORT && p.having_star) {
                 // HAVING over count(*) alone (C4a: count(*) > 1): decided from the state's row count before any fold;
                 // a state it drops (most (key, window) states hold one row) reads no value at all
@@ -389,6 +445,9 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
             uint64_t sres[kMaxSortAggs];
             uint8_t stag[kMaxSortAggs];
             Part<NVC> part{};
+#ifdef EK_KM_CHECK
+            if (d.dbg_mode == 1) { k = kend; continue; }
+#endif
             const bool agg_err = km_fold<NVC, SORT>(p, d, j0, j1, fl, isf, s_seg, part, sres, stag);
             const SortRes sr{sres, stag, 0, 1};
             if (agg_err) {   // "run Select error" replaces each of these windows' output

@@ -90,6 +90,7 @@ class ek_plan(C.Structure):
         ("n_filter", C.c_int32),
         ("filter_prog", ek_instr * EK_MAX_PROG),
         ("sliding_send_twice", C.c_int32),
+        ("inc_unaligned", C.c_int32),
     ]
 
 

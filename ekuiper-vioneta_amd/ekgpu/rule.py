@@ -330,12 +330,14 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
 def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True, late_tolerance_ms: int = 0,
                  timestamp: Optional[str] = "ts", num_keys: int = 0, tz_offset_s: int = 0,
                  debug_membership: bool = False, nullable=(), incremental: bool = False,
-                 window_version: str = "", sliding_send_twice: bool = False) -> CompiledRule:
+                 window_version: str = "", sliding_send_twice: bool = False, inc_unaligned: bool = False) -> CompiledRule:
     """schema: ordered {column: "bigint" | "float" | "key" | "string"}; the TIMESTAMP column must be bigint (epoch
     ms). A GROUP BY other than one key column adds the synthetic `__group_key` column (see the module docstring).
     sliding_send_twice: the rule option planOptimizeStrategy.windowOption.enableSendSlidingWindowTwice
     (def/rule.go:104-112): a delayed SLIDINGWINDOW emits its first part at the trigger and its second part when the
-    delay expires (window_op.go:98,355-373, event_window_trigger.go:156-161); no effect on other windows."""
+    delay expires (window_op.go:98,355-373, event_window_trigger.go:156-161); no effect on other windows.
+    inc_unaligned: node.EnableAlignWindow = false (the reference's tests): processing-time incremental TUMBLING /
+    HOPPING tick from the rule's start (window_inc_agg_op.go:369-377,693-699)."""
     rule = _compile_rule(sql, schema, is_event_time=is_event_time, late_tolerance_ms=late_tolerance_ms,
                          timestamp=timestamp, num_keys=num_keys, tz_offset_s=tz_offset_s,
                          debug_membership=debug_membership, nullable=nullable, incremental=incremental,
@@ -345,6 +347,7 @@ def compile_rule(sql: str, schema: Dict[str, str], *, is_event_time: bool = True
                                          rule.plan.delay > 0) else 0
     rule.options.setdefault("planOptimizeStrategy", {}).setdefault("windowOption", {})[
         "enableSendSlidingWindowTwice"] = bool(sliding_send_twice)
+    rule.plan.inc_unaligned = 1 if inc_unaligned else 0
     return rule
 
 

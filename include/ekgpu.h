@@ -175,6 +175,11 @@ typedef struct {
      * rows (t, t + D] when the delay expires (handleInputsForSlidingWindow, window_op.go:576-603; the second part's
      * WindowRange is [t, t + D]). Ignored for every other window. */
     int32_t sliding_send_twice;
+    /* ABI v11. node.EnableAlignWindow = false (window_inc_agg_op.go:34-38,369-377,693-699; the reference's own tests set
+     * it): processing-time incremental TUMBLING / HOPPING windows tick every interval from the rule's start instead of
+     * from the aligned window end (getFirstTimer), and a tumbling window is opened by its first row only. 0 = the
+     * production default (aligned). Ignored for every other window. */
+    int32_t inc_unaligned;
 } ek_plan;
 
 enum { EK_MEM_HOST = 0, EK_MEM_DEVICE = 1 };

@@ -689,9 +689,10 @@ static int inc_supported_fn(int fn) {
 
 /* One incremental window: content = the rows incAggCal added, in processing order. A window none of whose
  * rows was added (created by a row outside its own range) is not reported. */
-static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc) {
+static void emit_inc_window_ex(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc,
+                               int report_empty) {
     const ek_plan* p = d->p;
-    if (nc == 0) return;
+    if (nc == 0 && !report_empty) return;
     int64_t w = ob->ws.n;
     v_push(&ob->ws, wstart);
     v_push(&ob->we, wend);
@@ -733,7 +734,33 @@ static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_
         for (int a = 0; a < p->n_aggs; ++a) inc_step(d, p->aggs[a].fn, p->aggs[a].column, content[k], &st[g * p->n_aggs + a]);
     }
     val_t aggv[EK_MAX_AGGS];
+    /* WHERE above the incremental window (FilterPlan over IncWindowPlan, planner.go:702-708; incAggPlan.go:76-78):
+     * FilterOp.Apply over the emitted collection (filter_operator.go:59-90), each row a group's LAST row: nil / false
+     * drops the row, an error or a non-bool replaces the window ("run Where error: ..."). The collection comes out of
+     * a Go map (window_inc_agg_op.go:443-457): of several failing rows, the one with the smallest key is reported. */
+    uint8_t* gkeep = (uint8_t*)malloc((size_t)(ng ? ng : 1));
+    for (int64_t g = 0; g < ng; ++g) gkeep[g] = 1;
+    if (p->n_where > 0) {
+        int64_t bad = -1;
+        val_t badv = mk_null();
+        for (int64_t g = 0; g < ng; ++g) {
+            const val_t r = eval_prog(p->where_prog, p->n_where, d, glast[g], NULL);
+            gkeep[g] = r.tag == V_BOOL && r.i;
+            if (r.tag != V_BOOL && r.tag != V_NULL && (bad < 0 || gkey[g] < gkey[bad])) { bad = g; badv = r; }
+        }
+        if (bad >= 0) {
+            status = EK_WIN_WHERE_ERROR;
+            if (badv.tag == V_ERR) snprintf(ob->werr + w * 128, 128, "run Where error: %s", err_text(badv));
+            else {
+                char tv[80];
+                go_typed(tv, sizeof tv, badv);
+                snprintf(ob->werr + w * 128, 128, "run Where error: invalid condition that returns non-bool value %s", tv);
+            }
+            ng = 0;
+        }
+    }
     for (int64_t g = 0; g < ng; ++g) {
+        if (!gkeep[g]) continue;
         for (int a = 0; a < p->n_aggs; ++a) aggv[a] = inc_value(p->aggs[a].fn, &st[g * p->n_aggs + a]);
         if (p->n_having > 0) {
             /* HavingOp IsIncAgg branch (having_operator.go:73-98): evaluated on each emitted row */
@@ -762,9 +789,12 @@ static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_
         ob->key.n = rows_before;
         for (int a = 0; a < p->n_aggs; ++a) { ob->aval[a].n = rows_before; ob->atag[a].n = rows_before; }
     }
-    free(slot); free(gkey); free(glast); free(st);
+    free(slot); free(gkey); free(glast); free(st); free(gkeep);
     v_push(&ob->rcnt, ob->key.n - rows_before);
     v_push(&ob->st, status);
+}
+static void emit_inc_window(const dataset* d, outbuf* ob, int64_t wstart, int64_t wend, const int64_t* content, int64_t nc) {
+    emit_inc_window_ex(d, ob, wstart, wend, content, nc, 0);
 }
 
 /* HoppingWindowIncAggEventOp (window_inc_agg_event_op.go:26-146), also TUMBLING (:298-307, Length = Interval) */
@@ -1267,11 +1297,6 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     if (inc_ok && p->window_type == EK_WINDOW_SLIDING && (!p->is_event_time || p->delay != 0)) {
         set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding windows are restated in event time without delay only"); return out->status;
     }
-    if (inc_ok && p->n_where > 0) {
-        /* FilterPlan stays above IncWindowPlan (IncWindowPlan.PushDownPredicate keeps it): WHERE would filter the
-         * emitted last rows; not restated */
-        set_status(out, EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates is not restated"); return out->status;
-    }
     if (p->window_type == EK_WINDOW_STATE && !p->is_event_time && p->n_where > 0) {
         /* windowPlan.PushDownPredicate (windowPlan.go:82-99) moves WHERE below a processing-time window */
         set_status(out, EK_ERR_UNSUPPORTED, "pushed-down WHERE below a processing-time state window is not restated"); return out->status;
@@ -1464,6 +1489,105 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
  * SESSION scans at the next session end computed over the inputs while <= restart + timeout (the reference panics on
  * inputs[0] once a replay emptied the inputs and re-scans the same end forever when none is found: both stop the
  * replay here). Rows must arrive with non-decreasing ts. */
+/* ------------------------------------------------------------------ processing-time incremental windows
+ * TumblingWindowIncAggOp / HoppingWindowIncAggOp / SlidingWindowIncAggOp (window_inc_agg_op.go:316-790) under the
+ * same deterministic clock as eko_run_proc (rows delivered at their arrival ts, every timer due at or before a row
+ * fires first; timers at one instant in creation order). A window's content = the rows incAggCal added to it, in
+ * delivery order; emit() broadcasts the window even when no row joined it (WindowRange [StartTime, now]).
+ *   TUMBLING (:359-457): aligned (EnableAlignWindow, the default): the window opened at the rule's start, the
+ *     FirstTimer at getAlignedWindowEndTime(start, rawInterval = length) emits it, then a ticker every length emits the
+ *     open window if a row opened one (newIncAggWindow at that row's ts); unaligned: ticker every length from the
+ *     start, no window before the first row.
+ *   HOPPING (:666-760): aligned: a window at the start that nothing emits (no timer), the FirstTimer at
+ *     getAlignedWindowEndTime(start, rawInterval = interval) then every interval opens a window with an emit timer at
+ *     its start + length; unaligned: the same from a window opened at the start; a row joins every window with
+ *     start <= ts < start + length (calIncAggWindow; gcIncAggWindow only drops windows no later row can join).
+ *   SLIDING (:536-566): per row: gcIncAggWindow(length + delay), a new window at its ts, the row joins every window;
+ *     a row matching OVER (WHEN) emits the oldest window (CurrWindowList[0]) at once, or with a delay D arms a timer
+ *     due at ts + D that gcs (length + delay) and emits the oldest window if any.
+ * The window FILTER op sits before the window (planner.go:360-365). WHERE stays above it (IncWindowPlan keeps the
+ * predicate, incAggPlan.go:76-78): it filters the emitted rows, each a group's LAST row (emit_inc_window_ex). */
+typedef struct { int64_t due, widx; } inc_timer;
+static int proc_inc_run(const ek_plan* p, const dataset* d, outbuf* ob, const int64_t* ts, int64_t n, int64_t start_ms,
+                        int64_t end_ms, int64_t* n_filter_err) {
+    const int wt = p->window_type;
+    const int64_t u = unit_ms(p->time_unit);
+    const int64_t L = (int64_t)p->length * u, D = wt == EK_WINDOW_SLIDING ? (int64_t)p->delay * u : 0;
+    const int64_t I = wt == EK_WINDOW_HOPPING ? (int64_t)p->interval * u : L;   /* IncWindowPlan.Init: tumbling I = L */
+    const int32_t raw = wt == EK_WINDOW_HOPPING ? p->interval : p->length;
+    const int aligned = !p->inc_unaligned;
+    incwin* w = NULL; int64_t nw = 0, cap = 0;   /* every window ever opened (index = creation order) */
+    inc_timer* tm = NULL; int64_t ntm = 0, tcap = 0, thead = 0;   /* emit timers (hopping / delayed sliding), due order */
+    int64_t cur = -1;                            /* tumbling: the open window */
+    int64_t head = 0;                            /* sliding: CurrWindowList = windows [head, nw) */
+#define PI_OPEN(st) do { if (nw == cap) { cap = cap ? 2 * cap : 16; w = (incwin*)realloc(w, (size_t)cap * sizeof(incwin)); } \
+                         memset(&w[nw], 0, sizeof(incwin)); w[nw++].start = (st); } while (0)
+#define PI_TIMER(d_, wi) do { if (ntm == tcap) { tcap = tcap ? 2 * tcap : 16; tm = (inc_timer*)realloc(tm, (size_t)tcap * sizeof(inc_timer)); } \
+                              tm[ntm].due = (d_); tm[ntm].widx = (wi); ntm++; } while (0)
+    int64_t tick = MAXT_MS;
+    if (wt == EK_WINDOW_TUMBLING) {
+        if (aligned) { PI_OPEN(start_ms); cur = nw - 1; tick = eko_aligned_window_end(start_ms, raw, p->time_unit, p->tz_offset_s); }
+        else tick = start_ms + I;
+    } else if (wt == EK_WINDOW_HOPPING) {
+        PI_OPEN(start_ms);
+        if (aligned) tick = eko_aligned_window_end(start_ms, raw, p->time_unit, p->tz_offset_s);
+        else { PI_TIMER(start_ms + L, nw - 1); tick = start_ms + I; }
+    }
+    /* timers due at or before `now`: the ticker (tumbling / hopping) and the emit timers, earliest first (an emit
+     * timer before a tick at the same instant: either order emits the same windows) */
+    for (int64_t i = 0; i <= n; ++i) {
+        const int64_t now = i < n ? ts[i] : end_ms;
+        for (;;) {
+            const int em = thead < ntm && tm[thead].due <= now;
+            const int tk = tick <= now;
+            if (em && (!tk || tm[thead].due <= tick)) {
+                const inc_timer t = tm[thead++];
+                if (wt == EK_WINDOW_SLIDING) {
+                    while (head < nw && t.due - w[head].start >= L + D) head++;   /* gcIncAggWindow(length + delay) */
+                    if (head < nw) emit_inc_window_ex(d, ob, w[head].start, t.due, w[head].mem.a, w[head].mem.n, 1);
+                } else {
+                    emit_inc_window_ex(d, ob, w[t.widx].start, t.due, w[t.widx].mem.a, w[t.widx].mem.n, 1);
+                }
+            } else if (tk) {
+                if (wt == EK_WINDOW_TUMBLING) {
+                    if (cur >= 0) emit_inc_window_ex(d, ob, w[cur].start, tick, w[cur].mem.a, w[cur].mem.n, 1);
+                    cur = -1;
+                } else {
+                    PI_OPEN(tick);
+                    PI_TIMER(tick + L, nw - 1);
+                }
+                tick += I;
+            } else break;
+        }
+        if (i == n) break;
+        if (!filter_pass(d, i, n_filter_err)) continue;   /* the window FILTER op before the window */
+        const int64_t t = ts[i];
+        if (wt == EK_WINDOW_TUMBLING) {
+            if (cur < 0) { PI_OPEN(t); cur = nw - 1; }
+            v_push(&w[cur].mem, i);
+        } else if (wt == EK_WINDOW_HOPPING) {
+            for (int64_t k = 0; k < nw; ++k)
+                if (w[k].start <= t && t < w[k].start + L) v_push(&w[k].mem, i);
+        } else {
+            while (head < nw && t - w[head].start >= L + D) head++;
+            PI_OPEN(t);
+            for (int64_t k = head; k < nw; ++k)
+                if (w[k].start <= t && t < w[k].start + L + D) v_push(&w[k].mem, i);
+            int trig = 1;
+            if (p->n_trigger > 0) { const val_t r = eval_prog(p->trigger_prog, p->n_trigger, d, i, NULL); trig = r.tag == V_BOOL && r.i; }
+            if (trig) {
+                if (D > 0) PI_TIMER(t + D, -1);
+                else emit_inc_window_ex(d, ob, w[head].start, t, w[head].mem.a, w[head].mem.n, 1);
+            }
+        }
+    }
+#undef PI_OPEN
+#undef PI_TIMER
+    for (int64_t k = 0; k < nw; ++k) free(w[k].mem.a);
+    free(w); free(tm);
+    return 0;
+}
+
 int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
                          int64_t start_ms, int64_t end_ms, const eko_restart* rs, eko_output* out) {
     memset(out, 0, sizeof *out);
@@ -1472,8 +1596,25 @@ int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns
     if (p->is_event_time || !(wt == EK_WINDOW_TUMBLING || wt == EK_WINDOW_HOPPING || wt == EK_WINDOW_SLIDING || wt == EK_WINDOW_SESSION)) {
         set_status(out, EK_ERR_UNSUPPORTED, "processing-time clock runs are for TUMBLING / HOPPING / SLIDING / SESSION"); return out->status;
     }
-    if (p->incremental || p->window_version == 2) { set_status(out, EK_ERR_UNSUPPORTED, "incremental / v2 windows are not restated in processing time"); return out->status; }
+    int inc_ok = p->incremental != 0 && p->n_aggs > 0 && wt != EK_WINDOW_SESSION;
+    for (int a = 0; a < p->n_aggs; ++a) inc_ok &= inc_supported_fn(p->aggs[a].fn);
+    if (p->window_version == 2) { set_status(out, EK_ERR_UNSUPPORTED, "v2 windows are not restated in processing time"); return out->status; }
     if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "processing-time rows need their arrival timestamp column"); return out->status; }
+    if (inc_ok) {
+        if (rs && rs->split >= 0) { set_status(out, EK_ERR_UNSUPPORTED, "restart of processing-time incremental windows is not restated"); return out->status; }
+        dataset d = { p, n, columns, validity, NULL };
+        outbuf ob; memset(&ob, 0, sizeof ob);
+        int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
+        for (int64_t i = 0; i < n; ++i) { val_t v = col_val(&d, p->ts_column, i); ts[i] = v.tag == V_F64 ? (int64_t)v.f : v.i; }
+        for (int64_t i = 0; i < n; ++i)
+            if ((i > 0 && ts[i] < ts[i - 1]) || ts[i] < start_ms) {
+                free(ts); set_status(out, EK_ERR_INVALID, "processing-time rows must arrive with non-decreasing timestamps after the start"); return out->status;
+            }
+        proc_inc_run(p, &d, &ob, ts, n, start_ms, end_ms, &out->records_filter_error);
+        free(ts);
+        finish_output(p, &ob, out);
+        return 0;
+    }
     const int64_t split = rs && rs->split >= 0 ? (rs->split < n ? rs->split : n) : -1;
     if (split >= 0 && (rs->export_ms < start_ms || rs->restart_ms < rs->export_ms)) {
         set_status(out, EK_ERR_INVALID, "restart: start <= export <= restart"); return out->status;

@@ -126,10 +126,32 @@ def test_count_window_blocks(oracle):
 
 def test_unsupported_incremental_shapes(oracle):
     ts = np.array([1541152481000], np.int64)
-    for sql in ("SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ss, 10, 2)",
-                "SELECT count(*) FROM demo WHERE a > 1 GROUP BY TUMBLINGWINDOW(ss, 10)"):
+    for sql in ("SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ss, 10, 2)",):
         with pytest.raises(RuntimeError, match="restated"):
             oracle.run(compile_rule(sql, SCHEMA, incremental=True).plan, [ts, np.zeros(1, np.int64)])
+
+
+def test_where_filters_the_emitted_last_rows(oracle):
+    """WHERE stays above the incremental window (FilterPlan over IncWindowPlan, planner.go:702-708; IncWindowPlan keeps
+    the predicate, incAggPlan.go:76-78): FilterOp runs over the emitted collection (filter_operator.go:59-90), whose
+    rows are each group's LAST row with the inc_* fields set (window_inc_agg_op.go:443-457). So a group is kept or
+    dropped by its last row alone, and its aggregates still count every row of the window. Hand-derived: two 10 s
+    windows, rows a = 5, 0, 3 (last 3 > 1: count 3, not 2) and a = 5, 3, 0 (last 0: no row); a last row that errors
+    (a / 0) replaces the window with "run Where error: divided by zero"."""
+    t0 = 1541152480000
+    ts = np.array([t0, t0 + 1, t0 + 2, t0 + 10_000, t0 + 10_001, t0 + 10_002, t0 + 30_000], np.int64)
+    a = np.array([5, 0, 3, 5, 3, 0, 0], np.int64)
+    rule = compile_rule("SELECT count(*), sum(a) FROM demo WHERE a > 1 GROUP BY TUMBLINGWINDOW(ss, 10)", SCHEMA,
+                        incremental=True)
+    run = oracle.run(rule.plan, [ts, a])
+    assert [len(w.keys) for w in run.windows[:2]] == [1, 0]
+    assert run.windows[0].value(0, 0) == 3 and run.windows[0].value(1, 0) == 8.0
+    rule = compile_rule("SELECT count(*) FROM demo WHERE 10 / a > 1 GROUP BY TUMBLINGWINDOW(ss, 10)", SCHEMA,
+                        incremental=True)
+    run = oracle.run(rule.plan, [ts, a])
+    assert run.windows[0].status == A.EK_WIN_OK and len(run.windows[0].keys) == 1   # last a = 3: 10 / 3 = 3 > 1
+    assert run.windows[1].status == A.EK_WIN_WHERE_ERROR
+    assert run.errors[1] == "run Where error: divided by zero"
 
 
 def test_inc_sliding_clones_the_oldest_open_window(oracle):

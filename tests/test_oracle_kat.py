@@ -193,3 +193,24 @@ def test_window_v2_sliding_left_open_and_arrival_cut(oracle):
     assert [list(map(int, m)) for m in v2.members] == [[1, 2]]
     assert v2.windows[0].value(1, 0) == 5 and (v2.windows[0].start, v2.windows[0].end) == (ts[2] - 4000, ts[2])
     assert [list(map(int, m)) for m in v1.members] == [[0, 1, 2, 3]]
+
+
+# ------------------------------------------------------------------ processing-time incremental windows (mock clock)
+@pytest.mark.parametrize("case", _load("kat_inc_proc.json")["tests"], ids=lambda c: c["name"])
+def test_inc_processing_window_kat(oracle, case):
+    """window_inc_agg_op_test.go: TumblingWindowIncAggOp / SlidingWindowIncAggOp (OVER, delay) / HoppingWindowIncAggOp
+    under the mock clock (eko_run_proc): windows, members, count(*) and the emitted last row."""
+    rows = case["rows"]
+    a = np.array([r[1] for r in rows], np.int64)
+    ts = np.array([r[0] for r in rows], np.int64)
+    rule = compile_rule(case["sql"].replace("stream", "demo"), {"a": "bigint", "ts": "bigint"}, is_event_time=False,
+                        incremental=True, inc_unaligned=case.get("inc_unaligned", False))
+    assert rule.plan.incremental == 1
+    run = oracle.run_proc(rule.plan, [a, ts], 0, case["end_ms"])
+    assert len(run.windows) == len(case["windows"])
+    for w, members, exp in zip(run.windows, run.members, case["windows"]):
+        m = sorted(int(x) for x in members)
+        assert m == exp["members"]
+        assert int(a[m[-1]]) == exp["last_a"]
+        assert (w.start, w.end) == (exp["window_start"], exp["window_end"])
+        assert w.value(0, 0) == exp["count"]
