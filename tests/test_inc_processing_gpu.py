@@ -74,7 +74,7 @@ def test_inc_proc_parity(oracle, engine_mod, name, sql, kw):
     exp = oracle.run_proc(rule.plan, cols, start, end)
     assert len(exp.windows) > 3
     n = len(ts)
-    for cuts in ([0, n], [0, 1, 777, 5000, n // 2, n - 3, n]):
+    for cuts in ([0, n], sorted({0, 1, 777, min(5000, n - 5), n // 2, n - 3, n})):
         got = run_engine(engine_mod, rule, cols, start, end, cuts)
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
     if name in ("tumbling", "hopping", "sliding_delay"):   # one row per push
