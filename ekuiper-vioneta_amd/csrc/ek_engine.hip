@@ -204,6 +204,11 @@ struct Engine {
     // ---- processing time (execProcessingWindow under the caller's clock, ek_advance_time)
     bool proc = false;                 // processing-time TUMBLING / HOPPING / SLIDING / SESSION
     bool proc_inc = false;             // processing-time incremental TUMBLING / HOPPING / SLIDING (proc_inc_triggers)
+    bool inc_where = false;            // WHERE above an incremental window: filters the groups' last rows (k_inc_where)
+    int inc_hidden = -1;               // its hidden result slot: the group's last row (MAX of the position column)
+    int n_res = 0;                     // value arrays per result row (n_out + the hidden slot)
+    DPlan* d_plan_incw = nullptr;      // the plan with WHERE and HAVING, for k_inc_where (d_plan aggregates without them)
+    DPlan dp_incw{};                   // its host copy (the window error texts re-evaluate its programs)
     bool proc_pushdown = false;        // WHERE / FILTER moved below the window (windowPlan.go:82-99): rows are pre-filtered
     bool pre_filter = false;           // a FilterOp in front of the window (pushed-down WHERE and / or the window FILTER)
     DPlan* d_plan_where = nullptr;     // the plan with WHERE, for the pre-filter (d_plan has n_where = 0 then)
@@ -387,12 +392,13 @@ struct Engine {
             has_first |= plan.aggs[k].fn == EK_AGG_FIRST;
         }
         n_out = plan.n_aggs;
+        n_res = n_out;
         if (wtype == EK_WINDOW_NONE) {
             // a rule without window and aggregates: FilterOp (WHERE) + SELECT * per event (C1 shape)
             if (plan.n_aggs != 0 || plan.key_column >= 0 || plan.n_having)
                 return fail(EK_ERR_UNSUPPORTED, "aggregates need a window in GROUP BY");
             if (plan.is_event_time) return fail(EK_ERR_UNSUPPORTED, "event-time ordering of a window-less rule is not on this path");
-            n_out = plan.n_columns;
+            n_out = n_res = plan.n_columns;
             if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
             if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(EK_ERR_DEVICE, "stream create failed");
             own_stream = true;
@@ -466,9 +472,11 @@ struct Engine {
             if (wtype == EK_WINDOW_SLIDING && plan.delay != 0 && !proc)
                 return fail(EK_ERR_UNSUPPORTED, "delayed incremental sliding windows (appendDelayIncAggWindowInEvent, "
                                                 "window_inc_agg_event_op.go:275-296: a window per row) are not built");
-            if (plan.n_where > 0)
-                return fail(EK_ERR_UNSUPPORTED, "WHERE with incremental window aggregates filters the groups' last rows "
-                                                "(FilterPlan above IncWindowPlan): not built");
+            if (plan.n_where > 0) {
+                // FilterPlan above IncWindowPlan (planner.go:702-708): WHERE filters the emitted last rows (k_inc_where)
+                if (plan.n_aggs >= EK_MAX_AGGS) return fail(EK_ERR_UNSUPPORTED, "WHERE over an incremental window needs a free aggregate slot");
+                inc_where = true;
+            }
             if (has_first)
                 return fail(EK_ERR_UNSUPPORTED, "incremental windows emit the group's LAST row (window_inc_agg_op.go:443-457): "
                                                 "first-row select fields are not on that path");
@@ -649,6 +657,30 @@ struct Engine {
             if (!nullable) f &= ~NEED_CNT;   // vcnt == count(*) when the column has no NULLs
             dp.vc_flags[v] |= f;
         }
+        if (inc_where) {
+            // the group's last row: MAX of the hidden position column (event-buffer index) in slot plan.n_aggs
+            if (rowpos_col < 0) {
+                if (plan.n_columns >= EK_MAX_COLUMNS) return fail(EK_ERR_UNSUPPORTED, "too many columns for WHERE over an incremental window");
+                rowpos_col = plan.n_columns;
+                dp.col_type[rowpos_col] = EK_COL_I64;
+            }
+            int v = -1;
+            for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == rowpos_col) v = x;
+            if (v < 0) {
+                if (dp.n_vc >= kMaxVC) return fail(EK_ERR_UNSUPPORTED, "too many aggregated columns");
+                v = dp.n_vc++;
+                dp.vc_col[v] = rowpos_col;
+                dp.vc_is_float[v] = 0;
+                dp.vc_flags[v] = 0;
+            }
+            inc_hidden = plan.n_aggs;
+            dp.agg_fn[inc_hidden] = EK_AGG_MAX;
+            dp.agg_vc[inc_hidden] = v;
+            dp.agg_sidx[inc_hidden] = -1;
+            dp.vc_flags[v] |= NEED_MAX;
+            dp.n_aggs = plan.n_aggs + 1;
+        }
+        n_res = dp.n_aggs > n_out ? dp.n_aggs : n_out;
         for (int v = 0; v < dp.n_vc; ++v) {
             // float sums feed the M2 merge and avg; int sums keep a float shadow only for var
             if (!dp.vc_is_float[v] && (dp.vc_flags[v] & NEED_M2)) dp.vc_flags[v] |= NEED_FSUM;
@@ -747,8 +779,21 @@ struct Engine {
             if (hipMemcpy(d_plan_where, &pre, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
             if (push_where) dp.n_where = 0;   // the pre-filter already dropped every row whose WHERE is not true
         }
-        where_can_fail = dp.n_where > 0 && prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
-        having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+        if (inc_where) {
+            // k_inc_where's plan keeps WHERE and HAVING; the aggregation runs without either
+            DPlan w = dp;
+            dp_incw = dp;
+            if (hipMalloc((void**)&d_plan_incw, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
+            if (hipMemcpy(d_plan_incw, &w, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+            where_can_fail = prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
+            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+            dp.n_where = 0;
+            dp.n_having = 0;
+            dp.having_star = 0;
+        } else {
+            where_can_fail = dp.n_where > 0 && prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
+            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+        }
         for (int k = 0; k < dp.n_aggs; ++k)
             agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC;
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
@@ -988,7 +1033,7 @@ struct Engine {
                 return 0;
             };
             if (int rc = grow(r_key, 4)) return rc;
-            for (int k = 0; k < n_out; ++k) {
+            for (int k = 0; k < n_res; ++k) {
                 if (int rc = grow(r_val[k], 8)) return rc;
                 if (int rc = grow(r_tag[k], 1)) return rc;
             }
@@ -1023,7 +1068,7 @@ struct Engine {
     Results results_view() {
         Results r{};
         r.key = (uint32_t*)r_key.p;
-        for (int k = 0; k < n_out; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
+        for (int k = 0; k < n_res; ++k) { r.val[k] = (int64_t*)r_val[k].p; r.tag[k] = (uint8_t*)r_tag[k].p; }
         r.win_cnt = (int64_t*)r_wcnt.p;
         r.win_err = (int32_t*)r_werr.p;
         r.wwit = (WitRec*)r_wwit.p;
@@ -1481,6 +1526,24 @@ struct Engine {
         return 0;
     }
     DevBuf ff_d;
+    // WHERE (and HAVING) over the fired incremental windows' last rows (ek_range.h k_inc_where)
+    int inc_where_pass(const std::vector<int32_t>& slots, const std::vector<int64_t>& obase) {
+        std::vector<int32_t> ws;
+        std::vector<int64_t> wb;
+        for (size_t w = 0; w < slots.size(); ++w)
+            if (slots[w] >= 0) { ws.push_back(slots[w]); wb.push_back(obase[w]); }
+        if (ws.empty()) return 0;
+        const size_t nw = ws.size();
+        if (int rc = ensure(ff_d, nw * 12 + 16)) return rc;
+        int64_t* d_wb = (int64_t*)ff_d.p;
+        int32_t* d_ws = (int32_t*)(d_wb + nw);
+        hipMemcpyAsync(d_wb, wb.data(), nw * 8, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(d_ws, ws.data(), nw * 4, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(k_inc_where, dim3((unsigned)nw), dim3(256), 0, stream, d_plan_incw, buffer_view(), (const int32_t*)d_ws,
+                           (const int64_t*)d_wb, inc_hidden, n_res, results_view());
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "incremental WHERE pass failed");
+        return 0;
+    }
     int launch_ung(const DBatch& db, GroupDesc gd, const uint8_t* d_acc, int32_t* perr, int64_t* pmc,
                    unsigned long long* pmh, bool any_fresh) {
         if (any_fresh) {
@@ -2010,6 +2073,8 @@ struct Engine {
         }
         if (dp.n_first > 0)
             if (int rc = first_fetch(slots, obase)) return rc;
+        if (inc_where)
+            if (int rc = inc_where_pass(slots, obase)) return rc;
         // windows never start below the last fired one's start (overlapping) or end (disjoint); send-twice windows do
         // not fire in start order (a timer's (t, t + D] precedes the next trigger's (t' - L, t']): proc_slide_delayed
         // and proc_slide_floor keep their floor
@@ -4684,6 +4749,7 @@ struct Engine {
             hipMemcpyAsync(as.data(), r_aslot.p, (size_t)nw * 4, hipMemcpyDeviceToHost, stream);
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "error witness copy failed");
+        const DPlan& dp = inc_where ? dp_incw : this->dp;   // WHERE over an incremental window: k_inc_where's programs
         for (int64_t w = 0; w < nw; ++w) {
             const int32_t st = we[w];
             if (!st) continue;
@@ -5097,6 +5163,7 @@ struct Engine {
         for (int k = 0; k < EK_MAX_AGGS; ++k) { release(r_val[k]); release(r_tag[k]); }
         if (d_plan) hipFree(d_plan);
         if (d_plan_where) hipFree(d_plan_where);
+        if (d_plan_incw) hipFree(d_plan_incw);
         if (h_stats) hipHostFree(h_stats);
         if (h_small) hipHostFree(h_small);
         if (h_wdesc) hipHostFree(h_wdesc);

@@ -566,6 +566,93 @@ __global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* _
 }
 #endif
 
+// ---------------------------------------------------------------- WHERE above an incremental window
+// FilterPlan stays above IncWindowPlan (planner.go:702-708; IncWindowPlan.PushDownPredicate keeps the predicate,
+// incAggPlan.go:76-78): FilterOp.Apply runs over the emitted collection (filter_operator.go:59-90), whose rows are the
+// groups' LAST rows with the inc_* fields set (window_inc_agg_op.go:443-457), then HavingOp over what is left. The
+// aggregation folds a hidden MAX over the event-buffer position column into result slot `hidden` (the last row), with
+// neither WHERE nor HAVING; one block per fired window then evaluates WHERE at each row's last row: an error or a
+// non-bool replaces the window (its witness: the failing row with the smallest key, as the host's text re-evaluation
+// expects), nil / false drops the row; HAVING (over the result values) decides the rest, and the kept rows are
+// compacted in place, tile by tile (a tile is read whole before any of it is written, and its writes land at or
+// below its own start).
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ __launch_bounds__(256) void k_inc_where(DPlan* __restrict__ pp, DBatch b, const int32_t* __restrict__ wslot,
+                                                   const int64_t* __restrict__ wbase, int hidden, int n_res, Results res) {
+    const DPlan& p = *pp;
+    const int32_t slot = wslot[blockIdx.x];
+    const int64_t base = wbase[blockIdx.x], cnt = res.win_cnt[slot];
+    __shared__ int s_err;
+    __shared__ uint32_t wsum[4];
+    __shared__ int64_t s_out;
+    if (threadIdx.x == 0) { s_err = 0; s_out = 0; }
+    __syncthreads();
+    // WHERE errors first: any one replaces the whole window (FilterOp returns the error, no HAVING runs)
+    for (int64_t r = base + threadIdx.x; r < base + cnt; r += blockDim.x) {
+        const int64_t pos = res.val[hidden][r];
+        if (where_decide_slow(p, b, pos) < 0) {
+            s_err = 1;
+            if (res.wwit) wit_where_row(&res.wwit[2 * slot], (unsigned long long)res.key[r], 0ull, p, b, pos);
+        }
+    }
+    __syncthreads();
+    if (s_err) {
+        if (threadIdx.x == 0) { atomicOr(&res.win_err[slot], EK_WIN_WHERE_ERROR); res.win_cnt[slot] = 0; }
+        return;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t t0 = base; t0 < base + cnt; t0 += blockDim.x) {
+        const int64_t r = t0 + threadIdx.x;
+        const bool in = r < base + cnt;
+        uint32_t key = 0;
+        int64_t v[EK_MAX_AGGS];
+        uint8_t tg[EK_MAX_AGGS];
+#pragma unroll
+        for (int q = 0; q < EK_MAX_AGGS; ++q) { v[q] = 0; tg[q] = EK_TAG_NULL; }
+        bool keep = false;
+        if (in) {
+            key = res.key[r];
+#pragma unroll
+            for (int q = 0; q < EK_MAX_AGGS; ++q)
+                if (q < n_res) { v[q] = res.val[q][r]; tg[q] = res.tag[q][r]; }
+            keep = where_decide_slow(p, b, v[hidden]) > 0;
+            if (keep && p.n_having > 0) {
+                auto aggf = [&](int k) {
+                    const uint8_t t = sel(tg, k);
+                    const int64_t x = sel(v, k);
+                    return t == EK_TAG_NULL ? Val{V_NULL, 0, 0.0} : t == EK_TAG_I64 ? Val{V_I64, x, 0.0} : Val{V_F64, 0, __longlong_as_double(x)};
+                };
+                const Val h = eval_prog(p.having_prog, p.n_having, p, nullptr, 0, aggf);
+                if (h.tag != V_BOOL) {
+                    atomicOr(&res.win_err[slot], EK_WIN_HAVING_ERROR);
+                    if (res.wwit) wit_having(&res.wwit[2 * slot + 1], key, p, aggf);
+                    keep = false;
+                } else {
+                    keep = h.i != 0;
+                }
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (lane == 0) wsum[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { if (w < wv) before += wsum[w]; total += wsum[w]; }
+        const int64_t out = s_out;
+        if (keep) {
+            const int64_t o = base + out + before + __popcll(m & ((1ull << lane) - 1ull));
+            res.key[o] = key;
+#pragma unroll
+            for (int q = 0; q < EK_MAX_AGGS; ++q)
+                if (q < n_res) { res.val[q][o] = v[q]; res.tag[q][o] = tg[q]; }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_out = out + total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) res.win_cnt[slot] = s_out;
+}
+#endif
+
 // ---------------------------------------------------------------- small range windows: one wave64 per window
 // For a window of at most kSmallWin rows (COUNTWINDOW(1000), state windows, short sliding windows) the pane/bucket
 // partition of k_part + k_agg costs a workgroup per (window, key bucket) that finds a handful of rows. Here ONE WAVE

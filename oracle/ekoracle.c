@@ -759,6 +759,7 @@ static void emit_inc_window_ex(const dataset* d, outbuf* ob, int64_t wstart, int
             ng = 0;
         }
     }
+    int64_t hkey = INT64_MAX;   /* HAVING: of several failing groups, the one with the smallest key is reported */
     for (int64_t g = 0; g < ng; ++g) {
         if (!gkeep[g]) continue;
         for (int a = 0; a < p->n_aggs; ++a) aggv[a] = inc_value(p->aggs[a].fn, &st[g * p->n_aggs + a]);
@@ -767,13 +768,16 @@ static void emit_inc_window_ex(const dataset* d, outbuf* ob, int64_t wstart, int
             val_t r = eval_prog(p->having_prog, p->n_having, d, glast[g], aggv);
             if (r.tag != V_BOOL) {
                 status = EK_WIN_HAVING_ERROR;
-                if (r.tag == V_ERR) snprintf(ob->werr + w * 128, 128, "run Having error: %s", err_text(r));
-                else {
-                    char tv[80];
-                    go_typed(tv, sizeof tv, r);
-                    snprintf(ob->werr + w * 128, 128, "run Having error: invalid condition that returns non-bool value %s", tv);
+                if (gkey[g] < hkey) {
+                    hkey = gkey[g];
+                    if (r.tag == V_ERR) snprintf(ob->werr + w * 128, 128, "run Having error: %s", err_text(r));
+                    else {
+                        char tv[80];
+                        go_typed(tv, sizeof tv, r);
+                        snprintf(ob->werr + w * 128, 128, "run Having error: invalid condition that returns non-bool value %s", tv);
+                    }
                 }
-                break;
+                continue;
             }
             if (!r.i) continue;
         }

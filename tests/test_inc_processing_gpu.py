@@ -128,3 +128,63 @@ def test_inc_event_time_filter(oracle, engine_mod, name, sql):
     got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=4)
     assert len(exp.windows) > 3
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+# ------------------------------------------------------------------ WHERE above the incremental window
+WSCHEMA = {"k": "key", "ts": "bigint", "x": "float", "z": "bigint"}
+
+
+def _wstream(n, keys, seed, zmax=6):
+    rng = np.random.default_rng(seed)
+    ts = 1541152480000 + 3_456 + np.cumsum(rng.integers(0, 7, n))
+    return [rng.integers(0, keys, n).astype(np.uint32), ts.astype(np.int64), rng.uniform(0, 100, n),
+            rng.integers(0, zmax, n).astype(np.int64)]
+
+
+WHERE_CASES = [
+    ("event_tumbling", "SELECT k, count(*), avg(x) FROM s WHERE z > 2 GROUP BY k, TUMBLINGWINDOW(ss, 1)", True),
+    ("event_hopping", "SELECT k, sum(x), max(z) FROM s WHERE x > 30 GROUP BY k, HOPPINGWINDOW(ss, 2, 1)", True),
+    ("event_sliding", "SELECT k, count(*), min(x) FROM s WHERE z < 4 GROUP BY k, SLIDINGWINDOW(ms, 300) OVER (WHEN x > 98)", True),
+    ("event_having", "SELECT k, count(*), sum(z) FROM s WHERE x > 20 GROUP BY k, TUMBLINGWINDOW(ss, 1) HAVING count(*) > 2", True),
+    ("proc_tumbling", "SELECT k, count(*), avg(x) FROM s WHERE z > 2 GROUP BY k, TUMBLINGWINDOW(ss, 1)", False),
+    ("proc_sliding_delay", "SELECT k, count(*), max(x) FROM s WHERE z <> 1 GROUP BY k, SLIDINGWINDOW(ms, 300, 200) OVER (WHEN x > 98)", False),
+    ("proc_count", "SELECT k, sum(x), count(*) FROM s WHERE x < 50 GROUP BY k, COUNTWINDOW(500)", False),
+]
+
+
+@pytest.mark.parametrize("name,sql,event", WHERE_CASES, ids=[c[0] for c in WHERE_CASES])
+def test_inc_where_last_rows(oracle, engine_mod, name, sql, event):
+    """FilterPlan above IncWindowPlan: a group is kept or dropped by its LAST row's WHERE, its aggregates count every
+    row (k_inc_where over the hidden last-row slot), then HAVING."""
+    keys = 23
+    cols = _wstream(20_000, keys, seed=sum(map(ord, name)))
+    rule = compile_rule(sql, WSCHEMA, is_event_time=event, num_keys=keys, debug_membership=True, incremental=True)
+    if event or "COUNTWINDOW" in sql:
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=3)
+    else:
+        ts = cols[1]
+        start, end = int(ts[0]) - 100, int(ts[-1]) + 3000
+        exp = oracle.run_proc(rule.plan, cols, start, end)
+        got = run_engine(engine_mod, rule, cols, start, end, [0, 7000, 20_000])
+    assert sum(len(w.keys) for w in exp.windows) > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_inc_where_error_texts(oracle, engine_mod):
+    """A last row whose WHERE errors (10 / z with z = 0) replaces the window with "run Where error: divided by zero";
+    the windows whose last rows all evaluate keep their filtered rows."""
+    keys = 5
+    cols = _wstream(3000, keys, seed=11, zmax=40)
+    rule = compile_rule("SELECT k, count(*) FROM s WHERE 10 / z > 0 GROUP BY k, TUMBLINGWINDOW(ms, 200)", WSCHEMA,
+                        num_keys=keys, debug_membership=True, incremental=True)
+    exp = oracle.run(rule.plan, cols)
+    bad = [i for i, w in enumerate(exp.windows) if w.status != 0]
+    assert bad and len(bad) < len(exp.windows)
+    eng = engine_mod.Engine(rule.plan)
+    eng.push_host(cols)
+    got = eng.poll()
+    texts = [eng.window_error(i) for i in range(len(got))]
+    eng.close()
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+    for i in bad:
+        assert texts[i] == exp.errors[i] == "run Where error: divided by zero"

@@ -127,7 +127,6 @@ def test_inc_checkpoint_restore(oracle, engine_mod, sql):
 
 def test_inc_unsupported_shapes_rejected(engine_mod):
     for sql, kw in (("SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ss, 10, 2)", {}),
-                    ("SELECT count(*) FROM demo WHERE temperature > 1 GROUP BY TUMBLINGWINDOW(ss, 10)", {}),
                     ("SELECT sum(temperature) FROM demo GROUP BY TUMBLINGWINDOW(ss, 10)", {"nullable": ("temperature",)})):
         rule = compile_rule(sql, IOT_SCHEMA, incremental=True, **kw)
         with pytest.raises(engine_mod.EngineError, match="not built"):
