@@ -204,6 +204,7 @@ struct Engine {
     // ---- processing time (execProcessingWindow under the caller's clock, ek_advance_time)
     bool proc = false;                 // processing-time TUMBLING / HOPPING / SLIDING / SESSION
     bool proc_inc = false;             // processing-time incremental TUMBLING / HOPPING / SLIDING (proc_inc_triggers)
+    bool proc_v2s = false;             // processing-time v2 SLIDINGWINDOW (SlidingWindowOp; proc_inc_triggers replays it)
     bool inc_where = false;            // WHERE above an incremental window: filters the groups' last rows (k_inc_where)
     int inc_hidden = -1;               // its hidden result slot: the group's last row (MAX of the position column)
     int n_res = 0;                     // value arrays per result row (n_out + the hidden slot)
@@ -369,12 +370,9 @@ struct Engine {
         }
         plan.n_columns += plan.n_derived;
         if (plan.window_version == 2 && plan.window_type == EK_WINDOW_SLIDING) {
-            // WindowV2Operator sliding windows (window_v2_op.go:39-58): the event-time op without delay is built
-            if (!plan.is_event_time)
-                return fail(EK_ERR_UNSUPPORTED, "processing-time v2 sliding windows are wall-clock driven (use event time)");
-            if (plan.delay != 0)
-                return fail(EK_ERR_UNSUPPORTED, "delayed v2 sliding windows re-emit every fired window at each later watermark "
-                                                "until a pending one is newer (window_v2_event_op.go:60-76): not built");
+            // WindowV2Operator sliding windows (window_v2_op.go:39-58): SlidingWindowOp (processing time, under the caller's
+            // clock, delay included) and EventSlidingWindowOp (its delayed form re-emits every due delay at each later
+            // WatermarkTuple until a newer one is pending, window_v2_event_op.go:56-76: v2_delay_triggers)
         } else if (plan.window_version != 0 && plan.window_version != 1 && plan.window_type != EK_WINDOW_STATE) {
             return fail(EK_ERR_UNSUPPORTED, "window version %d (WindowV2Operator) is built for STATEWINDOW and SLIDINGWINDOW only",
                         plan.window_version);
@@ -434,8 +432,8 @@ struct Engine {
             // to the rule's start, rows delivered at their arrival timestamps
             if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING && wtype != EK_WINDOW_SLIDING && wtype != EK_WINDOW_SESSION)
                 return fail(EK_ERR_UNSUPPORTED, "unsupported processing-time window type %d", wtype);
-            if (plan.window_version == 2)
-                return fail(EK_ERR_UNSUPPORTED, "v2 processing-time windows are not built");
+            if (plan.window_version == 2 && wtype != EK_WINDOW_SLIDING)
+                return fail(EK_ERR_UNSUPPORTED, "v2 processing-time windows other than SLIDINGWINDOW are not built");
             if (!col_ok(plan.ts_column) || plan.column_type[plan.ts_column] != EK_COL_I64 || (plan.nullable_mask & (1u << plan.ts_column)))
                 return fail(EK_ERR_INVALID, "processing-time windows need the rows' arrival timestamps (a non-nullable i64 column)");
             proc = true;
@@ -458,6 +456,14 @@ struct Engine {
             const bool win = (wtype == EK_WINDOW_COUNT && plan.interval <= 0) || wtype == EK_WINDOW_SLIDING ||
                              wtype == EK_WINDOW_HOPPING || wtype == EK_WINDOW_TUMBLING;
             inc = plan.incremental != 0 && fns && win;
+        }
+        if (proc && plan.window_version == 2 && !inc) {
+            // WindowV2Operator SlidingWindowOp (window_v2_op.go:160-215): replayed on the host like the incremental ops;
+            // the window FILTER op in front of it, WHERE above it
+            proc_v2s = true;
+            proc_pushdown = plan.n_filter > 0;
+            slide_delay = 0;
+            send_twice = false;
         }
         if (inc && proc) {
             // TumblingWindowIncAggOp / HoppingWindowIncAggOp / SlidingWindowIncAggOp (window_inc_agg_op.go:316-790) under
@@ -948,6 +954,9 @@ struct Engine {
         sw2_gcx = 0;
         h_rtrig.clear();
         pi_reset();
+        v2q.clear();
+        v2q_head = v2q_seen = 0;
+        v2_lastW = INT64_MIN;
         g_wa = g_wt = nullptr;
         g_nwm = 0;
         g_sess_last_end = INT64_MIN;
@@ -2589,7 +2598,7 @@ struct Engine {
     int range_triggers(int64_t rel_prev) {
         std::vector<PendWin> pw;
         const int64_t n_new = eb_rel - rel_prev;
-        if (proc_inc) return proc_inc_triggers(rel_prev);
+        if (proc_inc || proc_v2s) return proc_inc_triggers(rel_prev);
         if (inc && wtype == EK_WINDOW_SLIDING) return inc_slide_triggers(rel_prev);
         if (inc && wtype == EK_WINDOW_COUNT) return inc_count_triggers(rel_prev);
         if (wtype == EK_WINDOW_SLIDING && gmode) {
@@ -2629,7 +2638,11 @@ struct Engine {
                     if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "trigger copy failed");
                     for (int64_t k = 0; k < nt; ++k) {
                         const int64_t i = pos[k], t = tts[k], r = trel[k];
-                        if (plan.window_version == 2) {
+                        if (plan.window_version == 2 && D > 0) {
+                            // EventSlidingWindowOp with a delay: the trigger queues ts + D (delayTS, emitted at the
+                            // WatermarkTuples, v2_delay_triggers below)
+                            v2q.push_back(V2Delay{t + D, r == INT64_MAX ? cur_arr_base + cur_nb : r});
+                        } else if (plan.window_version == 2) {
                             // EventSlidingWindowOp (window_v2_event_op.go:78-96): scanWindow over the rows added so far,
                             // left-open (t - L, t] (window_v2_op.go:252-263); WindowRange (t - L, t)
                             PendWin p{};
@@ -2658,7 +2671,9 @@ struct Engine {
                     }
                 }
             }
-            if (D > 0) {
+            if (D > 0 && plan.window_version == 2) {
+                if (int rc = v2_delay_triggers(rel_prev, pw)) return rc;
+            } else if (D > 0) {
                 while (delayq_head < delayq.size()) {
                     const DelayTrig& d = delayq[delayq_head];
                     if (!(W >= d.ts + D && W > d.w_rel)) break;
@@ -3101,6 +3116,14 @@ struct Engine {
                         PiHop& hw = pi_hop[pi_hop_head++];
                         const int64_t a = hw.first_abs < 0 ? upto : hw.first_abs;
                         emit(hw.start, due_h, a, upto);
+                    } else if (proc_v2s) {
+                        // scanWindow(t - length, t + D) over the scanner as the rows delivered since left it (each row's
+                        // gc(ts - length)): rows with ts > max(t - length, last delivered ts - length)
+                        pi_dq_head++;
+                        const int64_t t = due_s - D;
+                        const int64_t g = upto > h_rts_base ? ts_at(upto - 1) - L_ : INT64_MIN;
+                        const int64_t a = first_gt(upto, std::max(t - L_, g));
+                        emit(t - L_, due_s, a, upto);
                     } else {
                         pi_dq_head++;
                         const int64_t a = first_gt(upto, due_s - L_ - D);
@@ -3132,7 +3155,7 @@ struct Engine {
                 for (size_t k = pi_hop.size(); k > pi_hop_head && pi_hop[k - 1].first_abs < 0; --k) pi_hop[k - 1].first_abs = r;
             } else if (h_rtrig[r - h_rts_base]) {
                 if (D > 0) pi_dq.push_back(t);
-                else { const int64_t a = first_gt(r + 1, t - L_); emit(ts_at(a), t, a, r + 1); }
+                else { const int64_t a = first_gt(r + 1, t - L_); emit(proc_v2s ? t - L_ : ts_at(a), t, a, r + 1); }
             }
         }
         pi_next_abs = end_abs;
@@ -3154,6 +3177,58 @@ struct Engine {
         if (pi_hop_head > 1024 && pi_hop_head * 2 > pi_hop.size()) { pi_hop.erase(pi_hop.begin(), pi_hop.begin() + (int64_t)pi_hop_head); pi_hop_head = 0; }
         if (pi_dq_head > 4096 && pi_dq_head * 2 > pi_dq.size()) { pi_dq.erase(pi_dq.begin(), pi_dq.begin() + (int64_t)pi_dq_head); pi_dq_head = 0; }
         return rc;
+    }
+
+    // ---- EventSlidingWindowOp with a delay (window_v2_event_op.go:56-76,90-93): each trigger queues ts + D (v2q, in
+    // release order); at every WatermarkTuple W (each accepted arrival that raises the running max,
+    // watermark_op.go:170-213) the queued delays <= W emit scanWindow(delay - L - D, W) over the scanner — the rows
+    // released by then with ts > the previous WatermarkTuple's gc(W' - L - D) — with WindowRange [delay - L - D, W], and
+    // the queue drops that prefix only when a later delay is still pending (newIndex != -1; otherwise every due delay
+    // is emitted again at the next WatermarkTuple). The WatermarkTuples of this push are replayed on the host from the
+    // batch's running max; the scanner's content is the buffer range [first ts > bound, rows released by the tuple).
+    struct V2Delay { int64_t due, step; };
+    std::vector<V2Delay> v2q;
+    size_t v2q_head = 0, v2q_seen = 0;   // v2q[v2q_seen..) were triggered in this push and not yet queued
+    int64_t v2_lastW = INT64_MIN;        // the previous WatermarkTuple (its gc bound)
+    int v2_delay_triggers(int64_t rel_prev, std::vector<PendWin>& pw) {
+        const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit), tol = plan.late_tolerance_ms;
+        const int64_t n_new = eb_rel - rel_prev;
+        std::vector<int64_t> h_rm((size_t)std::max<int64_t>(cur_nb, 0)), h_rel((size_t)std::max<int64_t>(n_new, 0));
+        if (cur_nb > 0 && runmax_p) hipMemcpyAsync(h_rm.data(), runmax_p, (size_t)cur_nb * 8, hipMemcpyDeviceToHost, stream);
+        if (n_new > 0) hipMemcpyAsync(h_rel.data(), (const int64_t*)eb.rel.p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "watermark replay copy failed");
+        int64_t prevmax = cur_prevmax;
+        for (int64_t i = 0; i < cur_nb && runmax_p; ++i) {
+            const int64_t m = h_rm[(size_t)i];
+            if (prevmax != INT64_MIN && m <= prevmax) continue;
+            prevmax = m;
+            const int64_t Wj = m - tol, step = cur_arr_base + i;
+            while (v2q_seen < v2q.size() && v2q[v2q_seen].step <= step) v2q_seen++;   // released before this tuple
+            if (v2q_head < v2q_seen) {
+                const int64_t rel_end = rel_prev + (int64_t)(std::upper_bound(h_rel.begin(), h_rel.end(), step) - h_rel.begin());
+                size_t k = v2q_head;
+                for (; k < v2q_seen && v2q[k].due <= Wj; ++k) {
+                    const int64_t ws = v2q[k].due - L - D;
+                    const int64_t bound = v2_lastW == INT64_MIN ? ws : std::max(ws, v2_lastW - L - D);
+                    PendWin p{};
+                    p.q.kind = RB_UPTO;
+                    p.q.lo_ts = bound + 1;
+                    p.q.pos = rel_end - 1;
+                    p.q.floor = eb_floor;
+                    p.start = ws;
+                    p.end = Wj;
+                    pw.push_back(p);
+                }
+                if (k < v2q_seen) v2q_head = k;
+            }
+            v2_lastW = Wj;
+        }
+        if (v2q_head > 4096 && v2q_head * 2 > v2q.size()) {
+            v2q.erase(v2q.begin(), v2q.begin() + (int64_t)v2q_head);
+            v2q_seen -= v2q_head;
+            v2q_head = 0;
+        }
+        return 0;
     }
 
     // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
@@ -3294,7 +3369,7 @@ struct Engine {
         } else if (wtype == EK_WINDOW_SESSION) {
             ps_tick = aligned_end(t0, raw_interval, plan.time_unit, plan.tz_offset_s);
         }
-        if (proc_inc) pi_start(t0);
+        if (proc_inc || proc_v2s) pi_start(t0);
     }
 
     // ---- batch statistics: one pass over ts (k_stats), or the shared ek_ts_stats the pushed batch carries (ABI v10:
@@ -3473,7 +3548,7 @@ struct Engine {
             const int64_t rel_prev = eb_rel;
             eb_rel = eb.n;
             rc = range_triggers(rel_prev);
-            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc) rc = proc_slide_floor();
+            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc && !proc_v2s) rc = proc_slide_floor();
         } else if (db.n > 0) {
             const int64_t save = arrivals;
             arrivals = arrival_base;
@@ -3507,7 +3582,7 @@ struct Engine {
         int rc = 0;
         if (range_mode) {
             rc = range_triggers(eb_rel);
-            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc) rc = proc_slide_floor();
+            if (!rc && wtype == EK_WINDOW_SLIDING && !proc_inc && !proc_v2s) rc = proc_slide_floor();
         } else {
             rc = proc_close();
         }
@@ -5001,6 +5076,9 @@ struct Engine {
             s.put(pi_hop.data() + pi_hop_head, (pi_hop.size() - pi_hop_head) * sizeof(PiHop));
             s.i64((int64_t)(pi_dq.size() - pi_dq_head));
             s.put(pi_dq.data() + pi_dq_head, (pi_dq.size() - pi_dq_head) * 8);
+            s.i64(v2_lastW);                                                  // delayed v2 sliding: delayTS queue
+            s.i64((int64_t)(v2q.size() - v2q_head));
+            s.put(v2q.data() + v2q_head, (v2q.size() - v2q_head) * sizeof(V2Delay));
         }
         *size = (int64_t)s.b.size();
         if (!buf) return 0;
@@ -5144,6 +5222,13 @@ struct Engine {
             pi_dq.resize((size_t)nq);
             pi_dq_head = 0;
             r.read(pi_dq.data(), nq * 8);
+            v2_lastW = r.i64();
+            const int64_t nv = r.i64();
+            if (!r.ok || nv < 0 || nv > size) return fail(EK_ERR_INVALID, "bad v2 delay queue in state blob");
+            v2q.resize((size_t)nv);
+            v2q_head = 0;
+            v2q_seen = (size_t)nv;
+            r.read(v2q.data(), nv * (int64_t)sizeof(V2Delay));
             if (!r.ok) return fail(EK_ERR_INVALID, "state blob truncated");
         }
         return 0;

@@ -447,8 +447,12 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
             Part<NVC> part{};
 #ifdef EK_KM_CHECK
             if (d.dbg_mode == 1) { k = kend; continue; }
+            if (SORT && !WRITE) printf("KMF> g=%d k=%d kend=%d j0=%lld j1=%lld s=%lld e=%lld\n", (int)g, k, kend, (long long)j0, (long long)j1, (long long)s, (long long)e);
 #endif
             const bool agg_err = km_fold<NVC, SORT>(p, d, j0, j1, fl, isf, s_seg, part, sres, stag);
+#ifdef EK_KM_CHECK
+            if (SORT && !WRITE) printf("KMF< g=%d k=%d err=%d\n", (int)g, k, (int)agg_err);
+#endif
             const SortRes sr{sres, stag, 0, 1};
             if (agg_err) {   // "run Select error" replaces each of these windows' output
                 int ea = 0;   // the first order statistic that failed

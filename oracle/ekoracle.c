@@ -1220,6 +1220,7 @@ static void v2slide_on_row(winop* o, int64_t e) {
         if (!(r.tag == V_BOOL && r.i)) return;
     }
     const int64_t t = ev_ts(o, e), ws = t - o->L;
+    if (o->D > 0) { v_push(&o->delay_ts, t + o->D); return; }   /* delayTS (window_v2_event_op.go:90-93) */
     o->content.n = 0;
     for (int64_t i = 0; i < o->inputs.n; ++i) {
         const int64_t x = ev_ts(o, o->inputs.a[i]);
@@ -1227,6 +1228,34 @@ static void v2slide_on_row(winop* o, int64_t e) {
         else if (x > t) break;
     }
     emit_window(o->d, o->ob, ws, t, o->content.a, o->content.n);
+}
+
+/* EventSlidingWindowOp's WatermarkTuple branch (window_v2_event_op.go:56-76): every queued delay time at or before the
+ * watermark emits scanWindow(delay - length - D, watermark) — WindowRange ends at the WATERMARK — and the queue drops
+ * the emitted prefix only when a later entry is still pending (newIndex != -1): while every entry is due, all of them
+ * are emitted again at each later watermark. Then scanner.gc(watermark - length - D). */
+static void v2slide_on_watermark(winop* o, int64_t wm) {
+    int64_t keep_from = -1;
+    for (int64_t k = 0; k < o->delay_ts.n; ++k) {
+        const int64_t dts = o->delay_ts.a[k];
+        if (dts <= wm) {
+            const int64_t ws = dts - o->L - o->D;
+            o->content.n = 0;
+            for (int64_t i = 0; i < o->inputs.n; ++i) {
+                const int64_t x = ev_ts(o, o->inputs.a[i]);
+                if (x > ws && x <= wm) v_push(&o->content, o->inputs.a[i]);
+                else if (x > wm) break;
+            }
+            emit_window(o->d, o->ob, ws, wm, o->content.a, o->content.n);
+        } else {
+            keep_from = k;
+            break;
+        }
+    }
+    if (keep_from >= 0) v_erase_front(&o->delay_ts, keep_from);
+    int64_t g = 0;
+    while (g < o->inputs.n && ev_ts(o, o->inputs.a[g]) <= wm - o->L - o->D) g++;
+    v_erase_front(&o->inputs, g);
 }
 
 /* ------------------------------------------------------------------ driver */
@@ -1306,8 +1335,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         set_status(out, EK_ERR_UNSUPPORTED, "pushed-down WHERE below a processing-time state window is not restated"); return out->status;
     }
     const int v2slide = p->window_version == 2 && p->window_type == EK_WINDOW_SLIDING;
-    if (v2slide && (!p->is_event_time || p->delay != 0)) {
-        set_status(out, EK_ERR_UNSUPPORTED, "only the event-time v2 sliding window without delay is restated"); return out->status;
+    if (v2slide && !p->is_event_time) {
+        set_status(out, EK_ERR_UNSUPPORTED, "processing-time v2 sliding windows run under the clock (eko_run_proc)"); return out->status;
     }
     stateop so; memset(&so, 0, sizeof so);
     so.d = &d; so.ob = &ob;
@@ -1381,12 +1410,7 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                 if (p->window_type == EK_WINDOW_STATE) { /* WatermarkTuple: no effect on StateWindowOp */ }
                 else if (inc_slide) incslide_on_watermark(&isl, wm);
                 else if (inc_count) inccount_on_watermark(&icn, wm);
-                else if (v2slide) {
-                    /* scanner.gc(now - Length - Delay): rows a later window can no longer hold */
-                    int64_t g = 0;
-                    while (g < o.inputs.n && ts[o.inputs.a[g]] <= wm - o.L) g++;
-                    v_erase_front(&o.inputs, g);
-                }
+                else if (v2slide) v2slide_on_watermark(&o, wm);
                 else if (inc) inc_on_watermark(&io, wm); else win_on_watermark(&o, wm);
                 last_wm = wm;
             }
@@ -1592,6 +1616,50 @@ static int proc_inc_run(const ek_plan* p, const dataset* d, outbuf* ob, const in
     return 0;
 }
 
+/* WindowV2Operator SlidingWindowOp (window_v2_op.go:160-215) in processing time, under the same clock: a row at t
+ * (its arrival = tuple.Timestamp) first gcs the scanner (WindowScanner.gc(t - length): rows with ts <= t - length go),
+ * is added, and when it matches OVER (WHEN) (isMatchCondition) emits scanWindow(t - length, t) — the scanner's rows with
+ * t - length < ts <= t (window_v2_op.go:252-263) — or, with a delay D, arms a timer due at t + D that emits
+ * scanWindow(t - length, t + D) over the scanner as the later rows' gcs left it. WindowRange [start, end]. The window
+ * FILTER op sits in front (planner.go:388-392); WHERE stays above the window (emit_window). */
+static void proc_v2slide_run(const ek_plan* p, const dataset* d, outbuf* ob, const int64_t* ts, int64_t n, int64_t end_ms,
+                             int64_t* n_filter_err) {
+    const int64_t u = unit_ms(p->time_unit);
+    const int64_t L = (int64_t)p->length * u, D = (int64_t)p->delay * u;
+    vec64 tup; memset(&tup, 0, sizeof tup);   /* the scanner: delivered rows, [head, n) live */
+    int64_t head = 0;
+    vec64 dq; memset(&dq, 0, sizeof dq);      /* timers: the trigger ts, due at ts + D */
+    int64_t dq_head = 0;
+    vec64 c; memset(&c, 0, sizeof c);
+    for (int64_t i = 0; i <= n; ++i) {
+        const int64_t now = i < n ? ts[i] : end_ms;
+        while (dq_head < dq.n && dq.a[dq_head] + D <= now) {
+            const int64_t t = dq.a[dq_head++], we = t + D, wsb = t - L;
+            c.n = 0;
+            for (int64_t k = head; k < tup.n; ++k) {
+                const int64_t x = ts[tup.a[k]];
+                if (x > wsb && x <= we) v_push(&c, tup.a[k]);
+                else if (x > we) break;
+            }
+            emit_window(d, ob, wsb, we, c.a, c.n);
+        }
+        if (i == n) break;
+        if (!filter_pass(d, i, n_filter_err)) continue;
+        const int64_t t = ts[i];
+        while (head < tup.n && ts[tup.a[head]] <= t - L) head++;   /* gc(t - length) */
+        v_push(&tup, i);
+        int trig = 1;
+        if (p->n_trigger > 0) { const val_t r = eval_prog(p->trigger_prog, p->n_trigger, d, i, NULL); trig = r.tag == V_BOOL && r.i; }
+        if (!trig) continue;
+        if (D > 0) { v_push(&dq, t); continue; }
+        c.n = 0;
+        for (int64_t k = head; k < tup.n; ++k)
+            if (ts[tup.a[k]] > t - L && ts[tup.a[k]] <= t) v_push(&c, tup.a[k]);
+        emit_window(d, ob, t - L, t, c.a, c.n);
+    }
+    free(tup.a); free(dq.a); free(c.a);
+}
+
 int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
                          int64_t start_ms, int64_t end_ms, const eko_restart* rs, eko_output* out) {
     memset(out, 0, sizeof *out);
@@ -1602,10 +1670,11 @@ int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns
     }
     int inc_ok = p->incremental != 0 && p->n_aggs > 0 && wt != EK_WINDOW_SESSION;
     for (int a = 0; a < p->n_aggs; ++a) inc_ok &= inc_supported_fn(p->aggs[a].fn);
-    if (p->window_version == 2) { set_status(out, EK_ERR_UNSUPPORTED, "v2 windows are not restated in processing time"); return out->status; }
+    const int v2slide = p->window_version == 2 && wt == EK_WINDOW_SLIDING && !inc_ok;
+    if (p->window_version == 2 && !v2slide) { set_status(out, EK_ERR_UNSUPPORTED, "v2 windows are not restated in processing time"); return out->status; }
     if (p->ts_column < 0) { set_status(out, EK_ERR_INVALID, "processing-time rows need their arrival timestamp column"); return out->status; }
-    if (inc_ok) {
-        if (rs && rs->split >= 0) { set_status(out, EK_ERR_UNSUPPORTED, "restart of processing-time incremental windows is not restated"); return out->status; }
+    if (inc_ok || v2slide) {
+        if (rs && rs->split >= 0) { set_status(out, EK_ERR_UNSUPPORTED, "restart of processing-time incremental / v2 windows is not restated"); return out->status; }
         dataset d = { p, n, columns, validity, NULL };
         outbuf ob; memset(&ob, 0, sizeof ob);
         int64_t* ts = (int64_t*)malloc((size_t)(n ? n : 1) * 8);
@@ -1614,7 +1683,8 @@ int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns
             if ((i > 0 && ts[i] < ts[i - 1]) || ts[i] < start_ms) {
                 free(ts); set_status(out, EK_ERR_INVALID, "processing-time rows must arrive with non-decreasing timestamps after the start"); return out->status;
             }
-        proc_inc_run(p, &d, &ob, ts, n, start_ms, end_ms, &out->records_filter_error);
+        if (v2slide) proc_v2slide_run(p, &d, &ob, ts, n, end_ms, &out->records_filter_error);
+        else proc_inc_run(p, &d, &ob, ts, n, start_ms, end_ms, &out->records_filter_error);
         free(ts);
         finish_output(p, &ob, out);
         return 0;

@@ -174,11 +174,35 @@ def _v2_cols(case, t0=1541152480000):
 def test_window_v2_sliding_kat(oracle, case):
     """window_v2_event_op_test.go: the first emitted window holds exactly the reference's rows."""
     a, ts = _v2_cols(case)
-    rule = compile_rule(case["sql"].replace("eventStream", "demo"), {"a": "bigint", "ts": "bigint"}, window_version="v2")
+    rule = compile_rule(case["sql"].replace("eventStream", "demo"), {"a": "bigint", "ts": "bigint"}, window_version="v2",
+                        late_tolerance_ms=case.get("late_tolerance_ms", 0))
     run = oracle.run(rule.plan, [a, ts])
     assert len(run.windows) >= 1
     assert [int(a[i]) for i in run.members[0]] == [r["a"] for r in case["content"]]
     assert run.windows[0].value(0, 0) == len(case["content"])
+    if "window" in case:
+        t0 = 1541152480000
+        assert (run.windows[0].start - t0, run.windows[0].end - t0) == (case["window"]["start_dt_ms"], case["window"]["end_dt_ms"])
+
+
+def test_window_v2_delayed_reemission(oracle):
+    """EventSlidingWindowOp drops the emitted delay prefix only when a later delay is still pending
+    (window_v2_event_op.go:56-76: newIndex stays -1 when every queued delay is due), so a due delay is emitted again at
+    every later watermark, its WindowRange ending at that watermark, until a newer trigger is queued. Hand-derived:
+    SLIDINGWINDOW(ss, 1, 1) OVER (WHEN a = 1), lateTolerance 0, rows (ts s, a): (0, 1) (0.5, 0) (2.5, 0) (3, 0) (3.5, 1)
+    (4, 0) (6, 0): the trigger at 0 is due at 1 s; watermarks 2.5, 3 and 3.5 re-emit it (window (-1 s, wm] over the
+    scanner, which gc(wm - 2 s) has cut to ts > 0.5 s after watermark 2.5); the trigger at 3.5 (due 4.5) is queued at
+    3.5, so that watermark drops the first entry, watermark 4 emits nothing and watermark 6 emits the second over
+    (2.5 s, 6 s]."""
+    t0 = 1541152480000
+    rows = [(0, 1), (500, 0), (2500, 0), (3000, 0), (3500, 1), (4000, 0), (6000, 0)]
+    a = np.array([r[1] for r in rows], np.int64)
+    ts = np.array([t0 + r[0] for r in rows], np.int64)
+    rule = compile_rule("SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ss, 1, 1) OVER (WHEN a = 1)",
+                        {"a": "bigint", "ts": "bigint"}, window_version="v2")
+    run = oracle.run(rule.plan, [a, ts])
+    got = [((w.start - t0), (w.end - t0), sorted(int(i) for i in m)) for w, m in zip(run.windows, run.members)]
+    assert got == [(-1000, 2500, [0, 1, 2]), (-1000, 3000, [2, 3]), (-1000, 3500, [2, 3, 4]), (2500, 6000, [3, 4, 5, 6])]
 
 
 def test_window_v2_sliding_left_open_and_arrival_cut(oracle):
@@ -214,3 +238,20 @@ def test_inc_processing_window_kat(oracle, case):
         assert int(a[m[-1]]) == exp["last_a"]
         assert (w.start, w.end) == (exp["window_start"], exp["window_end"])
         assert w.value(0, 0) == exp["count"]
+
+
+@pytest.mark.parametrize("case", _load("kat_v2_proc.json")["tests"], ids=lambda c: c["name"])
+def test_v2_processing_sliding_kat(oracle, case):
+    """window_v2_op_test.go: WindowV2Operator SlidingWindowOp (OVER, delay) under the clock (eko_run_proc)."""
+    t0 = 1541152480000
+    a = np.array([r[1] for r in case["rows"]], np.int64)
+    ts = np.array([t0 + r[0] for r in case["rows"]], np.int64)
+    rule = compile_rule(case["sql"].replace("stream", "demo"), {"a": "bigint", "ts": "bigint"}, is_event_time=False,
+                        window_version="v2")
+    assert rule.plan.window_version == 2
+    run = oracle.run_proc(rule.plan, [a, ts], t0, t0 + case["end_ms"])
+    assert len(run.windows) >= 1
+    w, m, exp = run.windows[0], run.members[0], case["first_window"]
+    assert [int(a[i]) for i in m] == exp["content_a"]
+    assert (w.start - t0, w.end - t0) == (exp["window_start"], exp["window_end"])
+    assert w.value(0, 0) == len(exp["content_a"])

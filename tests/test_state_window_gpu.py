@@ -98,7 +98,7 @@ def test_window_v2_sliding_kat_engine(oracle, engine_mod, case):
     a = np.array([r["a"] for r in case["rows"]], np.int64)
     ts = np.array([1541152480000 + r["dt_ms"] for r in case["rows"]], np.int64)
     rule = compile_rule(case["sql"].replace("eventStream", "demo"), {"a": "bigint", "ts": "bigint"}, window_version="v2",
-                        debug_membership=True)
+                        debug_membership=True, late_tolerance_ms=case.get("late_tolerance_ms", 0))
     got, exp, _ = run_both(oracle, engine_mod, rule, [a, ts], batches=len(a))
     assert got[0].value(0, 0) == len(case["content"])
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
@@ -129,14 +129,68 @@ def test_window_v2_sliding_every_row_with_ties(oracle, engine_mod):
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
 
 
-def test_window_v2_rejections(engine_mod):
-    for kw in (dict(is_event_time=False), dict()):
-        sql = "SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ms, 20, 10)" if kw == {} else \
-              "SELECT count(*) FROM demo GROUP BY SLIDINGWINDOW(ms, 20)"
-        r = compile_rule(sql, TRIG_SCHEMA, window_version="v2", **kw)
-        with pytest.raises(engine_mod.EngineError) as e:
-            engine_mod.Engine(r.plan)
-        assert e.value.code == A.EK_ERR_UNSUPPORTED
+@pytest.mark.parametrize("batches", [1, 6])
+def test_window_v2_sliding_delayed_event(oracle, engine_mod, batches):
+    """EventSlidingWindowOp with a delay (window_v2_event_op.go:56-76): each due delay emits at every WatermarkTuple
+    (WindowRange ending at it) until a newer trigger is pending; the scanner is cut by gc(W - L - D) at each tuple.
+    Sparse triggers over a dense out-of-order stream exercise the re-emission; dense ones the prefix drop."""
+    for every, n in ((400, 6000), (25, 6000)):
+        sql = ("SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo "
+               "GROUP BY deviceId, SLIDINGWINDOW(ms, 200, 150) OVER (WHEN trig = 1)")
+        rule = compile_rule(sql, TRIG_SCHEMA, num_keys=20, late_tolerance_ms=40, debug_membership=True, window_version="v2")
+        cols = _with_trig(_iot(n, 20, seed=every, epm=2), every)
+        rng = np.random.default_rng(every)
+        cols[1] = (cols[1] + rng.integers(-30, 30, len(cols[1]))).astype(np.int64)
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(exp.windows) > 20
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+    small = [c[:400] for c in cols]
+    got, exp, _ = run_both(oracle, engine_mod, rule, small, batches=400)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+PROC_SCHEMA = {"k": "key", "ts": "bigint", "x": "float", "y": "float"}
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLD, "kat_v2_proc.json")))["tests"], ids=lambda c: c["name"])
+def test_window_v2_proc_kat_engine(oracle, engine_mod, case):
+    from test_processing_gpu import run_engine
+    t0 = 1541152480000
+    a = np.array([r[1] for r in case["rows"]], np.int64)
+    ts = np.array([t0 + r[0] for r in case["rows"]], np.int64)
+    rule = compile_rule(case["sql"].replace("stream", "demo"), {"a": "bigint", "ts": "bigint"}, is_event_time=False,
+                        window_version="v2", debug_membership=True)
+    exp = oracle.run_proc(rule.plan, [a, ts], t0, t0 + case["end_ms"])
+    for cuts in ([0, len(a)], list(range(len(a) + 1))):
+        got = run_engine(engine_mod, rule, [a, ts], t0, t0 + case["end_ms"], cuts)
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+        assert (got[0].start - t0, got[0].end - t0) == (case["first_window"]["window_start"], case["first_window"]["window_end"])
+
+
+V2_PROC = [
+    ("over", "SELECT k, count(*), avg(x) FROM s GROUP BY k, SLIDINGWINDOW(ms, 400) OVER (WHEN x > 97)"),
+    ("delay", "SELECT k, count(*), max(y), min(x) FROM s GROUP BY k, SLIDINGWINDOW(ms, 300, 500) OVER (WHEN x > 98)"),
+    ("every_row_where", "SELECT k, count(*), sum(y) FROM s WHERE y > 30 GROUP BY k, SLIDINGWINDOW(ms, 60)"),
+    ("delay_filter", "SELECT k, count(*) FROM s GROUP BY k, SLIDINGWINDOW(ms, 300, 200) FILTER (WHERE y < 70) OVER (WHEN x > 97)"),
+]
+
+
+@pytest.mark.parametrize("name,sql", V2_PROC, ids=[c[0] for c in V2_PROC])
+def test_window_v2_proc_parity(oracle, engine_mod, name, sql):
+    """SlidingWindowOp (window_v2_op.go:160-215) under the caller's clock: left-open windows over the scanner, a delayed
+    window over the rows the later rows' gc(ts - length) left."""
+    from test_processing_gpu import run_engine
+    rng = np.random.default_rng(sum(map(ord, name)))
+    n = 4000 if name == "every_row_where" else 20_000
+    ts = (1541152480000 + 999 + np.cumsum(rng.integers(0, 9, n))).astype(np.int64)
+    cols = [rng.integers(0, 17, n).astype(np.uint32), ts, rng.uniform(0, 100, n), rng.uniform(0, 100, n)]
+    rule = compile_rule(sql, PROC_SCHEMA, is_event_time=False, num_keys=17, debug_membership=True, window_version="v2")
+    start, end = int(ts[0]) - 300, int(ts[-1]) + 2000
+    exp = oracle.run_proc(rule.plan, cols, start, end)
+    assert len(exp.windows) > 10
+    for cuts in ([0, n], [0, 1, 999, n // 2, n - 1, n]):
+        got = run_engine(engine_mod, rule, cols, start, end, cuts)
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
 
 
 @pytest.mark.parametrize("batches", [1, 5])
