@@ -742,7 +742,7 @@ struct Engine {
         km_packed = env_int("EKGPU_KM_PACKED", 1);
         km_states = env_int("EKGPU_KM_STATES", 1);
         km_single = env_int("EKGPU_KM_SINGLE", 1);
-        km_merge_sort = env_int("EKGPU_KM_MERGE_SORT", 0);
+        km_merge_sort = env_int("EKGPU_KM_MERGE_SORT", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
@@ -2133,7 +2133,7 @@ struct Engine {
     // heavily (each event re-aggregated >= 4 times by the window-major path) or need order statistics over short
     // per-key runs; 1 = whenever eligible, 0 = never. Ineligible: no GROUP BY, non-monotone window ranges, WHERE
     // errors in the span (attributed per window by the window-major path), order statistics over a (key, window)
-    // run longer than kKmSelMax. The windows it aggregates are marked in `done`.
+    // run longer than kKmSegMax. The windows it aggregates are marked in `done`.
     int km_mode = 2;
     DevBuf km_k[2], km_p[2], km_tmp, km_start, km_val[kMaxVC], km_ok[kMaxVC], km_ab, km_bcnt, km_flag;
     unsigned int* h_kmf = nullptr;     // pinned: WHERE errors, longest key run, long order-statistic run, scratch
@@ -2159,7 +2159,7 @@ struct Engine {
     int count_direct = 1;   // EKGPU_COUNT_DIRECT=0: every COUNTWINDOW row goes through the event buffer
     int km_states = 1;   // EKGPU_KM_STATES=0: multi-window launches emit one record per (state, window) (k_km_unpack)
     int km_single = 1;   // EKGPU_KM_SINGLE=0: state emission keeps the count pass (states sorted as they are stored)
-    int km_merge_sort = 0;   // EKGPU_KM_MERGE_SORT=1: order-statistic launches walk by the E / X merge too
+    int km_merge_sort = 1;   // EKGPU_KM_MERGE_SORT=0: order-statistic launches walk by binary search over the window bounds
     DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount, km_ex;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
@@ -2328,7 +2328,7 @@ struct Engine {
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major sort failed");
         if (h_kmf[0] > 0) return 0;                                                       // WHERE errors
         if (km_mode == 2 && !sort && (double)h_kmf[1] * overlap > (double)(1 << 22)) return 0;   // one key dominates
-        if (one && sort && h_kmf[1] > (unsigned)kKmSelMax) return 0;   // single pass: no (key, window) run too long
+        if (one && sort && h_kmf[1] > (unsigned)kKmSegMax) return 0;   // single pass: no (key, window) run too long
         // value columns in key order
         KmCols cols{};
         for (int v = 0; v < dp.n_vc; ++v) {

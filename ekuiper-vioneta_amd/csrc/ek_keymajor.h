@@ -11,7 +11,7 @@
 // trigger order), which holds for every window type the engine fires in order.
 //
 // Per (key, window) the thread folds the sub-run (count, sum, min, max, centred two-pass M2; median /
-// percentile_* by rank counting over at most kKmSelMax values), finalises (funcs_agg.go), applies HAVING and
+// percentile_* over at most kKmSegMax values sorted in LDS), finalises (funcs_agg.go), applies HAVING and
 // emits. Result rows of window k land in its region [obase_k, obase_k + kept_k): a counting pass keeps a
 // per-(window, block) histogram in LDS, one workgroup per window scans it over the blocks, and the write pass
 // recomputes and stores at the block's offset + an LDS cursor (groups come in unspecified order, like the
@@ -23,8 +23,7 @@ namespace ek {
 
 constexpr int kKmBlock = 256;
 constexpr int kKmMaxWin = 4096;    // windows per launch: the per-block LDS histogram
-constexpr int kKmSelMax = 256;     // order statistics: longest (key, window) sub-run selected by one thread
-constexpr int kKmSegMax = 32;      // ... sorted in the thread's LDS lane (longer ones: rank counting in memory)
+constexpr int kKmSegMax = 32;      // order statistics: longest (key, window) sub-run, sorted in the thread's LDS lane
 
 struct KmDesc {
     int64_t n;                     // rows of the span (relative positions [0, n))
@@ -40,7 +39,7 @@ struct KmDesc {
     const uint8_t* sok[kMaxVC];    // their validity (nullptr: all valid)
     uint32_t* bcnt;                // [nw][nblk + 1] kept rows per (window, block) -> exclusive offsets after k_km_scan
                                    // (the window's total at [nblk])
-    int32_t* flags;                // [0] a (key, window) sub-run longer than kKmSelMax (order statistics), [1] scratch
+    int32_t* flags;                // [0] a (key, window) sub-run longer than kKmSegMax (order statistics), [1] scratch
     // packed emission (write pass of multi-window launches, n_aggs <= kKmRecAggs): rows go out as one 32-byte record
     // each, window k's at rec[rbase[k] + i] for its row obase[k] + i, and k_km_unpack transposes them to the result
     // columns with coalesced stores (the walk's threads emit into ~30 windows each: per-column scattered stores
@@ -195,24 +194,6 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
 }
 
 
-// rank-r value (ordered bits) among the valid values of sub-run [j0, j1) of column v: O(n^2) counting
-__device__ __forceinline__ uint64_t km_select(const int64_t* __restrict__ val, const uint8_t* __restrict__ ok, bool isf,
-                                              int64_t j0, int64_t j1, int64_t r) {
-    for (int64_t i = j0; i < j1; ++i) {
-        if (ok && !ok[i]) continue;
-        const uint64_t x = isf ? f64_to_ord(__longlong_as_double(val[i])) : i64_to_ord(val[i]);
-        int64_t less = 0, eq = 0;
-        for (int64_t j = j0; j < j1; ++j) {
-            if (ok && !ok[j]) continue;
-            const uint64_t y = isf ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
-            less += y < x;
-            eq += y == x;
-        }
-        if (less <= r && r < less + eq) return x;
-    }
-    return 0;
-}
-
 // HAVING (having_operator.go:41-56): 1 keeps the group, 0 drops it, -1 = a non-bool result (window error)
 template <int NVC>
 __device__ __forceinline__ int km_having(const DPlan& p, const Part<NVC>& s, const SortRes* sr) {
@@ -228,6 +209,16 @@ template <int NVC, bool SORT>
 __device__ __forceinline__ bool km_fold(const DPlan& p, const KmDesc& d, int64_t j0, int64_t j1, const int (&fl)[NVC],
                                         const bool (&isf)[NVC], uint64_t* s_seg, Part<NVC>& part,
                                         uint64_t (&sres)[kMaxSortAggs], uint8_t (&stag)[kMaxSortAggs]) {
+    // ---- order statistics: a sub-run of more than kKmSegMax values is not folded here at all (the launch falls back to
+    // the window-major radix select): its in-memory rank counting faulted on MI355X
+    if constexpr (SORT) {
+        for (int sc = 0; sc < p.n_scol; ++sc) {
+            const uint8_t* __restrict__ ok = d.sok[p.scol_vc[sc]];
+            int64_t n = j1 - j0;
+            if (ok && n > kKmSegMax) { n = 0; for (int64_t j = j0; j < j1; ++j) n += ok[j] ? 1 : 0; }
+            if (n > kKmSegMax) { d.flags[0] = 1; return true; }
+        }
+    }
     // ---- fold the sub-run [j0, j1): first pass (count, sums, min, max), centred second pass (M2)
 #ifdef EK_KM_CHECK
     if (!(j0 >= 0 && j0 < j1 && j1 <= d.n)) { km_bad(d.dbg, 20, j0, j1, d.n, 0); return true; }
@@ -271,42 +262,32 @@ __device__ __forceinline__ bool km_fold(const DPlan& p, const KmDesc& d, int64_t
 #pragma unroll
     for (int a = 0; a < kMaxSortAggs; ++a) { sres[a] = 0; stag[a] = EK_TAG_NULL; }
     if constexpr (SORT) {
-        // per sort column: the sub-run's valid values (ordered bits), insertion-sorted in this thread's LDS
-        // lane (interleaved, conflict-free) when at most kKmSegMax, else ranked by counting in memory
+        // per sort column: the sub-run's valid values (ordered bits, at most kKmSegMax: checked above), insertion-sorted
+        // in this thread's LDS lane (interleaved, conflict-free)
         for (int sc = 0; sc < p.n_scol; ++sc) {
             const int v = p.scol_vc[sc];
             const int64_t* __restrict__ val = d.sval[v];
             const uint8_t* __restrict__ ok = d.sok[v];
             const bool fv = p.vc_is_float[v] != 0;
-            int64_t n = 0;
-            for (int64_t j = j0; j < j1; ++j) n += (!ok || ok[j]) ? 1 : 0;
-            if (n > kKmSelMax) { d.flags[0] = 1; agg_err = true; continue; }
-            const bool inl = n <= kKmSegMax;
-            if (inl) {
-                int m = 0;
-                for (int64_t j = j0; j < j1; ++j) {
-                    if (ok && !ok[j]) continue;
-                    const uint64_t x = fv ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
-                    int q = m;
-                    while (q > 0 && s_seg[(q - 1) * kKmBlock + threadIdx.x] > x) {
-                        s_seg[q * kKmBlock + threadIdx.x] = s_seg[(q - 1) * kKmBlock + threadIdx.x];
-                        --q;
-                    }
-                    s_seg[q * kKmBlock + threadIdx.x] = x;
-                    ++m;
+            int m = 0;
+            for (int64_t j = j0; j < j1; ++j) {
+                if (ok && !ok[j]) continue;
+                const uint64_t x = fv ? f64_to_ord(__longlong_as_double(val[j])) : i64_to_ord(val[j]);
+                int q = m;
+                while (q > 0 && s_seg[(q - 1) * kKmBlock + threadIdx.x] > x) {
+                    s_seg[q * kKmBlock + threadIdx.x] = s_seg[(q - 1) * kKmBlock + threadIdx.x];
+                    --q;
                 }
+                s_seg[q * kKmBlock + threadIdx.x] = x;
+                ++m;
             }
+            const int64_t n = m;
 #pragma unroll
             for (int a = 0; a < kMaxSortAggs; ++a) {
                 if (a >= p.n_sagg || p.sagg_scol[a] != sc) continue;
                 const int ka = p.sagg_agg[a];
                 order_stat(p.agg_fn[ka], fv, p.agg_p[ka], n,
-                           [&](int64_t r) {
-#ifdef EK_KM_CHECK
-                               if (r < 0 || r >= n) { km_bad(d.dbg, 23, r, n, j0, j1); return (uint64_t)0; }
-#endif
-                               return inl ? s_seg[r * kKmBlock + threadIdx.x] : km_select(val, ok, fv, j0, j1, r);
-                           },
+                           [&](int64_t r) { return s_seg[(r < 0 ? 0 : r >= kKmSegMax ? kKmSegMax - 1 : r) * kKmBlock + threadIdx.x]; },
                            &sres[a], &stag[a]);
                 agg_err |= stag[a] == kTagErr;
             }
