@@ -107,6 +107,14 @@ struct Val {
     double f;
 };
 __device__ __forceinline__ Val mkb(bool b) { return Val{V_BOOL, b ? 1 : 0, 0.0}; }
+// column c of row i as an evaluator value (NULL when invalid; a BOOLEAN column is a bool)
+__device__ __forceinline__ Val col_val(const DPlan& p, const DBatch& b, int c, int64_t i) {
+    if (!col_valid(b, c, i)) return Val{V_NULL, 0, 0.0};
+    const int t = p.col_type[c];
+    if (t == EK_COL_F64) return Val{V_F64, 0, col_f64(b, c, i)};
+    const int64_t v = col_i64(p, b, c, i);
+    return t == EK_COL_BOOL ? mkb(v != 0) : Val{V_I64, v, 0.0};
+}
 
 // valuer.go:823-1000 SimpleDataEval over the plan ISA
 __device__ inline Val simple_eval(Val l, Val r, int op) {
@@ -187,12 +195,7 @@ __device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, con
         const int op = prog[k].op;
         const int arg = prog[k].arg;
         if (op == EK_OP_COL) {
-            Val v{V_NULL, 0, 0.0};
-            if (b && col_valid(*b, arg, row)) {
-                if (p.col_type[arg] == EK_COL_F64) v = Val{V_F64, 0, col_f64(*b, arg, row)};
-                else v = Val{V_I64, col_i64(p, *b, arg, row), 0.0};
-            }
-            st.push(v);
+            st.push(b ? col_val(p, *b, arg, row) : Val{V_NULL, 0, 0.0});
             sp++;
         } else if (op == EK_OP_AGG) {
             st.push(aggf(arg));
@@ -202,6 +205,9 @@ __device__ inline Val eval_prog(const ek_instr* prog, int n, const DPlan& p, con
             sp++;
         } else if (op == EK_OP_CONST_F64) {
             st.push(Val{V_F64, 0, prog[k].f64});
+            sp++;
+        } else if (op == EK_OP_CONST_BOOL) {
+            st.push(mkb(prog[k].i64 != 0));
             sp++;
         } else {
             const Val r = st.pop();

@@ -119,7 +119,7 @@ int prog_depth_ok(const ek_instr* prog, int n) {
     int sp = 0;
     for (int k = 0; k < n; ++k) {
         int op = prog[k].op;
-        if (op == EK_OP_COL || op == EK_OP_AGG || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) sp++;
+        if (op == EK_OP_COL || op == EK_OP_AGG || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64 || op == EK_OP_CONST_BOOL) sp++;
         else if (op >= EK_OP_EQ && op <= EK_OP_MOD) { if (sp < 2) return 0; sp--; }
         else return 0;
         if (sp > kEvalDepth) return 0;   // the device interpreter's register stack
@@ -132,13 +132,15 @@ int prog_depth_ok(const ek_instr* prog, int n) {
 // (comparisons, AND / OR). Division / modulo by a possible zero, bool-number mixes, AND / OR over numbers, a non-bool
 // root and order statistics (their "Input is outside of range") can; a plan whose conditions cannot fail records no
 // error witnesses.
-bool prog_can_fail(const ek_instr* prog, int n, const int32_t* agg_fn) {
+bool prog_can_fail(const ek_instr* prog, int n, const int32_t* agg_fn, const int32_t* col_type) {
     bool st[EK_MAX_PROG + 1];   // true: bool-typed
     int sp = 0;
     bool f = false;
     for (int k = 0; k < n; ++k) {
         const int op = prog[k].op;
-        if (op == EK_OP_COL || op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) { st[sp++] = false; continue; }
+        if (op == EK_OP_CONST_BOOL) { st[sp++] = true; continue; }
+        if (op == EK_OP_COL) { st[sp++] = col_type[prog[k].arg] == EK_COL_BOOL; continue; }
+        if (op == EK_OP_CONST_I64 || op == EK_OP_CONST_F64) { st[sp++] = false; continue; }
         if (op == EK_OP_AGG) {
             const int fn = agg_fn[prog[k].arg];
             f |= fn == EK_AGG_PERCENTILE_CONT || fn == EK_AGG_PERCENTILE_DISC;
@@ -318,7 +320,9 @@ struct Engine {
             !prog_depth_ok(plan.emit_prog, plan.n_emit))
             return fail(EK_ERR_INVALID, "malformed expression program");
         for (int c = 0; c < plan.n_columns; ++c)
-            if (plan.column_type[c] < EK_COL_I64 || plan.column_type[c] > EK_COL_U32) return fail(EK_ERR_INVALID, "bad column type %d", c);
+            if (plan.column_type[c] != EK_COL_I64 && plan.column_type[c] != EK_COL_F64 && plan.column_type[c] != EK_COL_U32 &&
+                plan.column_type[c] != EK_COL_BOOL)
+                return fail(EK_ERR_INVALID, "bad column type %d", c);
         auto col_ok = [&](int c) { return c >= 0 && c < plan.n_columns; };
         for (int k = 0; k < plan.n_where; ++k)
             if (plan.where_prog[k].op == EK_OP_COL && !col_ok(plan.where_prog[k].arg)) return fail(EK_ERR_INVALID, "WHERE column out of range");
@@ -354,8 +358,10 @@ struct Engine {
                 const int op = pr[k].op;
                 if (op == EK_OP_COL) {
                     if (!col_ok(pr[k].arg)) return fail(EK_ERR_INVALID, "derived column reference out of range");
+                    if (plan.column_type[pr[k].arg] == EK_COL_BOOL)
+                        return fail(EK_ERR_UNSUPPORTED, "derived columns are arithmetic over numeric columns");
                     nullable |= (plan.nullable_mask >> pr[k].arg) & 1u;
-                } else if (op == EK_OP_AGG || (op >= EK_OP_EQ && op <= EK_OP_OR)) {
+                } else if (op == EK_OP_AGG || op == EK_OP_CONST_BOOL || (op >= EK_OP_EQ && op <= EK_OP_OR)) {
                     return fail(EK_ERR_UNSUPPORTED, "derived columns are arithmetic over columns and constants");
                 } else if (op == EK_OP_DIV || op == EK_OP_MOD) {
                     const ek_instr& r = pr[k - 1];   // postfix: the divisor is the instruction before the operator
@@ -597,6 +603,7 @@ struct Engine {
                 // the group's first row = the minimum of the hidden position column (value = event-buffer index,
                 // buffer_view) over its rows; k_first_fetch reads the source column there
                 if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "first-row field column out of range");
+                if (plan.column_type[a.column] == EK_COL_BOOL) return fail(EK_ERR_UNSUPPORTED, "a BOOLEAN column is a count() argument only");
                 if (rowpos_col < 0) {
                     if (plan.n_columns >= EK_MAX_COLUMNS) return fail(EK_ERR_UNSUPPORTED, "too many columns for a first-row field");
                     rowpos_col = plan.n_columns;
@@ -618,6 +625,8 @@ struct Engine {
                 continue;
             }
             if (!col_ok(a.column)) return fail(EK_ERR_INVALID, "aggregate column out of range");
+            if (plan.column_type[a.column] == EK_COL_BOOL && a.fn != EK_AGG_COUNT)
+                return fail(EK_ERR_UNSUPPORTED, "a BOOLEAN column is a count() argument only");
             int v = -1;
             for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == a.column) v = x;
             if (v < 0) {
@@ -791,14 +800,14 @@ struct Engine {
             dp_incw = dp;
             if (hipMalloc((void**)&d_plan_incw, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
             if (hipMemcpy(d_plan_incw, &w, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
-            where_can_fail = prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
-            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+            where_can_fail = prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn, dp.col_type);
+            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn, dp.col_type);
             dp.n_where = 0;
             dp.n_having = 0;
             dp.having_star = 0;
         } else {
-            where_can_fail = dp.n_where > 0 && prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn);
-            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn);
+            where_can_fail = dp.n_where > 0 && prog_can_fail(dp.where_prog, dp.n_where, dp.agg_fn, dp.col_type);
+            having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn, dp.col_type);
         }
         for (int k = 0; k < dp.n_aggs; ++k)
             agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC;
@@ -2394,11 +2403,6 @@ struct Engine {
             }
             glds = (size_t)nw * 8;
         }
-#ifdef EK_KM_CHECK
-        fprintf(stderr, "KMH n=%lld nw=%d K=%u nvc=%d sort=%d one=%d vsort=%d glds=%zu lds=%zu km_ex=%p/%zu E=%p X=%p eb.n=%lld lo=%lld\n",
-                (long long)n, nw, K, nvc, (int)sort, (int)one, (int)vsort, glds, lds, km_ex.p, km_ex.bytes, (void*)cols.E,
-                (void*)cols.X, (long long)eb.n, (long long)lo);
-#endif
         if (!vsort) switch (nvc) {
         case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
@@ -2410,7 +2414,6 @@ struct Engine {
         if (hipError_t e = hipStreamSynchronize(stream); e != hipSuccess)
             return fail(EK_ERR_DEVICE, "key-major gather failed: %s", hipGetErrorName(e));
         if (int rc = km_check_report("gather")) return rc;
-        fprintf(stderr, "KMH gather ok\n");
 #endif
         auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
         if (one) {
@@ -4921,7 +4924,7 @@ struct Engine {
             i32(n);
             for (int k = 0; k < n; ++k) {
                 i32(p[k].op); i32(p[k].arg);
-                if (p[k].op == EK_OP_CONST_I64) i64(p[k].i64);
+                if (p[k].op == EK_OP_CONST_I64 || p[k].op == EK_OP_CONST_BOOL) i64(p[k].i64);
                 if (p[k].op == EK_OP_CONST_F64) mix(&p[k].f64, 8);
             }
         };

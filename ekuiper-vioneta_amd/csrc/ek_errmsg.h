@@ -183,6 +183,7 @@ inline HVal h_eval_prog(const ek_instr* prog, int n, COLF colf, AGGF aggf) {
         else if (op == EK_OP_AGG) st[sp++] = aggf(prog[k].arg);
         else if (op == EK_OP_CONST_I64) { HVal v; v.tag = HVal::I64; v.i = prog[k].i64; st[sp++] = v; }
         else if (op == EK_OP_CONST_F64) { HVal v; v.tag = HVal::F64; v.f = prog[k].f64; st[sp++] = v; }
+        else if (op == EK_OP_CONST_BOOL) st[sp++] = hv_bool(prog[k].i64 != 0);
         else {
             if (sp < 2) return hv_err("malformed program");
             HVal r = std::move(st[--sp]);

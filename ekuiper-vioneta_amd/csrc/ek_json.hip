@@ -1,8 +1,11 @@
 // ek_json.hip — columnar JSON ingest on the GPU (north-star item 1).
 //
-// Replaces, for flat JSON objects with numeric fields, the reference's per-message decode
+// Replaces, for flat JSON objects with numeric, string and boolean fields, the reference's per-message decode
 //   FastJsonConverter.Decode -> decodeWithSchema -> decodeObject   internal/converter/json/converter.go:92-171,246-410
 //   extractNumberValue (schema BIGINT -> Int64, FLOAT -> Float64)  converter.go:429-460
+//   extractStringValue / extractBooleanFromValue / getBooleanFromValue  converter.go:462-505,600-625
+// STRING fields leave as dense u32 dictionary ids (the engine's key column type; see the dictionary section below),
+// BOOLEAN fields as int64 0 / 1 that the engine evaluates as Go bools (EK_COL_BOOL).
 // A micro-batch of messages (concatenated payload bytes + offsets) is parsed by one thread per message
 // straight into the columns of an ek_batch in device memory (one pass, no per-message maps).
 //
@@ -12,6 +15,10 @@
 //   * BIGINT: the number must be an integer literal that fits int64 (fastfloat.ParseInt64), else error
 //   * FLOAT: the number as float64, correctly rounded (fastfloat.Parse / strconv.ParseFloat)
 //   * a string / bool / object / array value for a numeric schema field -> "has wrong type" error
+//   * STRING: a JSON string (unescaped as fastjson does); a bool / object / array -> "has wrong type"; a number ->
+//     cast.ToStringAlways(float64) on the host converter (EK_JSON_ERR_UNSUPPORTED here)
+//   * BOOLEAN: true / false; a number -> != 0 (cast.ToBool, pkg/cast/cast.go:809-837); a string -> strconv.ParseBool;
+//     an object / array -> "has wrong type"
 //   * any syntax error -> the message fails to decode; the message is dropped and its error reported
 //     (DecodeOp forwards the error, node/decode_op.go:146-193)
 // Numbers are converted exactly on the Clinger fast path (mantissa <= 2^53, |exp10| <= 22: one IEEE
@@ -21,11 +28,13 @@
 // 19 significant digits whose truncation straddles a rounding boundary.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ekgpu.h"
@@ -46,9 +55,24 @@ struct JSchema {
 struct JOut {
     void* col[EK_MAX_COLUMNS];
     uint8_t* valid[EK_MAX_COLUMNS];
+    int64_t* soff[EK_MAX_COLUMNS];   // string columns: the value's first content byte (offset into the payload)
+    int32_t* slen[EK_MAX_COLUMNS];   // ... its raw length, | EK_JSON_STR_ESCAPED when it holds a backslash escape
     uint8_t* err;
     unsigned int* nulls;   // [EK_MAX_COLUMNS]: decoded messages with column c nil (0 -> no validity array)
 };
+
+// strconv.ParseBool over raw string content (cast.ToBool(string, CONVERT_ALL), converter.go:600-625): 1 true, 0 false,
+// -1 not a bool literal
+__device__ int parse_bool_str(const uint8_t* s, int n) {
+    auto is = [&](const char* w) {
+        int k = 0;
+        for (; w[k]; ++k) if (k >= n || s[k] != (uint8_t)w[k]) return false;
+        return k == n;
+    };
+    if (is("1") || is("t") || is("T") || is("TRUE") || is("true") || is("True")) return 1;
+    if (is("0") || is("f") || is("F") || is("FALSE") || is("false") || is("False")) return 0;
+    return -1;
+}
 
 __device__ __forceinline__ bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
@@ -326,6 +350,8 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
     const uint8_t* p = bytes + off[i];
     const uint8_t* e = bytes + off[i + 1];
     int64_t ival[EK_MAX_COLUMNS];
+    int64_t soff[EK_MAX_COLUMNS];
+    int32_t slen[EK_MAX_COLUMNS];
     uint32_t seen = 0, isnull = 0;
     uint8_t err = EK_JSON_OK;
     while (p < e && is_ws(*p)) ++p;
@@ -372,6 +398,56 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
                 if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
                 seen |= 1u << col;
                 isnull |= 1u << col;
+            } else if (S.type[col] == EK_COL_STR || S.type[col] == EK_COL_BOOL) {
+                // string / boolean schema fields (converter.go:328-400 -> extractStringValue / extractBooleanFromValue /
+                // extractNumberValue, getBooleanFromValue :600-625)
+                const int t = S.type[col];
+                if (c0 == '"') {
+                    const uint8_t* cs = p + 1;
+                    uint64_t h = 0xCBF29CE484222325ull;
+                    bool sesc = false;
+                    ++p;
+                    while (p < e && *p != '"') {
+                        if (*p == '\\') {
+                            sesc = true;
+                            if (p + 1 >= e) { p = e; break; }
+                            h = fnv_step(h, *p);
+                            ++p;
+                        }
+                        h = fnv_step(h, *p);
+                        ++p;
+                    }
+                    if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
+                    const int n_raw = (int)(p - cs);
+                    ++p;
+                    if (t == EK_COL_STR) {
+                        ival[col] = (int64_t)h;   // FNV-1a 64 of the raw content (= of the string when nothing is escaped)
+                        soff[col] = (int64_t)(cs - bytes);
+                        slen[col] = n_raw | (sesc ? (int32_t)EK_JSON_STR_ESCAPED : 0);
+                    } else {
+                        const int b = sesc ? -1 : parse_bool_str(cs, n_raw);
+                        if (b < 0) { err = EK_JSON_ERR_TYPE; break; }   // strconv.ParseBool: invalid syntax
+                        ival[col] = b;
+                    }
+                } else if (c0 == 't' || c0 == 'f') {
+                    p = skip_value(p, e);
+                    if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
+                    if (t == EK_COL_STR) { err = EK_JSON_ERR_TYPE; break; }   // "has wrong type:true, expect:string"
+                    ival[col] = c0 == 't' ? 1 : 0;
+                } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+                    Num num;
+                    p = parse_number(p, e, &num);
+                    if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
+                    // a number for a string field is cast.ToStringAlways(f64) (%v of the float): left to the host converter
+                    if (t == EK_COL_STR) { err = EK_JSON_ERR_UNSUPPORTED; break; }
+                    if (!num.exact) { err = EK_JSON_ERR_NUMBER; break; }
+                    ival[col] = num.f64 != 0.0 ? 1 : 0;   // cast.ToBool(float64): != 0
+                } else {
+                    err = EK_JSON_ERR_TYPE;   // object / array
+                    break;
+                }
+                seen |= 1u << col;
+                isnull &= ~(1u << col);
             } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
                 Num num;
                 p = parse_number(p, e, &num);
@@ -411,6 +487,10 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
         const int64_t v = ok ? ival[c] : 0;
         if (S.type[c] == EK_COL_U32) ((uint32_t*)out.col[c])[i] = (uint32_t)v;
         else ((int64_t*)out.col[c])[i] = v;
+        if (S.type[c] == EK_COL_STR) {
+            out.soff[c][i] = ok ? soff[c] : 0;
+            out.slen[c][i] = ok ? slen[c] : 0;
+        }
     }
 }
 
@@ -474,6 +554,153 @@ __global__ void k_compact_col(const int64_t* __restrict__ pos, int64_t n, const 
     }
 }
 
+// ---------------------------------------------------------------- STRING columns: the per-column dictionary
+// Each STRING column of a decoded batch leaves the decoder as dense u32 ids (first-seen order over the decoder's life),
+// the engine's key column type. The device holds an open-addressing table FNV-1a 64 hash -> id (Fibonacci-hashed slot,
+// linear probing, load <= 1/2); a row whose hash is in the table takes its id there. The rest — strings never seen
+// and strings holding a backslash escape (their device hash covers the escaped form) — are the misses: the host
+// reads their bytes, unescapes them (valyala/fastjson v1.6.4 unescapeStringBestEffort, go.mod:82), enters new
+// strings in its dictionary and scatters the ids. In steady state (a bounded key set, e.g. deviceId) every row hits
+// and the resolution is one kernel plus a 8-byte readback.
+struct MissRec {
+    int64_t row, off;
+    int32_t len, pad;
+};
+__host__ __device__ __forceinline__ uint64_t str_key(uint64_t h) { return h ? h : 1; }   // 0 marks an empty slot
+__host__ __device__ __forceinline__ uint64_t str_slot(uint64_t h, int bits) { return (h * 0x9E3779B97F4A7C15ull) >> (64 - bits); }
+
+__global__ __launch_bounds__(256) void k_str_lookup(const int64_t* __restrict__ hash, const int64_t* __restrict__ soff,
+                                                    const int32_t* __restrict__ slen, const uint8_t* __restrict__ valid,
+                                                    int64_t n, const uint64_t* __restrict__ tkey,
+                                                    const uint32_t* __restrict__ tval, int bits, uint32_t* __restrict__ id,
+                                                    MissRec* __restrict__ miss, unsigned long long* __restrict__ n_miss) {
+    const uint64_t mask = bits ? (1ull << bits) - 1ull : 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+        if (valid[i]) {
+            const int32_t L = slen[i];
+            bool found = false;
+            if (!(L & EK_JSON_STR_ESCAPED) && bits) {
+                const uint64_t h = str_key((uint64_t)hash[i]);
+                for (uint64_t k = str_slot(h, bits);; k = (k + 1) & mask) {
+                    const uint64_t t = tkey[k];
+                    if (t == h) { v = tval[k]; found = true; break; }
+                    if (t == 0) break;
+                }
+            }
+            if (!found) {
+                const unsigned long long m = atomicAdd(n_miss, 1ull);
+                MissRec r;
+                r.row = i;
+                r.off = soff[i];
+                r.len = L;
+                r.pad = 0;
+                miss[m] = r;
+            }
+        }
+        id[i] = v;
+    }
+}
+// the misses' bytes (device payloads): record k's string -> dst[dpos[k], dpos[k] + len)
+__global__ void k_str_gather(const uint8_t* __restrict__ bytes, const MissRec* __restrict__ miss, const int64_t* __restrict__ dpos,
+                             int64_t nm, uint8_t* __restrict__ dst) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nm; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = miss[k].off, d = dpos[k];
+        const int32_t L = miss[k].len & ~(int32_t)EK_JSON_STR_ESCAPED;
+        for (int32_t j = 0; j < L; ++j) dst[d + j] = bytes[o + j];
+    }
+}
+__global__ void k_str_scatter(const int64_t* __restrict__ rows, const uint32_t* __restrict__ ids, int64_t nm, uint32_t* __restrict__ id) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nm; k += (int64_t)gridDim.x * blockDim.x) id[rows[k]] = ids[k];
+}
+
+// fastjson unescapeStringBestEffort (valyala/fastjson v1.6.4 parser.go): \" \\ \/ \b \f \n \r \t, \uXXXX (a surrogate
+// pair as one rune, an unpaired or invalid pair as U+FFFD via utf16.DecodeRune), anything else left as is
+void utf8_put(std::string& o, uint32_t r) {
+    if (r < 0x80) o += (char)r;
+    else if (r < 0x800) { o += (char)(0xC0 | (r >> 6)); o += (char)(0x80 | (r & 0x3F)); }
+    else if (r < 0x10000) { o += (char)(0xE0 | (r >> 12)); o += (char)(0x80 | ((r >> 6) & 0x3F)); o += (char)(0x80 | (r & 0x3F)); }
+    else {
+        o += (char)(0xF0 | (r >> 18)); o += (char)(0x80 | ((r >> 12) & 0x3F));
+        o += (char)(0x80 | ((r >> 6) & 0x3F)); o += (char)(0x80 | (r & 0x3F));
+    }
+}
+int hex4(const uint8_t* s) {
+    int v = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int c = s[k];
+        const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+        if (d < 0) return -1;
+        v = v * 16 + d;
+    }
+    return v;
+}
+std::string json_unescape(const uint8_t* s, int64_t n) {
+    std::string o;
+    o.reserve((size_t)n);
+    int64_t i = 0;
+    while (i < n) {
+        if (s[i] != '\\' || i + 1 >= n) { o += (char)s[i++]; continue; }
+        const uint8_t c = s[i + 1];
+        switch (c) {
+        case '"': o += '"'; i += 2; break;
+        case '\\': o += '\\'; i += 2; break;
+        case '/': o += '/'; i += 2; break;
+        case 'b': o += '\b'; i += 2; break;
+        case 'f': o += '\f'; i += 2; break;
+        case 'n': o += '\n'; i += 2; break;
+        case 'r': o += '\r'; i += 2; break;
+        case 't': o += '\t'; i += 2; break;
+        case 'u': {
+            const int x = i + 6 <= n ? hex4(s + i + 2) : -1;
+            if (x < 0) { o += "\\u"; i += 2; break; }
+            if (x < 0xD800 || x >= 0xE000) { utf8_put(o, (uint32_t)x); i += 6; break; }
+            const int y = (i + 12 <= n && s[i + 6] == '\\' && s[i + 7] == 'u') ? hex4(s + i + 8) : -1;
+            if (y < 0) { o += "\\u"; i += 2; break; }
+            uint32_t r = 0xFFFD;   // utf16.DecodeRune: a high then a low surrogate, else U+FFFD
+            if (x < 0xDC00 && y >= 0xDC00 && y < 0xE000) r = 0x10000 + (((uint32_t)x - 0xD800) << 10) + ((uint32_t)y - 0xDC00);
+            utf8_put(o, r);
+            i += 12;
+            break;
+        }
+        default: o += '\\'; o += (char)c; i += 2; break;   // unknown escape: kept
+        }
+    }
+    return o;
+}
+uint64_t fnv1a64(const std::string& s) {
+    uint64_t h = 0xCBF29CE484222325ull;
+    for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
+    return h;
+}
+
+struct StrDict {
+    std::unordered_map<std::string, uint32_t> ids;
+    std::unordered_map<uint64_t, uint32_t> by_key;   // str_key(hash) -> id (collision check)
+    std::vector<std::string> values;
+    std::vector<uint64_t> hkey;                      // host mirror of the device table
+    std::vector<uint32_t> hval;
+    int bits = 0;
+    bool dirty = false;
+    void put(uint64_t key, uint32_t id) {
+        const uint64_t mask = (1ull << bits) - 1ull;
+        for (uint64_t k = str_slot(key, bits);; k = (k + 1) & mask)
+            if (hkey[k] == 0) { hkey[k] = key; hval[k] = id; return; }
+    }
+    void insert(uint64_t key, uint32_t id) {
+        if (bits == 0 || (by_key.size() + 1) * 2 > ((size_t)1 << bits)) {   // grow: load <= 1/2
+            bits = std::max(bits + 1, 10);
+            while (((size_t)1 << bits) < (by_key.size() + 1) * 2) ++bits;
+            hkey.assign((size_t)1 << bits, 0);
+            hval.assign((size_t)1 << bits, 0);
+            for (const auto& kv : by_key) put(kv.first, kv.second);
+        }
+        put(key, id);
+        by_key.emplace(key, id);
+        dirty = true;
+    }
+};
+
 struct Buf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -487,6 +714,11 @@ struct JsonDecoder {
     std::string err;
     Buf in_bytes, in_off, raw_col[EK_MAX_COLUMNS], raw_valid[EK_MAX_COLUMNS], out_col[EK_MAX_COLUMNS],
         out_valid[EK_MAX_COLUMNS], msg_err, pos, cnt, nulls;
+    Buf raw_soff[EK_MAX_COLUMNS], raw_slen[EK_MAX_COLUMNS], out_soff[EK_MAX_COLUMNS], out_slen[EK_MAX_COLUMNS];
+    const int64_t* str_off[EK_MAX_COLUMNS] = {};   // the last decode's string references (ek_json_strings)
+    const int32_t* str_len[EK_MAX_COLUMNS] = {};
+    StrDict dict[EK_MAX_COLUMNS];
+    Buf id_col[EK_MAX_COLUMNS], tkey[EK_MAX_COLUMNS], tval[EK_MAX_COLUMNS], miss, n_miss, gat_pos, gat_bytes, fix_rows, fix_ids;
     std::vector<uint8_t> h_err;
     int64_t last_n = 0, last_ok = 0;
     ek_json_stats st{};
@@ -510,9 +742,12 @@ struct JsonDecoder {
     }
     ~JsonDecoder() {
         if (stream) hipStreamSynchronize(stream);
-        for (Buf* b : {&in_bytes, &in_off, &msg_err, &pos, &cnt, &nulls}) if (b->p) hipFree(b->p);
+        for (Buf* b : {&in_bytes, &in_off, &msg_err, &pos, &cnt, &nulls, &miss, &n_miss, &gat_pos, &gat_bytes, &fix_rows, &fix_ids})
+            if (b->p) hipFree(b->p);
         for (int c = 0; c < EK_MAX_COLUMNS; ++c)
-            for (Buf* b : {&raw_col[c], &raw_valid[c], &out_col[c], &out_valid[c]}) if (b->p) hipFree(b->p);
+            for (Buf* b : {&raw_col[c], &raw_valid[c], &out_col[c], &out_valid[c], &raw_soff[c], &raw_slen[c], &out_soff[c],
+                           &out_slen[c], &id_col[c], &tkey[c], &tval[c]})
+                if (b->p) hipFree(b->p);
         if (d_sch) hipFree(d_sch);
         if (stream) hipStreamDestroy(stream);
     }
@@ -522,7 +757,8 @@ struct JsonDecoder {
         sch.n = s->n_fields;
         for (int c = 0; c < sch.n; ++c) {
             const int t = s->column_type[c];
-            if (t != EK_COL_I64 && t != EK_COL_F64 && t != EK_COL_U32) return fail(EK_ERR_INVALID, "bad column type");
+            if (t != EK_COL_I64 && t != EK_COL_F64 && t != EK_COL_U32 && t != EK_COL_STR && t != EK_COL_BOOL)
+                return fail(EK_ERR_INVALID, "bad column type");
             sch.type[c] = t;
             const size_t L = strnlen(s->names[c], EK_JSON_MAX_NAME);
             if (L == 0 || L >= EK_JSON_MAX_NAME) return fail(EK_ERR_INVALID, "bad field name %d", c);
@@ -565,6 +801,14 @@ struct JsonDecoder {
             if (int rc = ensure(raw_valid[c], (size_t)n)) return rc;
             jo.col[c] = raw_col[c].p;
             jo.valid[c] = (uint8_t*)raw_valid[c].p;
+            str_off[c] = nullptr;
+            str_len[c] = nullptr;
+            if (sch.type[c] == EK_COL_STR) {
+                if (int rc = ensure(raw_soff[c], (size_t)n * 8)) return rc;
+                if (int rc = ensure(raw_slen[c], (size_t)n * 4)) return rc;
+                jo.soff[c] = (int64_t*)raw_soff[c].p;
+                jo.slen[c] = (int32_t*)raw_slen[c].p;
+            }
         }
         if (int rc = ensure(msg_err, (size_t)n)) return rc;
         if (int rc = ensure(nulls, EK_MAX_COLUMNS * 4)) return rc;
@@ -591,8 +835,10 @@ struct JsonDecoder {
             for (int c = 0; c < sch.n; ++c) {
                 out->columns[c] = raw_col[c].p;
                 out->validity[c] = h_nulls[c] ? (const uint8_t*)raw_valid[c].p : nullptr;   // no nil: no validity array
+                str_off[c] = (const int64_t*)raw_soff[c].p;
+                str_len[c] = (const int32_t*)raw_slen[c].p;
             }
-            return 0;
+            return resolve_all(n, false, d_bytes, memory == EK_MEM_HOST ? (const uint8_t*)bytes : nullptr, out);
         }
         // drop the messages that failed to decode (their errors are kept for ek_json_errors)
         if (int rc = ensure(pos, (size_t)n * 8)) return rc;
@@ -607,8 +853,113 @@ struct JsonDecoder {
             hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_valid[c].p, out_valid[c].p, 1);
             out->columns[c] = out_col[c].p;
             out->validity[c] = h_nulls[c] ? (const uint8_t*)out_valid[c].p : nullptr;
+            if (sch.type[c] == EK_COL_STR) {
+                if (int rc = ensure(out_soff[c], (size_t)std::max<int64_t>(ok, 1) * 8)) return rc;
+                if (int rc = ensure(out_slen[c], (size_t)std::max<int64_t>(ok, 1) * 4)) return rc;
+                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_soff[c].p, out_soff[c].p, 8);
+                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_slen[c].p, out_slen[c].p, 4);
+                str_off[c] = (const int64_t*)out_soff[c].p;
+                str_len[c] = (const int32_t*)out_slen[c].p;
+            }
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json compaction failed");
+        return resolve_all(ok, true, d_bytes, memory == EK_MEM_HOST ? (const uint8_t*)bytes : nullptr, out);
+    }
+
+    // STRING column c of the decoded batch (rows n, hashes / validity / string refs at the given device arrays) ->
+    // dense ids in id_col[c]. host_bytes: the payload on the host (EK_MEM_HOST) or null (d_bytes on the device only).
+    int resolve_strings(int c, int64_t n, const int64_t* hash, const uint8_t* valid, const int64_t* soff, const int32_t* slen,
+                        const uint8_t* d_bytes, const uint8_t* host_bytes, ek_batch* out) {
+        StrDict& D = dict[c];
+        if (int rc = ensure(id_col[c], (size_t)std::max<int64_t>(n, 1) * 4)) return rc;
+        if (int rc = ensure(miss, (size_t)std::max<int64_t>(n, 1) * sizeof(MissRec))) return rc;
+        if (int rc = ensure(n_miss, 8)) return rc;
+        if (D.dirty) {
+            if (int rc = ensure(tkey[c], D.hkey.size() * 8)) return rc;
+            if (int rc = ensure(tval[c], D.hval.size() * 4)) return rc;
+            hipMemcpyAsync(tkey[c].p, D.hkey.data(), D.hkey.size() * 8, hipMemcpyHostToDevice, stream);
+            hipMemcpyAsync(tval[c].p, D.hval.data(), D.hval.size() * 4, hipMemcpyHostToDevice, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string table upload failed");
+            D.dirty = false;
+        }
+        hipMemsetAsync(n_miss.p, 0, 8, stream);
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256));
+        hipLaunchKernelGGL(k_str_lookup, dim3(g), dim3(256), 0, stream, hash, soff, slen, valid, n,
+                           (const uint64_t*)tkey[c].p, (const uint32_t*)tval[c].p, D.bits, (uint32_t*)id_col[c].p,
+                           (MissRec*)miss.p, (unsigned long long*)n_miss.p);
+        unsigned long long nm = 0;
+        hipMemcpyAsync(&nm, n_miss.p, 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string lookup failed");
+        out->columns[c] = id_col[c].p;
+        if (nm == 0) return 0;
+        std::vector<MissRec> mr((size_t)nm);
+        hipMemcpyAsync(mr.data(), miss.p, (size_t)nm * sizeof(MissRec), hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string miss copy failed");
+        std::sort(mr.begin(), mr.end(), [](const MissRec& a, const MissRec& b) { return a.row < b.row; });   // first-seen order
+        std::vector<uint8_t> gathered;
+        std::vector<int64_t> gpos((size_t)nm);
+        const uint8_t* src = host_bytes;
+        if (!src) {   // device payloads: gather the misses' bytes into one buffer, one copy back
+            int64_t tot = 0;
+            for (size_t k = 0; k < mr.size(); ++k) { gpos[k] = tot; tot += mr[k].len & ~(int32_t)EK_JSON_STR_ESCAPED; }
+            if (int rc = ensure(gat_pos, mr.size() * 8)) return rc;
+            if (int rc = ensure(gat_bytes, (size_t)std::max<int64_t>(tot, 1))) return rc;
+            if (int rc = ensure(fix_rows, mr.size() * sizeof(MissRec))) return rc;
+            hipMemcpyAsync(gat_pos.p, gpos.data(), mr.size() * 8, hipMemcpyHostToDevice, stream);
+            hipMemcpyAsync(fix_rows.p, mr.data(), mr.size() * sizeof(MissRec), hipMemcpyHostToDevice, stream);
+            const unsigned gg = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (mr.size() + 255) / 256));
+            hipLaunchKernelGGL(k_str_gather, dim3(gg), dim3(256), 0, stream, d_bytes, (const MissRec*)fix_rows.p,
+                               (const int64_t*)gat_pos.p, (int64_t)mr.size(), (uint8_t*)gat_bytes.p);
+            gathered.resize((size_t)std::max<int64_t>(tot, 1));
+            hipMemcpyAsync(gathered.data(), gat_bytes.p, (size_t)tot, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string gather failed");
+        }
+        std::vector<int64_t> rows(mr.size());
+        std::vector<uint32_t> ids(mr.size());
+        std::string str;
+        for (size_t k = 0; k < mr.size(); ++k) {
+            const int32_t L = mr[k].len & ~(int32_t)EK_JSON_STR_ESCAPED;
+            const uint8_t* b = src ? src + mr[k].off : gathered.data() + gpos[k];
+            if (mr[k].len & EK_JSON_STR_ESCAPED) str = json_unescape(b, L);
+            else str.assign((const char*)b, (size_t)L);
+            auto it = D.ids.find(str);
+            uint32_t id;
+            if (it != D.ids.end()) {
+                id = it->second;
+            } else {
+                if (D.values.size() >= 0xFFFFFFFFull) return fail(EK_ERR_NOMEM, "string dictionary full (2^32 - 1 strings)");
+                id = (uint32_t)D.values.size();
+                const uint64_t key = str_key(fnv1a64(str));
+                auto hk = D.by_key.find(key);
+                if (hk != D.by_key.end())
+                    return fail(EK_ERR_UNSUPPORTED, "string hash collision: \"%s\" and \"%s\" share an FNV-1a 64 hash",
+                                str.c_str(), D.values[hk->second].c_str());
+                D.values.push_back(str);
+                D.ids.emplace(str, id);
+                D.insert(key, id);
+            }
+            rows[k] = mr[k].row;
+            ids[k] = id;
+        }
+        if (int rc = ensure(fix_rows, rows.size() * 8)) return rc;
+        if (int rc = ensure(fix_ids, ids.size() * 4)) return rc;
+        hipMemcpyAsync(fix_rows.p, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, stream);
+        hipMemcpyAsync(fix_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, stream);
+        const unsigned gs = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (rows.size() + 255) / 256));
+        hipLaunchKernelGGL(k_str_scatter, dim3(gs), dim3(256), 0, stream, (const int64_t*)fix_rows.p, (const uint32_t*)fix_ids.p,
+                           (int64_t)rows.size(), (uint32_t*)id_col[c].p);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string id scatter failed");
+        return 0;
+    }
+    int resolve_all(int64_t n, bool compacted, const uint8_t* d_bytes, const uint8_t* host_bytes, ek_batch* out) {
+        for (int c = 0; c < sch.n; ++c) {
+            if (sch.type[c] != EK_COL_STR) continue;
+            const Buf& col = compacted ? out_col[c] : raw_col[c];
+            const Buf& val = compacted ? out_valid[c] : raw_valid[c];
+            if (int rc = resolve_strings(c, n, (const int64_t*)col.p, (const uint8_t*)val.p, str_off[c], str_len[c], d_bytes,
+                                         host_bytes, out))
+                return rc;
+        }
         return 0;
     }
 
@@ -673,6 +1024,36 @@ int ek_json_errors(void* h, int64_t* msg_index, uint8_t* code, int64_t cap, int6
     if (!h || !n_errors) return EK_ERR_INVALID;
     JsonDeviceGuard dg(((JsonDecoder*)h)->dev);
     return ((JsonDecoder*)h)->errors(msg_index, code, cap, n_errors);
+}
+
+int ek_json_strings(void* h, int column, const int64_t** offsets, const int32_t** lengths) {
+    if (!h || !offsets || !lengths) return EK_ERR_INVALID;
+    JsonDecoder* d = (JsonDecoder*)h;
+    if (column < 0 || column >= d->sch.n || d->sch.type[column] != EK_COL_STR) {
+        d->err = "not a string column";
+        return EK_ERR_INVALID;
+    }
+    *offsets = d->str_off[column];
+    *lengths = d->str_len[column];
+    return 0;
+}
+
+int ek_json_dict_size(void* h, int column, int64_t* n) {
+    if (!h || !n) return EK_ERR_INVALID;
+    JsonDecoder* d = (JsonDecoder*)h;
+    if (column < 0 || column >= d->sch.n || d->sch.type[column] != EK_COL_STR) { d->err = "not a string column"; return EK_ERR_INVALID; }
+    *n = (int64_t)d->dict[column].values.size();
+    return 0;
+}
+
+int ek_json_dict_string(void* h, int column, uint32_t id, const char** s, int64_t* len) {
+    if (!h || !s || !len) return EK_ERR_INVALID;
+    JsonDecoder* d = (JsonDecoder*)h;
+    if (column < 0 || column >= d->sch.n || d->sch.type[column] != EK_COL_STR) { d->err = "not a string column"; return EK_ERR_INVALID; }
+    if (id >= d->dict[column].values.size()) { d->err = "string id out of range"; return EK_ERR_INVALID; }
+    *s = d->dict[column].values[id].data();
+    *len = (int64_t)d->dict[column].values[id].size();
+    return 0;
 }
 
 int ek_json_get_stats(void* h, ek_json_stats* out) {

@@ -427,9 +427,7 @@ __device__ inline void wit_where_row(WitRec* r, unsigned long long o1, unsigned 
         for (int k = 0; k < p.n_where; ++k) {
             if (p.where_prog[k].op != EK_OP_COL) continue;
             const int c = p.where_prog[k].arg;
-            Val v{V_NULL, 0, 0.0};
-            if (col_valid(b, c, row)) v = p.col_type[c] == EK_COL_F64 ? Val{V_F64, 0, col_f64(b, c, row)} : Val{V_I64, col_i64(p, b, c, row), 0.0};
-            wit_put(w, c, v);
+            wit_put(w, c, col_val(p, b, c, row));
         }
     });
 }

@@ -169,11 +169,6 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
     const int64_t m = kstart[p.num_keys];
 #ifdef EK_KM_CHECK
     if (m > out.n) { if (threadIdx.x == 0) km_bad(out.dbg, 1, m, out.n, p.num_keys, 0); return; }
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        printf("KMG m=%lld n=%lld nw=%d K=%u lo=%lld bn=%lld grid=%u E=%p X=%p ab=%p v0=%p v1=%p ok0=%p spos=%p kstart=%p nvc=%d\n",
-               (long long)m, (long long)out.n, out.nw, p.num_keys, (long long)lo, (long long)b.n, gridDim.x, (void*)out.E,
-               (void*)out.X, (const void*)out.ab, (void*)out.val[0], (void*)(NVC > 1 ? out.val[1 < NVC ? 1 : 0] : nullptr),
-               (void*)out.ok[0], (const void*)spos, (const void*)kstart, p.n_vc);
 #endif
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
         KM_CHECK(out.dbg, (int64_t)spos[i] < out.n, 2, i, spos[i], out.n, m)
@@ -334,9 +329,6 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     int32_t* s_b = s_a + nw;                        // SORT: [nw] window ends
     uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
-#ifdef EK_KM_CHECK
-    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) printf("KMW0 wave %d start\n", (int)(threadIdx.x >> 6));
-#endif
     __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
     if (!SORT && threadIdx.x == 0 && p.having_star) {
         Part<NVC> cp{};
@@ -365,11 +357,6 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
         const bool merge = !SORT || d.sE != nullptr;   // uniform
 #ifdef EK_KM_CHECK
         if (!(s <= e && e <= d.n)) { km_bad(d.dbg, 10, g, s, e, d.n); return; }
-        if (g == 0)
-            printf("KMW n=%lld nw=%d nblk=%d K=%u grid=%u lds? kstart=%p spos=%p sE=%p v0=%p v1=%p bcnt=%p flags=%p skend=%p rec=%p SORT=%d WRITE=%d ONE=%d\n",
-                   (long long)d.n, d.nw, d.nblk, d.nkeys, gridDim.x, (const void*)d.kstart, (const void*)d.spos,
-                   (const void*)d.sE, (const void*)d.sval[0], (const void*)d.sval[NVC > 1 ? 1 : 0], (void*)d.bcnt, (void*)d.flags,
-                   (void*)d.skend, (void*)d.rec, (int)SORT, (int)WRITE, (int)ONE);
 #endif
         int k = s < e ? (ONE ? 0 : !merge ? km_first_gt(s_b, 0, nw, (int64_t)d.spos[s]) : min((int)d.sE[s], (int)d.sX[s])) : nw;
         while (k < nw) {
@@ -428,12 +415,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
             Part<NVC> part{};
 #ifdef EK_KM_CHECK
             if (d.dbg_mode == 1) { k = kend; continue; }
-            if (SORT && !WRITE) printf("KMF> g=%d k=%d kend=%d j0=%lld j1=%lld s=%lld e=%lld\n", (int)g, k, kend, (long long)j0, (long long)j1, (long long)s, (long long)e);
 #endif
             const bool agg_err = km_fold<NVC, SORT>(p, d, j0, j1, fl, isf, s_seg, part, sres, stag);
-#ifdef EK_KM_CHECK
-            if (SORT && !WRITE) printf("KMF< g=%d k=%d err=%d\n", (int)g, k, (int)agg_err);
-#endif
             const SortRes sr{sres, stag, 0, 1};
             if (agg_err) {   // "run Select error" replaces each of these windows' output
                 int ea = 0;   // the first order statistic that failed

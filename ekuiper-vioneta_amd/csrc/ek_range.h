@@ -310,7 +310,7 @@ __global__ void k_filter_emit(DPlan* __restrict__ pp, DBatch b, const int64_t* _
             const bool ok = col_valid(b, c, i);
             const int t = p.col_type[c];
             res.val[c][o] = !ok ? 0 : (t == EK_COL_U32 ? (int64_t)((const uint32_t*)b.col[c])[i] : ((const int64_t*)b.col[c])[i]);
-            res.tag[c][o] = !ok ? EK_TAG_NULL : (t == EK_COL_F64 ? EK_TAG_F64 : EK_TAG_I64);
+            res.tag[c][o] = !ok ? EK_TAG_NULL : (t == EK_COL_F64 ? EK_TAG_F64 : t == EK_COL_BOOL ? EK_TAG_BOOL : EK_TAG_I64);
         }
         if (k == 0) res.win_cnt[widx] = ns;
     }

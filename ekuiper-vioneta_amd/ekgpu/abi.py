@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 11
+EKGPU_ABI_VERSION = 12
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -22,6 +22,7 @@ UNIT_BY_NAME = {"dd": EK_UNIT_DD, "hh": EK_UNIT_HH, "mi": EK_UNIT_MI, "ss": EK_U
 UNIT_MS = {EK_UNIT_DD: 86400000, EK_UNIT_HH: 3600000, EK_UNIT_MI: 60000, EK_UNIT_SS: 1000, EK_UNIT_MS: 1}
 
 EK_COL_I64, EK_COL_F64, EK_COL_U32 = 1, 2, 3
+EK_COL_STR, EK_COL_BOOL = 4, 5   # STR: ingest only (ek_json_decode); BOOL: int64 0 / 1 evaluated as a Go bool
 
 (EK_AGG_COUNT_STAR, EK_AGG_COUNT, EK_AGG_SUM, EK_AGG_AVG, EK_AGG_MIN, EK_AGG_MAX, EK_AGG_STDDEV,
  EK_AGG_STDDEVS, EK_AGG_VAR, EK_AGG_VARS, EK_AGG_MEDIAN, EK_AGG_PERCENTILE_CONT,
@@ -35,10 +36,10 @@ AGG_BY_NAME = {
 
 (EK_OP_COL, EK_OP_AGG, EK_OP_CONST_I64, EK_OP_CONST_F64, EK_OP_EQ, EK_OP_NEQ, EK_OP_LT, EK_OP_LTE,
  EK_OP_GT, EK_OP_GTE, EK_OP_AND, EK_OP_OR, EK_OP_ADD, EK_OP_SUB, EK_OP_MUL, EK_OP_DIV,
- EK_OP_MOD) = range(1, 18)
+ EK_OP_MOD, EK_OP_CONST_BOOL) = range(1, 19)
 
 EK_MEM_HOST, EK_MEM_DEVICE = 0, 1
-EK_TAG_NULL, EK_TAG_I64, EK_TAG_F64 = 0, 1, 2
+EK_TAG_NULL, EK_TAG_I64, EK_TAG_F64, EK_TAG_BOOL = 0, 1, 2, 3
 EK_WIN_OK, EK_WIN_WHERE_ERROR, EK_WIN_HAVING_ERROR, EK_WIN_AGG_ERROR = 0, 1, 2, 3
 EK_OK, EK_ERR_INVALID, EK_ERR_UNSUPPORTED, EK_ERR_DEVICE, EK_ERR_NOMEM, EK_ERR_STATE = 0, -1, -2, -3, -4, -5
 
@@ -192,6 +193,7 @@ def mix64(x: int) -> int:
 # columnar JSON ingest (ek_json_*)
 EK_JSON_MAX_NAME = 32
 EK_JSON_OK, EK_JSON_ERR_SYNTAX, EK_JSON_ERR_TYPE, EK_JSON_ERR_NUMBER, EK_JSON_ERR_UNSUPPORTED = range(5)
+EK_JSON_STR_ESCAPED = 0x40000000
 
 
 class ek_json_schema(C.Structure):

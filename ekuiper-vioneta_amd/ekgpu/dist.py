@@ -226,6 +226,8 @@ def _eval_having(prog, aggs):
             st.append(int(i64))
         elif op == A.EK_OP_CONST_F64:
             st.append(float(f64))
+        elif op == A.EK_OP_CONST_BOOL:
+            st.append(bool(i64))
         elif op == A.EK_OP_COL:
             return "ERR"
         else:
@@ -243,6 +245,10 @@ def _eval_having(prog, aggs):
                 continue
             if l is None or r is None:
                 st.append(False if op <= A.EK_OP_GTE else None)
+                continue
+            if isinstance(l, bool) or isinstance(r, bool):   # bools compare with bools by = / != only (valuer.go)
+                ok = isinstance(l, bool) and isinstance(r, bool) and op in (A.EK_OP_EQ, A.EK_OP_NEQ)
+                st.append(((l == r) if op == A.EK_OP_EQ else (l != r)) if ok else "ERR")
                 continue
             if isinstance(l, float) or isinstance(r, float):
                 l, r = float(l), float(r)

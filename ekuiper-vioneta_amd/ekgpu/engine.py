@@ -76,6 +76,12 @@ def lib():
         L.ek_json_get_stats.restype = C.c_int
         L.ek_json_last_error.argtypes = [C.c_void_p]
         L.ek_json_last_error.restype = C.c_char_p
+        L.ek_json_strings.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ek_json_strings.restype = C.c_int
+        L.ek_json_dict_size.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
+        L.ek_json_dict_size.restype = C.c_int
+        L.ek_json_dict_string.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.ek_json_dict_string.restype = C.c_int
         L.ek_json_destroy.argtypes = [C.c_void_p]
         L.ek_json_destroy.restype = C.c_int
         L.ek_export_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -93,9 +99,9 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
                     "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
-                    "ek_window_error", "ek_batch_ts_stats"]
+                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string"]
 
-_NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
+_NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32, A.EK_COL_BOOL: np.int64}
 
 
 class Engine:
@@ -329,14 +335,20 @@ class JsonDecoder:
         numeric expressions then reject) drops the message with EK_JSON_ERR_TYPE."""
         return cls({f: "float" for f in fields}, device)
 
+    TYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32, "string": A.EK_COL_STR,
+             "boolean": A.EK_COL_BOOL}
+
     def __init__(self, schema: dict, device: int = 0):
-        """schema: ordered {field: "bigint" | "float" | "key"} (same column order as the rule's schema)."""
-        from .rule import COLTYPES
+        """schema: ordered {field: "bigint" | "float" | "key" | "string" | "boolean"} (same column order as the rule's
+        schema). A "string" field reaches the engine as dense u32 ids of the decoder's dictionary (strings()); a
+        "boolean" field as int64 0 / 1 (the rule's "boolean" column)."""
         L = lib()
         s = A.ek_json_schema()
         s.n_fields = len(schema)
+        self.names = list(schema)
+        self.types = [self.TYPES[t] for t in schema.values()]
         for k, (name, t) in enumerate(schema.items()):
-            s.column_type[k] = COLTYPES[t]
+            s.column_type[k] = self.TYPES[t]
             s.names[k].value = name.encode()
         self.h = C.c_void_p()
         rc = L.ek_json_create(C.byref(s), device, C.byref(self.h))
@@ -377,6 +389,26 @@ class JsonDecoder:
         code = np.zeros(max(n.value, 1), np.uint8)
         lib().ek_json_errors(self.h, idx.ctypes.data, code.ctypes.data, n.value, C.byref(n))
         return idx[: n.value], code[: n.value]
+
+    def rule_schema(self) -> dict:
+        """The schema a rule over this decoder's batches compiles with: a "string" field arrives as dictionary ids,
+        i.e. a "key" column (GROUP BY it directly; strings() maps the ids back)."""
+        return {n: ("key" if t == A.EK_COL_STR else {v: k for k, v in self.TYPES.items()}[t])
+                for n, t in zip(self.names, self.types)}
+
+    def strings(self, column) -> list:
+        """The dictionary of a string column (index or field name): id -> str, in id order."""
+        c = self.names.index(column) if isinstance(column, str) else int(column)
+        n = C.c_int64()
+        rc = lib().ek_json_dict_size(self.h, c, C.byref(n))
+        if rc != 0:
+            raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
+        out = []
+        p, ln = C.c_void_p(), C.c_int64()
+        for i in range(n.value):
+            lib().ek_json_dict_string(self.h, c, i, C.byref(p), C.byref(ln))
+            out.append(C.string_at(p.value, ln.value).decode("utf-8", errors="surrogateescape") if ln.value else "")
+        return out
 
     def stats(self) -> A.ek_json_stats:
         s = A.ek_json_stats()

@@ -29,6 +29,8 @@ class WindowResult:
         if t == A.EK_TAG_NULL:
             return None
         v = self.values[a][r:r + 1]
+        if t == A.EK_TAG_BOOL:
+            return bool(v[0])
         return int(v[0]) if t == A.EK_TAG_I64 else float(v.view(np.float64)[0])
 
     def rows(self) -> Dict[int, tuple]:

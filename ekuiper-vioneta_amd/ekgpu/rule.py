@@ -42,7 +42,8 @@ _CMP = {"=": A.EK_OP_EQ, "!=": A.EK_OP_NEQ, "<>": A.EK_OP_NEQ, "<": A.EK_OP_LT, 
         ">": A.EK_OP_GT, ">=": A.EK_OP_GTE}
 _ADD = {"+": A.EK_OP_ADD, "-": A.EK_OP_SUB}
 _MUL = {"*": A.EK_OP_MUL, "/": A.EK_OP_DIV, "%": A.EK_OP_MOD}
-COLTYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32, "string": A.EK_COL_U32}
+COLTYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32, "string": A.EK_COL_U32,
+            "boolean": A.EK_COL_BOOL}
 GROUP_KEY = "__group_key"
 
 
@@ -205,6 +206,8 @@ class _Parser:
             op = ins[0]
             if op == A.EK_OP_COL:
                 t = self.schema[self.columns[ins[1]].lower()][1]
+                if t == "boolean":
+                    raise RuleError("aggregate arguments are arithmetic over numeric columns")
                 types.append("float" if t == "float" else "int")
             elif op == A.EK_OP_CONST_I64:
                 types.append("int")
@@ -290,8 +293,9 @@ class _Parser:
         if re.match(r"[\d.]", t):
             self.i += 1
             return [self._num(t)]
-        if t.lower() in ("true", "false"):
-            raise RuleError("boolean literals are not supported in the GPU plan")
+        if t.lower() in ("true", "false"):   # ast.BooleanLiteral
+            self.i += 1
+            return [(A.EK_OP_CONST_BOOL, 1 if t.lower() == "true" else 0)]
         self.i += 1
         if self.peek() == "(":
             if not aa or t.lower() not in A.AGG_BY_NAME:
@@ -311,7 +315,7 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
         raise RuleError("expression too long")
     depth = top = 0   # the device evaluates with an 8-value register stack (ek_device.h EvalStack)
     for ins in prog:
-        top += 1 if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG, A.EK_OP_CONST_I64, A.EK_OP_CONST_F64) else -1
+        top += 1 if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG, A.EK_OP_CONST_I64, A.EK_OP_CONST_F64, A.EK_OP_CONST_BOOL) else -1
         depth = max(depth, top)
     if depth > 8:
         raise RuleError("expression nests too deeply (more than 8 pending operands)")
@@ -319,7 +323,7 @@ def _fill_prog(dst, prog: List[Tuple]) -> int:
         dst[k].op = ins[0]
         if ins[0] in (A.EK_OP_COL, A.EK_OP_AGG):
             dst[k].arg = ins[1]
-        elif ins[0] == A.EK_OP_CONST_I64:
+        elif ins[0] in (A.EK_OP_CONST_I64, A.EK_OP_CONST_BOOL):
             dst[k].i64 = ins[1]
             dst[k].f64 = float(ins[1])
         elif ins[0] == A.EK_OP_CONST_F64:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 11
+#define EKGPU_ABI_VERSION 12
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -54,6 +54,11 @@ enum { EK_UNIT_DD = 1, EK_UNIT_HH = 2, EK_UNIT_MI = 3, EK_UNIT_SS = 4, EK_UNIT_M
 /* Column storage types. Stream schema BIGINT -> EK_COL_I64, FLOAT -> EK_COL_F64
  * (converter/json/converter.go:429-460); group ids are dictionary-encoded EK_COL_U32. */
 enum { EK_COL_I64 = 1, EK_COL_F64 = 2, EK_COL_U32 = 3 };
+/* BOOLEAN (converter.go:362-380 -> Go bool): stored as int64 0 / 1, evaluated as a bool (the literals true / false are
+ * EK_OP_CONST_BOOL); a WHERE / FILTER / window-condition operand, a count() argument and a SELECT * column.
+ * EK_COL_STR is an ingest type only (ek_json_decode): the string's FNV-1a 64 hash in an int64 column plus its byte range
+ * (ek_json_strings), resolved to a dense EK_COL_U32 id by the host dictionary before the engine sees it. */
+enum { EK_COL_STR = 4, EK_COL_BOOL = 5 };
 
 /* Aggregate functions (internal/binder/function/funcs_agg.go:28-370). */
 enum {
@@ -85,7 +90,8 @@ enum {
     EK_OP_CONST_F64 = 4, /* push f64                                                          */
     EK_OP_EQ = 5, EK_OP_NEQ = 6, EK_OP_LT = 7, EK_OP_LTE = 8, EK_OP_GT = 9, EK_OP_GTE = 10,
     EK_OP_AND = 11, EK_OP_OR = 12,
-    EK_OP_ADD = 13, EK_OP_SUB = 14, EK_OP_MUL = 15, EK_OP_DIV = 16, EK_OP_MOD = 17
+    EK_OP_ADD = 13, EK_OP_SUB = 14, EK_OP_MUL = 15, EK_OP_DIV = 16, EK_OP_MOD = 17,
+    EK_OP_CONST_BOOL = 18 /* push bool (i64 != 0): the literals true / false (ast.BooleanLiteral)     */
 };
 
 typedef struct {
@@ -210,7 +216,7 @@ typedef struct {
 } ek_batch;
 
 /* Per-row value tags of aggregate outputs (Go dynamic type of the reference's result). */
-enum { EK_TAG_NULL = 0, EK_TAG_I64 = 1, EK_TAG_F64 = 2 };
+enum { EK_TAG_NULL = 0, EK_TAG_I64 = 1, EK_TAG_F64 = 2, EK_TAG_BOOL = 3 /* value 0 / 1: a BOOLEAN column of SELECT * */ };
 
 /* Window status (window-level error replaces the window's output, node/operations.go:108-113). */
 enum { EK_WIN_OK = 0, EK_WIN_WHERE_ERROR = 1, EK_WIN_HAVING_ERROR = 2, EK_WIN_AGG_ERROR = 3 };
@@ -406,11 +412,14 @@ int ek_shard_triggers(void* h, const ek_batch* batch, const ek_global_ctx* g, in
 /* ---------------------------------------------------------------- columnar JSON ingest
  * Replaces the per-message FastJsonConverter.Decode of a schema-typed stream
  * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) for flat JSON objects
- * with numeric fields: a micro-batch of messages (payload bytes concatenated, message i =
+ * with numeric, string and boolean fields: a micro-batch of messages (payload bytes concatenated, message i =
  * bytes[offsets[i], offsets[i+1])) is decoded on the GPU straight into the columns of an ek_batch
  * (device memory owned by the decoder, valid until its next decode), ready for ek_push_batch.
  * Schema type BIGINT -> EK_COL_I64 (integer literal, fastfloat.ParseInt64), FLOAT -> EK_COL_F64
- * (correctly rounded), a dense key id column -> EK_COL_U32 (integer literal in [0, 2^32)). null or an
+ * (correctly rounded), a dense key id column -> EK_COL_U32 (integer literal in [0, 2^32)),
+ * STRING -> EK_COL_STR (a JSON string, delivered as its dense dictionary id, ek_json_dict_*; a number is EK_JSON_ERR_UNSUPPORTED — the Go converter's %v formatting —, a bool,
+ * object or array EK_JSON_ERR_TYPE), BOOLEAN -> EK_COL_BOOL (true / false; a number n as n != 0; a string
+ * by strconv.ParseBool, converter.go:600-625; anything else EK_JSON_ERR_TYPE). null or an
  * absent field -> validity 0; fields outside the schema are skipped. Messages that fail to decode are
  * dropped from the batch and reported by ek_json_errors. */
 #define EK_JSON_MAX_NAME 32
@@ -440,6 +449,17 @@ int ek_json_decode(void* h, const char* bytes, int64_t n_bytes, const int64_t* o
                    ek_batch* out);
 /* messages of the last decode that failed: their indices and EK_JSON_ERR_* codes (up to cap) */
 int ek_json_errors(void* h, int64_t* msg_index, uint8_t* code, int64_t cap, int64_t* n_errors);
+/* String column `column` of the last decode (EK_COL_STR): per decoded message, offsets[i] = the value's first content
+ * byte in the payload (after the opening quote) and lengths[i] = its raw byte length, with EK_JSON_STR_ESCAPED set
+ * when it holds a backslash escape (the hash then covers the escaped form: the host re-hashes the unescaped
+ * string). Device pointers, valid until the next decode; 0 for a null / absent value. */
+#define EK_JSON_STR_ESCAPED 0x40000000
+int ek_json_strings(void* h, int column, const int64_t** offsets, const int32_t** lengths);
+/* The decoder's dictionary of STRING column `column`: ek_json_decode hands the column to the engine as dense u32 ids
+ * (EK_COL_U32, first-seen order over the decoder's life; 0 for a null row) — the group key a GROUP BY deviceId needs.
+ * ek_json_dict_string yields id's bytes (not NUL-terminated; valid until the next decode). */
+int ek_json_dict_size(void* h, int column, int64_t* n);
+int ek_json_dict_string(void* h, int column, uint32_t id, const char** s, int64_t* len);
 int ek_json_get_stats(void* h, ek_json_stats* out);
 const char* ek_json_last_error(void* h);
 int ek_json_destroy(void* h);

@@ -126,6 +126,7 @@ static val_t col_val(const dataset* d, int c, int64_t row) {
     case EK_COL_I64: v.tag = V_I64; v.i = ((const int64_t*)d->cols[c])[row]; break;
     case EK_COL_U32: v.tag = V_I64; v.i = ((const uint32_t*)d->cols[c])[row]; break;
     case EK_COL_F64: v.tag = V_F64; v.f = ((const double*)d->cols[c])[row]; break;
+    case EK_COL_BOOL: v.tag = V_BOOL; v.i = ((const int64_t*)d->cols[c])[row] != 0; break;   /* Go bool */
     }
     return v;
 }
@@ -283,6 +284,7 @@ static val_t eval_prog(const ek_instr* prog, int n, const dataset* d, int64_t ro
         case EK_OP_AGG: st[sp++] = aggs ? aggs[in->arg] : mk_null(); break;
         case EK_OP_CONST_I64: { val_t v; v.tag = V_I64; v.i = in->i64; v.f = 0; st[sp++] = v; } break;
         case EK_OP_CONST_F64: { val_t v; v.tag = V_F64; v.i = 0; v.f = in->f64; st[sp++] = v; } break;
+        case EK_OP_CONST_BOOL: st[sp++] = mk_bool(in->i64 != 0); break;   /* ast.BooleanLiteral */
         default: {
             if (sp < 2) return mk_err_text("malformed program");
             val_t r = st[--sp], l = st[--sp], res;
@@ -1447,7 +1449,8 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
                     int64_t bits = v.i;
                     if (v.tag == V_F64) memcpy(&bits, &v.f, 8);
                     v_push(&ob.aval[c], v.tag == V_NULL ? 0 : bits);
-                    v_push(&ob.atag[c], v.tag == V_NULL ? EK_TAG_NULL : (v.tag == V_F64 ? EK_TAG_F64 : EK_TAG_I64));
+                    v_push(&ob.atag[c], v.tag == V_NULL ? EK_TAG_NULL
+                                        : v.tag == V_F64 ? EK_TAG_F64 : v.tag == V_BOOL ? EK_TAG_BOOL : EK_TAG_I64);
                 }
             }
             v_push(&ob.mcnt, n);

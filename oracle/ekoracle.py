@@ -86,7 +86,7 @@ class OracleRun:
 
 
 def _col_arrays(plan: A.ek_plan, columns: List[np.ndarray]):
-    dtypes = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32}
+    dtypes = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32, A.EK_COL_BOOL: np.int64}
     keep = []
     for k in range(plan.n_columns):
         keep.append(np.ascontiguousarray(columns[k], dtype=dtypes[plan.column_type[k]]))
