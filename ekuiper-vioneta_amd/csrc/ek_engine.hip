@@ -233,6 +233,8 @@ struct Engine {
     int64_t E1 = 0, first_ts = 0;
     int64_t next_win = 0;              // next window index to emit
     int64_t arrivals = 0;
+    bool time_pending = false;         // the last push's end event is recorded but not yet read (fold_time)
+    bool async_push = false;           // ek_set_async: pushes return with their work queued
     std::vector<int64_t> slot_pane;    // pane id held by each ring slot (INT64_MIN = free)
     PaneGrid grid{};
     ek_stats stats{};
@@ -714,6 +716,7 @@ struct Engine {
         kbits = 0;
         while ((1u << kbits) < K && kbits < want) kbits++;
         while (kbits > 0 && ((1 << kbits) * bytes_per_key) > 48 * 1024) kbits--;
+        if ((1 << kbits) > kMaxBucketKeys) kbits = 13;   // k_agg's present mask (kMaxBucketKeys)
         NB = (int)((K + (1u << kbits) - 1) >> kbits);
         Kpad = (int64_t)NB << kbits;
         // LDS layout (8-byte fields first for alignment)
@@ -756,6 +759,7 @@ struct Engine {
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
+        variant = env_int("EKGPU_VARIANT", 0);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
         group_events = (int64_t)env_int("EKGPU_GROUP_EVENTS", 1 << 30);
         // chunk-local partitions k_part can sort through LDS: 8 B each next to the 4096-row staging (~13 K)
@@ -972,7 +976,12 @@ struct Engine {
         g_trig.clear();
         wins.clear();
         r_rows_used = 0;
+        // counters restart with the stream; the running device-time totals (ek_stats *_total) span resets
+        const ek_stats keep = stats;
         stats = ek_stats{};
+        stats.device_ms_total = keep.device_ms_total;
+        stats.pushes_timed = keep.pushes_timed;
+        for (int k = 0; k < 4; ++k) { stats.phase_ms_total[k] = keep.phase_ms_total[k]; stats.phase_launches_total[k] = keep.phase_launches_total[k]; }
     }
 
     // ------------------------------------------------------------------ pane geometry
@@ -1389,6 +1398,7 @@ struct Engine {
         gd.has_accept = d_acc != nullptr;
         gd.sorted = pbnd_host != nullptr;
         gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
+        gd.pad2 = variant;
         gd.pwit = (WitRec*)pane_wit.p;   // pane witnesses in release order: (ts, this launch, row)
         gd.wit_ts = 1;
         gd.wit_o2 = (wit_seq++) << 36;
@@ -1756,6 +1766,7 @@ struct Engine {
     DevBuf sw_d;                        // small-window launch lists
     bool small_win_on = true;           // EKGPU_SMALL_WIN=0: every range window through k_part + k_agg
     int stats_blocks = 1024;            // k_stats grid (EKGPU_STATS_BLOCKS)
+    int variant = 0;                    // layout variants under measurement (EKGPU_VARIANT bits)
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
 
@@ -2585,6 +2596,7 @@ struct Engine {
         gd.np = npn * NB;
         gd.has_accept = 0;
         gd.pad = env_int("EKGPU_DEBUG_AGG", 0);   // diagnostic knobs (timing only; results invalid when set)
+        gd.pad2 = variant;
         if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
         if (int rc = ensure(vp_err, (size_t)npn * 4)) return rc;
         if (int rc = ensure(vp_mc, (size_t)npn * 8)) return rc;
@@ -3575,7 +3587,7 @@ struct Engine {
         if (!clock_started) { start_clock(now); return 0; }
         if (now < clock_ms) return fail(EK_ERR_INVALID, "the clock cannot move back (%lld < %lld)", (long long)now, (long long)clock_ms);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream failed");
-        phase_used = 0;
+        fold_time();
         hipEventRecord(ev0, stream);
         h_wdesc_used = 0;
         h_desc_used = 0;
@@ -4161,7 +4173,7 @@ struct Engine {
             if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
         }
         if (gmode) return fail(EK_ERR_STATE, "the handle takes its watermark from ek_push_batch_global (shard mode)");
-        phase_used = 0;
+        fold_time();
         hipEventRecord(ev0, stream);
         DBatch db{};
         if (int rc = stage_batch(b, db)) return rc;
@@ -4335,12 +4347,24 @@ struct Engine {
         return record_time();
     }
 
+    // Asynchronous pushes (ek_set_async) return once their work is queued: the end event is recorded here and read
+    // back (fold_time) by the next push or by ek_get_stats — so the caller's own work between pushes overlaps the
+    // device tail of the previous one instead of idling the GPU behind a host round trip.
     int record_time() {
         hipEventRecord(ev1, stream);
+        time_pending = true;
+        if (!async_push) fold_time();   // synchronous pushes (the default) complete before they return
+        return 0;
+    }
+    void fold_time() {
+        if (!time_pending) { phase_used = 0; return; }
+        time_pending = false;
         if (hipEventSynchronize(ev1) == hipSuccess) {
             float ms = 0;
             hipEventElapsedTime(&ms, ev0, ev1);
             stats.last_batch_device_ms = ms;
+            stats.device_ms_total += ms;
+            stats.pushes_timed++;
             for (int k = 0; k < 4; ++k) { stats.phase_ms[k] = 0; stats.phase_launches[k] = 0; }
             for (size_t k = 0; k < phase_used; ++k) {
                 float t = 0;
@@ -4349,9 +4373,12 @@ struct Engine {
                     stats.phase_launches[phase_ev[k].phase]++;
                 }
             }
+            for (int k = 0; k < 4; ++k) {
+                stats.phase_ms_total[k] += stats.phase_ms[k];
+                stats.phase_launches_total[k] += stats.phase_launches[k];
+            }
         }
         phase_used = 0;
-        return 0;
     }
 
 
@@ -4505,7 +4532,7 @@ struct Engine {
                 if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
             }
         }
-        phase_used = 0;
+        fold_time();
         hipEventRecord(ev0, stream);
         h_wdesc_used = 0;
         h_desc_used = 0;
@@ -4886,10 +4913,11 @@ struct Engine {
     }
 
     int reset() {
-        hipStreamSynchronize(stream);
+        // asynchronous mode: stream-ordered, the zeroing of the result counters queues behind the previous push
+        if (!async_push) hipStreamSynchronize(stream);
         release_results();
         reset_state();
-        return hipStreamSynchronize(stream) == hipSuccess ? 0 : fail(EK_ERR_DEVICE, "reset sync failed");
+        return async_push || hipStreamSynchronize(stream) == hipSuccess ? 0 : fail(EK_ERR_DEVICE, "reset sync failed");
     }
 
     // ------------------------------------------------------------------ checkpoint (ek_export_state / ek_import_state)
@@ -4899,8 +4927,8 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 5;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
-                                                  // 5: processing-time incremental windows
+    static constexpr int64_t kStateVersion = 6;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
+                                                  // 5: processing-time incremental windows; 6: ek_stats totals
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -5380,8 +5408,19 @@ int ek_set_stream(void* h, void* s) {
     return 0;
 }
 
+int ek_set_async(void* h, int32_t on) {
+    if (!h) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
+    Engine* e = (Engine*)h;
+    if (!on) { hipStreamSynchronize(e->stream); e->fold_time(); }
+    e->async_push = on != 0;
+    return 0;
+}
+
 int ek_get_stats(void* h, ek_stats* out) {
     if (!h || !out) return EK_ERR_INVALID;
+    DeviceGuard dg(h);
+    ((Engine*)h)->fold_time();
     *out = ((Engine*)h)->stats;
     return 0;
 }

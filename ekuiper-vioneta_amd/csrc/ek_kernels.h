@@ -471,12 +471,18 @@ struct GroupDesc {
     WitRec* pwit;
     int64_t wit_o2;
     int32_t wit_ts;
-    int32_t pad2;
+    int32_t pad2;          // layout variants (EKGPU_VARIANT; results stay valid)
 };
 
 constexpr int kMaxGroupPanes = 64;
-constexpr int kPartBlock = 512;              // k_part workgroup (8 wave64s)
-constexpr int kTile = 4096;                  // events staged and sorted in LDS per k_part tile
+#ifndef EK_PART_BLOCK
+#define EK_PART_BLOCK 512
+#endif
+#ifndef EK_PART_TILE
+#define EK_PART_TILE 4096
+#endif
+constexpr int kPartBlock = EK_PART_BLOCK;    // k_part workgroup (8 wave64s)
+constexpr int kTile = EK_PART_TILE;          // events staged and sorted in LDS per k_part tile
 constexpr int kTileE = kTile / kPartBlock;   // events per thread per tile
 constexpr int kMaxLocalParts = 2048;         // chunk-local partitions sorted through LDS
 
@@ -1010,6 +1016,10 @@ constexpr int kAggBlock = 512;
 // then either (a) direct emission of the final rows when the pane is a whole tumbling window that
 // closes in this batch (direct[2*rel] = out_base >= 0), or (b) write / merge into the pane state.
 constexpr int kMaxRuns = 1024;
+#ifndef EK_AGG_PIPE
+#define EK_AGG_PIPE 0
+#endif
+constexpr int kMaxBucketKeys = 8192;   // keys per bucket (1 << kbits) the direct emission's present mask covers
 
 // Runs of partition (rel, bucket): chunk c in [c_lo, c_hi] holds ctab[c][lp .. lp+1) of it.
 __device__ __forceinline__ void part_chunks(const GroupDesc& gd, int rel, int* c_lo, int* c_hi) {
@@ -1233,7 +1243,14 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                                                    int64_t scr_stride) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const DPlan& p = *pp;
-    const int pid = blockIdx.x;
+    // XCD-aware order: dispatch slot b runs on XCD b % 8, which takes a contiguous share of the partitions, so the
+    // neighbours (pane, bucket) and (pane, bucket + 1) — whose runs share a 128-B line at every chunk's run boundary —
+    // are in flight together on one XCD and read that line once from its L2 (FETCH 2.15 -> 1.87 GB on C2)
+    int pid = blockIdx.x;
+    {
+        const int xcd = pid % 8, q8 = (int)gridDim.x / 8, r8 = (int)gridDim.x % 8;
+        pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pid / 8;
+    }
     const int kk = 1 << gd.kbits;
     const int rel = pid / gd.nb, bucket = pid % gd.nb;
     const int64_t q = gd.q_lo + rel;
@@ -1299,7 +1316,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
     // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}.
     // Each wave takes a span of 64*U consecutive rows (coalesced loads); its first run is found by
     // one binary search, and every lane then advances its run pointer monotonically.
-    constexpr int U = EK_AGG_U;   // rows in flight per lane
+    constexpr int U = EK_AGG_U;   // rows in flight per lane (per pipeline stage with EK_AGG_PIPE)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto run_of = [&](uint32_t v) {
         int lo = 0, hi = nruns - 1;
@@ -1307,12 +1324,15 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         return lo;
     };
     int64_t dbg_sink = 0;
-    for (uint32_t span = (uint32_t)wave * 64u * U; span < total; span += (uint32_t)kAggBlock * U) {
-        int j = run_of(span);
-        int64_t pos[U];
+    struct Span {
         int klu[U];
         int64_t rv[NVC][U];
         uint8_t vd[NVC][U];
+    };
+    // the rows [span, span + 64 U) of this lane: key low bits (-1 past the end), values, validity
+    auto load_span = [&](uint32_t span, Span& sp) {
+        int j = run_of(span);
+        int64_t pos[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t v = span + u * 64 + lane;
@@ -1324,28 +1344,30 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            klu[u] = pos[u] >= 0 ? (int)st.klo[pos[u]] : -1;
+            sp.klu[u] = pos[u] >= 0 ? (int)st.klo[pos[u]] : -1;
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
-                rv[v][u] = (pos[u] >= 0 && fl[v]) ? st.val[v][pos[u]] : 0;
-                vd[v][u] = (pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
+                sp.rv[v][u] = (pos[u] >= 0 && fl[v]) ? st.val[v][pos[u]] : 0;
+                sp.vd[v][u] = (pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
             }
         }
+    };
+    auto fold_span = [&](const Span& sp) {
         if (gd.pad & 32) {   // diagnostic knob 32: loads only, no LDS atomics (timing only)
 #pragma unroll
-            for (int u = 0; u < U; ++u) { dbg_sink += klu[u]; for (int v = 0; v < NVC; ++v) dbg_sink += rv[v][u]; }
-            continue;
+            for (int u = 0; u < U; ++u) { dbg_sink += sp.klu[u]; for (int v = 0; v < NVC; ++v) dbg_sink += sp.rv[v][u]; }
+            return;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int kl = klu[u];
+            const int kl = sp.klu[u];
             if (kl < 0) break;
             atomicAdd(&lcnt[kl], 1u);
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
                 const int f = fl[v];
-                if (f == 0 || !vd[v][u]) continue;
-                const int64_t raw = rv[v][u];
+                if (f == 0 || !sp.vd[v][u]) continue;
+                const int64_t raw = sp.rv[v][u];
                 if (f & NEED_CNT) atomicAdd(&((uint32_t*)(lds + lay.off_vcnt[v]))[kl], 1u);
                 if (isf[v]) {
                     const double x = __longlong_as_double(raw);
@@ -1360,7 +1382,29 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                 }
             }
         }
+    };
+    constexpr uint32_t kSpanStep = (uint32_t)kAggBlock * U;
+#if EK_AGG_PIPE
+    // software pipeline: the next span's loads are in flight while this span's rows are folded into LDS
+    {
+        uint32_t span = (uint32_t)wave * 64u * U;
+        Span a, b;
+        if (span < total) load_span(span, a);
+        for (; span < total; span += 2 * kSpanStep) {
+            if (span + kSpanStep < total) load_span(span + kSpanStep, b);
+            fold_span(a);
+            if (span + kSpanStep >= total) break;
+            if (span + 2 * kSpanStep < total) load_span(span + 2 * kSpanStep, a);
+            fold_span(b);
+        }
     }
+#else
+    for (uint32_t span = (uint32_t)wave * 64u * U; span < total; span += kSpanStep) {
+        Span a;
+        load_span(span, a);
+        fold_span(a);
+    }
+#endif
     if ((gd.pad & 32) && dbg_sink == 0x5A5A5A5A5A5ALL) lcnt[0] = 1;   // keeps the knob-32 loads alive
     __syncthreads();
     bool need_m2 = false;
@@ -1501,11 +1545,14 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
             }
             return;
         }
+        // (1) decide every key of the bucket (aggregate errors, HAVING) into a present bitmask, (2) one result-row
+        // reservation for the workgroup, (3) each present key's row at its rank among the present keys (key order)
         const uint32_t K = p.key_col >= 0 ? p.num_keys : 1u;
+        __shared__ uint32_t pmask[kMaxBucketKeys / 32];     // present keys of the bucket
+        __shared__ uint32_t ppre[kMaxBucketKeys / 64 + 1];  // present keys before each 64-key chunk
         for (int kb = 0; kb < kk; kb += kAggBlock) {
             const int kl = kb + threadIdx.x;
             const int64_t key = (int64_t)bucket * kk + kl;
-            Part<NVC> s{};
             bool present = false;
             if (kl < kk && key < K) {
                 int64_t c, vc[NVC], is[NVC];
@@ -1513,6 +1560,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                 uint64_t mn[NVC], mx[NVC];
                 lds_part(kl, c, vc, is, fs, m2, mn, mx);
                 if (c > 0) {
+                    Part<NVC> s{};
                     part_merge(p, s, c, vc, is, fs, m2, mn, mx);
                     int ea = -1;   // the first order statistic that failed
                     if constexpr (SORT) {
@@ -1529,8 +1577,46 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                     }
                 }
             }
+            const unsigned long long m = __ballot(present);
+            const int ch = (kb >> 6) + wave;
+            if (lane == 0 && kb + wave * 64 < kk) { pmask[2 * ch] = (uint32_t)m; pmask[2 * ch + 1] = (uint32_t)(m >> 32); }
+        }
+        __syncthreads();
+        const int nchk = (kk + 63) >> 6;
+        if (wave == 0) {
+            uint32_t run = 0;
+            for (int c0 = 0; c0 < nchk; c0 += 64) {
+                const int c = c0 + lane;
+                const uint32_t n = c < nchk ? (uint32_t)(__popc(pmask[2 * c]) + __popc(pmask[2 * c + 1])) : 0u;
+                uint32_t x = n;
+                for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+                if (c < nchk) ppre[c] = run + x - n;
+                run += __shfl(x, 63, 64);
+            }
+            if (lane == 0) esh[16] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[widx], (unsigned long long)run) : 0u;
+        }
+        __syncthreads();
+        const int64_t rbase = dbase + (int64_t)esh[16];
+        for (int kl = threadIdx.x; kl < kk; kl += kAggBlock) {
+            const int c = kl >> 6;
+            const unsigned long long m = (unsigned long long)pmask[2 * c] | ((unsigned long long)pmask[2 * c + 1] << 32);
+            if (!((m >> (kl & 63)) & 1ull)) continue;
+            const int64_t pos = rbase + ppre[c] + __popcll(m & ((1ull << (kl & 63)) - 1ull));
+            int64_t cc, vc[NVC], is[NVC];
+            double fs[NVC], m2[NVC];
+            uint64_t mn[NVC], mx[NVC];
+            lds_part(kl, cc, vc, is, fs, m2, mn, mx);
+            Part<NVC> s{};
+            part_merge(p, s, cc, vc, is, fs, m2, mn, mx);
             const SortRes sr{(const uint64_t*)(lds + lay.off_sres), (const uint8_t*)(lds + lay.off_stag), kl, kk};
-            emit_rows(p, present, s, key, dbase, widx, res, esh, SORT ? &sr : nullptr);
+            res.key[pos] = (uint32_t)((int64_t)bucket * kk + kl);
+#pragma unroll
+            for (int k = 0; k < EK_MAX_AGGS; ++k) {
+                if (k >= p.n_aggs) break;
+                const Val a = agg_value(p, s, k, SORT ? &sr : nullptr);
+                res.tag[k][pos] = a.tag == V_NULL ? EK_TAG_NULL : (a.tag == V_I64 ? EK_TAG_I64 : EK_TAG_F64);
+                res.val[k][pos] = a.tag == V_F64 ? __double_as_longlong(a.f) : a.i;
+            }
         }
         return;
     }

@@ -150,6 +150,10 @@ class ek_stats(C.Structure):
         ("records_filter_error", C.c_int64),
         ("records_discarded", C.c_int64),
         ("windows_keymajor", C.c_int64),
+        ("device_ms_total", C.c_double),
+        ("phase_ms_total", C.c_double * 4),
+        ("phase_launches_total", C.c_int64 * 4),
+        ("pushes_timed", C.c_int64),
     ]
 
 

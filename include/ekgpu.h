@@ -259,6 +259,12 @@ typedef struct {
                                    * (handleInputs returns inputs[:0], window_op.go:605-655)          */
     int64_t windows_keymajor;     /* range windows aggregated key-major (sorted once by key, one thread
                                    * per key walks the windows)                        */
+    /* Running totals over every timed push (ek_push_batch returns once its work is queued; its device time is read
+     * back by the next push or by ek_get_stats, so per-push fields describe the last push read back). */
+    double device_ms_total;
+    double phase_ms_total[4];
+    int64_t phase_launches_total[4];
+    int64_t pushes_timed;
 } ek_stats;
 
 enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };
@@ -318,6 +324,11 @@ int ek_reset(void* h);
 int ek_sync(void* h);
 /* Use the caller's HIP stream (hipStream_t passed as void*; NULL = handle-owned stream). */
 int ek_set_stream(void* h, void* hip_stream);
+/* Asynchronous pushes (on != 0; default off): ek_push_batch / ek_advance_time return once their work is queued on
+ * the handle's stream, and ek_reset queues its zeroing behind it, so the caller's work between two pushes overlaps
+ * the device tail of the first. A device-memory batch stays borrowed until the next push, ek_sync, ek_poll_results
+ * or ek_get_stats returns; errors of queued work surface there. Turning it off waits for queued work. */
+int ek_set_async(void* h, int32_t on);
 int ek_get_stats(void* h, ek_stats* out);
 const char* ek_last_error(void* h);
 int ek_destroy(void* h);
