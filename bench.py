@@ -31,8 +31,11 @@ sys.path.insert(0, os.path.join(ROOT, "ekuiper-vioneta_amd"))
 
 HBM_PEAK_GBS = 8000.0                   # MI355X_MICROARCH.md: 8.0 TB/s spec
 PHASES = ("stats", "partition", "aggregate", "finalize")
-KERNEL_OF_PHASE = {"stats": "k_stats (+k_pane_bounds)", "partition": "k_part", "aggregate": "k_agg / k_small_win",
-                   "finalize": "k_finalize"}
+# the engine's phase clock (ek_stats.phase_ms, HIP events on the engine stream) per phase, and what runs in it
+KERNEL_OF_PHASE = {"stats": "ts pass (k_stats, incl. a shared ek_batch_ts_stats) + pane bounds",
+                   "partition": "partition (pane mode k_part | range mode key sort / MSD k_grp_hist+scatter)",
+                   "aggregate": "aggregate (k_agg | k_small_win | key-major / grouping walk)",
+                   "finalize": "finalize (k_finalize*)"}
 T0 = 1541152480000
 
 CONFIGS = {
@@ -686,7 +689,7 @@ def main():
     dominant = max(kernels.items(), key=lambda kv: kv[1]["launch_ms"] * kv[1]["launches_per_step"])[0] if kernels else None
     traffic, traffic_src = None, None
     sim = f"_sim{world}" if args.sim_world > 1 else ""
-    for rnd in ("r04", "r03"):
+    for rnd in ("r05", "r04", "r03"):
         pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.config}{sim}.json")
         if not os.path.exists(pmc):
             continue

@@ -1511,7 +1511,7 @@ struct Engine {
                 pbase = (const int64_t*)sort_pbase.p;
                 scr = (uint64_t*)sort_scr.p;
             }
-            ek::launch_agg(nvc, pbase != nullptr, ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
+            ek::launch_agg(nvc, pbase != nullptr, dp.n_having > 0, ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
                        scr_stride);
             phase_end(ph);
         }
@@ -4357,7 +4357,9 @@ struct Engine {
         return 0;
     }
     void fold_time() {
-        if (!time_pending) { phase_used = 0; return; }
+        // (not pending: phases recorded since the last fold — a shared ek_batch_ts_stats pass before this push — stay
+        // and are folded with the push they serve)
+        if (!time_pending) return;
         time_pending = false;
         if (hipEventSynchronize(ev1) == hipSuccess) {
             float ms = 0;

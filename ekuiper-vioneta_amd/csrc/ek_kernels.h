@@ -1157,7 +1157,7 @@ constexpr int kSmallSeg = 32;   // segments up to this length are selected by on
 constexpr int kSparseRows = kAggBlock;
 inline size_t sparse_lds_bytes(int nvc) { return (size_t)kSparseRows * (4 + 9 * (size_t)(nvc > 0 ? nvc : 1)); }
 
-template <int NVC>
+template <int NVC, bool HV>
 __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Staging& st, unsigned char* lds,
                                   const uint32_t* r_start, const uint32_t* r_pre, int nruns, uint32_t total, int bucket,
                                   int kk, int64_t slot, int rel, int64_t dbase, const int32_t* pane_err, Results& res) {
@@ -1228,14 +1228,15 @@ __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Sta
                 }
             }
             part_merge(p, s, c, vc, is, fs, m2, mn, mx);
-            present = having_keep(p, s, res, widx, (uint32_t)((int64_t)bucket * kk + kl));
+            present = !HV || having_keep(p, s, res, widx, (uint32_t)((int64_t)bucket * kk + kl));
         }
     }
     __shared__ uint32_t esh[20];
     emit_rows(p, present, s, (int64_t)bucket * kk + kl, dbase, widx, res, esh);
 }
 
-template <int NVC, bool SORT>
+// HV: the plan has a HAVING clause (without one, the emission carries no expression evaluator: fewer registers)
+template <int NVC, bool SORT, bool HV>
 __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AGG_WAVES_PER_EU))) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
                                                    Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err,
@@ -1300,7 +1301,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         return;
     }
     if (!SORT && dbase >= 0 && total <= (uint32_t)kSparseRows) {
-        agg_sparse<NVC>(p, gd, st, lds, r_start, r_pre, nruns, total, bucket, kk, slot, rel, dbase, pane_err, res);
+        agg_sparse<NVC, HV>(p, gd, st, lds, r_start, r_pre, nruns, total, bucket, kk, slot, rel, dbase, pane_err, res);
         return;
     }
 
@@ -1573,7 +1574,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
                     }
                     else {
                         const SortRes sr{(const uint64_t*)(lds + lay.off_sres), (const uint8_t*)(lds + lay.off_stag), kl, kk};
-                        present = having_keep(p, s, res, widx, (uint32_t)key, SORT ? &sr : nullptr);
+                        present = !HV || having_keep(p, s, res, widx, (uint32_t)key, SORT ? &sr : nullptr);
                     }
                 }
             }

@@ -1,4 +1,4 @@
-// ek_lib.h — host wrappers implemented in ek_lib.hip (library-backed, off the hot path).
+// ek_lib.h — host wrappers implemented in ek_lib.hip (hipCUB radix sorts; see that file for where they run).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

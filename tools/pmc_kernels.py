@@ -10,7 +10,7 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", "")
-        if pat not in name:
+        if pat not in name and not (pat == "ek::" and "__amd_rocclr_" in name):   # the engine's copies / fills too
             continue
         per[(name.split("(")[0].replace("void ", ""), r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (k, _, c), v in per.items():

@@ -2,7 +2,8 @@
 """Per-config rocprofv3 summaries -> profiles/<round>_* (round = $EKGPU_ROUND, default r03):
   <round>_kernels_<cfg>.csv  rocprofv3 --kernel-trace --stats of `bench.py --config <cfg> --steps S --warmup W`
   <round>_pmc_<cfg>.json     FETCH_SIZE / WRITE_SIZE passes (each its own run, --steps 1 --warmup 1): HBM bytes of the
-                         engine's kernels (ek::*) per step; FETCH_SIZE doubled (gfx950: it reports half the bytes of
+                         engine's kernels (ek::*) and of the runtime copy / fill kernels dispatched inside the pushes,
+                         per step; FETCH_SIZE doubled (gfx950: it reports half the bytes of
                          wide coalesced reads, MI355X_MICROARCH.md "HBM"), sizes KiB -> bytes.
 usage: profile_configs.py <cfg> <events_per_gpu> <steps_in_pmc_runs> <trace_dir> <pmc_fetch_dir> <pmc_write_dir>
 """
@@ -15,16 +16,28 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND = os.environ.get("EKGPU_ROUND", "r03")
+ROUND = os.environ.get("EKGPU_ROUND", "r05")
+
+
+COPY_KERNELS = ("__amd_rocclr_copyBuffer", "__amd_rocclr_fillBuffer")
 
 
 def counters(d):
+    """Per-kernel sums of every counter over the engine's dispatches: the ek:: kernels, and the runtime's copy / fill
+    kernels (hipMemcpyAsync / hipMemsetAsync, e.g. the event-buffer append) dispatched between the first and the last
+    ek:: kernel of the process — the step's own copies; the synthetic-input setup before the first push is excluded."""
     per = defaultdict(lambda: defaultdict(float))
     n = defaultdict(lambda: defaultdict(int))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        ek_ids = [int(r["Dispatch_Id"]) for r in rows if "ek::" in r.get("Kernel_Name", "")]
+        if not ek_ids:
+            continue
+        lo, hi = min(ek_ids), max(ek_ids)
+        for r in rows:
             name = r.get("Kernel_Name", "")
-            if "ek::" not in name:
+            did = int(r["Dispatch_Id"])
+            if "ek::" not in name and not (any(c in name for c in COPY_KERNELS) and lo <= did <= hi):
                 continue
             k = name.split("(")[0].replace("void ", "")
             per[k][r["Counter_Name"]] += float(r["Counter_Value"])
