@@ -755,6 +755,7 @@ struct Engine {
         km_states = env_int("EKGPU_KM_STATES", 1);
         km_single = env_int("EKGPU_KM_SINGLE", 1);
         km_merge_sort = env_int("EKGPU_KM_MERGE_SORT", 1);
+        km_msd_on = env_int("EKGPU_KM_MSD", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
@@ -2223,7 +2224,7 @@ struct Engine {
         hipMemcpyAsync(d_t1, grp_ht.data(), (size_t)nt1 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
         hipMemsetAsync(grp_cnt.p, 0, (size_t)(2 * n1 + 2 * nsub) * 4, stream);
         const int ph = phase_begin(EK_PHASE_PARTITION);
-        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, K,
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, 255u, K,
                            kRep1, tot1);
         grp_h.resize(n1);
         hipMemcpyAsync(grp_h.data(), tot1, (size_t)n1 * 4, hipMemcpyDeviceToHost, stream);
@@ -2240,11 +2241,12 @@ struct Engine {
         const int64_t nt2 = (int64_t)grp_ht.size();
         hipMemcpyAsync(base1, grp_hb.data(), (size_t)n1 * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0) hipMemcpyAsync(d_t2, grp_ht.data(), (size_t)nt2 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt1), dim3(kGrpScatBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1, K,
-                           kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p);
+        hipLaunchKernelGGL(k_grp_scatter<false>, dim3((unsigned)nt1), dim3(kGrpScatBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1,
+                           255u, K, kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p, (const uint32_t*)nullptr,
+                           (uint32_t*)nullptr);
         if (nt2 > 0)
             hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const GrpTile*)d_t2, s2, K, 1, tot2);
+                               (const GrpTile*)d_t2, s2, 255u, K, 1, tot2);
         grp_h.resize((size_t)nsub);
         hipMemcpyAsync(grp_h.data(), tot2, (size_t)nsub * 4, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping pass 1 failed");
@@ -2255,9 +2257,9 @@ struct Engine {
         if (mx > (unsigned int)kGrpCap) { phase_end(ph); return 0; }
         hipMemcpyAsync(base2, grp_hb.data() + n1, (size_t)(nsub + 1) * 8, hipMemcpyHostToDevice, stream);
         if (nt2 > 0)
-            hipLaunchKernelGGL(k_grp_scatter, dim3((unsigned)nt2), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, K, 1, (const int64_t*)base2, cur2,
-                               (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p);
+            hipLaunchKernelGGL(k_grp_scatter<false>, dim3((unsigned)nt2), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[0].p,
+                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, 255u, K, 1, (const int64_t*)base2, cur2,
+                               (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p, (const uint32_t*)nullptr, (uint32_t*)nullptr);
         phase_end(ph);
         GrpDesc g{};
         g.base2 = base2;
@@ -2280,6 +2282,83 @@ struct Engine {
         *ok = true;
         return 0;
     }
+    // Key-major span sort by MSD partition (replaces the radix sort of (key, position) pairs and the value gather by
+    // position): two k_grp_scatter<true> passes on 8-bit digits of the dense key carry (key, value, position) into
+    // sub-buckets of 2^s2 keys, k_kmsd_fix sorts each sub-bucket by (key, position) in LDS and writes kstart and the
+    // longest key run. Input: km_k[0] (k_km_keys: dropped rows carry key K). Output, sorted by (key, position):
+    // keys km_k[0], positions km_p[1], values km_val[0]. *ok = false: a sub-bucket exceeds kGrpCap rows (skewed keys;
+    // the caller takes the radix sort — its inputs must be rebuilt, km_k[0] is overwritten).
+    int km_msd(const int64_t* val0, int64_t n, unsigned int* d_flag) {
+        int kb = 17;
+        while ((1ull << kb) < (uint64_t)K) kb++;
+        // sub-buckets of 2^s2 keys holding ~1 000 rows (<= kKmFixCap with room for the spread): one k_kmsd_fix thread per
+        // key (up to 256), one workgroup per sub-bucket; the second pass's digit is the s1 - s2 (<= 8) bits between
+        const int s1 = kb - 8;
+        int s2 = 8;
+        while (s2 > 1 && ((double)n / (double)K) * (double)(1 << s2) > 1000.0) s2--;
+        s2 = std::max(s2, s1 - 8);
+        const int w2 = s1 - s2;
+        const int nb1 = (int)(((uint64_t)K - 1) >> s1) + 1, nsub = nb1 << w2;
+        for (int i = 0; i < 2; ++i) {
+            if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
+            if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
+            if (int rc = ensure(km_val[i], (size_t)n * 8)) return rc;
+        }
+        const int64_t nt1 = (n + kGrpTile - 1) / kGrpTile;
+        const int64_t nt2c = nt1 + 256;   // pass 2's tiles: at most one partial tile per digit beyond pass 1's count
+        if (int rc = ensure(grp_tiles, (size_t)(nt1 + nt2c) * sizeof(GrpTile))) return rc;
+        constexpr int kRep1 = 64;
+        const int n1 = kRep1 * 256;
+        if (int rc = ensure(grp_cnt, (size_t)(n1 + nsub) * 2 * 4)) return rc;
+        if (int rc = ensure(grp_base, (size_t)(n1 + nsub + 1) * 8)) return rc;
+        if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
+        GrpTile* d_t1 = (GrpTile*)grp_tiles.p;
+        GrpTile* d_t2 = d_t1 + nt1;
+        unsigned int* tot1 = (unsigned int*)grp_cnt.p;
+        unsigned int* cur1 = tot1 + n1;
+        unsigned int* tot2 = cur1 + n1;
+        unsigned int* cur2 = tot2 + nsub;
+        int64_t* base1 = (int64_t*)grp_base.p;
+        int64_t* base2 = base1 + n1;
+        const uint32_t* key0 = (const uint32_t*)km_k[0].p;
+        if (msd_ht_n != n) {   // pass 1's tiles: the span in kGrpTile pieces (pinned: the copy is asynchronous)
+            if (msd_ht_cap < (size_t)nt1) {
+                if (msd_ht) { hipStreamSynchronize(stream); hipHostFree(msd_ht); }
+                msd_ht_cap = (size_t)nt1;
+                if (hipHostMalloc((void**)&msd_ht, msd_ht_cap * sizeof(GrpTile)) != hipSuccess) { msd_ht = nullptr; msd_ht_cap = 0; return fail(EK_ERR_NOMEM, "pinned"); }
+            } else {
+                hipStreamSynchronize(stream);   // the previous launch's copy has completed
+            }
+            for (int64_t t = 0; t < nt1; ++t)
+                msd_ht[t] = GrpTile{t * kGrpTile, (int32_t)std::min<int64_t>(kGrpTile, n - t * kGrpTile), 0};
+            msd_ht_n = n;
+        }
+        hipMemcpyAsync(d_t1, msd_ht, (size_t)nt1 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
+        hipMemsetAsync(grp_cnt.p, 0, (size_t)(2 * n1 + 2 * nsub) * 4, stream);
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, 255u, K, kRep1, tot1);
+        hipLaunchKernelGGL(k_msd_plan1, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot1, kRep1, w2, (int)nt2c, base1, d_t2);
+        hipLaunchKernelGGL(k_grp_scatter<true>, dim3((unsigned)nt1), dim3(kGrpScatBlock), 0, stream, key0, val0, (const GrpTile*)d_t1,
+                           s1, 255u, K, kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p,
+                           (const uint32_t*)nullptr, (uint32_t*)km_p[0].p);
+        const uint32_t m2 = (1u << w2) - 1u;
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2c), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[1].p,
+                           (const GrpTile*)d_t2, s2, m2, K, 1, tot2);
+        hipLaunchKernelGGL(k_msd_plan2, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot2, nsub, base2, d_flag + 4);
+        hipLaunchKernelGGL(k_grp_scatter<true>, dim3((unsigned)nt2c), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[1].p,
+                           (const int64_t*)km_val[1].p, (const GrpTile*)d_t2, s2, m2, K, 1, (const int64_t*)base2, cur2,
+                           (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p, (const uint32_t*)km_p[0].p, (uint32_t*)km_p[1].p);
+        const int nk = 1 << s2;
+        const size_t flds = (((size_t)(2 * nk + 1) * 4 + 15) & ~(size_t)15) + (size_t)kKmFixCap * 12 + 16;
+        hipLaunchKernelGGL(k_kmsd_fix, dim3((unsigned)nsub), dim3(kKmFixBlock), flds, stream, (const int64_t*)base2, nsub, s2, K,
+                           (const uint32_t*)km_k[0].p, (uint32_t*)km_p[1].p, (int64_t*)km_val[0].p, (uint32_t*)km_start.p,
+                           d_flag + 1);
+        return 0;
+    }
+    GrpTile* msd_ht = nullptr;   // km_msd's pass-1 tiles (pinned, rebuilt when the span length changes)
+    size_t msd_ht_cap = 0;
+    int64_t msd_ht_n = -1;
+    int km_msd_on = 1;   // EKGPU_KM_MSD=0: the key-major span sort is the radix sort + value gather
+
     int km_run(const std::vector<int>& wl, const std::vector<int64_t>& obase, const std::vector<int32_t>& slots,
                bool* handled) {
         *handled = false;
@@ -2309,48 +2388,69 @@ struct Engine {
         // one window over the whole span: the walk needs no positions; with one value column (no validity) the
         // column itself is sorted by key (no position payload, no gather)
         const bool one = nw == 1 && km_one;
-        const bool vsort = one && dp.n_vc == 1 && !bv.valid[dp.vc_col[0]];
-        size_t tb = 0;
-        if (vsort) ekl_sort_pairs_u32_i64(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
-        else ekl_sort_pairs_u32(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
-        for (int i = 0; i < 2; ++i) {
-            if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
-            if (!vsort)
-                if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
-        }
-        if (vsort)
-            if (int rc = ensure(km_val[0], (size_t)n * 8)) return rc;
-        if (int rc = ensure(km_tmp, tb)) return rc;
-        if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
         if (int rc = ensure(km_flag, 64)) return rc;   // [0..3] flags, [8..15] EK_KM_CHECK report
-        if (!h_kmf && hipHostMalloc((void**)&h_kmf, 16) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
+        if (!h_kmf && hipHostMalloc((void**)&h_kmf, 32) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
         unsigned int* d_flag = (unsigned int*)km_flag.p;
-        hipMemsetAsync(d_flag, 0, 64, stream);
-        const int ph = phase_begin(EK_PHASE_PARTITION);
-        hipLaunchKernelGGL(k_km_keys, dim3((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                           d_plan, bv, lo, n, (uint32_t*)km_k[0].p, vsort ? (uint32_t*)nullptr : (uint32_t*)km_p[0].p, d_flag);
-        if (vsort) {
-            if (ekl_sort_pairs_u32_i64(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p,
-                                       (const int64_t*)bv.col[dp.vc_col[0]] + lo, (int64_t*)km_val[0].p, n, end_bit, stream))
+        const dim3 gk((unsigned)std::min<int64_t>(8192, (n + kBlock - 1) / kBlock));
+        // the (key, position) order of the span's rows, with the value column carried along (km_msd) or gathered after
+        // the radix sort
+        bool msd = km_msd_on && dp.n_vc == 1 && !bv.valid[dp.vc_col[0]] && K >= 65536 && K <= (1u << 27) && (double)n <= 64.0 * K;
+        int ph = -1;
+        if (msd) {
+            if (int rc = ensure(km_k[0], (size_t)n * 4)) return rc;
+            hipMemsetAsync(d_flag, 0, 64, stream);
+            ph = phase_begin(EK_PHASE_PARTITION);
+            hipLaunchKernelGGL(k_km_keys, gk, dim3(kBlock), 0, stream, d_plan, bv, lo, n, (uint32_t*)km_k[0].p, (uint32_t*)nullptr, d_flag);
+            if (int rc = km_msd((const int64_t*)bv.col[dp.vc_col[0]] + lo, n, d_flag)) return rc;
+            phase_end(ph);
+            hipMemcpyAsync(h_kmf, d_flag, 32, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key partition failed");
+            if (h_kmf[4]) msd = false;   // a sub-bucket above kKmFixCap rows (skewed keys): the radix sort below
+        }
+        const bool vsort = !msd && one && dp.n_vc == 1 && !bv.valid[dp.vc_col[0]];
+        if (!msd) {
+            size_t tb = 0;
+            if (vsort) ekl_sort_pairs_u32_i64(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
+            else ekl_sort_pairs_u32(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, stream);
+            for (int i = 0; i < 2; ++i) {
+                if (int rc = ensure(km_k[i], (size_t)n * 4)) return rc;
+                if (!vsort)
+                    if (int rc = ensure(km_p[i], (size_t)n * 4)) return rc;
+            }
+            if (vsort)
+                if (int rc = ensure(km_val[0], (size_t)n * 8)) return rc;
+            if (int rc = ensure(km_tmp, tb)) return rc;
+            if (int rc = ensure(km_start, ((size_t)K + 2) * 4)) return rc;
+            hipMemsetAsync(d_flag, 0, 64, stream);
+            ph = phase_begin(EK_PHASE_PARTITION);
+            hipLaunchKernelGGL(k_km_keys, gk, dim3(kBlock), 0, stream, d_plan, bv, lo, n, (uint32_t*)km_k[0].p,
+                               vsort ? (uint32_t*)nullptr : (uint32_t*)km_p[0].p, d_flag);
+            if (vsort) {
+                if (ekl_sort_pairs_u32_i64(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p,
+                                           (const int64_t*)bv.col[dp.vc_col[0]] + lo, (int64_t*)km_val[0].p, n, end_bit, stream))
+                    return fail(EK_ERR_DEVICE, "key sort failed");
+            } else if (ekl_sort_pairs_u32(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p, (const uint32_t*)km_p[0].p,
+                                          (uint32_t*)km_p[1].p, n, end_bit, stream))
                 return fail(EK_ERR_DEVICE, "key sort failed");
-        } else if (ekl_sort_pairs_u32(km_tmp.p, &tb, (const uint32_t*)km_k[0].p, (uint32_t*)km_k[1].p, (const uint32_t*)km_p[0].p,
-                                      (uint32_t*)km_p[1].p, n, end_bit, stream))
-            return fail(EK_ERR_DEVICE, "key sort failed");
-        const uint32_t* sk = (const uint32_t*)km_k[1].p;
+        }
+        const uint32_t* sk = (const uint32_t*)km_k[msd ? 0 : 1].p;
         const uint32_t* spos = vsort ? nullptr : (const uint32_t*)km_p[1].p;
         uint32_t* kstart = (uint32_t*)km_start.p;
-        hipLaunchKernelGGL(k_km_starts, dim3((unsigned)std::min<int64_t>(8192, (n + 1 + 255) / 256)), dim3(256), 0, stream, sk, n,
-                           K, kstart);
-        hipLaunchKernelGGL(k_km_maxrun, dim3((unsigned)std::min<int64_t>(256, ((int64_t)K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           stream, (const uint32_t*)kstart, K, d_flag + 1);
-        phase_end(ph);
-        hipMemcpyAsync(h_kmf, d_flag, 16, hipMemcpyDeviceToHost, stream);
-        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major sort failed");
+        if (!msd) {
+            hipLaunchKernelGGL(k_km_starts, dim3((unsigned)std::min<int64_t>(8192, (n + 1 + 255) / 256)), dim3(256), 0, stream, sk, n,
+                               K, kstart);
+            hipLaunchKernelGGL(k_km_maxrun, dim3((unsigned)std::min<int64_t>(256, ((int64_t)K + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               stream, (const uint32_t*)kstart, K, d_flag + 1);
+            phase_end(ph);
+            hipMemcpyAsync(h_kmf, d_flag, 32, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "key-major sort failed");
+        }
         if (h_kmf[0] > 0) return 0;                                                       // WHERE errors
         if (km_mode == 2 && !sort && (double)h_kmf[1] * overlap > (double)(1 << 22)) return 0;   // one key dominates
         if (one && sort && h_kmf[1] > (unsigned)kKmSegMax) return 0;   // single pass: no (key, window) run too long
         // value columns in key order
         KmCols cols{};
+        cols.no_vals = msd ? 1 : 0;   // km_msd carried the value column: the gather computes E / X only
         for (int v = 0; v < dp.n_vc; ++v) {
             if (int rc = ensure(km_val[v], (size_t)n * 8)) return rc;
             cols.val[v] = (int64_t*)km_val[v].p;
@@ -2414,7 +2514,7 @@ struct Engine {
             }
             glds = (size_t)nw * 8;
         }
-        if (!vsort) switch (nvc) {
+        if (!vsort && !(msd && !cols.E)) switch (nvc) {
         case 1: hipLaunchKernelGGL(k_km_gather<1>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 2: hipLaunchKernelGGL(k_km_gather<2>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
         case 3: hipLaunchKernelGGL(k_km_gather<3>, gg, dim3(kBlock), glds, stream, d_plan, bv, lo, spos, (const uint32_t*)kstart, cols); break;
@@ -5299,6 +5399,7 @@ struct Engine {
             release(*d);
         for (int v = 0; v < kMaxVC; ++v) { release(km_val[v]); release(km_ok[v]); }
         if (h_kmf) hipHostFree(h_kmf);
+        if (msd_ht) hipHostFree(msd_ht);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
         for (auto& e : phase_ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }

@@ -1770,7 +1770,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
     __shared__ uint32_t esh[20];
     int par = 0;
     bool pd_has = false, pd_present = false;
-    int32_t pd_idx = 0;
     int64_t pd_out = 0;
     unsigned long long pd_mask = 0;
     int64_t pd_cnt = 0, pd_vcn = 0, pd_isum = 0;
@@ -1887,7 +1886,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
                 }
                 pd_has = true;
                 pd_present = present;
-                pd_idx = wd.idx;
                 pd_out = wd.out_base;
                 pd_mask = mask;
                 pd_cnt = cnt; pd_vcn = vcn; pd_isum = isum; pd_fsum = fsum; pd_omn = omn; pd_omx = omx;

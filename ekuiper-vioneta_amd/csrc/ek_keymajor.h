@@ -153,6 +153,7 @@ struct KmCols {
     int32_t nw;
     int64_t n;           // rows of the span
     int32_t* dbg;        // EK_KM_CHECK
+    int32_t no_vals;     // the value columns are already in key order (km_msd): E / X only
 };
 
 // value columns (and validity) of the rows that passed WHERE, in key order
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_km_gather(DPlan* __restrict__ pp, DB
         }
 #pragma unroll
         for (int v = 0; v < NVC; ++v) {
-            if (v >= p.n_vc) break;
+            if (v >= p.n_vc || out.no_vals) break;
             const int c = p.vc_col[v];
             out.val[v][i] = ((const int64_t*)b.col[c])[r];
             if (out.ok[v]) out.ok[v][i] = b.valid[c] ? b.valid[c][r] : (uint8_t)1;
@@ -688,7 +689,7 @@ struct GrpTile {
 // regions out consecutively inside each digit's region.
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restrict__ keys, const GrpTile* __restrict__ tiles,
-                                                        int shift, uint32_t K, int rep, unsigned int* __restrict__ tot) {
+                                                        int shift, uint32_t dmask, uint32_t K, int rep, unsigned int* __restrict__ tot) {
     __shared__ unsigned int h[256];
     const GrpTile t = tiles[blockIdx.x];
     h[threadIdx.x] = 0;
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restri
     }
 #pragma unroll
     for (int j = 0; j < R; ++j)
-        if (k[j] < K) atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
+        if (k[j] < K) atomicAdd(&h[(k[j] >> shift) & dmask], 1u);
     __syncthreads();
     if (h[threadIdx.x]) atomicAdd(&tot[(blockIdx.x % rep) * 256 + t.pre + threadIdx.x], h[threadIdx.x]);
 }
@@ -711,22 +712,27 @@ __global__ __launch_bounds__(kGrpBlock) void k_grp_hist(const uint32_t* __restri
 // rows of a tile -> their (replica, pre + digit) region: base[] exclusive region starts, cur[] reservation cursors.
 // 512 threads (8 rows each): the 52 KB of LDS staging allow two workgroups per CU, so 16 waves keep loads in flight
 // (256 threads left 8 waves per CU and ran the pass at 2.7 TB/s). The digit is re-derived from the staged key.
+// POS: the rows also carry their span position (pass 1: the row index itself; pass 2: the pass-1 output), for the
+// key-major path of range windows (km_msd), whose walk needs the rows of a key in position order.
 constexpr int kGrpScatBlock = 512;
-#ifndef EK_NO_PLAIN_KERNELS
+template <bool POS>
 __global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* __restrict__ keys, const int64_t* __restrict__ vals,
-                                                               const GrpTile* __restrict__ tiles, int shift, uint32_t K, int rep,
+                                                               const GrpTile* __restrict__ tiles, int shift, uint32_t dmask,
+                                                               uint32_t K, int rep,
                                                                const int64_t* __restrict__ base, unsigned int* __restrict__ cur,
-                                                               uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
+                                                               uint32_t* __restrict__ okeys, int64_t* __restrict__ ovals,
+                                                               const uint32_t* __restrict__ pos, uint32_t* __restrict__ opos) {
     __shared__ unsigned int h[256], lofs[257];
     __shared__ int64_t gb[256];
     __shared__ uint32_t s_key[kGrpTile];
     __shared__ int64_t s_val[kGrpTile];
+    __shared__ uint32_t s_pos[POS ? kGrpTile : 1];
     __shared__ unsigned int wsum[kGrpScatBlock / 64];
     const GrpTile t = tiles[blockIdx.x];
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
     constexpr int R = kGrpTile / kGrpScatBlock;
-    uint32_t k[R];
+    uint32_t k[R], ps[R];
     int64_t v[R];
     int rk[R];
 #pragma unroll
@@ -736,10 +742,11 @@ __global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* _
         if (i >= t.len) continue;
         k[j] = keys[t.start + i];
         v[j] = vals[t.start + i];
+        if (POS) ps[j] = pos ? pos[t.start + i] : (uint32_t)(t.start + i);
     }
 #pragma unroll
     for (int j = 0; j < R; ++j)
-        if (threadIdx.x + j * kGrpScatBlock < t.len && k[j] < K) rk[j] = (int)atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
+        if (threadIdx.x + j * kGrpScatBlock < t.len && k[j] < K) rk[j] = (int)atomicAdd(&h[(k[j] >> shift) & dmask], 1u);
     __syncthreads();
     if (threadIdx.x < 256) {
         const unsigned int c = h[threadIdx.x];
@@ -752,18 +759,148 @@ __global__ __launch_bounds__(kGrpScatBlock) void k_grp_scatter(const uint32_t* _
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         if (rk[j] < 0) continue;
-        const unsigned int p = lofs[(k[j] >> shift) & 255u] + (unsigned int)rk[j];
+        const unsigned int p = lofs[(k[j] >> shift) & dmask] + (unsigned int)rk[j];
         s_key[p] = k[j];
         s_val[p] = v[j];
+        if (POS) s_pos[p] = ps[j];
     }
     __syncthreads();
     const unsigned int m = lofs[256];
     for (unsigned int p = threadIdx.x; p < m; p += kGrpScatBlock) {
         const uint32_t kk = s_key[p];
-        const unsigned int d = (kk >> shift) & 255u;
+        const unsigned int d = (kk >> shift) & dmask;
         const int64_t dst = gb[d] + (int64_t)(p - lofs[d]);
         okeys[dst] = kk;
         ovals[dst] = s_val[p];
+        if (POS) opos[dst] = s_pos[p];
+    }
+}
+
+// km_msd's last step, one workgroup per sub-bucket of 2^s2 keys (the two k_grp_scatter<true> passes grouped the rows
+// by key >> s2, in no order inside): the sub-bucket's rows are counted by key and placed in LDS in key order, each
+// key's segment is insertion-sorted by span position (one thread per key), and the rows go back to the same range
+// sorted by (key, position) — the order the radix sort gave — with kstart[key] for every key of the sub-bucket and
+// the longest key run (maxrun). Dynamic LDS: (nk + 1) counters + cursors, then m positions and m values (m <=
+// kKmFixCap). The sorted keys are not written back: kstart is all the walk reads of them.
+constexpr int kKmFixBlock = 256;
+constexpr int kKmFixCap = 2048;   // rows of one sub-bucket k_kmsd_fix holds in LDS (more: the radix-sort fallback)
+#ifndef EK_NO_PLAIN_KERNELS
+// km_msd's offsets on the device (no host round trip): pass 1's per-(replica, digit) counts -> region starts in digit-major,
+// replica-minor order, and pass 2's tiles (each digit's rows cut into kGrpTile pieces, digit << w2 as their sub-bucket
+// base; the tiles past the last are empty). One workgroup of 1024 threads; ntc = the tile list's capacity.
+__global__ __launch_bounds__(1024) void k_msd_plan1(const unsigned int* __restrict__ tot1, int rep, int w2, int ntc,
+                                                    int64_t* __restrict__ base1, GrpTile* __restrict__ tiles2) {
+    __shared__ int64_t s_cnt[257], s_nt[257];
+    const int b = threadIdx.x;
+    if (b < 256) {
+        int64_t c = 0;
+        for (int q = 0; q < rep; ++q) c += tot1[q * 256 + b];
+        s_cnt[b] = c;
+        s_nt[b] = (c + kGrpTile - 1) / kGrpTile;
+    }
+    __syncthreads();
+    if (b == 0) {   // 256 exclusive prefixes
+        int64_t r = 0, t = 0;
+        for (int d = 0; d < 256; ++d) { const int64_t c = s_cnt[d], nt = s_nt[d]; s_cnt[d] = r; s_nt[d] = t; r += c; t += nt; }
+        s_cnt[256] = r;
+        s_nt[256] = t;
+    }
+    __syncthreads();
+    if (b < 256) {
+        int64_t r = s_cnt[b];
+        const int64_t c_end = s_cnt[b + 1];
+        for (int q = 0; q < rep; ++q) { base1[q * 256 + b] = r; r += tot1[q * 256 + b]; }
+        int64_t t = s_nt[b];
+        for (int64_t x = s_cnt[b]; x < c_end; x += kGrpTile, ++t)
+            tiles2[t] = GrpTile{x, (int32_t)min<int64_t>(kGrpTile, c_end - x), b << w2};
+    }
+    for (int64_t t = s_nt[256] + b; t < ntc; t += 1024) tiles2[t] = GrpTile{0, 0, 0};
+}
+// pass 2's sub-bucket counts -> exclusive starts base2[nsub + 1]; a sub-bucket above kKmFixCap rows sets *over
+__global__ __launch_bounds__(1024) void k_msd_plan2(const unsigned int* __restrict__ tot2, int nsub, int64_t* __restrict__ base2,
+                                                    unsigned int* __restrict__ over) {
+    __shared__ int64_t s_part[1024];
+    const int per = (nsub + 1023) / 1024;
+    const int a = threadIdx.x * per, e = min(nsub, a + per);
+    int64_t sm = 0;
+    unsigned int mx = 0;
+    for (int i = a; i < e; ++i) { sm += tot2[i]; mx = max(mx, tot2[i]); }
+    s_part[threadIdx.x] = sm;
+    if (mx > (unsigned int)kKmFixCap) atomicOr(over, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t r = 0;
+        for (int t = 0; t < 1024; ++t) { const int64_t x = s_part[t]; s_part[t] = r; r += x; }
+        base2[nsub] = r;
+    }
+    __syncthreads();
+    int64_t r = s_part[threadIdx.x];
+    for (int i = a; i < e; ++i) { base2[i] = r; r += tot2[i]; }
+}
+
+__global__ __launch_bounds__(kKmFixBlock) void k_kmsd_fix(const int64_t* __restrict__ base2, int nsub, int s2, uint32_t K,
+                                                          const uint32_t* __restrict__ keys, uint32_t* __restrict__ pos,
+                                                          int64_t* __restrict__ vals, uint32_t* __restrict__ kstart,
+                                                          unsigned int* __restrict__ maxrun) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int sb = blockIdx.x;
+    const int64_t b0 = base2[sb], b1 = base2[sb + 1];
+    const int m = (int)(b1 - b0);
+    if (m > kKmFixCap) return;   // k_msd_plan2 flagged it: the caller falls back
+    const int nk = 1 << s2;
+    uint32_t* cnt = (uint32_t*)smem;                      // [nk + 1] -> exclusive starts
+    uint32_t* cur = cnt + nk + 1;                         // [nk]
+    int64_t* s_val = (int64_t*)(smem + (((size_t)(2 * nk + 1) * 4 + 15) & ~(size_t)15));   // [m]
+    uint32_t* s_pos = (uint32_t*)(s_val + m);             // [m]
+    __shared__ unsigned int wsum[kKmFixBlock / 64];
+    (void)cur;
+    for (int k = threadIdx.x; k <= nk; k += kKmFixBlock) cnt[k] = 0;
+    __syncthreads();
+    // one read of the sub-bucket: every row's (local key, position, value) in registers, its rank within its key from
+    // the LDS count, then its slot = the key's start + rank
+    constexpr int RR = kKmFixCap / kKmFixBlock;
+    uint32_t kl[RR], pp[RR], rk[RR];
+    int64_t vv[RR];
+#pragma unroll
+    for (int j = 0; j < RR; ++j) {
+        const int i = threadIdx.x + j * kKmFixBlock;
+        if (i < m) { kl[j] = keys[b0 + i] & (uint32_t)(nk - 1); pp[j] = pos[b0 + i]; vv[j] = vals[b0 + i]; }
+    }
+#pragma unroll
+    for (int j = 0; j < RR; ++j)
+        if (threadIdx.x + j * kKmFixBlock < m) rk[j] = atomicAdd(&cnt[kl[j]], 1u);
+    __syncthreads();
+    block_excl_scan<kKmFixBlock>(cnt, nk, wsum);
+#pragma unroll
+    for (int j = 0; j < RR; ++j) {
+        if (threadIdx.x + j * kKmFixBlock >= m) continue;
+        const uint32_t d = cnt[kl[j]] + rk[j];
+        s_pos[d] = pp[j];
+        s_val[d] = vv[j];
+    }
+    __syncthreads();
+    unsigned int mr = 0;
+    for (int k = threadIdx.x; k < nk; k += kKmFixBlock) {
+        const int a = (int)cnt[k], e = (int)cnt[k + 1];
+        for (int i = a + 1; i < e; ++i) {   // insertion sort by position (a key holds ~n / K rows)
+            const uint32_t pp = s_pos[i];
+            const int64_t vv = s_val[i];
+            int j = i - 1;
+            while (j >= a && s_pos[j] > pp) { s_pos[j + 1] = s_pos[j]; s_val[j + 1] = s_val[j]; --j; }
+            s_pos[j + 1] = pp;
+            s_val[j + 1] = vv;
+        }
+        mr = max(mr, (unsigned int)(e - a));
+        const int64_t g = ((int64_t)sb << s2) + k;
+        if (g < (int64_t)K) kstart[g] = (uint32_t)(b0 + a);
+    }
+    if (sb == nsub - 1 && threadIdx.x == 0) kstart[K] = (uint32_t)base2[nsub];
+    for (int o = 32; o > 0; o >>= 1) mr = max(mr, (unsigned int)__shfl_xor((int)mr, o, 64));
+    if ((threadIdx.x & 63) == 0 && mr) atomicMax(maxrun, mr);
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += kKmFixBlock) {   // (the sorted keys themselves: kstart holds them)
+        pos[b0 + i] = s_pos[i];
+        vals[b0 + i] = s_val[i];
     }
 }
 #endif

@@ -256,3 +256,34 @@ def test_km_one_window_grouped_skewed_falls_back(oracle, engine_mod):
     got, exp, st = _push_per_window(oracle, engine_mod, rule, cols, 1000)
     assert len(exp.windows) >= 2
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+@pytest.mark.parametrize("msd", ["1", "0"])
+@pytest.mark.parametrize("sql", [
+    "SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
+    "GROUP BY deviceId, SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1) HAVING count(*) > 1",
+    "SELECT deviceId, median(temperature), count(*) FROM demo GROUP BY deviceId, SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1)",
+])
+def test_km_msd_span_sort(oracle, engine_mod, monkeypatch, msd, sql):
+    """The key-major span sort by MSD partition (km_msd: two k_grp_scatter<true> passes carrying value and position,
+    k_kmsd_fix sorting each 2^s2-key sub-bucket by (key, position)) against the radix sort + gather (EKGPU_KM_MSD=0):
+    both equal the oracle, over 80 000 keys (>= 65 536: the MSD path's range) and several pushes."""
+    monkeypatch.setenv("EKGPU_KM_MSD", msd)
+    rule = compile_rule(sql, R.TRIG_SCHEMA, num_keys=80_000, debug_membership=True)
+    cols = R._with_trig(R._iot(300_000, 80_000, seed=67, epm=10), 400)
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=3)
+    assert st.windows_keymajor > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_km_msd_skewed_sub_bucket_falls_back(oracle, engine_mod, monkeypatch):
+    """A sub-bucket above kGrpCap rows (half the rows on one key) sends km_msd back to the radix sort: same results."""
+    monkeypatch.setenv("EKGPU_KM_MSD", "1")
+    sql = ("SELECT deviceId, stddev(temperature), count(*) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ss, 3) OVER (WHEN trig = 1)")
+    rule = compile_rule(sql, R.TRIG_SCHEMA, num_keys=70_000, debug_membership=True)
+    cols = R._with_trig(R._iot(200_000, 70_000, seed=71, epm=10), 400)
+    cols[0][::2] = 12_345
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=2)
+    assert st.windows_keymajor > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
