@@ -2343,15 +2343,19 @@ struct Engine {
         const uint32_t m2 = (1u << w2) - 1u;
         hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2c), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[1].p,
                            (const GrpTile*)d_t2, s2, m2, K, 1, tot2);
-        hipLaunchKernelGGL(k_msd_plan2, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot2, nsub, base2, d_flag + 4);
+        // LDS per k_kmsd_fix workgroup sized for twice the mean sub-bucket (a sub-bucket beyond it: the radix-sort fallback)
+        const double mean = (double)n / (double)nsub;
+        const int cap = (int)std::min<double>(kKmFixCap, std::max(512.0, std::ceil(2.0 * mean / 256.0) * 256.0));
+        hipLaunchKernelGGL(k_msd_plan2, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot2, nsub, base2, (unsigned int)cap,
+                           d_flag + 4);
         hipLaunchKernelGGL(k_grp_scatter<true>, dim3((unsigned)nt2c), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[1].p,
                            (const int64_t*)km_val[1].p, (const GrpTile*)d_t2, s2, m2, K, 1, (const int64_t*)base2, cur2,
                            (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p, (const uint32_t*)km_p[0].p, (uint32_t*)km_p[1].p);
         const int nk = 1 << s2;
-        const size_t flds = (((size_t)(2 * nk + 1) * 4 + 15) & ~(size_t)15) + (size_t)kKmFixCap * 12 + 16;
+        const size_t flds = (((size_t)(2 * nk + 1) * 4 + 15) & ~(size_t)15) + (size_t)cap * 12 + 16;
         hipLaunchKernelGGL(k_kmsd_fix, dim3((unsigned)nsub), dim3(kKmFixBlock), flds, stream, (const int64_t*)base2, nsub, s2, K,
                            (const uint32_t*)km_k[0].p, (uint32_t*)km_p[1].p, (int64_t*)km_val[0].p, (uint32_t*)km_start.p,
-                           d_flag + 1);
+                           d_flag + 1, cap);
         return 0;
     }
     GrpTile* msd_ht = nullptr;   // km_msd's pass-1 tiles (pinned, rebuilt when the span length changes)

@@ -788,70 +788,82 @@ constexpr int kKmFixCap = 2048;   // rows of one sub-bucket k_kmsd_fix holds in 
 // km_msd's offsets on the device (no host round trip): pass 1's per-(replica, digit) counts -> region starts in digit-major,
 // replica-minor order, and pass 2's tiles (each digit's rows cut into kGrpTile pieces, digit << w2 as their sub-bucket
 // base; the tiles past the last are empty). One workgroup of 1024 threads; ntc = the tile list's capacity.
+// 256-wide exclusive scan of s[0..255] into s (s[256] = total) by the first 4 waves (all 1024 threads call it)
+__device__ __forceinline__ void scan256(int64_t* s) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    __shared__ int64_t wsum[4];
+    int64_t x = t < 256 ? s[t] : 0, v = x;
+    for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(v, o, 64); if (lane >= o) v += y; }
+    if (t < 256 && lane == 63) wsum[w] = v;
+    __syncthreads();
+    if (t < 256) {
+        int64_t base = 0;
+        for (int k = 0; k < w; ++k) base += wsum[k];
+        s[t] = base + v - x;
+        if (t == 255) s[256] = base + v;
+    }
+    __syncthreads();
+}
 __global__ __launch_bounds__(1024) void k_msd_plan1(const unsigned int* __restrict__ tot1, int rep, int w2, int ntc,
                                                     int64_t* __restrict__ base1, GrpTile* __restrict__ tiles2) {
     __shared__ int64_t s_cnt[257], s_nt[257];
-    const int b = threadIdx.x;
-    if (b < 256) {
-        int64_t c = 0;
-        for (int q = 0; q < rep; ++q) c += tot1[q * 256 + b];
-        s_cnt[b] = c;
-        s_nt[b] = (c + kGrpTile - 1) / kGrpTile;
+    __shared__ unsigned int s_rep[64][256];   // replica counts, then their exclusive prefixes inside each digit
+    const int t = threadIdx.x;
+    for (int i = t; i < rep * 256; i += 1024) s_rep[i >> 8][i & 255] = tot1[i];
+    __syncthreads();
+    if (t < 256) {
+        unsigned int c = 0;
+        for (int q = 0; q < rep; ++q) { const unsigned int x = s_rep[q][t]; s_rep[q][t] = c; c += x; }
+        s_cnt[t] = c;
+        s_nt[t] = ((int64_t)c + kGrpTile - 1) / kGrpTile;
     }
     __syncthreads();
-    if (b == 0) {   // 256 exclusive prefixes
-        int64_t r = 0, t = 0;
-        for (int d = 0; d < 256; ++d) { const int64_t c = s_cnt[d], nt = s_nt[d]; s_cnt[d] = r; s_nt[d] = t; r += c; t += nt; }
-        s_cnt[256] = r;
-        s_nt[256] = t;
+    scan256(s_cnt);
+    scan256(s_nt);
+    for (int i = t; i < rep * 256; i += 1024) base1[i] = s_cnt[i & 255] + s_rep[i >> 8][i & 255];
+    if (t < 256) {
+        const int64_t c_end = s_cnt[t + 1];
+        int64_t k = s_nt[t];
+        for (int64_t x = s_cnt[t]; x < c_end; x += kGrpTile, ++k)
+            tiles2[k] = GrpTile{x, (int32_t)min<int64_t>(kGrpTile, c_end - x), t << w2};
     }
-    __syncthreads();
-    if (b < 256) {
-        int64_t r = s_cnt[b];
-        const int64_t c_end = s_cnt[b + 1];
-        for (int q = 0; q < rep; ++q) { base1[q * 256 + b] = r; r += tot1[q * 256 + b]; }
-        int64_t t = s_nt[b];
-        for (int64_t x = s_cnt[b]; x < c_end; x += kGrpTile, ++t)
-            tiles2[t] = GrpTile{x, (int32_t)min<int64_t>(kGrpTile, c_end - x), b << w2};
-    }
-    for (int64_t t = s_nt[256] + b; t < ntc; t += 1024) tiles2[t] = GrpTile{0, 0, 0};
+    for (int64_t k = s_nt[256] + t; k < ntc; k += 1024) tiles2[k] = GrpTile{0, 0, 0};
 }
 // pass 2's sub-bucket counts -> exclusive starts base2[nsub + 1]; a sub-bucket above kKmFixCap rows sets *over
 __global__ __launch_bounds__(1024) void k_msd_plan2(const unsigned int* __restrict__ tot2, int nsub, int64_t* __restrict__ base2,
-                                                    unsigned int* __restrict__ over) {
-    __shared__ int64_t s_part[1024];
+                                                    unsigned int cap, unsigned int* __restrict__ over) {
+    __shared__ int64_t wsum[16];
     const int per = (nsub + 1023) / 1024;
     const int a = threadIdx.x * per, e = min(nsub, a + per);
     int64_t sm = 0;
     unsigned int mx = 0;
     for (int i = a; i < e; ++i) { sm += tot2[i]; mx = max(mx, tot2[i]); }
-    s_part[threadIdx.x] = sm;
-    if (mx > (unsigned int)kKmFixCap) atomicOr(over, 1u);
+    if (mx > cap) atomicOr(over, 1u);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int64_t v = sm;
+    for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(v, o, 64); if (lane >= o) v += y; }
+    if (lane == 63) wsum[w] = v;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t r = 0;
-        for (int t = 0; t < 1024; ++t) { const int64_t x = s_part[t]; s_part[t] = r; r += x; }
-        base2[nsub] = r;
-    }
-    __syncthreads();
-    int64_t r = s_part[threadIdx.x];
+    int64_t r = v - sm;
+    for (int k = 0; k < w; ++k) r += wsum[k];
+    if (threadIdx.x == 1023) base2[nsub] = r + sm;
     for (int i = a; i < e; ++i) { base2[i] = r; r += tot2[i]; }
 }
 
 __global__ __launch_bounds__(kKmFixBlock) void k_kmsd_fix(const int64_t* __restrict__ base2, int nsub, int s2, uint32_t K,
                                                           const uint32_t* __restrict__ keys, uint32_t* __restrict__ pos,
                                                           int64_t* __restrict__ vals, uint32_t* __restrict__ kstart,
-                                                          unsigned int* __restrict__ maxrun) {
+                                                          unsigned int* __restrict__ maxrun, int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int sb = blockIdx.x;
     const int64_t b0 = base2[sb], b1 = base2[sb + 1];
     const int m = (int)(b1 - b0);
-    if (m > kKmFixCap) return;   // k_msd_plan2 flagged it: the caller falls back
+    if (m > cap) return;   // k_msd_plan2 flagged it: the caller falls back
     const int nk = 1 << s2;
     uint32_t* cnt = (uint32_t*)smem;                      // [nk + 1] -> exclusive starts
     uint32_t* cur = cnt + nk + 1;                         // [nk]
     int64_t* s_val = (int64_t*)(smem + (((size_t)(2 * nk + 1) * 4 + 15) & ~(size_t)15));   // [m]
-    uint32_t* s_pos = (uint32_t*)(s_val + m);             // [m]
+    uint32_t* s_pos = (uint32_t*)(s_val + cap);           // [m <= cap]
     __shared__ unsigned int wsum[kKmFixBlock / 64];
     (void)cur;
     for (int k = threadIdx.x; k <= nk; k += kKmFixBlock) cnt[k] = 0;
