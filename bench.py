@@ -193,6 +193,19 @@ def cpu_model():
     return None
 
 
+def committed_traffic(config, sim, events):
+    """HBM bytes per step from the newest committed rocprofv3 PMC summary of this workload (tools/profile_configs.py);
+    (None, None) when none matches its size."""
+    for rnd in ("r05", "r04", "r03"):
+        pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config}{sim}.json")
+        if not os.path.exists(pmc):
+            continue
+        pm = json.load(open(pmc))
+        if pm.get("events_per_gpu") == events:
+            return pm.get("hbm_bytes_per_step"), os.path.relpath(pmc, ROOT)
+    return None, None
+
+
 def cpu_baseline(name, cfg, sample_events):
     """The CPU oracle (C restatement of the reference per-tuple path, oracle/ekoracle.c) on the first
     `sample_events` events of the config's stream (the same synthetic generator, numpy side): single thread (the
@@ -379,6 +392,7 @@ def bench_c1(args):
     eng.sync()
     dth = (time.perf_counter() - t1) / args.steps
     alg = len(blob) + 8 * (n + 1) + rows * (8 + 8 + 8)
+    traffic, traffic_src = committed_traffic("C1", "", 0)   # the C1 PMC summary carries no event count (messages)
     out = {"metric": "messages/sec decoded and filtered (C1 JSON ingest + WHERE)", "value": n / dt, "unit": "messages/s",
            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -386,7 +400,7 @@ def bench_c1(args):
            "config": {"workload": "C1: JSON decode + SELECT * FROM demo WHERE temperature > 50", "messages": n,
                       "payload_bytes": int(len(blob)), "rows_out": rows},
            "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                         "what": "payload bytes + offsets read + passing rows x (row index + 2 f64 columns) written, over ms_per_step"},
            "host_fed": {"messages_per_s": n / dth, "ms_per_step": dth * 1e3,
                         "what": "payloads in pinned host memory: H2D inside ek_json_decode, then the filter"}}
@@ -687,17 +701,8 @@ def main():
                                         "algorithmic_bytes_per_launch": kb_launch,
                                         "achieved_gbs": kb_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else None}
     dominant = max(kernels.items(), key=lambda kv: kv[1]["launch_ms"] * kv[1]["launches_per_step"])[0] if kernels else None
-    traffic, traffic_src = None, None
     sim = f"_sim{world}" if args.sim_world > 1 else ""
-    for rnd in ("r05", "r04", "r03"):
-        pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.config}{sim}.json")
-        if not os.path.exists(pmc):
-            continue
-        pm = json.load(open(pmc))
-        if pm.get("events_per_gpu") == n and (world == 1 or sim):
-            traffic = pm.get("hbm_bytes_per_step")
-            traffic_src = os.path.relpath(pmc, ROOT)
-            break
+    traffic, traffic_src = committed_traffic(args.config, sim, n) if (world == 1 or sim) else (None, None)
     out = {
         "metric": "events/sec (whole node) for windowed GROUP BY at 1/2/4/8 GPUs; % HBM peak",
         "value": value,
