@@ -504,9 +504,12 @@ struct Engine {
                      (wtype == EK_WINDOW_HOPPING && plan.is_event_time && plan.late_tolerance_ms > 0) ||
                      wtype == EK_WINDOW_STATE || sort_aggs || has_first ||
                      inc || env_int("EKGPU_FORCE_RANGE", 0) != 0;
-        if (plan.sliding_send_twice && wtype == EK_WINDOW_SLIDING && plan.delay > 0 && plan.is_event_time)
-            return fail(EK_ERR_UNSUPPORTED, "enableSlidingWindowSendTwice is built for processing-time sliding windows "
-                                            "(window_op.go:355-373); event-time send-twice is not");
+        if (plan.sliding_send_twice && wtype == EK_WINDOW_SLIDING && plan.delay > 0 && plan.is_event_time &&
+            plan.window_version != 2 && !inc) {
+            // event_window_trigger.go:129-135,156-161: the first part at the trigger, the last part at its delay
+            // (et2_triggers); WindowV2's EventSlidingWindowOp and the incremental op have no send-twice
+            send_twice = true;
+        }
         if (plan.is_event_time && wtype == EK_WINDOW_COUNT && !inc)
             return fail(EK_ERR_UNSUPPORTED, "COUNTWINDOW in event time needs the incremental path (every aggregate incremental)");
         need_rel = (wtype == EK_WINDOW_SLIDING && !proc) || (inc && wtype == EK_WINDOW_COUNT) ||
@@ -967,6 +970,7 @@ struct Engine {
         sw2_gcb = INT64_MIN;
         sw2_gcx = 0;
         h_rtrig.clear();
+        et2_prev = kYear1Ms;
         pi_reset();
         v2q.clear();
         v2q_head = v2q_seen = 0;
@@ -2726,6 +2730,7 @@ struct Engine {
             if (int rc = proc_slide_triggers(rel_prev, pw)) return rc;
         } else if (wtype == EK_WINDOW_SLIDING) {
             const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
+            std::vector<DelayTrig> et2_new;   // send-twice: this push's triggers (abs position, ts, release step)
             if (n_new > 0) {
                 // trigger events among the newly released rows (OVER (WHEN ...)), in release order
                 if (int rc = ensure(flags_d, (size_t)n_new)) return rc;
@@ -2783,6 +2788,8 @@ struct Engine {
                             p.start = t - L;   // scan(): windowStart = t - length (window_op.go:697-707)
                             p.end = t;
                             pw.push_back(p);
+                        } else if (send_twice) {
+                            et2_new.push_back(DelayTrig{eb_base + i, t, r});
                         } else {
                             // W at the release step: the delayed window fires at a LATER watermark advance
                             delayq.push_back(DelayTrig{eb_base + i, t, r == INT64_MAX ? W : relstep_w(r)});
@@ -2792,6 +2799,8 @@ struct Engine {
             }
             if (D > 0 && plan.window_version == 2) {
                 if (int rc = v2_delay_triggers(rel_prev, pw)) return rc;
+            } else if (D > 0 && send_twice) {
+                if (int rc = et2_triggers(rel_prev, et2_new, pw)) return rc;
             } else if (D > 0) {
                 while (delayq_head < delayq.size()) {
                     const DelayTrig& d = delayq[delayq_head];
@@ -3349,6 +3358,129 @@ struct Engine {
         }
         return 0;
     }
+
+    // ---- Delayed SLIDINGWINDOW with enableSlidingWindowSendTwice in event time (event_window_trigger.go:124-180,
+    // window_op.go:576-603,675-721). At every WatermarkTuple W (replayed from the batch's running max, as above):
+    //   1. each queued delay t + D <= W scans the last part (t, t + D];
+    //   2. getNextWindow(prevWindowEndTs, W) — the earliest input in (prevWindowEndTs, W] — gates the triggers: when it
+    //      finds one, every queued trigger t scans the first part (t - L, t] and queues t + D; prevWindowEndTs then walks
+    //      to the last input <= W. With no input in that range the triggers stay queued.
+    // Each scan keeps, by handleInputsForSlidingWindow, only the EXPIRED prefix of the inputs (ts < windowEnd - L - D)
+    // whenever some but not all inputs expired (all expired: none kept). Restated on the host like the processing-time
+    // rule: sw2_e holds the ts of the expired inputs kept (never in a later window: every later window starts at or
+    // after their bound), the buffer rows [sw2_cut, released by the tuple) are the live inputs, a window is the fixed
+    // range of live rows with ts in its bounds. Triggers wait in delayq (pos_abs, ts, release step), timers in proc_dq.
+    int64_t et2_prev = kYear1Ms;          // prevWindowEndTs
+    int et2_triggers(int64_t rel_prev, const std::vector<DelayTrig>& trig, std::vector<PendWin>& pw) {
+        const int64_t D = slide_delay_et(), tol = plan.late_tolerance_ms;
+        const int64_t n_new = eb_rel - rel_prev;
+        std::vector<int64_t> h_rm((size_t)std::max<int64_t>(cur_nb, 0)), h_rel((size_t)std::max<int64_t>(n_new, 0));
+        if (h_rts.empty()) h_rts_base = eb_base + rel_prev;
+        const size_t o = h_rts.size();
+        h_rts.resize(o + (size_t)std::max<int64_t>(n_new, 0));
+        if (cur_nb > 0 && runmax_p) hipMemcpyAsync(h_rm.data(), runmax_p, (size_t)cur_nb * 8, hipMemcpyDeviceToHost, stream);
+        if (n_new > 0) {
+            hipMemcpyAsync(h_rel.data(), (const int64_t*)eb.rel.p + rel_prev, (size_t)n_new * 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(h_rts.data() + o, (const int64_t*)eb.col[dp.ts_col].p + rel_prev, (size_t)n_new * 8,
+                           hipMemcpyDeviceToHost, stream);
+        }
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "send-twice replay copy failed");
+        if (sw2_cut < h_rts_base) sw2_cut = h_rts_base;
+        auto ts_at = [&](int64_t abs) { return h_rts[abs - h_rts_base]; };
+        auto first_gt = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts > x
+            return h_rts_base + (std::upper_bound(h_rts.begin() + (lo - h_rts_base), h_rts.begin() + (hi - h_rts_base), x) - h_rts.begin());
+        };
+        auto first_ge = [&](int64_t lo, int64_t hi, int64_t x) {   // first abs index in [lo, hi) with ts >= x
+            return h_rts_base + (std::lower_bound(h_rts.begin() + (lo - h_rts_base), h_rts.begin() + (hi - h_rts_base), x) - h_rts.begin());
+        };
+        // the last input present with rows [.., P) released (none: INT64_MIN)
+        auto last_input = [&](int64_t P) {
+            if (P > sw2_cut) return ts_at(P - 1);
+            return sw2_e.empty() ? INT64_MIN : sw2_e.back();
+        };
+        auto scan2 = [&](int64_t ws, int64_t we, int64_t P) {
+            const int64_t a = first_gt(sw2_cut, P, ws);
+            const int64_t b = std::max(a, first_gt(a, P, we));
+            PendWin p{};
+            p.q.kind = RB_FIXED;
+            p.q.pos = a - eb_base;
+            p.q.rstep = b - eb_base;
+            p.start = ws;   // WindowRange [t - length, t] for both parts (window_op.go:683-690)
+            p.end = we;
+            pw.push_back(p);
+            const int64_t dl = we - (L + D);
+            const int64_t ne = std::lower_bound(sw2_e.begin(), sw2_e.end(), dl) - sw2_e.begin();
+            const int64_t nl = first_ge(sw2_cut, P, dl) - sw2_cut;
+            const int64_t present = (int64_t)sw2_e.size() + (P - sw2_cut);
+            if (ne + nl == 0) return;
+            if (ne + nl == present) {
+                sw2_e.clear();
+            } else {
+                sw2_e.resize((size_t)ne);
+                for (int64_t k = 0; k < nl; ++k) sw2_e.push_back(ts_at(sw2_cut + k));
+            }
+            sw2_cut = P;
+        };
+        const int64_t rel0 = eb_base + rel_prev;
+        size_t tk = 0;                  // this push's triggers not queued yet
+        int64_t lazy_P = -1;            // a WatermarkTuple that only moved prevWindowEndTs (applied before the next scan)
+        auto settle = [&]() {
+            if (lazy_P < 0) return;
+            const int64_t x = last_input(lazy_P);
+            if (x != INT64_MIN && x > et2_prev) et2_prev = x;
+            lazy_P = -1;
+        };
+        int64_t prevmax = cur_prevmax;
+        for (int64_t i = 0; i < cur_nb && runmax_p; ++i) {
+            const int64_t m = h_rm[(size_t)i];
+            if (prevmax != INT64_MIN && m <= prevmax) continue;
+            prevmax = m;
+            const int64_t Wj = m - tol, step = cur_arr_base + i;
+            const int64_t P = rel0 + (int64_t)(std::upper_bound(h_rel.begin(), h_rel.end(), step) - h_rel.begin());
+            while (tk < trig.size() && trig[tk].w_rel <= step) delayq.push_back(trig[tk++]);
+            const bool due = proc_dq_head < proc_dq.size() && proc_dq[proc_dq_head] + D <= Wj;
+            if (!due && delayq_head == delayq.size()) { lazy_P = P; continue; }
+            settle();
+            while (proc_dq_head < proc_dq.size() && proc_dq[proc_dq_head] + D <= Wj) {
+                const int64_t t = proc_dq[proc_dq_head++];
+                scan2(t, t + D, P);   // the last part
+            }
+            // getNextWindow: the earliest input in (prevWindowEndTs, W] (expired inputs kept count too)
+            int64_t we1 = INT64_MAX;
+            {
+                auto e = std::upper_bound(sw2_e.begin(), sw2_e.end(), et2_prev);
+                if (e != sw2_e.end()) we1 = *e;
+                const int64_t f = first_gt(sw2_cut, P, et2_prev);
+                if (f < P) we1 = std::min(we1, ts_at(f));
+            }
+            if (we1 == INT64_MAX || we1 > Wj) continue;
+            for (; delayq_head < delayq.size(); ++delayq_head) {
+                const int64_t t = delayq[delayq_head].ts;
+                proc_dq.push_back(t);
+                scan2(t - L, t, P);   // the first part
+            }
+            const int64_t x = last_input(P);
+            et2_prev = std::max(we1, x);
+        }
+        while (tk < trig.size()) delayq.push_back(trig[tk++]);   // (a release step past this batch's tuples)
+        settle();
+        eb_floor = std::max(eb_floor, sw2_cut - eb_base);
+        const int64_t drop = sw2_cut - h_rts_base;
+        if (drop > 65536 && drop * 2 > (int64_t)h_rts.size()) {
+            h_rts.erase(h_rts.begin(), h_rts.begin() + drop);
+            h_rts_base = sw2_cut;
+        }
+        if (delayq_head > 4096 && delayq_head * 2 > delayq.size()) {
+            delayq.erase(delayq.begin(), delayq.begin() + (int64_t)delayq_head);
+            delayq_head = 0;
+        }
+        if (proc_dq_head > 4096 && proc_dq_head * 2 > proc_dq.size()) {
+            proc_dq.erase(proc_dq.begin(), proc_dq.begin() + (int64_t)proc_dq_head);
+            proc_dq_head = 0;
+        }
+        return 0;
+    }
+    int64_t slide_delay_et() const { return (int64_t)plan.delay * unit_ms(plan.time_unit); }
 
     // W at a release step r (arrival index inside the current batch): runmax[r - batch base] - lateTol
     int64_t cur_arr_base = 0, cur_nb = 0, cur_prevmax = INT64_MIN;
@@ -5033,8 +5165,9 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 6;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
-                                                  // 5: processing-time incremental windows; 6: ek_stats totals
+    static constexpr int64_t kStateVersion = 7;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
+                                                  // 5: processing-time incremental windows; 6: ek_stats totals;
+                                                  // 7: event-time send-twice prevWindowEndTs
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -5216,6 +5349,7 @@ struct Engine {
             s.i64(v2_lastW);                                                  // delayed v2 sliding: delayTS queue
             s.i64((int64_t)(v2q.size() - v2q_head));
             s.put(v2q.data() + v2q_head, (v2q.size() - v2q_head) * sizeof(V2Delay));
+            s.i64(et2_prev);                                                  // event-time send-twice (v7)
         }
         *size = (int64_t)s.b.size();
         if (!buf) return 0;
@@ -5366,6 +5500,7 @@ struct Engine {
             v2q_head = 0;
             v2q_seen = (size_t)nv;
             r.read(v2q.data(), nv * (int64_t)sizeof(V2Delay));
+            et2_prev = r.i64();
             if (!r.ok) return fail(EK_ERR_INVALID, "state blob truncated");
         }
         return 0;

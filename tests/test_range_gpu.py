@@ -113,6 +113,45 @@ def test_sliding_with_delay(oracle, engine_mod):
         assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
 
 
+@pytest.mark.parametrize("late", [0, 150])
+def test_sliding_send_twice_event_time(oracle, engine_mod, late):
+    """enableSlidingWindowSendTwice in event time (event_window_trigger.go:129-135,156-161): the first part
+    (t - L, t] when the watermark passes the trigger, the last part (t, t + D] when it passes t + D, each scan keeping
+    only the expired prefix of the inputs (handleInputsForSlidingWindow, window_op.go:576-603) and the triggers gated
+    by getNextWindow over what is left. No reference KAT covers this path: parity is against the oracle's restatement
+    (oracle/ekoracle.c win_on_watermark / scan), in order and out of order within lateTolerance."""
+    sql = ("SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo "
+           "GROUP BY deviceId, SLIDINGWINDOW(ms, 200, 100) OVER (WHEN trig = 1)")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=30, late_tolerance_ms=late, debug_membership=True,
+                        sliding_send_twice=True)
+    assert rule.plan.sliding_send_twice == 1
+    cols = _with_trig(_iot(30_000, 30, seed=66, epm=3), 300)
+    if late:
+        rng = np.random.default_rng(7)
+        cols[1] = (cols[1] + rng.integers(-200, 200, len(cols[1]))).astype(np.int64)
+    for batches in (1, 6, 97):
+        got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(exp.windows) > 10
+        assert st.records_late == exp.records_late
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
+def test_sliding_send_twice_event_time_small(oracle, engine_mod):
+    """A hand-sized stream, one row per push: sparse triggers with idle gaps longer than length + delay (every
+    input expires: none kept) and dense ones (some expire: only those are kept, the live inputs are lost)."""
+    sql = "SELECT count(*), sum(temperature) FROM demo GROUP BY SLIDINGWINDOW(ms, 50, 30) OVER (WHEN trig = 1)"
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=1, debug_membership=True, sliding_send_twice=True)
+    t0 = 1541152480000
+    ts = np.array([0, 10, 20, 25, 40, 60, 61, 90, 200, 210, 215, 230, 260, 300, 305, 500, 520, 540, 545, 600], np.int64)
+    trig = np.array([0, 1, 0, 1, 0, 1, 0, 0, 1, 0, 1, 1, 0, 0, 1, 1, 0, 1, 0, 0], np.int64)
+    n = len(ts)
+    cols = [np.zeros(n, np.uint32), ts + t0, np.arange(n, dtype=np.float64), np.zeros(n), trig]
+    for batches in (1, 3, n):
+        got, exp, _ = run_both(oracle, engine_mod, rule, cols, batches=batches)
+        assert len(exp.windows) >= 6
+        assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
 @pytest.mark.parametrize("n,m", [(1000, 0), (500, 200), (300, 700)])
 def test_count_window(oracle, engine_mod, n, m):
     """COUNTWINDOW(n[, m]) in processing time (C4b shape, reduced) with stddev/var + HAVING."""

@@ -69,6 +69,10 @@ CASES = [
     ("sliding_delay", "SELECT deviceId, count(*), sum(temperature) FROM demo "
      "GROUP BY deviceId, SLIDINGWINDOW(ms, 200, 100) OVER (WHEN trig = 1)", TRIG_SCHEMA, dict(num_keys=30),
      lambda: _with_trig(_iot(30_000, 30, seed=85, epm=3), 300), 0.5),
+    # event-time send-twice: the expired inputs kept, the queued triggers / timers and prevWindowEndTs travel (v7)
+    ("sliding_send_twice_event", "SELECT deviceId, count(*), max(temperature) FROM demo "
+     "GROUP BY deviceId, SLIDINGWINDOW(ms, 200, 100) OVER (WHEN trig = 1)", TRIG_SCHEMA,
+     dict(num_keys=30, sliding_send_twice=True), lambda: _with_trig(_iot(30_000, 30, seed=90, epm=3), 300), 0.45),
     ("count_window", "SELECT deviceId, avg(temperature), count(*) FROM demo GROUP BY deviceId, COUNTWINDOW(700, 300)",
      IOT_SCHEMA, dict(num_keys=60, is_event_time=False), lambda: _iot(20_000, 60, seed=86, epm=10), 0.43),
     ("state_window_proc", "SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo "
