@@ -4649,8 +4649,9 @@ struct Engine {
             if (inc || plan.window_version == 2 || wtype == EK_WINDOW_STATE)
                 return fail(EK_ERR_UNSUPPORTED, "shard mode: state, v2 and incremental windows depend on every row "
                                                 "of the stream (not shardable by key)");
-            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0)
-                return fail(EK_ERR_UNSUPPORTED, "shard mode: delayed sliding windows are not built");
+            if (wtype == EK_WINDOW_SLIDING && plan.delay != 0 && send_twice)
+                return fail(EK_ERR_UNSUPPORTED, "shard mode: send-twice sliding windows keep an expired prefix of EVERY "
+                                                "input of the stream (window_op.go:576-603; not shardable by key)");
             if (wtype == EK_WINDOW_HOPPING && plan.late_tolerance_ms != 0)
                 return fail(EK_ERR_UNSUPPORTED, "shard mode: the hopping empty-window discard is built for lateTolerance 0");
             if (plan.n_filter > 0)
@@ -4883,6 +4884,52 @@ struct Engine {
     // (ts < W, or ts == W and it arrived no later than that tuple's event), over the rows released so far with
     // t - L <= ts <= t and release step <= the trigger's (window_op.go:605-655, event_window_trigger.go:147-166).
     int global_slide_triggers(std::vector<PendWin>& pw) {
+        const int64_t D = (int64_t)plan.delay * unit_ms(plan.time_unit);
+        if (D > 0) {
+            // delayed: a released trigger queues t + D (event_window_trigger.go:154-166); its window [t - L, t + D) over
+            // the shard's rows fires at the first LATER global tuple reaching t + D — in this push iff its last tuple
+            // does (W only grows) — in trigger order, as the single-stream delay loop (the queue is ts-ordered)
+            if (int rc = global_release_triggers([&](const GTrig& x, int64_t k) {
+                    delayq.push_back(DelayTrig{x.a, x.t, g_wt[k]});
+                    return 0;
+                }))
+                return rc;
+            while (delayq_head < delayq.size()) {
+                const DelayTrig& d = delayq[delayq_head];
+                if (!(has_W && W >= d.ts + D && W > d.w_rel)) break;
+                PendWin p{};
+                p.q.kind = RB_LB;
+                p.q.lo_ts = d.ts - L;
+                p.q.hi_ts = d.ts + D;
+                p.q.floor = eb_floor;
+                p.start = 0;     // second-part scan leaves WindowRange unset
+                p.end = 0;
+                pw.push_back(p);
+                delayq_head++;
+            }
+            if (delayq_head > 4096 && delayq_head * 2 > delayq.size()) {
+                delayq.erase(delayq.begin(), delayq.begin() + (int64_t)delayq_head);
+                delayq_head = 0;
+            }
+            return 0;
+        }
+        return global_release_triggers([&](const GTrig& x, int64_t k) {
+            PendWin p{};
+            p.q.kind = RB_SLIDE;
+            p.q.lo_ts = x.t - L;
+            p.q.hi_ts = x.t;
+            p.q.pos = eb_floor - 1;      // the search starts at the floor: every row before the trigger's run is a member candidate
+            p.q.rstep = g_wa[k];
+            p.q.floor = eb_floor;
+            p.start = x.t - L;
+            p.end = x.t;
+            pw.push_back(p);
+            return 0;
+        });
+    }
+    // the global triggers the push's tuples release, in (ts, arrival) order, each with the index of its releasing tuple
+    template <typename F>
+    int global_release_triggers(F on_release) {
         if (!has_W || g_trig.empty()) return 0;
         std::vector<GTrig> rel, keep;
         for (const GTrig& x : g_trig) {
@@ -4897,16 +4944,7 @@ struct Engine {
             const int64_t k1 = std::lower_bound(g_wt, g_wt + g_nwm, x.t) - g_wt;
             const int64_t k = std::max(k0, k1);
             if (k >= g_nwm) return fail(EK_ERR_INVALID, "trigger at arrival %lld is not released by this batch's tuples", (long long)x.a);
-            PendWin p{};
-            p.q.kind = RB_SLIDE;
-            p.q.lo_ts = x.t - L;
-            p.q.hi_ts = x.t;
-            p.q.pos = eb_floor - 1;      // the search starts at the floor: every row before the trigger's run is a member candidate
-            p.q.rstep = g_wa[k];
-            p.q.floor = eb_floor;
-            p.start = x.t - L;
-            p.end = x.t;
-            pw.push_back(p);
+            if (int rc = on_release(x, k)) return rc;
         }
         return 0;
     }

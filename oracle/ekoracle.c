@@ -1137,9 +1137,12 @@ static void win_on_watermark(winop* o, int64_t wm) {
         else we = next_window(o, o->prev_end, wm);
     }
     if (o->shard && o->wtype == EK_WINDOW_SLIDING) {
-        /* shard model: every trigger fires at the tuple that released it (its window = the rows released so far) */
+        /* shard model: every trigger fires at the tuple that released it (its window = the rows released so far);
+         * with a delay it queues t + D and the window (t - L, t + D] fires at a later tuple reaching it (the delay
+         * loop above), as in the trigger loop below (event_window_trigger.go:154-166) */
         while (o->trigger_ts.n > 0 && o->trigger_ts.a[0] <= wm) {
-            scan(o, o->trigger_ts.a[0], o->L, 1);
+            if (o->D > 0) v_push(&o->delay_ts, o->trigger_ts.a[0] + o->D);
+            else scan(o, o->trigger_ts.a[0], o->L, 1);
             v_erase_front(&o->trigger_ts, 1);
         }
         return;
@@ -1843,6 +1846,9 @@ int eko_run_proc(const ek_plan* p, int64_t n, const void* const* columns, const 
  *   count:    processing-time COUNTWINDOW blocks over the GLOBAL arrival order (window_op.go:390-418)
  *   session:  the sessions the router closed over the WHOLE stream (g->sess_*), each at its tuple, over the
  *             shard's inputs with ts < end
+ *   sliding:  every global trigger fires at the tuple releasing it; with a delay D it queues t + D and the window
+ *             [t - L, t + D) over the shard's inputs fires at the first LATER tuple reaching it (send-twice is not
+ *             shardable: its expired-prefix rule depends on every input of the stream)
  * The union of the shards' rows (and the sum of their membership fingerprints) is compared with eko_run on the
  * whole stream by the tests. */
 int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity,
@@ -1850,7 +1856,7 @@ int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION || !g) { set_status(out, EK_ERR_INVALID, "bad plan / context"); return out->status; }
     if (p->incremental || p->window_version == 2 || p->window_type == EK_WINDOW_STATE ||
-        p->window_type == EK_WINDOW_NONE || (p->window_type == EK_WINDOW_SLIDING && p->delay != 0) ||
+        p->window_type == EK_WINDOW_NONE || (p->window_type == EK_WINDOW_SLIDING && p->delay != 0 && p->sliding_send_twice) ||
         (p->window_type == EK_WINDOW_HOPPING && p->late_tolerance_ms != 0) ||
         (p->window_type == EK_WINDOW_COUNT && p->is_event_time)) {
         set_status(out, EK_ERR_UNSUPPORTED, "window not shardable"); return out->status;
@@ -1883,7 +1889,8 @@ int eko_run_shard(const ek_plan* p, int64_t n, const void* const* columns, const
     winop o; memset(&o, 0, sizeof o);
     o.d = &d; o.ob = &ob; o.wtype = p->window_type; o.ts = ts;
     const int64_t u = unit_ms(p->time_unit);
-    o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u; o.D = 0;
+    o.L = (int64_t)p->length * u; o.I = (int64_t)p->interval * u;
+    o.D = p->window_type == EK_WINDOW_SLIDING ? (int64_t)p->delay * u : 0;   /* delayed sliding: the delay loop */
     o.raw_interval = (p->window_type == EK_WINDOW_HOPPING) ? p->interval : p->length;
     o.unit = p->time_unit; o.tz = p->tz_offset_s;
     o.next_end = MAXT_MS; o.prev_end = ZERO_MS;

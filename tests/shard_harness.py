@@ -21,6 +21,11 @@ CASES = {
                           "GROUP BY deviceId, SLIDINGWINDOW(ss, 2) OVER (WHEN trig = 1) HAVING count(*) > 1", 0, True, "ooo"),
     "sliding_over_when_tol": ("SELECT deviceId, avg(temperature), count(*) FROM demo "
                               "GROUP BY deviceId, SLIDINGWINDOW(ss, 2) OVER (WHEN trig = 1)", 300, True, "ooo"),
+    # delayed sliding: each global trigger queues t + D, the window [t - L, t + D) fires at a later global tuple
+    "sliding_delay": ("SELECT deviceId, count(*), sum(temperature), max(humidity) FROM demo "
+                      "GROUP BY deviceId, SLIDINGWINDOW(ms, 700, 300) OVER (WHEN trig = 1)", 0, True, "ooo"),
+    "sliding_delay_tol": ("SELECT deviceId, avg(temperature), count(*) FROM demo "
+                          "GROUP BY deviceId, SLIDINGWINDOW(ss, 1, 1) OVER (WHEN trig = 1)", 250, True, "ooo"),
     "count_window": ("SELECT deviceId, stddev(temperature), var(temperature), count(*) FROM demo "
                      "GROUP BY deviceId, COUNTWINDOW(1000) HAVING count(*) > 1", 0, False, "sorted"),
     "tumbling_median": ("SELECT deviceId, median(temperature), count(*) FROM demo "

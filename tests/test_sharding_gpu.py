@@ -108,6 +108,13 @@ def test_shard_mode_rejections(engine_mod):
         eng.advance_watermark(1541152480000, 1)
     assert ei.value.code == A.EK_ERR_UNSUPPORTED
     eng.close()
+    # send-twice keeps an expired prefix of every input of the stream: not shardable by key
+    st2 = compile_rule(H.CASES["sliding_delay"][0], H.SCHEMA, num_keys=4, sliding_send_twice=True)
+    eng = engine_mod.Engine(st2.plan)
+    with pytest.raises(engine_mod.EngineError) as ei:
+        eng.advance_watermark(1541152480000, 1)
+    assert ei.value.code == A.EK_ERR_UNSUPPORTED
+    eng.close()
     tum = compile_rule(H.CASES["tumbling_ooo_late"][0], H.SCHEMA, num_keys=300)
     eng = engine_mod.Engine(tum.plan)
     cols = H.global_stream("sorted", n=100)
