@@ -365,6 +365,27 @@ __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wm
 }
 #endif
 
+// Panes no group touched (bound by a window before any event reached them): their ring slots are zeroed — the count
+// row (per_words u64) plus the per-slot error / membership / witness words — in one launch, blockIdx.y = list entry
+// (instead of five fills per slot, most of them of a few bytes)
+constexpr int kZeroSlotsMax = 64;
+struct SlotList { int32_t n; int32_t s[kZeroSlotsMax]; };
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_zero_slots(SlotList L, uint64_t* __restrict__ cnt, int64_t per_words, int32_t* __restrict__ perr,
+                             int64_t* __restrict__ pmc, uint64_t* __restrict__ pmh, uint8_t* __restrict__ pwit, int wit_bytes) {
+    if ((int)blockIdx.y >= L.n) return;
+    const int64_t s = L.s[blockIdx.y];
+    uint64_t* row = cnt + s * per_words;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < per_words; i += (int64_t)gridDim.x * blockDim.x)
+        row[i] = 0;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) { perr[s] = 0; pmc[s] = 0; pmh[s] = 0; }
+        if (pwit)
+            for (int b = threadIdx.x; b < wit_bytes; b += blockDim.x) pwit[s * wit_bytes + b] = 0;
+    }
+}
+#endif
+
 // first index in [lo, hi) with ts >= bound[k] (sorted batches)
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_lower_bound(const int64_t* __restrict__ ts, int64_t lo, int64_t hi, const int64_t* bound, int nb,
