@@ -2238,9 +2238,6 @@ struct Engine {
     DevBuf km_rbase, km_rec, km_skend, km_urec, km_ukend, km_scount, km_ex;
     int grp_on = 1;   // EKGPU_GRP=0: one-window launches over huge key spaces use the radix-sorted key-major walk
     DevBuf grp_tiles, grp_cnt, grp_base;
-    std::vector<unsigned int> grp_h;
-    std::vector<int64_t> grp_hb;
-    std::vector<GrpTile> grp_ht;
 
     // ek_keymajor.h k_grp_*: two MSD partition passes (8-bit digits of the key) into sub-buckets of 2^s2 keys,
     // then one workgroup per sub-bucket groups its rows by key in LDS and emits. *ok = false: a sub-bucket holds
@@ -2258,65 +2255,59 @@ struct Engine {
             if (int rc = ensure(km_val[i], (size_t)n * 8)) return rc;
         }
         const int64_t nt1 = (n + kGrpTile - 1) / kGrpTile;
-        const int64_t nt_cap = nt1 + nb1 + 1;
-        if (int rc = ensure(grp_tiles, (size_t)nt_cap * sizeof(GrpTile) * 2)) return rc;
+        if (int rc = ensure(grp_tiles, (size_t)(nt1 + nt1 + 256) * sizeof(GrpTile))) return rc;
         constexpr int kRep1 = 64;   // counter replicas of the first pass (k_grp_hist)
         const int n1 = kRep1 * 256;
         if (int rc = ensure(grp_cnt, (size_t)(n1 + nsub) * 2 * 4)) return rc;
         if (int rc = ensure(grp_base, (size_t)(n1 + nsub + 1) * 8)) return rc;
         GrpTile* d_t1 = (GrpTile*)grp_tiles.p;
-        GrpTile* d_t2 = d_t1 + nt_cap;
+        GrpTile* d_t2 = d_t1 + nt1;
         unsigned int* tot1 = (unsigned int*)grp_cnt.p;
         unsigned int* cur1 = tot1 + n1;
         unsigned int* tot2 = cur1 + n1;
         unsigned int* cur2 = tot2 + nsub;
         int64_t* base1 = (int64_t*)grp_base.p;
         int64_t* base2 = base1 + n1;
-        grp_ht.resize((size_t)nt1);
-        for (int64_t t = 0; t < nt1; ++t)
-            grp_ht[t] = GrpTile{t * kGrpTile, (int32_t)std::min<int64_t>(kGrpTile, n - t * kGrpTile), 0};
-        // (host <-> device lists through the pinned block: pageable copies cost tens of µs of staging each)
-        if (int rc = up_pinned(d_t1, grp_ht.data(), (size_t)nt1)) return rc;
+        // offsets and pass-2 tiles planned on the device (k_msd_plan1 / k_msd_plan2, as km_msd): one host round trip,
+        // after the second scatter, for the largest sub-bucket (register depth of the walk, or the fallback)
+        if (int rc = ensure(km_flag, 64)) return rc;
+        if (!h_kmf && hipHostMalloc((void**)&h_kmf, 32) != hipSuccess) { h_kmf = nullptr; return fail(EK_ERR_NOMEM, "pinned"); }
+        unsigned int* d_flag = (unsigned int*)km_flag.p;
+        if (msd_ht_n != n) {   // pass 1's tiles: the span in kGrpTile pieces (pinned, shared with km_msd)
+            if (msd_ht_cap < (size_t)nt1) {
+                if (msd_ht) { hipStreamSynchronize(stream); hipHostFree(msd_ht); }
+                msd_ht_cap = (size_t)nt1;
+                if (hipHostMalloc((void**)&msd_ht, msd_ht_cap * sizeof(GrpTile)) != hipSuccess) { msd_ht = nullptr; msd_ht_cap = 0; return fail(EK_ERR_NOMEM, "pinned"); }
+            } else {
+                hipStreamSynchronize(stream);   // the previous launch's copy has completed
+            }
+            for (int64_t t = 0; t < nt1; ++t)
+                msd_ht[t] = GrpTile{t * kGrpTile, (int32_t)std::min<int64_t>(kGrpTile, n - t * kGrpTile), 0};
+            msd_ht_n = n;
+        }
+        const int64_t nt2c = nt1 + 256;
+        hipMemcpyAsync(d_t1, msd_ht, (size_t)nt1 * sizeof(GrpTile), hipMemcpyHostToDevice, stream);
         hipMemsetAsync(grp_cnt.p, 0, (size_t)(2 * n1 + 2 * nsub) * 4, stream);
+        hipMemsetAsync(d_flag, 0, 64, stream);
         const int ph = phase_begin(EK_PHASE_PARTITION);
         hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt1), dim3(kGrpBlock), 0, stream, key0, (const GrpTile*)d_t1, s1, 255u, K,
                            kRep1, tot1);
-        grp_h.resize(n1);
-        if (int rc = down_pinned(grp_h.data(), tot1, (size_t)n1 * 4)) return rc;
-        if (int rc = sync_downs("grouping histogram failed")) return rc;
-        grp_hb.assign(n1 + nsub + 1, 0);
-        int64_t acc = 0;
-        grp_ht.clear();
-        for (int b = 0; b < 256; ++b) {   // digit b's region holds its replicas' sub-regions one after another
-            const int64_t b0 = acc;
-            for (int q = 0; q < kRep1; ++q) { grp_hb[q * 256 + b] = acc; acc += grp_h[q * 256 + b]; }
-            for (int64_t r = b0; r < acc; r += kGrpTile)
-                grp_ht.push_back(GrpTile{r, (int32_t)std::min<int64_t>(kGrpTile, acc - r), b * 256});
-        }
-        const int64_t nt2 = (int64_t)grp_ht.size();
-        if (int rc = up_pinned(base1, grp_hb.data(), (size_t)n1)) return rc;
-        if (nt2 > 0)
-            if (int rc = up_pinned(d_t2, grp_ht.data(), (size_t)nt2)) return rc;
+        hipLaunchKernelGGL(k_msd_plan1, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot1, kRep1, 8, (int)nt2c, base1, d_t2);
         hipLaunchKernelGGL(k_grp_scatter<false>, dim3((unsigned)nt1), dim3(kGrpScatBlock), 0, stream, key0, val0, (const GrpTile*)d_t1, s1,
                            255u, K, kRep1, (const int64_t*)base1, cur1, (uint32_t*)km_k[0].p, (int64_t*)km_val[0].p, (const uint32_t*)nullptr,
                            (uint32_t*)nullptr);
-        if (nt2 > 0)
-            hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const GrpTile*)d_t2, s2, 255u, K, 1, tot2);
-        grp_h.resize((size_t)nsub);
-        if (int rc = down_pinned(grp_h.data(), tot2, (size_t)nsub * 4)) return rc;
-        if (int rc = sync_downs("grouping pass 1 failed")) return rc;
-        acc = 0;
-        unsigned int mx = 0;
-        for (int i = 0; i < nsub; ++i) { grp_hb[n1 + i] = acc; acc += grp_h[i]; mx = std::max(mx, grp_h[i]); }
-        grp_hb[n1 + nsub] = acc;
-        if (mx > (unsigned int)kGrpCap) { phase_end(ph); return 0; }
-        if (int rc = up_pinned(base2, grp_hb.data() + n1, (size_t)(nsub + 1))) return rc;
-        if (nt2 > 0)
-            hipLaunchKernelGGL(k_grp_scatter<false>, dim3((unsigned)nt2), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[0].p,
-                               (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, 255u, K, 1, (const int64_t*)base2, cur2,
-                               (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+        hipLaunchKernelGGL(k_grp_hist, dim3((unsigned)nt2c), dim3(kGrpBlock), 0, stream, (const uint32_t*)km_k[0].p,
+                           (const GrpTile*)d_t2, s2, 255u, K, 1, tot2);
+        hipLaunchKernelGGL(k_msd_plan2, dim3(1), dim3(1024), 0, stream, (const unsigned int*)tot2, nsub, base2, (unsigned int)kGrpCap,
+                           d_flag + 4);
+        hipLaunchKernelGGL(k_grp_scatter<false>, dim3((unsigned)nt2c), dim3(kGrpScatBlock), 0, stream, (const uint32_t*)km_k[0].p,
+                           (const int64_t*)km_val[0].p, (const GrpTile*)d_t2, s2, 255u, K, 1, (const int64_t*)base2, cur2,
+                           (uint32_t*)km_k[1].p, (int64_t*)km_val[1].p, (const uint32_t*)nullptr, (uint32_t*)nullptr);
         phase_end(ph);
+        hipMemcpyAsync(h_kmf, d_flag, 32, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping partition failed");
+        const unsigned int mx = h_kmf[5];
+        if (h_kmf[4]) return 0;   // a sub-bucket above kGrpCap rows (skewed keys): the caller's path
         GrpDesc g{};
         g.base2 = base2;
         g.keys = (const uint32_t*)km_k[1].p;

@@ -829,7 +829,8 @@ __global__ __launch_bounds__(1024) void k_msd_plan1(const unsigned int* __restri
     }
     for (int64_t k = s_nt[256] + t; k < ntc; k += 1024) tiles2[k] = GrpTile{0, 0, 0};
 }
-// pass 2's sub-bucket counts -> exclusive starts base2[nsub + 1]; a sub-bucket above kKmFixCap rows sets *over
+// pass 2's sub-bucket counts -> exclusive starts base2[nsub + 1]; a sub-bucket above cap rows sets over[0], and
+// over[1] gets the largest sub-bucket (atomicMax)
 __global__ __launch_bounds__(1024) void k_msd_plan2(const unsigned int* __restrict__ tot2, int nsub, int64_t* __restrict__ base2,
                                                     unsigned int cap, unsigned int* __restrict__ over) {
     __shared__ int64_t wsum[16];
@@ -839,6 +840,7 @@ __global__ __launch_bounds__(1024) void k_msd_plan2(const unsigned int* __restri
     unsigned int mx = 0;
     for (int i = a; i < e; ++i) { sm += tot2[i]; mx = max(mx, tot2[i]); }
     if (mx > cap) atomicOr(over, 1u);
+    if (mx) atomicMax(over + 1, mx);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int64_t v = sm;
     for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(v, o, 64); if (lane >= o) v += y; }
