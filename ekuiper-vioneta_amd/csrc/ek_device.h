@@ -57,6 +57,9 @@ struct DPlan {
     ek_instr begin_prog[EK_MAX_PROG];
     ek_instr emit_prog[EK_MAX_PROG];
     int32_t having_star;          // HAVING reads no aggregate but count(*): decidable from a group's row count alone
+    // median over a nullable f64 column: its hidden EK_AGG_FIRST slot (the group's first row), -1 otherwise; a nil
+    // there is the reference's "<nil> should be number" (funcs_agg.go:36-52)
+    int32_t med_first[EK_MAX_AGGS];
 };
 
 // Columns of one micro-batch (device pointers).

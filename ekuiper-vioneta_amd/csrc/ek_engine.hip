@@ -654,8 +654,15 @@ struct Engine {
             case EK_AGG_MAX: f = NEED_MAX; break;
             case EK_AGG_MEDIAN: case EK_AGG_PERCENTILE_CONT: case EK_AGG_PERCENTILE_DISC: {
                 // order statistics over the group's values (range mode, k_agg sort pass)
-                if (a.fn == EK_AGG_MEDIAN && nullable)
-                    return fail(EK_ERR_UNSUPPORTED, "median over a nullable column (nil first element is a type error)");
+                if (a.fn == EK_AGG_MEDIAN && nullable) {
+                    // funcs_agg.go:29-55: a group whose first value is nil is a type error, an f64 column ignores the
+                    // other nils. Built for f64 columns without HAVING (the check runs on the emitted rows); a BIGINT
+                    // column fails on any nil with a text naming the whole group
+                    if (!fl || plan.n_having > 0)
+                        return fail(EK_ERR_UNSUPPORTED, "median over a nullable %s column (nil first element is a type error)",
+                                    fl ? "float column with HAVING" : "bigint");
+                    med_nullable.push_back(k);
+                }
                 if (dp.n_sagg >= kMaxSortAggs) return fail(EK_ERR_UNSUPPORTED, "too many median/percentile calls");
                 int sc = -1;
                 for (int x = 0; x < dp.n_scol; ++x) if (dp.scol_vc[x] == v) sc = x;
@@ -699,6 +706,34 @@ struct Engine {
             dp.agg_sidx[inc_hidden] = -1;
             dp.vc_flags[v] |= NEED_MAX;
             dp.n_aggs = plan.n_aggs + 1;
+        }
+        for (int k = 0; k < EK_MAX_AGGS; ++k) dp.med_first[k] = -1;
+        for (int k : med_nullable) {
+            // the group's first row over the median's column: a hidden EK_AGG_FIRST slot (k_first_fetch checks it)
+            if (dp.n_aggs >= EK_MAX_AGGS) return fail(EK_ERR_UNSUPPORTED, "median over a nullable column needs a free aggregate slot");
+            if (rowpos_col < 0) {
+                if (plan.n_columns >= EK_MAX_COLUMNS) return fail(EK_ERR_UNSUPPORTED, "too many columns for a first-row field");
+                rowpos_col = plan.n_columns;
+                dp.col_type[rowpos_col] = EK_COL_I64;
+            }
+            int v = -1;
+            for (int x = 0; x < dp.n_vc; ++x) if (dp.vc_col[x] == rowpos_col) v = x;
+            if (v < 0) {
+                if (dp.n_vc >= kMaxVC) return fail(EK_ERR_UNSUPPORTED, "too many aggregated columns");
+                v = dp.n_vc++;
+                dp.vc_col[v] = rowpos_col;
+                dp.vc_is_float[v] = 0;
+                dp.vc_flags[v] = 0;
+            }
+            const int h = dp.n_aggs++;
+            dp.agg_fn[h] = EK_AGG_FIRST;
+            dp.agg_vc[h] = v;
+            dp.agg_sidx[h] = -1;
+            dp.agg_p[h] = 0;
+            dp.vc_flags[v] |= NEED_MIN;
+            dp.first_col[h] = plan.aggs[k].column;
+            dp.n_first++;
+            dp.med_first[k] = h;
         }
         n_res = dp.n_aggs > n_out ? dp.n_aggs : n_out;
         for (int v = 0; v < dp.n_vc; ++v) {
@@ -818,7 +853,7 @@ struct Engine {
             having_can_fail = dp.n_having > 0 && prog_can_fail(dp.having_prog, dp.n_having, dp.agg_fn, dp.col_type);
         }
         for (int k = 0; k < dp.n_aggs; ++k)
-            agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC;
+            agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC || dp.med_first[k] >= 0;
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
         if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
         if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
@@ -3413,6 +3448,7 @@ struct Engine {
     // after their bound), the buffer rows [sw2_cut, released by the tuple) are the live inputs, a window is the fixed
     // range of live rows with ts in its bounds. Triggers wait in delayq (pos_abs, ts, release step), timers in proc_dq.
     int64_t et2_prev = kYear1Ms;          // prevWindowEndTs
+    std::vector<int> med_nullable;        // median slots over a nullable f64 column (their nil-first check)
     int et2_triggers(int64_t rel_prev, const std::vector<DelayTrig>& trig, std::vector<PendWin>& pw) {
         const int64_t D = slide_delay_et(), tol = plan.late_tolerance_ms;
         const int64_t n_new = eb_rel - rel_prev;
@@ -5159,6 +5195,7 @@ struct Engine {
     // host over the window's witness (ek_errmsg.h). Precedence follows the reference's operator order: FilterOp, then
     // HavingOp, then ProjectOp (planner.go:387-446) — a window the WHERE failed never reaches HAVING.
     static const char* order_stat_error(int fn) {   // funcs_agg.go:321-326,357-362 over stats v0.7.1 ErrBounds
+        if (fn == EK_AGG_MEDIAN) return "<nil> should be number";   // funcs_agg.go:51-52 (a nil first value)
         return fn == EK_AGG_PERCENTILE_DISC ? "PopulationVariance exec with error: Input is outside of range."
                                             : "percentile exec with error: Input is outside of range.";
     }

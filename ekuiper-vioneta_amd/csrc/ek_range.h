@@ -562,6 +562,14 @@ __global__ void k_first_fetch(DPlan* __restrict__ pp, DBatch b, const int32_t* _
                 res.val[q][r] = col_i64(p, b, c, pos);
             }
         }
+        // median over a nullable f64 column whose group starts with a nil (arg0[0] is not a number): the window's
+        // aggregate error, at the smallest failing order-statistic slot; a WHERE error already replaced the window
+        for (int q = 0; q < p.n_aggs; ++q) {
+            const int h = p.med_first[q];
+            if (h < 0 || res.tag[h][r] != EK_TAG_NULL || (res.win_err[slot] & EK_WIN_WHERE_ERROR)) continue;
+            atomicOr(&res.win_err[slot], EK_WIN_AGG_ERROR);
+            if (res.aslot) atomicMax(&res.aslot[slot], kMaxSortAggs - p.agg_sidx[q]);
+        }
     }
 }
 #endif
