@@ -19,6 +19,7 @@ constexpr uint32_t kPseudoKeys = 65536;   // partial slots of an un-grouped pane
 enum : int { NEED_CNT = 1, NEED_SUM = 2, NEED_MIN = 4, NEED_MAX = 8, NEED_M2 = 16, NEED_FSUM = 32, NEED_SORT = 64 };
 constexpr int kMaxScol = 2;       // value columns of median / percentile_* (key-grouped scatter each)
 constexpr int kMaxSortAggs = 4;   // median / percentile_* calls per rule
+constexpr int kHStarTab = 2049;   // HAVING over count(*) alone decided per row count 0..2048 (k_small_win's windows)
 
 struct DPlan {
     int32_t n_columns;
@@ -60,6 +61,9 @@ struct DPlan {
     // median over a nullable f64 column: its hidden EK_AGG_FIRST slot (the group's first row), -1 otherwise; a nil
     // there is the reference's "<nil> should be number" (funcs_agg.go:36-52)
     int32_t med_first[EK_MAX_AGGS];
+    // having_star: the decision for a group of c rows (1 keep, 0 drop, -1 non-bool), c < kHStarTab, filled on the
+    // device at create time by k_hstar_tab (the same evaluator), so k_small_win<HS> carries no interpreter
+    int8_t hstar_tab[kHStarTab];
 };
 
 // Columns of one micro-batch (device pointers).

@@ -795,6 +795,7 @@ struct Engine {
         km_merge_sort = env_int("EKGPU_KM_MERGE_SORT", 1);
         km_msd_on = env_int("EKGPU_KM_MSD", 1);
         count_direct = env_int("EKGPU_COUNT_DIRECT", 1);
+        sw_cap_on = env_int("EKGPU_SW_CAP", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
@@ -856,6 +857,13 @@ struct Engine {
             agg_can_fail |= dp.agg_fn[k] == EK_AGG_PERCENTILE_CONT || dp.agg_fn[k] == EK_AGG_PERCENTILE_DISC || dp.med_first[k] >= 0;
         if (hipMalloc((void**)&d_plan, sizeof(DPlan)) != hipSuccess) return fail(EK_ERR_NOMEM, "plan alloc");
         if (hipMemcpy(d_plan, &dp, sizeof(DPlan), hipMemcpyHostToDevice) != hipSuccess) return fail(EK_ERR_DEVICE, "plan copy");
+        if (dp.having_star) {
+            // HAVING over count(*) alone, decided once per row count by the device evaluator (k_small_win<HS> reads it)
+            hipLaunchKernelGGL(k_hstar_tab, dim3(1), dim3(256), 0, stream, d_plan);
+            if (hipMemcpyAsync(dp.hstar_tab, d_plan->hstar_tab, sizeof dp.hstar_tab, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                hipStreamSynchronize(stream) != hipSuccess)
+                return fail(EK_ERR_DEVICE, "HAVING table failed");
+        }
         if (hipHostMalloc((void**)&h_stats, sizeof(BatchStats)) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned alloc");
         if (int rc = ensure(bstats, sizeof(BatchStats))) return rc;
         if (int rc = alloc_state()) return rc;
@@ -2070,10 +2078,35 @@ struct Engine {
     int sw_grid = 4096;   // EKGPU_SW_GRID: waves of a k_small_win launch
     bool fin_ring = true;       // EKGPU_FIN_RING=0: hopping windows always through k_finalize
     int fin_ring_chunks = 0;    // EKGPU_FIN_RING_CHUNKS: window chunks of a k_finalize_ring launch (0: by the key blocks)
-    void small_win_launch(int nb, const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot,
-                          const int64_t* ob, int max_n, SwArith ar) {
-        ek::launch_small_win(std::max(1, dp.n_vc), dp.n_where > 0, max_n <= 16 * kSwLanes ? 16 : kSwRows, std::min(nb, sw_grid), nb,
-                             sw_lds_bytes(max_n), stream, d_plan, src, ab, wl, slot, ob, results_view(), ar);
+    // HS: HAVING absent or over count(*) alone (decided from dp.hstar_tab): the kernel carries no interpreter. When the
+    // full candidate tables would cost more LDS than the bitmaps, the launch caps them (kSwCandCap rows) and a second
+    // launch redoes the few windows with more candidates (their list and count stay on the device)
+    DevBuf sw_redo;
+    int sw_cap_on = 1;   // EKGPU_SW_CAP=0: one launch with the full tables
+    int small_win_launch(int nb, const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot,
+                         const int64_t* ob, int max_n, SwArith ar) {
+        const int nvc = std::max(1, dp.n_vc), rm = max_n <= 16 * kSwLanes ? 16 : kSwRows;
+        const bool hs = dp.n_having == 0 || dp.having_star;
+        const bool capped = sw_cap_on && sw_lds_bytes_capped(max_n) < sw_lds_bytes(max_n);
+        SwRedo rd{};
+        if (capped) {
+            if (int rc = ensure(sw_redo, ((size_t)nb + 1) * 4)) return rc;
+            rd.cap = kSwCandCap;
+            rd.cnt = (int32_t*)sw_redo.p;
+            rd.out = rd.cnt + 1;
+            hipMemsetAsync(rd.cnt, 0, 4, stream);
+        }
+        ek::launch_small_win(nvc, dp.n_where > 0, rm, hs, std::min(nb, sw_grid), nb,
+                             capped ? sw_lds_bytes_capped(max_n) : sw_lds_bytes(max_n), stream, d_plan, src, ab, wl, slot, ob,
+                             results_view(), ar, rd);
+        if (capped) {
+            SwRedo r2{};
+            r2.cnt = rd.cnt;
+            r2.in = rd.out;
+            ek::launch_small_win(nvc, dp.n_where > 0, rm, hs, std::min(nb, 256), nb, sw_lds_bytes(max_n), stream, d_plan, src, ab,
+                                 wl, slot, ob, results_view(), ar, r2);
+        }
+        return 0;
     }
 
     int fire_windows(std::vector<PendWin>& pw) {
@@ -5669,7 +5702,7 @@ struct Engine {
         for (DevBuf* d : {&rq_d, &ab_d, &slot_d, &trig_d, &flags_d, &cnts_d, &runmax_d, &runcm_d, &mrg_keys[0], &mrg_keys[1],
                           &mrg_src[0], &mrg_src[1], &mrg_tmp, &mrg_tail, &mrg_bidx, &mrg_col, &vp_err, &vp_mc, &vp_mh, &sort_pbase, &sort_scr, &chunk_pa, &sw_d,
                           &km_k[0], &km_k[1], &km_p[0], &km_p[1], &km_tmp, &km_start, &km_ab, &km_bcnt, &km_flag, &rowpos, &ff_d,
-                          &grp_tiles, &grp_cnt, &grp_base})
+                          &grp_tiles, &grp_cnt, &grp_base, &sw_redo})
             release(*d);
         for (int v = 0; v < kMaxVC; ++v) { release(km_val[v]); release(km_ok[v]); }
         if (h_kmf) hipHostFree(h_kmf);

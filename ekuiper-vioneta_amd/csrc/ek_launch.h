@@ -27,11 +27,12 @@ void launch_fin_ring(int r, bool vc, bool hv, dim3 grid, hipStream_t s, DPlan* p
 void launch_ung(int nvc, bool where, dim3 grid, hipStream_t s, DPlan* p, const DBatch& db, const GroupDesc& gd,
                 const uint8_t* acc, const DState& ds, int64_t tile, int32_t* pane_err);
 
-// small range windows (ek_range.h): k_small_win<NVC, WHERE, RM>, RM = rows per lane (16: windows up to 1024 rows);
-// `grid` persistent waves over `nwin` windows
-void launch_small_win(int nvc, bool where, int rm, int grid, int nwin, size_t lds, hipStream_t s, DPlan* p,
+// small range windows (ek_range.h): k_small_win<NVC, WHERE, RM, HS>, RM = rows per lane (16: windows up to 1024 rows),
+// HS = HAVING absent or over count(*) alone (table-decided); `grid` persistent waves over `nwin` windows, rd: the
+// candidate cap and redo list
+void launch_small_win(int nvc, bool where, int rm, bool hs, int grid, int nwin, size_t lds, hipStream_t s, DPlan* p,
                       const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot, const int64_t* ob,
-                      const Results& res, const SwArith& ar);
+                      const Results& res, const SwArith& ar, const SwRedo& rd);
 
 // key-major walks (ek_keymajor.h): k_km_walk<NVC, SORT, WRITE, ONE>, k_grp_walk<SORT, ISF, R>
 void launch_km_walk(int nvc, bool sort, bool write, bool one, int nblk, size_t lds, hipStream_t s, DPlan* p,

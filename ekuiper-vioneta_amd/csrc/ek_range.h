@@ -686,6 +686,16 @@ inline size_t sw_lds_bytes(int max_n) {
     const size_t tab = (size_t)sw_slots(max_n) * 6 + (((size_t)max_n * 2 + 3) & ~(size_t)3) + (size_t)max_n * 4;
     return std::max(tab, (size_t)sw_bits(max_n) / 4);
 }
+// A launch whose candidate tables are capped at kSwCandCap rows: the LDS is about the bitmaps alone (8 KB at 1 000
+// rows), so 4 waves share a SIMD; a window with more candidate rows is left to a second launch with the full tables
+// (its index in the redo list). Typical windows over a large key space hold a handful of candidates.
+constexpr int kSwCandCap = 256;
+inline size_t sw_lds_bytes_capped(int max_n) {
+    const int c = std::min(max_n, kSwCandCap);
+    const size_t tab = (size_t)sw_slots(c) * 6 + (((size_t)c * 2 + 3) & ~(size_t)3) + (size_t)c * 4;
+    return std::max(tab, (size_t)sw_bits(max_n) / 4);
+}
+static_assert(kSmallWin + 1 <= kHStarTab, "the count-decision table covers every small window");
 
 // a window group's rows (indices into the window, distinct) into ascending order, so the group folds its values in
 // the window's row order: the f64 sums are the reference's sequential ones, whatever order the LDS atomics of the
@@ -732,6 +742,14 @@ struct SwArith {
     int64_t a0, ob0, rowcap;
     int32_t len, slot0;
 };
+// k_small_win's redo list: cap > 0 (the capped launch) appends the work items with more candidate rows to out[] via
+// *cnt; in != nullptr (the redo launch) runs in[0 .. *cnt)
+struct SwRedo {
+    int32_t cap;
+    int32_t* out;
+    int32_t* cnt;
+    const int32_t* in;
+};
 
 // HAVING decision (1 keep, 0 drop, -1 non-bool: a window error) of a group's partial, without side effects
 template <int NVC>
@@ -741,22 +759,38 @@ __device__ __forceinline__ int having_decide(const DPlan& p, const Part<NVC>& s)
     if (h.tag != V_BOOL) return -1;
     return h.i != 0 ? 1 : 0;
 }
-// HAVING over count(*) alone, decided from a group's row count c (the decisions for 1 and 2 rows are cached)
-template <int NVC>
+// HAVING over count(*) alone, decided from a group's row count c (the decisions for 1 and 2 rows are cached; HS: all
+// of them, from the plan's table)
+template <int NVC, bool HS>
 __device__ __forceinline__ int having_star_decide(const DPlan& p, int c, int h1, int h2) {
     if (c == 1) return h1;
     if (c == 2) return h2;
-    Part<NVC> cp{};
-    cp.cnt = c;
-    return having_decide(p, cp);
+    if constexpr (HS) {
+        return p.hstar_tab[c < kHStarTab ? c : kHStarTab - 1];
+    } else {
+        Part<NVC> cp{};
+        cp.cnt = c;
+        return having_decide(p, cp);
+    }
 }
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_hstar_tab(DPlan* __restrict__ pp) {
+    for (int c = threadIdx.x; c < kHStarTab; c += blockDim.x) {
+        Part<1> cp{};
+        cp.cnt = c;
+        pp->hstar_tab[c] = (int8_t)having_decide(*pp, cp);
+    }
+}
+#endif
 
 // One small window per call: rows [a, a + n) of b, keys already in key[] (lane + 64 j), result region out, slot widx.
-// Returns the rows emitted (-1: a WHERE error replaced the window's output).
-template <int NVC, bool WHERE, int RM>
+// Returns the rows emitted (-1: a WHERE error replaced the window's output; -2: more than cand_cap candidate rows —
+// nothing was written, the window goes to the redo launch). HS: HAVING is absent or reads count(*) alone (decided
+// from the plan's table; no interpreter in the kernel).
+template <int NVC, bool WHERE, int RM, bool HS>
 __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, const uint32_t* kcol, int64_t a, int n,
                                              int32_t widx, int64_t out, const uint32_t (&key)[RM], Results& res,
-                                             uint32_t* s_dyn, int h1, int h2) {
+                                             uint32_t* s_dyn, int h1, int h2, int cand_cap) {
     const int lane = threadIdx.x;
     uint32_t live = 0;   // bit j: row lane + 64 j is in the window (and its WHERE is true)
 #pragma unroll
@@ -804,6 +838,10 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
         if ((s_dupb[h >> 5] >> (h & 31u)) & 1u) cand |= 1u << j;
     }
     __syncthreads();   // the bitmaps are dead: their LDS is reused below
+    int nc = __popc(cand);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, kSwLanes);
+    if (cand_cap > 0 && nc > cand_cap) return -2;   // the capped launch's tables cannot hold them: redo launch
     const uint32_t single = live & ~cand;
     int fl[NVC], col[NVC];
     bool isf[NVC];
@@ -908,11 +946,12 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
     };
     auto keep = [&](const Part<NVC>& s, int c, uint32_t k) -> bool {
         if (p.having_star) {
-            const int d = having_star_decide<NVC>(p, c, h1, h2);
+            const int d = having_star_decide<NVC, HS>(p, c, h1, h2);
             if (d < 0) { herr = true; star_wit(c, k); }
             return d > 0;
         }
-        return having_keep(p, s, res, widx, k);
+        if constexpr (HS) return true;   // no HAVING
+        else return having_keep(p, s, res, widx, k);
     };
     // ---- one-row groups, straight from their lanes (coalesced value loads; a rolled loop: one copy of the fold)
     if (__any(single != 0u) && !(p.having_star && h1 == 0)) {
@@ -928,9 +967,6 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
             emit(present, s, sel(key, j));
         }
     }
-    int nc = __popc(cand);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o, kSwLanes);
     if (nc > 0) {
         // ---- the candidates (real duplicates + hash collisions): an LDS hash table over them sized by their count
         // (linear probing, 16-bit counts packed two per word), a slot scan into group offsets (groups HAVING over
@@ -968,7 +1004,7 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
                 if (c == 0) continue;
                 int d = 1;
                 if (p.having_star) {
-                    d = having_star_decide<NVC>(p, c, h1, h2);
+                    d = having_star_decide<NVC, HS>(p, c, h1, h2);
                     if (d < 0) { herr = true; star_wit(c, s_key[s0 + q + hh]); }
                 }
                 if (d > 0) x += 0x10000u + (uint32_t)c;
@@ -989,7 +1025,7 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
                 for (int hh = 0; hh < 2; ++hh) {
                     const int c = (int)((wd >> (16 * hh)) & 0xFFFFu);
                     int d = c > 0 ? 1 : 0;
-                    if (c > 0 && p.having_star) d = having_star_decide<NVC>(p, c, h1, h2);
+                    if (c > 0 && p.having_star) d = having_star_decide<NVC, HS>(p, c, h1, h2);
                     if (d > 0) {
                         s_grp[run >> 16] = ((run & 0xFFFFu) << 16) | (uint32_t)c;
                         cur |= (run & 0xFFFFu) << (16 * hh);
@@ -1026,7 +1062,8 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
                     k = kcol ? kcol[a + s_row[g0]] : 0u;
                     fold(s, c, [&](int u) { return (int)s_row[g0 + u]; });
                     // HAVING over count(*) alone was decided by the slot scan
-                    present = p.having_star ? true : having_keep(p, s, res, widx, k);
+                    if constexpr (HS) present = true;
+                    else present = p.having_star ? true : having_keep(p, s, res, widx, k);
                 }
                 emit(present, s, k);
             }
@@ -1038,23 +1075,33 @@ __device__ __forceinline__ int64_t sw_window(const DPlan& p, const DBatch& b, co
 }
 
 // Persistent waves over the launch's windows (grid-stride): the next window's keys are loaded while this one is
-// grouped, so a wave never waits for its keys after the first window.
-template <int NVC, bool WHERE, int RM>
+// grouped, so a wave never waits for its keys after the first window. Redo: cand_cap > 0 sends a window with more
+// candidate rows to redo_out (work-item indices, counter redo_cnt); a launch with redo_in runs those items alone
+// (their count read from redo_cnt) with cand_cap 0 and the full tables.
+template <int NVC, bool WHERE, int RM, bool HS>
 __global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, DBatch b, const int64_t* __restrict__ ab,
                                                        const int32_t* __restrict__ wlist, const int32_t* __restrict__ slots,
-                                                       const int64_t* __restrict__ obase, Results res, int nwin, SwArith ar) {
+                                                       const int64_t* __restrict__ obase, Results res, int nwin, SwArith ar,
+                                                       SwRedo rd) {
     const DPlan& p = *pp;
     const int lane = threadIdx.x;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     const uint32_t* kcol = p.key_col >= 0 ? (const uint32_t*)b.col[p.key_col] : nullptr;
+    if (rd.in) nwin = *rd.cnt;   // the redo launch: the items the capped launch left
+    auto item = [&](int t) { return rd.in ? rd.in[t] : t; };
     // HAVING over count(*) alone: the decisions for one- and two-row groups, once per wave
     int h1 = 1, h2 = 1;
     if (p.having_star) {
-        Part<NVC> cp{};
-        cp.cnt = 1;
-        h1 = having_decide(p, cp);
-        cp.cnt = 2;
-        h2 = having_decide(p, cp);
+        if constexpr (HS) {
+            h1 = p.hstar_tab[1];
+            h2 = p.hstar_tab[2];
+        } else {
+            Part<NVC> cp{};
+            cp.cnt = 1;
+            h1 = having_decide(p, cp);
+            cp.cnt = 2;
+            h2 = having_decide(p, cp);
+        }
     }
     auto window_a = [&](int i) { return wlist ? ab[2 * wlist[i]] : ar.a0 + (int64_t)i * ar.len; };
     auto window_n = [&](int i) { return wlist ? (int)(ab[2 * wlist[i] + 1] - ab[2 * wlist[i]]) : ar.len; };   // 1..kSmallWin
@@ -1065,18 +1112,20 @@ __global__ __launch_bounds__(kSwLanes) void k_small_win(DPlan* __restrict__ pp, 
 #pragma unroll
         for (int j = 0; j < RM; ++j) k[j] = (kcol && lane + j * kSwLanes < n) ? kcol[a + lane + j * kSwLanes] : 0u;
     };
-    int i = blockIdx.x;
-    if (i < nwin) load_keys(i, key);
-    for (; i < nwin; i += gridDim.x) {
+    int t = blockIdx.x;
+    if (t < nwin) load_keys(item(t), key);
+    for (; t < nwin; t += gridDim.x) {
+        const int i = item(t);
         const int w = wlist ? wlist[i] : i;
         const int64_t a = window_a(i);
         const int n = window_n(i);
         const int32_t widx = wlist ? slots[w] : ar.slot0 + i;
         const int64_t out = wlist ? obase[w] : ar.ob0 + (int64_t)i * ar.rowcap;
         uint32_t nkey[RM] = {};
-        if (i + (int)gridDim.x < nwin) load_keys(i + gridDim.x, nkey);
-        const int64_t e = sw_window<NVC, WHERE, RM>(p, b, kcol, a, n, widx, out, key, res, s_dyn, h1, h2);
+        if (t + (int)gridDim.x < nwin) load_keys(item(t + gridDim.x), nkey);
+        const int64_t e = sw_window<NVC, WHERE, RM, HS>(p, b, kcol, a, n, widx, out, key, res, s_dyn, h1, h2, rd.cap);
         if (e >= 0 && lane == 0) res.win_cnt[widx] = e;
+        if (e == -2 && lane == 0) rd.out[atomicAdd(rd.cnt, 1)] = i;
 #pragma unroll
         for (int j = 0; j < RM; ++j) key[j] = nkey[j];
     }
