@@ -2391,7 +2391,7 @@ struct Engine {
         const size_t gl = grp_walk_lds(s2, rdep);
         const dim3 gg((unsigned)nsub), gb(kGrpWalkBlock);
         const bool isf = dp.vc_is_float[0] != 0;
-        ek::launch_grp_walk(sort, isf, rdep, gg, gb, gl, stream, d_plan, g, rv);
+        ek::launch_grp_walk(sort, isf, rdep, dp.n_having > 0, gg, gb, gl, stream, d_plan, g, rv);
         phase_end(ph2);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "grouping walk failed");
         *ok = true;

@@ -933,7 +933,8 @@ struct GrpDesc {
 // SORT, every row's rank inside its key's segment (values below it, ties broken by position) is counted from the
 // grouped LDS copy with independent reads, then the row is stored at its rank: the segments come out sorted with no
 // dependent per-key insertion chain (the time of a wave is its longest segment, not that segment squared).
-template <bool SORT, bool ISF, int R>
+// HV: the plan has a HAVING (without one the kernel carries no interpreter: 123 -> 85 VGPRs, 5 waves/SIMD).
+template <bool SORT, bool ISF, int R, bool HV>
 __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ pp, GrpDesc g, Results res) {
     extern __shared__ __attribute__((aligned(16))) unsigned char g_lds[];
     const DPlan& p = *pp;
@@ -1049,7 +1050,8 @@ __global__ __launch_bounds__(kGrpWalkBlock) void k_grp_walk(DPlan* __restrict__ 
                     for (int a = p.n_sagg - 1; a >= 0; --a) if (sel(stag, a) == kTagErr) ea = a;
                     if (res.aslot) atomicMax(&res.aslot[g.widx], kMaxSortAggs - ea);
                 } else {
-                    const int hv = km_having(p, part, SORT ? &sr : nullptr);
+                    int hv = 1;
+                    if constexpr (HV) hv = km_having(p, part, SORT ? &sr : nullptr);
                     if (hv < 0) {
                         atomicOr(&res.win_err[g.widx], EK_WIN_HAVING_ERROR);
                         if (res.wwit)
