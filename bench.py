@@ -642,6 +642,10 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    # the engine's library links the system HIP runtime, torch its own: wait on the engines' streams themselves
+    eng.sync()
+    if cnt_eng is not None:
+        cnt_eng.sync()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -689,7 +693,9 @@ def main():
         if ph == "stats":
             kb = n * 8 if iet else 0
         elif ph == "partition":
-            kb = n * sum(COL_BYTES[c] for c in cfg["in_cols"] if c != "ts")
+            # (the fused sorted pass reads ts in the partition pass itself: no stats phase then)
+            fused = iet and ph_n[PHASES.index("stats")] == 0
+            kb = n * sum(COL_BYTES[c] for c in cfg["in_cols"] if c != "ts" or fused)
         elif ph_n[PHASES.index("partition")] == 0:
             # no partition pass (range windows: k_small_win / the key-major walks read the event columns
             # themselves): the aggregate kernels move the step's bytes less what the stats pass read
@@ -735,6 +741,7 @@ def main():
                      "required_bytes": required,
                      "dominant_kernel": dominant, "kernels": kernels},
     }
+    out["config"]["fused_sorted_batches_last_step"] = int(st1.fused_batches)   # (stream counters restart at ek_reset)
     if global_count is not None:
         out["config"]["global_count"] = str(global_count)[:200]
         out["config"]["shared_ts_stats"] = bool(share_stats)

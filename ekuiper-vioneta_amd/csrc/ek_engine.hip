@@ -235,6 +235,8 @@ struct Engine {
     int64_t arrivals = 0;
     bool time_pending = false;         // the last push's end event is recorded but not yet read (fold_time)
     bool async_push = false;           // ek_set_async: pushes return with their work queued
+    hipEvent_t ev_h2d = nullptr;       // asynchronous pushes: the host batch's copies are done
+    bool h2d_pending = false;
     std::vector<int64_t> slot_pane;    // pane id held by each ring slot (INT64_MIN = free)
     PaneGrid grid{};
     ek_stats stats{};
@@ -782,6 +784,9 @@ struct Engine {
         }
         chunk = env_int("EKGPU_CHUNK", 8192);
         sorted_chunk = env_int("EKGPU_SORTED_CHUNK", kTile);
+        // the fused sorted pass is built and parity-tested but off by default: measured on MI355X it moves the same
+        // bytes at the same mixed read/write rate as k_stats + k_part and keeps two round trips
+        fz_on = env_int("EKGPU_FUSED", 0);
         small_win_on = env_int("EKGPU_SMALL_WIN", 1) != 0;
         sw_grid = std::max(1, env_int("EKGPU_SW_GRID", 4096));
         fin_ring = env_int("EKGPU_FIN_RING", 1) != 0;
@@ -1361,21 +1366,27 @@ struct Engine {
         struct Grp { int64_t lo, hi, qa, qb; int64_t q_done; int64_t bk; };
         const int64_t pane_cap = (int64_t)(kMaxRuns - 2) * chunk;   // k_agg run list bound per pane
         std::vector<Grp> groups;
+        const int64_t* fz_b = nullptr;   // the fused sorted pass's pane bounds (k_part MODE 3 already ran)
         if (sorted) {
-            // pane boundaries by binary search on the sorted ts column
             int64_t nq = q_hi - q_lo + 1;
             int nb = (int)nq + 1;
-            if (h_small_cap < (size_t)(2 * nb)) {
-                if (h_small) { hipStreamSynchronize(stream); hipHostFree(h_small); }
-                h_small_cap = std::max<size_t>(2 * nb, 4096);
-                if (hipHostMalloc((void**)&h_small, h_small_cap * 8) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
+            if (fz_pass.on) {
+                if (fz_pass.q_lo != q_lo || fz_pass.nq != nq) return fail(EK_ERR_STATE, "fused pass pane range mismatch");
+                fz_b = fz_pass.pbnd;
+            } else {
+                // pane boundaries by binary search on the sorted ts column
+                if (h_small_cap < (size_t)(2 * nb)) {
+                    if (h_small) { hipStreamSynchronize(stream); hipHostFree(h_small); }
+                    h_small_cap = std::max<size_t>(2 * nb, 4096);
+                    if (hipHostMalloc((void**)&h_small, h_small_cap * 8) != hipSuccess) return fail(EK_ERR_NOMEM, "pinned");
+                }
+                if (int rc = ensure(bounds_idx, (size_t)nb * 8)) return rc;
+                hipLaunchKernelGGL(k_pane_bounds, dim3((nb + kBoundsBlock / 64 - 1) / (kBoundsBlock / 64)), dim3(kBoundsBlock), 0, stream,
+                                   (const int64_t*)db.col[dp.ts_col], start, n, grid, q_lo, nb, (int64_t*)bounds_idx.p);
+                hipMemcpyAsync(h_small + nb, bounds_idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream);
+                if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "bounds sync failed");
             }
-            if (int rc = ensure(bounds_idx, (size_t)nb * 8)) return rc;
-            hipLaunchKernelGGL(k_pane_bounds, dim3((nb + kBoundsBlock / 64 - 1) / (kBoundsBlock / 64)), dim3(kBoundsBlock), 0, stream,
-                               (const int64_t*)db.col[dp.ts_col], start, n, grid, q_lo, nb, (int64_t*)bounds_idx.p);
-            hipMemcpyAsync(h_small + nb, bounds_idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream);
-            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "bounds sync failed");
-            const int64_t* b = h_small + nb;
+            const int64_t* b = fz_b ? fz_b : h_small + nb;
             // greedy grouping of consecutive panes; a pane larger than the target is split
             int64_t k = 0;
             while (k < nq) {
@@ -1412,7 +1423,8 @@ struct Engine {
             }
         }
 
-        const int64_t* bidx = sorted ? h_small + (q_hi - q_lo + 2) : nullptr;
+        const int64_t* bidx = sorted ? (fz_b ? fz_b : h_small + (q_hi - q_lo + 2)) : nullptr;
+        if (fz_pass.on && groups.size() != 1) return fail(EK_ERR_STATE, "fused pass split into %zu groups", groups.size());
         for (const Grp& g : groups) {
             if (g.hi > g.lo) {
                 // pane boundaries of the group (sorted batches): pbnd[k] = first event of pane qa + k
@@ -1476,6 +1488,8 @@ struct Engine {
             csz >>= 1;
             mp = max_panes_in_chunk(pbnd_host, gd, csz);
         }
+        if (fz_pass.on && (csz != kTile || mp > fz_pass.mp))
+            return fail(EK_ERR_STATE, "fused pass geometry mismatch (chunk %lld, %d panes per chunk)", (long long)csz, mp);
         gd.chunk = csz;
         gd.key_col = dp.key_col;
         gd.ts_col = dp.ts_col;
@@ -1510,11 +1524,12 @@ struct Engine {
         }
         if (int rc = upload_aux(aux, aux_words, npn, gd)) return rc;
         // largest chunk-local partition count: sorted chunks touch at most the panes their index range spans
-        const int lp_stride = gd.sorted ? std::min(gd.np, NB * mp) : gd.np;
+        const int lp_stride = fz_pass.on ? fz_pass.ls - 1 : (gd.sorted ? std::min(gd.np, NB * mp) : gd.np);
         if (lp_stride > np_max || (gd.sorted && mp > kMaxChunkBnd + 1))
             return fail(EK_ERR_UNSUPPORTED, "chunk spans %d partitions (split the batch)", lp_stride);
-        if (int mc = max_chunks_in_pane(pbnd_host, gd, gd.chunk); mc > kMaxRuns)
-            return fail(EK_ERR_UNSUPPORTED, "a pane spans %d chunks of one group (max %d)", mc, kMaxRuns);
+        const int mc = max_chunks_in_pane(pbnd_host, gd, gd.chunk);
+        if (mc > kMaxRuns) return fail(EK_ERR_UNSUPPORTED, "a pane spans %d chunks of one group (max %d)", mc, kMaxRuns);
+        gd.mruns = std::max(1, mc);
         return launch_part_agg(db, gd, gd.sorted ? 1 : 0, d_acc, (int32_t*)pane_err.p, (int64_t*)pane_mcnt.p,
                                (unsigned long long*)pane_mhash.p, lp_stride, any_fresh);
     }
@@ -1573,7 +1588,7 @@ struct Engine {
         if (any_fresh)
             hipLaunchKernelGGL(k_group_prep, dim3((gd.n_panes + 255) / 256), dim3(256), 0, stream, gd, perr, pmc, pmh);
         const bool wh = dp.n_where > 0;
-        {
+        if (!fz_pass.on) {   // (the fused sorted pass already partitioned the batch: same staging, ctab and cpa)
             const int nvc = std::max(1, dp.n_vc);
             const size_t lds_p = part_lds_bytes(nvc, lp_stride, any_nullable, gd.chunk <= kTile);
             uint32_t* ct = (uint32_t*)chist.p;
@@ -1601,7 +1616,8 @@ struct Engine {
                 pbase = (const int64_t*)sort_pbase.p;
                 scr = (uint64_t*)sort_scr.p;
             }
-            ek::launch_agg(nvc, pbase != nullptr, dp.n_having > 0, ga, lay.bytes, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
+            const size_t lds_a = (size_t)lay.bytes + agg_run_lds_bytes(gd.mruns);
+            ek::launch_agg(nvc, pbase != nullptr, dp.n_having > 0, ga, lds_a, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
                        scr_stride);
             phase_end(ph);
         }
@@ -2194,7 +2210,7 @@ struct Engine {
                 if (int rc = up_pinned(d_slot, slots.data(), (size_t)nq)) return rc;
                 if (int rc = up_pinned(d_ob, obase.data(), (size_t)nq)) return rc;
                 const int ph = phase_begin(EK_PHASE_AGGREGATE);
-                small_win_launch(nw, buffer_view(), (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{});
+                if (int rc = small_win_launch(nw, buffer_view(), (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{})) return rc;
                 phase_end(ph);
             }
         }
@@ -2645,9 +2661,12 @@ struct Engine {
             return fail(EK_ERR_DEVICE, "key-major gather failed: %s", hipGetErrorName(e));
         if (int rc = km_check_report("gather")) return rc;
 #endif
-        auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, nblk, lds, stream, d_plan, d, rv); };
+        // HAVING absent, or over count(*) alone with every key run (h_kmf[1], the longest) inside the decision table:
+        // the walk decides each state from DPlan.hstar_tab and carries no interpreter
+        const bool hs = !sort && (dp.n_having == 0 || (dp.having_star && h_kmf[1] < (unsigned)kHStarTab));
+        auto walk = [&](bool write) { ek::launch_km_walk(nvc, sort, write, false, hs, nblk, lds, stream, d_plan, d, rv); };
         if (one) {
-            ek::launch_km_walk(nvc, sort, true, true, nblk, lds, stream, d_plan, d, rv);
+            ek::launch_km_walk(nvc, sort, true, true, hs, nblk, lds, stream, d_plan, d, rv);
             phase_end(ph2);
             if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "key-major launch failed");
             stats.windows_keymajor += nw;
@@ -2682,7 +2701,7 @@ struct Engine {
             du.skend = (uint16_t*)km_ukend.p;
             du.sk = du.skend + (size_t)n * 2;
             du.scount = (uint32_t*)km_scount.p;
-            ek::launch_km_walk(nvc, sort, true, false, nblk, lds, stream, d_plan, du, rv);
+            ek::launch_km_walk(nvc, sort, true, false, hs, nblk, lds, stream, d_plan, du, rv);
             hipLaunchKernelGGL(k_km_scan, dim3(nw), dim3(1024), 0, stream, d, rv);
             if (int rc = ensure(km_rbase, (size_t)(nw + 1) * 8)) return rc;
             hipLaunchKernelGGL(k_km_rbase, dim3(1), dim3(1024), 0, stream, d, (int64_t*)km_rbase.p);
@@ -2806,6 +2825,7 @@ struct Engine {
             return fail(EK_ERR_UNSUPPORTED, "window sizes in one launch too uneven (%d windows per chunk, %lld events)",
                         mp, (long long)V);
         gd.chunk = (int32_t)csz;
+        gd.mruns = std::max(1, max_chunks_in_pane(h_pbnd, gd, csz));
         gd.key_col = dp.key_col;
         gd.ts_col = dp.ts_col;
         gd.n_where = dp.n_where;
@@ -3516,7 +3536,7 @@ struct Engine {
             p.q.kind = RB_FIXED;
             p.q.pos = a - eb_base;
             p.q.rstep = b - eb_base;
-            p.start = ws;   // WindowRange [t - length, t] for both parts (window_op.go:683-690)
+            p.start = ws;   // WindowRange: [t - L, t] for the first part, [t, t + D] for the last (window_op.go:683-703)
             p.end = we;
             pw.push_back(p);
             const int64_t dl = we - (L + D);
@@ -3788,6 +3808,186 @@ struct Engine {
         return 0;
     }
 
+    // ---- the fused sorted pass (k_part MODE 3): a pane-mode batch presumed ts-sorted is partitioned straight from
+    // its first and last timestamps, and the partition pass itself checks the presumption (sortedness, panes per
+    // chunk, the hopping gap), writes the pane bounds and reports back in one read-back; the separate ts pass
+    // (k_stats), its reduction, the pane-bounds search and one host round trip are gone. A batch that fails the
+    // check is redone on the general path before any engine state changes (the pass only wrote scratch).
+    struct FzPass { bool on; int64_t q_lo, nq; int mp, ls; const int64_t* pbnd; };
+    FzPass fz_pass{};
+    int fz_on = 0;            // EKGPU_FUSED=1: try the fused pass (default off)
+    int fz_skip = 0;          // pushes that skip the attempt after a discarded pass (an unsorted stream pays once)
+    DevBuf fz_buf;            // [FzStatus][ends 2][pbnd_out n_panes + 1]
+    int64_t* h_fz = nullptr;  // pinned landing block
+    size_t h_fz_cap = 0;
+    static constexpr int kFzFallback = -1;
+    static constexpr int64_t kFzMinRows = 1 << 16;
+
+    bool fz_eligible(int64_t n) {
+        // (WHERE plans keep the general path: k_part<3, WHERE> measured corrupted value registers on MI355X — the
+        // interpreter call inside the partition loop with the direct-to-LDS ts loads of the tile)
+        if (!fz_on || range_mode || gmode || ts_hint || plan.n_filter > 0 || dp.n_where > 0 || dp.pseudo_keys) return false;
+        if (wtype != EK_WINDOW_TUMBLING && wtype != EK_WINDOW_HOPPING) return false;
+        if (n < kFzMinRows || sorted_chunk != kTile || chunk < kTile) return false;
+        if (fz_skip > 0) { fz_skip--; return false; }
+        return true;
+    }
+
+    int push_fused(const DBatch& db, const int64_t* ts, int64_t n) {
+        const size_t hdr = (sizeof(FzStatus) + 7) / 8 + 2;   // words before pbnd_out
+        if (int rc = ensure(fz_buf, hdr * 8 + 64 * 8)) return rc;
+        if (h_fz_cap < hdr + 64) {
+            if (h_fz) { hipStreamSynchronize(stream); hipHostFree(h_fz); }
+            h_fz_cap = std::max<size_t>(hdr + 64, 4096);
+            if (hipHostMalloc((void**)&h_fz, h_fz_cap * 8) != hipSuccess) { h_fz = nullptr; h_fz_cap = 0; return fail(EK_ERR_NOMEM, "pinned"); }
+        }
+        FzStatus* d_st = (FzStatus*)fz_buf.p;
+        int64_t* d_ends = (int64_t*)fz_buf.p + hdr - 2;
+        hipLaunchKernelGGL(k_fz_prep, dim3(1), dim3(64), 0, stream, ts, n, d_st, d_ends);
+        hipMemcpyAsync(h_fz, d_ends, 16, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "fused pass: ts read failed");
+        const int64_t t0 = h_fz[0], t1 = h_fz[1];
+        const int64_t T = plan.late_tolerance_ms;
+        if (t0 > t1) { fz_skip = 8; return kFzFallback; }     // not sorted: the general path
+        if (has_M && t0 < M - T) return kFzFallback;           // a late prefix: the general path drops it
+        const int64_t M1 = has_M ? std::max(M, t1) : t1, W1 = M1 - T;
+        const bool hop_gap = wtype == EK_WINDOW_HOPPING && T == 0;
+        if (hop_gap && has_M && t0 - M > L) return kFzFallback;   // the empty-window discard pass (k_hop_drop)
+        // the first window's alignment, tentatively (restored if the pass is discarded)
+        const bool e1_was = e1_known;
+        const int64_t E1_was = E1, first_was = first_ts;
+        const PaneGrid grid_was = grid;
+        auto restore = [&]() { e1_known = e1_was; E1 = E1_was; first_ts = first_was; grid = grid_was; };
+        if (!e1_known) {
+            if (pend_n != 0 || W1 < t0) return kFzFallback;
+            first_ts = t0;
+            E1 = aligned_end(first_ts, raw_interval, plan.time_unit, plan.tz_offset_s);
+            grid.tumbling = wtype == EK_WINDOW_TUMBLING;
+            grid.origin = grid.tumbling ? E1 : E1 - L;
+            grid.P = P;
+        }
+        int64_t q_lo = std::max<int64_t>(0, pane_host(t0));
+        const int64_t q_hi = pane_host(t1);
+        q_lo = std::max(q_lo, win_first_pane(next_win));
+        const int64_t nq = q_hi - q_lo + 1;
+        if (q_hi < 0 || nq < 1 || nq > max_panes_group || n > group_events || (size_t)nq + 1 + hdr > (size_t)INT32_MAX) {
+            restore();
+            return kFzFallback;
+        }
+        // panes a 4096-row chunk may span: from the batch's mean rows per pane (a chunk past it discards the pass)
+        const int64_t per_pane = std::max<int64_t>(1, n / nq);
+        int mp = (int)std::min<int64_t>(nq, std::max<int64_t>(2, (kTile + per_pane - 1) / per_pane + 1));
+        mp = std::min(mp, std::min(kMaxChunkBnd + 1, np_max / std::max(1, NB)));
+        if (mp < 1 || (int64_t)NB * mp > np_max) { restore(); return kFzFallback; }
+        if (int rc = ensure(fz_buf, (hdr + (size_t)nq + 1) * 8)) { restore(); return rc; }
+        if (h_fz_cap < hdr + (size_t)nq + 1) {
+            hipHostFree(h_fz);
+            h_fz_cap = std::max<size_t>(hdr + nq + 1, 2 * h_fz_cap);
+            if (hipHostMalloc((void**)&h_fz, h_fz_cap * 8) != hipSuccess) { h_fz = nullptr; h_fz_cap = 0; restore(); return fail(EK_ERR_NOMEM, "pinned"); }
+        }
+        hipMemsetAsync(fz_buf.p, 0, sizeof(FzStatus), stream);   // (ensure may have moved the block)
+        GroupDesc gd{};
+        gd.lo = 0;
+        gd.hi = n;
+        gd.q_lo = q_lo;
+        gd.n_panes = (int32_t)nq;
+        gd.nb = NB;
+        gd.kbits = kbits;
+        gd.chunk = kTile;
+        gd.abase = 0;
+        gd.nch = (int32_t)((n + kTile - 1) / kTile);
+        gd.np = (int32_t)nq * NB;
+        gd.ring = ring;
+        gd.has_accept = 0;
+        gd.sorted = 1;
+        gd.key_col = dp.key_col;
+        gd.ts_col = dp.ts_col;
+        gd.n_where = dp.n_where;
+        gd.num_keys = dp.num_keys;
+        gd.nbatch = n;
+        gd.pad = env_int("EKGPU_DEBUG_AGG", 0);
+        gd.pad2 = variant;
+        gd.fz_mp = mp;
+        gd.fz_gap = hop_gap ? 1 : 0;
+        gd.pbnd_out = (int64_t*)fz_buf.p + hdr;
+        gd.fz_st = (FzStatus*)fz_buf.p;
+        const int ls = NB * mp + 1;
+        // the same staging / run-table buffers (and sizes) launch_part_agg uses for this group
+        const int64_t ne = (int64_t)gd.nch * kTile + 64;
+        if (ne > st_cap) {
+            if (int rc = ensure(st_klo, (size_t)ne * 2)) { restore(); return rc; }
+            for (int v = 0; v < dp.n_vc; ++v) {
+                if (int rc = ensure(st_val[v], (size_t)ne * 8)) { restore(); return rc; }
+                if ((plan.nullable_mask >> dp.vc_col[v]) & 1u)
+                    if (int rc = ensure(st_valid[v], (size_t)ne)) { restore(); return rc; }
+            }
+            st_cap = ne;
+        }
+        Staging st{};
+        st.klo = (uint16_t*)st_klo.p;
+        bool any_nullable = false;
+        for (int v = 0; v < dp.n_vc; ++v) {
+            st.val[v] = (int64_t*)st_val[v].p;
+            if (db.valid[dp.vc_col[v]]) {
+                st.valid[v] = (uint8_t*)st_valid[v].p;
+                st.nullable_mask |= 1u << v;
+                any_nullable = true;
+            }
+        }
+        if (int rc = ensure(chist, (size_t)gd.nch * ls * 4)) { restore(); return rc; }
+        if (int rc = ensure(chunk_pa, (size_t)gd.nch * 4)) { restore(); return rc; }
+        gd.cpa = (int32_t*)chunk_pa.p;
+        {
+            const int nvc = std::max(1, dp.n_vc);
+            const size_t lds_p = std::max(part_lds_bytes(nvc, ls - 1, any_nullable, true), fz_lds_bytes(ls - 1));
+            const int ph = phase_begin(EK_PHASE_PARTITION);
+            ek::launch_part(3, dp.n_where > 0, nvc, dim3(gd.nch), lds_p, stream, d_plan, db, grid, gd, nullptr, st,
+                            (uint32_t*)chist.p, ls, kTile, (int32_t*)pane_err.p);
+            phase_end(ph);
+        }
+        hipMemcpyAsync(h_fz, fz_buf.p, (hdr + (size_t)nq + 1) * 8, hipMemcpyDeviceToHost, stream);
+        if (hipStreamSynchronize(stream) != hipSuccess) { restore(); return fail(EK_ERR_DEVICE, "fused partition pass failed"); }
+        const FzStatus fs = *(const FzStatus*)h_fz;
+        int64_t* pb = h_fz + hdr;
+        pb[0] = 0;
+        pb[nq] = n;
+        bool ok = !fs.unsorted && !fs.overflow && (!hop_gap || (int64_t)fs.max_gap <= L);
+        if (ok) {
+            // the general path's grouping would form exactly this one group with single-tile chunks
+            const int64_t pane_cap = (int64_t)(kMaxRuns - 2) * chunk;
+            for (int64_t k = 0; k < nq && ok; ++k) ok = pb[k + 1] - pb[k] <= std::min(group_events, pane_cap);
+            GroupDesc chk = gd;
+            ok = ok && max_chunks_in_pane(pb, chk, kTile) <= kMaxRuns && max_panes_in_chunk(pb, chk, kTile) <= mp;
+        }
+        if (!ok) {
+            restore();
+            fz_skip = 8;
+            stats.fused_discarded++;
+            return kFzFallback;
+        }
+        // ---- commit: the batch is sorted, nothing is late; the rest is the general path's sorted branch
+        int64_t arrival_base = arrivals;
+        arrivals += n;
+        h_wdesc_used = 0;   // the read-back sync drained every earlier descriptor upload
+        h_desc_used = 0;
+        aux_used = 0;
+        if (!has_M || t1 > M) {
+            M = t1;
+            has_M = true;
+            W = M - T;
+            has_W = true;
+        }
+        if (!e1_was) e1_known = true;   // (E1 / grid / first_ts set above, as the general path's step 4)
+        stats.fused_batches++;
+        fz_pass = FzPass{true, q_lo, nq, mp, ls, pb};
+        int64_t save = arrivals;
+        arrivals = arrival_base;
+        const int rc = process(db, true, 0, nullptr, t0, t1, nullptr);
+        arrivals = save;
+        fz_pass = FzPass{};
+        return rc;
+    }
+
     // ek_batch_ts_stats: the shareable form of the statistics above
     int ts_stats_of(const ek_batch* b, ek_ts_stats* out) {
         if (!b || !out) return fail(EK_ERR_INVALID, "null batch / output");
@@ -3934,7 +4134,7 @@ struct Engine {
         if (!clock_started) { start_clock(now); return 0; }
         if (now < clock_ms) return fail(EK_ERR_INVALID, "the clock cannot move back (%lld < %lld)", (long long)now, (long long)clock_ms);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "stream failed");
-        fold_time();
+        if (int rc = fold_time()) return rc;
         hipEventRecord(ev0, stream);
         h_wdesc_used = 0;
         h_desc_used = 0;
@@ -4328,7 +4528,7 @@ struct Engine {
         ar.ob0 = r_rows_used;
         ar.slot0 = (int32_t)wins.size();
         const int ph = phase_begin(EK_PHASE_AGGREGATE);
-        small_win_launch(nq, src, nullptr, nullptr, nullptr, nullptr, (int)len, ar);
+        if (int rc = small_win_launch(nq, src, nullptr, nullptr, nullptr, nullptr, (int)len, ar)) return rc;
         phase_end(ph);
         if (hipGetLastError() != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");
         // the host's record of the windows (slot0 + w, rows from ob0 + w * rowcap) is written while the kernel runs:
@@ -4396,7 +4596,7 @@ struct Engine {
             hipLaunchKernelGGL(k_range_members, dim3(nq), dim3(kBlock), 0, stream, (const int64_t*)nullptr, (const int64_t*)ab_d.p,
                                (const int32_t*)d_slot, (int64_t*)r_wmc.p, (unsigned long long*)r_wmh.p, arr_base);
         const int ph = phase_begin(EK_PHASE_AGGREGATE);
-        small_win_launch(nq, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{});
+        if (int rc = small_win_launch(nq, src, (const int64_t*)ab_d.p, d_wl, d_slot, d_ob, max_n, SwArith{})) return rc;
         phase_end(ph);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "small-window launch failed");   // host lists reused
         return 0;
@@ -4498,6 +4698,13 @@ struct Engine {
                     db.valid[c] = (const uint8_t*)in_valid[c].p;
                 }
             }
+            // a pinned caller buffer makes these copies truly asynchronous: an asynchronous push waits for them before
+            // it returns (record_time), so a host batch is never borrowed past its push
+            if (async_push) {
+                if (!ev_h2d) hipEventCreateWithFlags(&ev_h2d, hipEventDisableTiming);
+                hipEventRecord(ev_h2d, stream);
+                h2d_pending = true;
+            }
         } else {
             for (int c = 0; c < user_cols; ++c) { db.col[c] = b->columns[c]; db.valid[c] = b->validity[c]; }
         }
@@ -4538,7 +4745,7 @@ struct Engine {
             if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
         }
         if (gmode) return fail(EK_ERR_STATE, "the handle takes its watermark from ek_push_batch_global (shard mode)");
-        fold_time();
+        if (int rc = fold_time()) return rc;
         hipEventRecord(ev0, stream);
         DBatch db{};
         if (int rc = stage_batch(b, db)) return rc;
@@ -4576,6 +4783,10 @@ struct Engine {
             return rc ? rc : record_time();
         }
         const int64_t* ts = (const int64_t*)db.col[dp.ts_col];
+        if (fz_eligible(n)) {   // pane mode: the fused sorted pass (push_fused), or the general path below
+            const int rc = push_fused(db, ts, n);
+            if (rc != kFzFallback) return rc ? rc : record_time();
+        }
 
         // ---- 1. batch statistics (one pass over ts, or the batch's shared ek_ts_stats)
         BatchStats s;
@@ -4718,15 +4929,25 @@ struct Engine {
     int record_time() {
         hipEventRecord(ev1, stream);
         time_pending = true;
-        if (!async_push) fold_time();   // synchronous pushes (the default) complete before they return
+        if (h2d_pending) {   // an asynchronous push of a host batch returns once its columns are copied
+            h2d_pending = false;
+            if (hipEventSynchronize(ev_h2d) != hipSuccess) return fail(EK_ERR_DEVICE, "host batch copy failed");
+        }
+        if (!async_push) return fold_time();   // synchronous pushes (the default) complete before they return
         return 0;
     }
-    void fold_time() {
+    int fold_time() {
         // (not pending: phases recorded since the last fold — a shared ek_batch_ts_stats pass before this push — stay
         // and are folded with the push they serve)
-        if (!time_pending) return;
+        if (!time_pending) return 0;
         time_pending = false;
-        if (hipEventSynchronize(ev1) == hipSuccess) {
+        // an asynchronous push's queued work that failed surfaces here: at the next push / advance / stats call
+        const hipError_t qe = hipEventSynchronize(ev1);
+        if (qe != hipSuccess) {
+            phase_used = 0;
+            return fail(EK_ERR_DEVICE, "queued work of the previous push failed: %s", hipGetErrorString(qe));
+        }
+        {
             float ms = 0;
             hipEventElapsedTime(&ms, ev0, ev1);
             stats.last_batch_device_ms = ms;
@@ -4746,6 +4967,7 @@ struct Engine {
             }
         }
         phase_used = 0;
+        return 0;
     }
 
 
@@ -4900,7 +5122,7 @@ struct Engine {
                 if (b->validity[c] && !((plan.nullable_mask >> c) & 1u)) return fail(EK_ERR_INVALID, "column %d is not declared nullable", c);
             }
         }
-        fold_time();
+        if (int rc = fold_time()) return rc;
         hipEventRecord(ev0, stream);
         h_wdesc_used = 0;
         h_desc_used = 0;
@@ -5333,9 +5555,9 @@ struct Engine {
     // events still waiting for the first window end, and either the partials of every open pane (pane mode) or the
     // event-buffer rows a future window can still contain (range mode). Sections are 8-byte aligned, host order.
     static constexpr uint64_t kStateMagic = 0x31305453474B4545ull;   // "EEKGST01"
-    static constexpr int64_t kStateVersion = 7;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
+    static constexpr int64_t kStateVersion = 8;   // 3: the processing-time clock and timers; 4: pane WHERE witnesses;
                                                   // 5: processing-time incremental windows; 6: ek_stats totals;
-                                                  // 7: event-time send-twice prevWindowEndTs
+                                                  // 7: event-time send-twice prevWindowEndTs; 8: ek_stats v13
 
     // FNV-1a over the plan fields that shape the state (a blob only restores into the same rule)
     uint64_t plan_hash() const {
@@ -5710,6 +5932,7 @@ struct Engine {
         if (msd_ht) hipHostFree(msd_ht);
         if (ev0) hipEventDestroy(ev0);
         if (ev1) hipEventDestroy(ev1);
+        if (ev_h2d) hipEventDestroy(ev_h2d);
         for (auto& e : phase_ev) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
         phase_ev.clear();
         if (stream && own_stream) hipStreamDestroy(stream);
@@ -5823,17 +6046,18 @@ int ek_set_async(void* h, int32_t on) {
     if (!h) return EK_ERR_INVALID;
     DeviceGuard dg(h);
     Engine* e = (Engine*)h;
-    if (!on) { hipStreamSynchronize(e->stream); e->fold_time(); }
+    int rc = 0;
+    if (!on) { hipStreamSynchronize(e->stream); rc = e->fold_time(); }
     e->async_push = on != 0;
-    return 0;
+    return rc;
 }
 
 int ek_get_stats(void* h, ek_stats* out) {
     if (!h || !out) return EK_ERR_INVALID;
     DeviceGuard dg(h);
-    ((Engine*)h)->fold_time();
+    const int rc = ((Engine*)h)->fold_time();
     *out = ((Engine*)h)->stats;
-    return 0;
+    return rc;
 }
 
 const char* ek_last_error(void* h) {

@@ -572,7 +572,8 @@ __host__ __device__ __forceinline__ uint64_t str_slot(uint64_t h, int bits) { re
 __global__ __launch_bounds__(256) void k_str_lookup(const int64_t* __restrict__ hash, const int64_t* __restrict__ soff,
                                                     const int32_t* __restrict__ slen, const uint8_t* __restrict__ valid,
                                                     int64_t n, const uint64_t* __restrict__ tkey,
-                                                    const uint32_t* __restrict__ tval, int bits, uint32_t* __restrict__ id,
+                                                    const uint32_t* __restrict__ tval, const uint32_t* __restrict__ tlen,
+                                                    int bits, uint32_t* __restrict__ id,
                                                     MissRec* __restrict__ miss, unsigned long long* __restrict__ n_miss) {
     const uint64_t mask = bits ? (1ull << bits) - 1ull : 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -584,7 +585,9 @@ __global__ __launch_bounds__(256) void k_str_lookup(const int64_t* __restrict__ 
                 const uint64_t h = str_key((uint64_t)hash[i]);
                 for (uint64_t k = str_slot(h, bits);; k = (k + 1) & mask) {
                     const uint64_t t = tkey[k];
-                    if (t == h) { v = tval[k]; found = true; break; }
+                    // a hit needs the hash AND the length: a colliding string of another length is a miss, and the
+                    // host's resolve (which holds the strings) reports the collision instead of merging the two groups
+                    if (t == h && tlen[k] == (uint32_t)L) { v = tval[k]; found = true; break; }
                     if (t == 0) break;
                 }
             }
@@ -680,12 +683,13 @@ struct StrDict {
     std::vector<std::string> values;
     std::vector<uint64_t> hkey;                      // host mirror of the device table
     std::vector<uint32_t> hval;
+    std::vector<uint32_t> hlen;                      // the string's byte length: a hash hit must match it too
     int bits = 0;
     bool dirty = false;
     void put(uint64_t key, uint32_t id) {
         const uint64_t mask = (1ull << bits) - 1ull;
         for (uint64_t k = str_slot(key, bits);; k = (k + 1) & mask)
-            if (hkey[k] == 0) { hkey[k] = key; hval[k] = id; return; }
+            if (hkey[k] == 0) { hkey[k] = key; hval[k] = id; hlen[k] = (uint32_t)values[id].size(); return; }
     }
     void insert(uint64_t key, uint32_t id) {
         if (bits == 0 || (by_key.size() + 1) * 2 > ((size_t)1 << bits)) {   // grow: load <= 1/2
@@ -693,6 +697,7 @@ struct StrDict {
             while (((size_t)1 << bits) < (by_key.size() + 1) * 2) ++bits;
             hkey.assign((size_t)1 << bits, 0);
             hval.assign((size_t)1 << bits, 0);
+            hlen.assign((size_t)1 << bits, 0);
             for (const auto& kv : by_key) put(kv.first, kv.second);
         }
         put(key, id);
@@ -718,7 +723,7 @@ struct JsonDecoder {
     const int64_t* str_off[EK_MAX_COLUMNS] = {};   // the last decode's string references (ek_json_strings)
     const int32_t* str_len[EK_MAX_COLUMNS] = {};
     StrDict dict[EK_MAX_COLUMNS];
-    Buf id_col[EK_MAX_COLUMNS], tkey[EK_MAX_COLUMNS], tval[EK_MAX_COLUMNS], miss, n_miss, gat_pos, gat_bytes, fix_rows, fix_ids;
+    Buf id_col[EK_MAX_COLUMNS], tkey[EK_MAX_COLUMNS], tval[EK_MAX_COLUMNS], tlen[EK_MAX_COLUMNS], miss, n_miss, gat_pos, gat_bytes, fix_rows, fix_ids;
     std::vector<uint8_t> h_err;
     int64_t last_n = 0, last_ok = 0;
     ek_json_stats st{};
@@ -746,7 +751,7 @@ struct JsonDecoder {
             if (b->p) hipFree(b->p);
         for (int c = 0; c < EK_MAX_COLUMNS; ++c)
             for (Buf* b : {&raw_col[c], &raw_valid[c], &out_col[c], &out_valid[c], &raw_soff[c], &raw_slen[c], &out_soff[c],
-                           &out_slen[c], &id_col[c], &tkey[c], &tval[c]})
+                           &out_slen[c], &id_col[c], &tkey[c], &tval[c], &tlen[c]})
                 if (b->p) hipFree(b->p);
         if (d_sch) hipFree(d_sch);
         if (stream) hipStreamDestroy(stream);
@@ -877,15 +882,18 @@ struct JsonDecoder {
         if (D.dirty) {
             if (int rc = ensure(tkey[c], D.hkey.size() * 8)) return rc;
             if (int rc = ensure(tval[c], D.hval.size() * 4)) return rc;
+            if (int rc = ensure(tlen[c], D.hlen.size() * 4)) return rc;
             hipMemcpyAsync(tkey[c].p, D.hkey.data(), D.hkey.size() * 8, hipMemcpyHostToDevice, stream);
             hipMemcpyAsync(tval[c].p, D.hval.data(), D.hval.size() * 4, hipMemcpyHostToDevice, stream);
+            hipMemcpyAsync(tlen[c].p, D.hlen.data(), D.hlen.size() * 4, hipMemcpyHostToDevice, stream);
             if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "string table upload failed");
             D.dirty = false;
         }
         hipMemsetAsync(n_miss.p, 0, 8, stream);
         const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256));
         hipLaunchKernelGGL(k_str_lookup, dim3(g), dim3(256), 0, stream, hash, soff, slen, valid, n,
-                           (const uint64_t*)tkey[c].p, (const uint32_t*)tval[c].p, D.bits, (uint32_t*)id_col[c].p,
+                           (const uint64_t*)tkey[c].p, (const uint32_t*)tval[c].p, (const uint32_t*)tlen[c].p, D.bits,
+                           (uint32_t*)id_col[c].p,
                            (MissRec*)miss.p, (unsigned long long*)n_miss.p);
         unsigned long long nm = 0;
         hipMemcpyAsync(&nm, n_miss.p, 8, hipMemcpyDeviceToHost, stream);

@@ -32,6 +32,14 @@ struct BatchStats {
     int64_t n_dropped;  // events removed by the hopping empty-window discard (k_hop_drop)
 };
 
+// What the fused sorted pass (k_part MODE 3) found: the batch is used only if it is ts-sorted, no chunk spans more
+// than fz_mp panes, and (hopping, lateTolerance 0) no arrival gap exceeds the window
+struct FzStatus {
+    int32_t unsorted;
+    int32_t overflow;
+    unsigned long long max_gap;
+};
+
 struct PaneGrid {
     int64_t origin;     // tumbling: E1 (pane 0 = (-inf,E1)); hopping: E1 - L (pane 0 = [origin, origin+P))
     int64_t P;          // pane length (ms)
@@ -353,6 +361,20 @@ __global__ __launch_bounds__(kBoundsBlock) void k_pane_bounds(const int64_t* __r
 }
 #endif
 
+// The fused sorted pass's first look at a batch: its first and last ts (the pane range, if it is sorted) and a
+// cleared verdict block — one tiny launch and one 16-byte read-back instead of the whole ts pass
+#ifndef EK_NO_PLAIN_KERNELS
+__global__ void k_fz_prep(const int64_t* __restrict__ ts, int64_t n, FzStatus* st, int64_t* ends) {
+    if (threadIdx.x == 0) {
+        ends[0] = ts[0];
+        ends[1] = ts[n - 1];
+        st->unsorted = 0;
+        st->overflow = 0;
+        st->max_gap = 0;
+    }
+}
+#endif
+
 // per-window result counters of the windows handed out by a poll: one launch instead of four fills
 #ifndef EK_NO_PLAIN_KERNELS
 __global__ void k_zero_wins(int64_t n, int64_t* wcnt, int32_t* werr, int64_t* wmc, int64_t* wmh) {
@@ -493,7 +515,14 @@ struct GroupDesc {
     int64_t wit_o2;
     int32_t wit_ts;
     int32_t pad2;          // layout variants (EKGPU_VARIANT; results stay valid)
+    int32_t mruns;         // k_agg: most chunk runs one partition of the launch holds (sizes its LDS run tables)
+    // k_part MODE 3 (the fused sorted pass, FzStatus): panes per chunk the ctab rows hold, 1 = also the widest
+    // arrival gap, the device pane bounds it writes (pbnd_out[k] = first row of pane q_lo + k, 0 < k < n_panes)
+    int32_t fz_mp, fz_gap;
+    int64_t* pbnd_out;
+    FzStatus* fz_st;
 };
+
 
 constexpr int kMaxGroupPanes = 64;
 #ifndef EK_PART_BLOCK
@@ -543,6 +572,22 @@ __device__ __forceinline__ int chunk_rel(const int64_t* lb, int nlb, int pa, int
     return rel;
 }
 
+// MODE 3: group-relative pane of a timestamp, clamped to the group's panes (rows before pane q_lo belong to the
+// first pane's index range, as pbnd[0] = lo makes them in MODE 1)
+__device__ __forceinline__ int fz_rel(const GroupDesc& gd, const PaneGrid& g, int64_t t) {
+    const int64_t q = pane_of(g, t);
+    return q <= gd.q_lo ? 0 : (q >= gd.q_lo + gd.n_panes - 1 ? gd.n_panes - 1 : (int)(q - gd.q_lo));
+}
+
+// MODE 3: start of group pane r (INT64_MAX past the group's last pane) — multiplications only: the per-row pane of a
+// chunk is counted against these bounds, never divided out (64-bit division is a long VALU sequence on gfx950)
+__device__ __forceinline__ int64_t fz_start(const GroupDesc& gd, const PaneGrid& g, int r) {
+    if (r > gd.n_panes - 1) return INT64_MAX;
+    const int64_t q = gd.q_lo + r;
+    if (g.tumbling) return q == 0 ? INT64_MIN : g.origin + (q - 1) * g.P;
+    return g.origin + q * g.P;
+}
+
 // Local partition of event row `i` (-1: dropped: late, outside the group's panes, or filtered by WHERE).
 // MODE 0 (unsorted): the pane comes from the event's ts. MODE 1 (sorted) / 2 (virtual panes): the
 // caller passes the pane `rel` derived from the (virtual) row index; `i` is the physical row.
@@ -556,7 +601,7 @@ __device__ __forceinline__ int local_part(const DPlan& p, const DBatch& b, const
         int64_t r = q - gd.q_lo;
         if (q < 0 || r < 0 || r >= gd.n_panes) return -1;
         rel = (int)r;
-    } else if (MODE == 1) {
+    } else if (MODE == 1 || MODE == 3) {
         if (gd.has_accept && !acc[i]) return -1;   // hopping empty-window discard (k_hop_drop)
     }
     if (gd.key_col >= 0 && key >= gd.num_keys) return -1;
@@ -616,6 +661,12 @@ __device__ inline void block_excl_scan(uint32_t* cnt, int n, uint32_t* wsum) {
 // LDS bytes of k_part for `nvc` value columns and `lp` chunk-local partitions
 // (single-tile chunks need no per-row partition array: their runs come straight from the tile sort)
 // (value columns are staged through LDS one at a time, so the footprint does not grow with their number)
+// MODE 3 (single-tile chunks): the tile's ts in LDS past the single-tile layout with its validity bytes
+__host__ __device__ inline size_t fz_lds_off(int lp) {
+    const size_t lpp = ((size_t)lp + 4 + 3) & ~(size_t)3;
+    return (((size_t)kTile * 8 + 2 * lpp * 4 + (size_t)kTile * 2 + (size_t)kTile) + 15) & ~(size_t)15;
+}
+inline size_t fz_lds_bytes(int lp) { return fz_lds_off(lp) + (size_t)kTile * 8; }
 inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
     size_t lpp = ((size_t)lp + 4 + 3) & ~(size_t)3;
     return (size_t)kTile * 8 + 2 * lpp * 4 + (size_t)kTile * (single_tile ? 2 : 4) + (nullable ? (size_t)kTile : 0);
@@ -631,6 +682,11 @@ inline size_t part_lds_bytes(int nvc, int lp, bool nullable, bool single_tile) {
 // MODE 0: unsorted batch (pane from ts); 1: ts-sorted batch (pane from the row index);
 // 2: virtual panes (range mode): the group's rows are the concatenation of possibly overlapping
 //    index ranges of the event buffer, virtual row v of pane r lives at physical row v + voff[r].
+// 3: the fused sorted pass (single-tile chunks of a batch presumed ts-sorted): the pane of each row comes from its
+//    own ts, and the same read of ts checks the presumption (arrival order non-decreasing, watermark_op.go:144-155:
+//    then no row is late and the running max is the row's own ts), finds the widest arrival gap when asked, and
+//    writes the pane bounds (pbnd_out) that k_agg walks — so no separate ts pass and no pane-bounds search precede
+//    it. Its verdict goes to fz_st; the host discards the pass and takes the general path when the batch is not sorted.
 template <int MODE, bool WHERE, int NVC>
 __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_PART_WAVES_PER_EU))) void k_part(DPlan* __restrict__ pp, DBatch b, PaneGrid g, GroupDesc gd,
                                                  const uint8_t* __restrict__ acc, Staging st, uint32_t* __restrict__ ctab,
@@ -640,12 +696,34 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
     int64_t a0, c0, c1;
     chunk_range(gd, &a0, &c0, &c1);
     int pa, pb;
-    chunk_panes(gd, c0, c1, &pa, &pb);
+    const int64_t* tsc = (const int64_t*)b.col[gd.ts_col];
+    if (MODE == 3) {
+        pa = fz_rel(gd, g, tsc[c0]);
+        pb = pa + gd.fz_mp - 1;
+    } else {
+        chunk_panes(gd, c0, c1, &pa, &pb);
+    }
     const int lp_n = (pb - pa + 1) * gd.nb;
     __shared__ int64_t lb[kMaxChunkBnd];
     __shared__ int64_t loff[kMaxChunkBnd + 1];
     __shared__ uint32_t wsum[kPartBlock / 64];
-    const int nlb = chunk_bounds(gd, pa, pb, lb);
+    __shared__ int s_fz_bad[2];                 // MODE 3: unsorted, pane overflow
+    __shared__ unsigned long long s_fz_gap;     // MODE 3: widest arrival gap
+    const int64_t fz_before = (MODE == 3 && c0 > 0) ? tsc[c0 - 1] : 0;              // MODE 3: the row before the chunk
+    const int fz_rp0 = (MODE == 3 && c0 > 0) ? fz_rel(gd, g, fz_before) : 0;         // ... and its pane (one division)
+    if (MODE == 3 && threadIdx.x == 0) { s_fz_bad[0] = 0; s_fz_bad[1] = 0; s_fz_gap = 0; }
+    const int nlb = MODE == 3 ? 0 : chunk_bounds(gd, pa, pb, lb);
+    // MODE 3: lb[k] = start of pane pa + 1 + k (k < fz_mp - 1); a row at or past the start of pane pa + fz_mp overflows
+    int64_t fz_ovf = INT64_MAX;
+    if constexpr (MODE == 3) {
+        for (int k = threadIdx.x; k < gd.fz_mp - 1; k += kPartBlock) lb[k] = fz_start(gd, g, pa + 1 + k);
+        fz_ovf = fz_start(gd, g, pa + gd.fz_mp);
+    }
+    auto fz_relb = [&](int64_t t) {   // group pane of a row of this chunk (t >= the chunk's first ts)
+        int r = pa;
+        for (int k = 0; k < gd.fz_mp - 1; ++k) r += t >= lb[k] ? 1 : 0;
+        return r;
+    };
     if (threadIdx.x == 0) gd.cpa[blockIdx.x] = pa;
     if (MODE == 2)
         for (int k = threadIdx.x; k <= pb - pa; k += kPartBlock) loff[k] = gd.voff[pa + k];
@@ -657,6 +735,7 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
     uint16_t* s_klo = (uint16_t*)(tcnt + lpp);                                // [kTile]
     uint16_t* s_lp = s_klo + kTile;                                           // [kTile] (multi-tile chunks)
     uint8_t* s_vd = (uint8_t*)(s_klo + (single ? 1 : 2) * kTile);             // [kTile] validity of that column
+    int64_t* s_ts = (int64_t*)(smem + fz_lds_off(lp_n));                       // MODE 3: [kTile] the tile's ts, row order
     const uint32_t* kcol = gd.key_col >= 0 ? (const uint32_t*)b.col[gd.key_col] : nullptr;
     const int64_t region = (int64_t)blockIdx.x * rs;
 
@@ -752,6 +831,20 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
                     key[2 * m] = (uint32_t)(i & (kPseudoKeys - 1));
                     key[2 * m + 1] = (uint32_t)((i + 1) & (kPseudoKeys - 1));
                 }
+                if constexpr (MODE == 3) {
+                    // ts straight into LDS (global_load_lds, no VGPRs: k_part is at its register cap), in row order:
+                    // a wave's 64 lanes x 16 B land at its 128 rows of this pair group (destination = wave base +
+                    // lane x 16); the barrier after the loads drains them
+                    int64_t* s_tm = s_ts + (int64_t)m * 2 * kPartBlock;
+                    if (full)
+                        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(tsc + i),
+                                                         (__attribute__((address_space(3))) void*)(s_tm + 2 * (threadIdx.x & ~63)),
+                                                         16, 0, 0);
+                    else if (i < gd.nbatch) {
+                        s_tm[2 * threadIdx.x] = tsc[i];
+                        s_tm[2 * threadIdx.x + 1] = 0;
+                    }
+                }
 #pragma unroll
                 for (int v = 0; v < NVC; ++v) {
                     if (v < p.n_vc && full) {
@@ -769,8 +862,24 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
         __syncthreads();
         int lp[kTileE];
         uint32_t rank[kTileE];
+        if constexpr (MODE == 3) {
+            // each row's pane from its ts in LDS, counted against the chunk's pane starts (a row past fz_mp panes —
+            // overflow: the pass is discarded — is not staged); the order check runs after the tile's writes
+#pragma unroll
+            for (int j = 0; j < kTileE; ++j) {
+                const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
+                const int loc = (j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
+                lp[j] = -1;
+                if (i < c1) {
+                    const int64_t t = s_ts[loc];
+                    if (t < fz_ovf) lp[j] = local_part<MODE, WHERE>(p, b, g, gd, fz_relb(t), acc, i, pa, key[j], pane_err, single);
+                }
+                if (lp[j] >= 0) rank[j] = atomicAdd(&tcnt[lp[j]], 1u);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < kTileE; ++j) {
+            if (MODE == 3) break;   // (MODE 3: partitioned in the check loop above)
             const int64_t i = t0 + (int64_t)(j >> 1) * 2 * kPartBlock + 2 * threadIdx.x + (j & 1);
             // (single-tile chunks flag WHERE errors here: there was no count pass)
             if (MODE == 2) {
@@ -827,6 +936,50 @@ __global__ __launch_bounds__(kPartBlock) __attribute__((amdgpu_waves_per_eu(EK_P
         __syncthreads();
         for (int k = threadIdx.x; k < lp_n; k += kPartBlock) cur[k] += tcnt[k + 1] - tcnt[k];
         __syncthreads();
+    }
+    if constexpr (MODE == 3) {
+        // the presumption check on the tile's ts (still in LDS): row i against row i - 1 (the chunk's first row against
+        // the row before the chunk), pane bounds at every pane change, the widest gap
+        {
+            bool bad = false, ovf = false;
+            int64_t gap = 0;
+#pragma unroll
+            for (int m = 0; m < kTileE / 2; ++m) {
+                const int64_t i = a0 + (int64_t)m * 2 * kPartBlock + 2 * threadIdx.x;
+                const int loc = m * 2 * kPartBlock + 2 * threadIdx.x;
+                if (i >= c1) continue;
+                const int64_t x = s_ts[loc];
+                const int rx = fz_relb(x);
+                ovf |= x >= fz_ovf;
+                if (i > 0) {
+                    const int64_t prev = loc > 0 ? s_ts[loc - 1] : fz_before;
+                    bad |= x < prev;
+                    gap = max(gap, x - prev);
+                    const int rp = loc > 0 ? fz_relb(prev) : fz_rp0;
+                    for (int k = rp + 1; k <= rx; ++k) gd.pbnd_out[k] = i;
+                }
+                if (i + 1 < c1) {
+                    const int64_t y = s_ts[loc + 1];
+                    const int ry = fz_relb(y);
+                    ovf |= y >= fz_ovf;
+                    bad |= y < x;
+                    gap = max(gap, y - x);
+                    for (int k = rx + 1; k <= ry; ++k) gd.pbnd_out[k] = i + 1;
+                }
+            }
+            if (bad) s_fz_bad[0] = 1;
+            if (ovf) s_fz_bad[1] = 1;
+            if (gd.fz_gap) {
+                gap = wave_max64(gap);
+                if ((threadIdx.x & 63) == 0 && gap > 0) atomicMax(&s_fz_gap, (unsigned long long)gap);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (s_fz_bad[0]) atomicOr(&gd.fz_st->unsorted, 1);
+            if (s_fz_bad[1]) atomicOr(&gd.fz_st->overflow, 1);
+            if (s_fz_gap) atomicMax(&gd.fz_st->max_gap, s_fz_gap);
+        }
     }
 }
 
@@ -1040,6 +1193,8 @@ constexpr int kMaxRuns = 1024;
 #ifndef EK_AGG_PIPE
 #define EK_AGG_PIPE 0
 #endif
+// k_agg's run tables in dynamic LDS after the aggregation tables: r_start[mr], r_pre[mr + 1]
+inline size_t agg_run_lds_bytes(int mruns) { return ((size_t)(2 * mruns + 1) * 4 + 15) & ~(size_t)15; }
 constexpr int kMaxBucketKeys = 8192;   // keys per bucket (1 << kbits) the direct emission's present mask covers
 
 // Runs of partition (rel, bucket): chunk c in [c_lo, c_hi] holds ctab[c][lp .. lp+1) of it.
@@ -1280,12 +1435,15 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
     const bool fresh = gd.fresh[rel] != 0;
     const int64_t dbase = gd.dbase[rel];
     // ---- the partition's rows are one run per chunk that holds rows of this pane (k_part)
-    __shared__ uint32_t r_start[kMaxRuns];   // staging index of each run (staging < 2^32 rows, host-checked)
-    __shared__ uint32_t r_pre[kMaxRuns + 1];
+    // run tables in dynamic LDS past the aggregation tables, sized by the launch's longest run list (gd.mruns):
+    // staging index of each run (staging < 2^32 rows, host-checked) and the exclusive prefix of the run lengths
+    const int mr = gd.mruns;
+    uint32_t* r_start = (uint32_t*)(lds + lay.bytes);
+    uint32_t* r_pre = r_start + mr;
     __shared__ uint32_t r_wsum[kAggBlock / 64];
     int c_lo, c_hi;
     part_chunks(gd, rel, &c_lo, &c_hi);
-    const int nruns = min(c_hi - c_lo + 1, kMaxRuns);
+    const int nruns = min(c_hi - c_lo + 1, mr);
     for (int j = threadIdx.x; j < nruns; j += kAggBlock) {
         const int c = c_lo + j;
         uint32_t o0, o1;

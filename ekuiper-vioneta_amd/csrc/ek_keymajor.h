@@ -314,7 +314,10 @@ __device__ __forceinline__ void km_row(const DPlan& p, const Part<NVC>& part, co
 // A key's membership [j0, j1) of its sorted rows only changes where a window start passes row j0 or a window end
 // passes row j1, so the thread folds, finalises and tests HAVING once per membership state and emits that row into
 // every window of the state's run [k, kend) — about two states per row instead of one fold per (key, window).
-template <int NVC, bool SORT, bool WRITE, bool ONE = false>
+// HS (no order statistics): HAVING is absent, or reads count(*) alone and every key run of the span is shorter than
+// kHStarTab rows: each state is decided from DPlan.hstar_tab (k_hstar_tab, create time) and the walk carries no
+// expression interpreter (C4a: fewer VGPRs, more waves per SIMD).
+template <int NVC, bool SORT, bool WRITE, bool ONE = false, bool HS = false>
 __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, KmDesc d, Results res) {
     extern __shared__ uint32_t s_dyn[];
     __shared__ uint32_t s_wc[kKmBlock / 64 + 1];
@@ -331,12 +334,14 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
     uint64_t* s_seg = (uint64_t*)(s_dyn + ((3 * nw + 1) & ~1));   // SORT: [kKmSegMax][kKmBlock] ordered values
     const DPlan& p = *pp;
     __shared__ int s_hc[2];   // HAVING over count(*) alone: the decisions for 1 and 2 rows (most states), once per block
-    if (!SORT && threadIdx.x == 0 && p.having_star) {
-        Part<NVC> cp{};
-        cp.cnt = 1;
-        s_hc[0] = km_having(p, cp, nullptr);
-        cp.cnt = 2;
-        s_hc[1] = km_having(p, cp, nullptr);
+    if constexpr (!SORT && !HS) {
+        if (threadIdx.x == 0 && p.having_star) {
+            Part<NVC> cp{};
+            cp.cnt = 1;
+            s_hc[0] = km_having(p, cp, nullptr);
+            cp.cnt = 2;
+            s_hc[1] = km_having(p, cp, nullptr);
+        }
     }
     for (int k = threadIdx.x; k < nw; k += kKmBlock) {
         // write pass: the cursor starts at this block's offset in the window's region (no per-row bcnt read)
@@ -394,7 +399,9 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                 // a state it drops (most (key, window) states hold one row) reads no value at all
                 Part<NVC> cp{};
                 cp.cnt = j1 - j0;
-                const int hc = cp.cnt <= 2 ? s_hc[cp.cnt - 1] : km_having(p, cp, nullptr);
+                int hc;
+                if constexpr (HS) hc = p.hstar_tab[cp.cnt < kHStarTab ? cp.cnt : kHStarTab - 1];
+                else hc = cp.cnt <= 2 ? s_hc[cp.cnt - 1] : km_having(p, cp, nullptr);
                 if (hc <= 0) {
                     if (WRITE && hc < 0)
                         for (int kk = k; kk < kend; ++kk) {
@@ -429,7 +436,8 @@ __global__ __launch_bounds__(kKmBlock) void k_km_walk(DPlan* __restrict__ pp, Km
                     }
             } else {
                 // (HAVING over count(*) alone already kept this state above)
-                const int hv = (!SORT && p.having_star) ? 1 : km_having(p, part, SORT ? &sr : nullptr);
+                int hv = 1;
+                if constexpr (!HS) hv = (!SORT && p.having_star) ? 1 : km_having(p, part, SORT ? &sr : nullptr);
                 if (WRITE && hv < 0)
                     for (int kk = k; kk < kend; ++kk) {
                         atomicOr(&res.win_err[d.widx[kk]], EK_WIN_HAVING_ERROR);

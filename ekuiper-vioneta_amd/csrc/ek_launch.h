@@ -34,8 +34,9 @@ void launch_small_win(int nvc, bool where, int rm, bool hs, int grid, int nwin, 
                       const DBatch& src, const int64_t* ab, const int32_t* wl, const int32_t* slot, const int64_t* ob,
                       const Results& res, const SwArith& ar, const SwRedo& rd);
 
-// key-major walks (ek_keymajor.h): k_km_walk<NVC, SORT, WRITE, ONE>, k_grp_walk<SORT, ISF, R, HV>
-void launch_km_walk(int nvc, bool sort, bool write, bool one, int nblk, size_t lds, hipStream_t s, DPlan* p,
+// key-major walks (ek_keymajor.h): k_km_walk<NVC, SORT, WRITE, ONE, HS>, k_grp_walk<SORT, ISF, R, HV>; hs: HAVING absent
+// or over count(*) alone with every key run shorter than kHStarTab (ignored with sort)
+void launch_km_walk(int nvc, bool sort, bool write, bool one, bool hs, int nblk, size_t lds, hipStream_t s, DPlan* p,
                     const KmDesc& d, const Results& res);
 void launch_grp_walk(bool sort, bool isf, int rdep, bool having, dim3 grid, dim3 block, size_t lds, hipStream_t s, DPlan* p,
                      const GrpDesc& g, const Results& res);

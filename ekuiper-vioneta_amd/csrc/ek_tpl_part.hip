@@ -1,4 +1,4 @@
-// ek_tpl_part.hip — instantiations of k_part<MODE, WHERE, NVC> (the pane-mode partition, ek_kernels.h) and its
+// ek_tpl_part.hip — instantiations of k_part<MODE, WHERE, NVC> (MODE 0-3) (the pane-mode partition, ek_kernels.h) and its
 // launcher (ek_launch.h). Units of their own so the device compile runs as parallel jobs.
 #define EK_NO_PLAIN_KERNELS
 #include "ek_launch.h"
@@ -12,7 +12,7 @@ void launch_part(int mode, bool where, int nvc, dim3 grid, size_t lds, hipStream
 #define EK_PART_N(M, W) switch (nvc) { case 1: EK_PART(M, W, 1); break; case 2: EK_PART(M, W, 2); break; \
                                        case 3: EK_PART(M, W, 3); break; default: EK_PART(M, W, 4); break; }
 #define EK_PART_W(M) if (where) { EK_PART_N(M, true) } else { EK_PART_N(M, false) }
-    if (mode == 0) { EK_PART_W(0) } else if (mode == 1) { EK_PART_W(1) } else { EK_PART_W(2) }
+    if (mode == 0) { EK_PART_W(0) } else if (mode == 1) { EK_PART_W(1) } else if (mode == 2) { EK_PART_W(2) } else { EK_PART_N(3, false) }   // (MODE 3: no WHERE plans, fz_eligible)
 #undef EK_PART_W
 #undef EK_PART_N
 #undef EK_PART

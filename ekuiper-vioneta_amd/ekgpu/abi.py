@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 12
+EKGPU_ABI_VERSION = 13
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -154,6 +154,8 @@ class ek_stats(C.Structure):
         ("phase_ms_total", C.c_double * 4),
         ("phase_launches_total", C.c_int64 * 4),
         ("pushes_timed", C.c_int64),
+        ("fused_batches", C.c_int64),
+        ("fused_discarded", C.c_int64),
     ]
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 12
+#define EKGPU_ABI_VERSION 13
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -250,7 +250,8 @@ typedef struct {
     int64_t rows_out;         /* result rows                                    */
     double last_batch_device_ms; /* device time of the last push (HIP events)   */
     /* Device time of the last push per phase (HIP events on the engine stream around each launch):
-     * [EK_PHASE_STATS] batch statistics + pane bounds, [EK_PHASE_PARTITION] k_part,
+     * [EK_PHASE_STATS] batch statistics + pane bounds, [EK_PHASE_PARTITION] k_part (with a fused sorted pass: the
+     * ts read too),
      * [EK_PHASE_AGGREGATE] k_agg, [EK_PHASE_FINALIZE] k_finalize. */
     double phase_ms[4];
     int64_t phase_launches[4];
@@ -265,6 +266,11 @@ typedef struct {
     double phase_ms_total[4];
     int64_t phase_launches_total[4];
     int64_t pushes_timed;
+    /* ABI v13. Pane-mode batches taken by the fused sorted pass (the partition pass checks the batch's ts order, finds
+     * its pane bounds and the hopping gap itself: no separate ts pass), and passes discarded because the batch was not
+     * sorted (or spanned more panes per chunk than presumed): those batches ran the general path instead. */
+    int64_t fused_batches;
+    int64_t fused_discarded;
 } ek_stats;
 
 enum { EK_PHASE_STATS = 0, EK_PHASE_PARTITION = 1, EK_PHASE_AGGREGATE = 2, EK_PHASE_FINALIZE = 3 };
@@ -327,7 +333,9 @@ int ek_set_stream(void* h, void* hip_stream);
 /* Asynchronous pushes (on != 0; default off): ek_push_batch / ek_advance_time return once their work is queued on
  * the handle's stream, and ek_reset queues its zeroing behind it, so the caller's work between two pushes overlaps
  * the device tail of the first. A device-memory batch stays borrowed until the next push, ek_sync, ek_poll_results
- * or ek_get_stats returns; errors of queued work surface there. Turning it off waits for queued work. */
+ * or ek_get_stats returns; a host-memory batch (pageable or pinned) is copied before its push returns. An error of
+ * queued work is returned by the next push, ek_advance_time, ek_get_stats or ek_set_async(h, 0) (EK_ERR_DEVICE).
+ * Turning it off waits for queued work. */
 int ek_set_async(void* h, int32_t on);
 int ek_get_stats(void* h, ek_stats* out);
 const char* ek_last_error(void* h);

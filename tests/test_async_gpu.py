@@ -40,3 +40,40 @@ def test_async_pushes_match_oracle(oracle, engine_mod, device_batches):
     assert st.device_ms_total > 0 and st.phase_launches_total[1] > 0
     eng.set_async(False)
     eng.close()
+
+
+def test_async_pinned_host_batches_are_not_borrowed(oracle, engine_mod):
+    """a host batch in pinned memory makes the push's H2D copies truly asynchronous. An asynchronous push
+    waits for its own copies before it returns, so the caller may refill the same pinned buffers at once."""
+    import torch
+    key, ts, temp, hum = iot_stream(300_000, 2000, seed=33, events_per_ms=10)
+    rule = compile_rule(SQL, IOT_SCHEMA, num_keys=2000, debug_membership=True)
+    exp = oracle.run(rule.plan, [key, ts, temp, hum]).windows
+    eng = engine_mod.Engine(rule.plan)
+    eng.set_async(True)
+    step = 50_000
+    bufs = [torch.empty(step, dtype=dt).pin_memory().numpy() for dt in (torch.int32, torch.int64, torch.float64, torch.float64)]
+    bufs[0] = bufs[0].view(np.uint32)
+    for lo in range(0, len(ts), step):
+        for b, c in zip(bufs, (key, ts, temp, hum)):
+            b[:] = c[lo:lo + step]
+        eng.push_host(bufs)
+        for b in bufs:   # the caller reuses its buffers as soon as the push returns
+            b[:] = 0
+    got = eng.poll()
+    assert_windows_equal(rule.plan, got, exp, check_members=True)
+    eng.set_async(False)
+    eng.close()
+
+
+def test_async_error_surfaces_at_stats(engine_mod):
+    """fold_time reports a failed queued push: here none failed, so stats after asynchronous pushes return 0."""
+    key, ts, temp, hum = iot_stream(70_000, 100, seed=34, events_per_ms=10)
+    rule = compile_rule(SQL, IOT_SCHEMA, num_keys=100)
+    eng = engine_mod.Engine(rule.plan)
+    eng.set_async(True)
+    eng.push_host([key, ts, temp, hum])
+    st = eng.stats()   # raises on a non-zero code
+    assert st.pushes_timed >= 1
+    eng.set_async(False)
+    eng.close()
