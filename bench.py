@@ -457,6 +457,10 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="one process plays rank 0 of an N-GPU run in shard mode (no collective; a single-GPU check of "
                          "the shard path: C4a then sees only its own triggers)")
+    ap.add_argument("--no-route", action="store_true",
+                    help="N > 1: every rank starts from its own key-hash shard of the global stream, partitioned at "
+                         "setup (the host-ingest model of SURVEY.md §8(e)); by default every rank ingests a contiguous "
+                         "slice of the global stream and the step routes it (ek_route_partition + all_to_all)")
     ap.add_argument("--disorder", type=int, default=0, metavar="MS",
                     help="event-time configs: every ts moved back by a hash-chosen 0..MS ms (the stream arrives out of "
                          "order) and the rule compiled with lateTolerance = MS, so nothing is late and the engine's "
@@ -507,9 +511,49 @@ def main():
     elif cfg.get("processing_time"):
         cols, n_glob, k_local = block_stream(cfg, world, rank, dev)
         arr = None
-    else:
+    elif args.no_route:
         cols, arr, n_glob, k_local = shard_stream(cfg, world, rank, dev)
+    else:
+        # the rank's ingest slice of the global stream (global keys, arrivals [rank n, (rank + 1) n)); the router in the
+        # step sends every row to its key's owner (ekgpu.route); the shard dictionaries are the owners' dense key ids
+        from ekgpu.route import owned_key_map
+        n_per, k_glob = cfg["n"], cfg["keys"] * world
+        n_glob = n_per * world
+        c = make_device_stream(n_glob, k_glob, dev, seed=cfg["seed"], events_per_ms=cfg["epm"] * world, t0=cfg["t0"],
+                               lo=rank * n_per, hi=(rank + 1) * n_per)
+        ingest = config_columns(cfg, c, torch.arange(rank * n_per, (rank + 1) * n_per, dtype=torch.int64, device=dev))
+        del c
+        if args.disorder > 0 and iet:
+            ingest[1] = disorder_ts(ingest[1], cfg["seed"] + rank, args.disorder)
+        key_map, owned = owned_key_map(k_glob, world, dev)
+        k_local = owned[rank]
+        cols, arr = None, None
+    routed = world > 1 and not cfg.get("processing_time") and not args.no_route
     blocks = world > 1 and bool(cfg.get("processing_time"))   # window-block shards: the single-GPU path per rank
+    route_ms = [0.0, 0.0]   # routed steps: partition, exchange (host clock around the synchronous calls)
+
+    def route():
+        """The step's router: this rank's ingest slice -> its owned rows of every rank, in global arrival order."""
+        from ekgpu.route import route_exchange, route_partition
+        nonlocal cols, arr, n, ptrs, ts_dev
+        ta = time.perf_counter()
+        types = [3] + [1] * (len(ingest) - 1)   # key EK_COL_U32, then 8-byte columns
+        outs, arr_o, cnts = route_partition(ingest, types, 0, world, key_map, rank * cfg["n"], local)
+        tb = time.perf_counter()
+        got = route_exchange(outs + [arr_o], cnts, dist)
+        torch.cuda.synchronize()
+        route_ms[0] += (tb - ta) * 1e3
+        route_ms[1] += (time.perf_counter() - tb) * 1e3
+        cols, arr = got[:-1], got[-1]
+        n = int(cols[0].numel())
+        ptrs = [x.data_ptr() for x in cols]
+        ts_dev = cols[1]
+
+    n = 0
+    ptrs = []
+    ts_dev = None
+    if routed:
+        route()
     n = int(cols[0].numel())
     rule = compile_rule(cfg["sql"], schema_of(cfg), num_keys=max(1, k_local), is_event_time=iet,
                         late_tolerance_ms=args.disorder if iet else 0)
@@ -580,7 +624,7 @@ def main():
         count_pp = make_partial_plan(crule)
 
     def step():
-        nonlocal ctx, tup, shared
+        nonlocal ctx, tup, shared, cols, arr, n, ptrs, ts_dev
         eng.reset()
         fut = None
         if world == 1 or blocks:
@@ -592,6 +636,8 @@ def main():
             if sent_ptrs:
                 eng.push_device(1, sent_ptrs)
         else:
+            if routed:
+                route()   # the key-hash partition and the exchange, inside the timed step
             if iet and dist is not None:
                 # the router (global WatermarkOp) runs inside the timed step, on the ranks' own rows
                 tup = device_watermark(ts_dev, arr, args.disorder, dist, want_list)
@@ -639,6 +685,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     st0 = eng.stats()   # running totals (the engine's pushes are asynchronous: read back after the loop)
+    route_ms[0] = route_ms[1] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -742,6 +789,15 @@ def main():
                      "dominant_kernel": dominant, "kernels": kernels},
     }
     out["config"]["fused_sorted_batches_last_step"] = int(st1.fused_batches)   # (stream counters restart at ek_reset)
+    if routed:
+        rt = torch.tensor(route_ms, dtype=torch.float64, device=dev)
+        dist.all_reduce(rt, op=dist.ReduceOp.MAX)
+        out["config"]["routing"] = {
+            "partition_ms_per_step": float(rt[0]) / args.steps, "exchange_ms_per_step": float(rt[1]) / args.steps,
+            "what": "inside the timed step, max over ranks: every rank ingests a contiguous slice of the global stream; "
+                    "ek_route_partition splits it by owner = mix64(key) mod N (HIP, stable, keys renamed to the owner's "
+                    "dense ids) and one all_to_all per column (RCCL) delivers every rank its rows in global arrival order"}
+        out["config"]["parallelism"] += " (routed in the step: ek_route_partition + all_to_all)"
     if global_count is not None:
         out["config"]["global_count"] = str(global_count)[:200]
         out["config"]["shared_ts_stats"] = bool(share_stats)

@@ -1,8 +1,9 @@
 // ek_lib.hip — hipCUB radix sorts (separate translation unit: hipCUB headers are heavy). Two users:
 //   * range mode, when an out-of-order batch is merged into the ts-ordered event buffer (the release order of
 //     WatermarkOp, watermark_op.go:157-168: stable in arrival order for equal ts) — off the in-order hot path;
-//   * the key-major span sort of range windows (ek_engine.hip key_major(): (key, position) or (key, value) pairs) —
-//     ON the C4a hot path (≈ 0.26 ms of its step in r04).
+//   * the key-major span sort of range windows (ek_engine.hip km_run(): (key, position) or (key, value) pairs) — only
+//     as the fallback of the MSD partition (km_msd / grp_run: skewed keys, validity, K outside [2^16, 2^27]); no
+//     BASELINE config runs it since round 5 (no rocPRIM kernel in profiles/r05_kernels_*.csv or r06).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 

@@ -101,7 +101,7 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
                     "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
-                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async"]
+                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async", "ek_route_partition"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32, A.EK_COL_BOOL: np.int64}
 

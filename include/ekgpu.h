@@ -405,6 +405,20 @@ typedef struct {
     int64_t n_sess;
 } ek_global_ctx;
 
+/* ---------------------------------------------------------------- key-hash router (ABI v13)
+ * a multi-GPU rule partitions every micro-batch by gpu = hash(key) mod G. The reference has no
+ * counterpart (one process; its channels fan a source out to rules, internal/topo/subtopo.go), so this entry point is
+ * the router's own: the rows of a device batch (one rank's slice of the global stream, global arrivals arrival_base
+ * + i) are split into n_dest segments of out_columns by owner = ek_mix64(key) & (2^62 - 1) mod n_dest, stably (each
+ * segment keeps arrival order); the key column is renamed through key_map (device, key_map_size entries, global key
+ * -> the owner's dense id; NULL keeps it; a key past the table is kept and the call returns EK_ERR_INVALID) and out_arrival (device, NULL = none) receives every routed row's global arrival. Segment d is
+ * rows [sum(dest_counts[<d]), + dest_counts[d]) (dest_counts: host, n_dest entries). column_type gives each
+ * column's width (EK_COL_U32: 4 bytes, else 8); the key column must be EK_COL_U32; validity is not routed.
+ * Synchronous on `stream` (hipStream_t; NULL = the null stream) of HIP device `device`. */
+int ek_route_partition(int device, void* stream, const ek_batch* batch, const int32_t* column_type, int32_t key_column,
+                       int32_t n_dest, const uint32_t* key_map, uint32_t key_map_size, int64_t arrival_base,
+                       void* const* out_columns, int64_t* out_arrival, int64_t* dest_counts);
+
 /* ---------------------------------------------------------------- processing-time clock
  * Processing-time TUMBLING / HOPPING / SLIDING / SESSION windows (WindowOperator.execProcessingWindow,
  * window_op.go:235-470) run under the caller's clock, the way the reference's tests drive them with its mock clock
