@@ -38,27 +38,51 @@
 #include <vector>
 
 #include "../../include/ekgpu.h"
+#include "ek_errmsg.h"
 #include "ek_json_pow5.h"
 
 namespace {
 
 constexpr int kJBlock = 256;
 
+constexpr int kMaxSeg = 8;                     // path segments per column (ABI v14 paths)
+constexpr int32_t kStrNumber = 0x20000000;     // slen flag: a number a STRING field received (soff = its f64 bits)
+constexpr int32_t kStrFlags = EK_JSON_STR_ESCAPED | kStrNumber;
+constexpr uint8_t kErrPending = 0x80;          // first pass: a top-level array payload (decoded by the row-based pass)
+
 struct JSchema {
     int32_t n;
     int32_t type[EK_MAX_COLUMNS];
-    int32_t len[EK_MAX_COLUMNS];
-    uint64_t hash[EK_MAX_COLUMNS];
+    int32_t elem[EK_MAX_COLUMNS];                  // EK_COL_LIST: element type
+    int32_t nseg[EK_MAX_COLUMNS];                  // path length (1: a top-level field)
+    int32_t seg_idx[EK_MAX_COLUMNS][kMaxSeg];      // -1: key segment; >= 0: array element index
+    int32_t seg_off[EK_MAX_COLUMNS][kMaxSeg];      // key segment: its bytes name[c][off, off + len)
+    int32_t seg_len[EK_MAX_COLUMNS][kMaxSeg];
+    uint64_t seg_hash[EK_MAX_COLUMNS][kMaxSeg];    // FNV-1a 64 of the key segment
+    uint32_t all;                                  // mask of the schema's columns
+    int32_t paths;                                 // some column has nseg > 1
     char name[EK_MAX_COLUMNS][EK_JSON_MAX_NAME];
+};
+
+struct JAux {
+    unsigned int nulls[EK_MAX_COLUMNS];            // decoded rows with column c nil (0 -> no validity array)
+    unsigned int pending;                          // first pass: some message is a top-level array
+    unsigned int pad;
+    unsigned long long lcnt[EK_MAX_COLUMNS];       // LIST columns: elements reserved
 };
 
 struct JOut {
     void* col[EK_MAX_COLUMNS];
     uint8_t* valid[EK_MAX_COLUMNS];
     int64_t* soff[EK_MAX_COLUMNS];   // string columns: the value's first content byte (offset into the payload)
-    int32_t* slen[EK_MAX_COLUMNS];   // ... its raw length, | EK_JSON_STR_ESCAPED when it holds a backslash escape
-    uint8_t* err;
-    unsigned int* nulls;   // [EK_MAX_COLUMNS]: decoded messages with column c nil (0 -> no validity array)
+    int32_t* slen[EK_MAX_COLUMNS];   // ... its raw length, | EK_JSON_STR_ESCAPED when it holds a backslash escape;
+                                     // LIST columns: the row's element count (col = its first element)
+    int64_t* lval[EK_MAX_COLUMNS];   // LIST columns: elements
+    uint8_t* lvalid[EK_MAX_COLUMNS];
+    uint8_t* err;                    // per message
+    uint8_t* rerr;                   // per row (== err when every message is one row)
+    const int64_t* rowbase;          // row of message i's first row (nullptr: row i = message i)
+    JAux* aux;
 };
 
 // strconv.ParseBool over raw string content (cast.ToBool(string, CONVERT_ALL), converter.go:600-625): 1 true, 0 false,
@@ -151,7 +175,7 @@ __device__ int big_cmp(const Big& a, const Big& b) {
     return 0;
 }
 // A (the decimal mantissa) * 10^q vs the midpoint above c0: returns c0 or the next double up
-__device__ uint64_t decide_exact_big(Big& A, int64_t q, uint64_t c0) {
+__device__ __noinline__ uint64_t decide_exact_big(Big& A, int64_t q, uint64_t c0) {
     const int64_t e = (int64_t)((c0 >> 52) & 0x7FF);
     const uint64_t m = (c0 & 0x000FFFFFFFFFFFFFull) | (1ull << 52);   // c0 = m * 2^(e - 1075)
     const int64_t E = e - 1076;                                        // midpoint = (2m + 1) * 2^E
@@ -171,13 +195,51 @@ __device__ uint64_t decide_exact(uint64_t w, int64_t q, uint64_t c0) {
     return decide_exact_big(A, q, c0);
 }
 
-// w * 10^q correctly rounded (|w| < 2^64, normal results); false for out-of-range results.
+// sign of w * 10^q - K * 2^-1075 for q < 0 (K odd: a midpoint between two subnormals): both sides times 2^1075 * 5^-q,
+// w * 2^(q + 1075) vs K * 5^-q (at most ~850 bits each)
+__device__ int sub_mid_cmp(uint64_t w, int64_t q, uint64_t K) {
+    Big A, B;
+    big_set(A, w);
+    big_set(B, K);
+    big_shl(A, q + 1075);
+    big_mul_pow5(B, -q);
+    return big_cmp(A, B);
+}
+
+// A result below 2^-1022 (strconv.ParseFloat returns subnormals without error): m = w * 10^q / 2^-1074 rounded half to
+// even, from a double-precision guess corrected by exact midpoint comparisons (the guess is within a few units).
+// bits = m is the binary64 encoding (m = 2^52 is the smallest normal). false: not decided (a guess far off).
+__device__ __noinline__ bool subnormal_exact(uint64_t w, int64_t q, uint64_t* bits) {
+    if (q >= 0) return false;
+    const double x = (double)w * pow(10.0, (double)(q + 300));   // q in [-343, -308]: a normal double
+    double g = x * ldexp(1e-300, 1074);
+    if (!(g >= 0.0) || g > 9007199254740992.0) g = 4503599627370496.0;
+    int64_t m = (int64_t)llrint(g);
+    for (int it = 0; it < 64; ++it) {
+        if (m > 0) {
+            const int c = sub_mid_cmp(w, q, 2 * (uint64_t)m - 1);
+            if (c < 0 || (c == 0 && (m & 1))) { m--; continue; }
+        }
+        const int c = sub_mid_cmp(w, q, 2 * (uint64_t)m + 1);
+        if (c > 0 || (c == 0 && (m & 1))) { m++; continue; }
+        if (m > (int64_t)(1ll << 52)) return false;
+        *bits = (uint64_t)m;
+        return true;
+    }
+    return false;
+}
+
+// w * 10^q correctly rounded (|w| < 2^64, subnormal results included); false for overflowing results.
 __device__ bool dec_to_f64(uint64_t w, int64_t q, bool neg, double* out) {
     if (w == 0 || q < -342) { *out = neg ? -0.0 : 0.0; return true; }   // below 2^-1075 for any 64-bit w
     if (q > 308) return false;
     uint64_t bits;
     bool amb;
-    if (!el_core(w, q, &bits, &amb)) return false;
+    if (!el_core(w, q, &bits, &amb)) {
+        // below the normal range (el_core's exponent <= 0; an overflow has q >= 290): decide the subnormal exactly
+        if (q > -290 || !subnormal_exact(w, q, &bits)) return false;
+        amb = false;
+    }
     if (amb) bits = decide_exact(w, q, bits);
     if (((bits >> 52) & 0x7FF) == 0x7FF) return false;
     if (neg) bits |= 1ull << 63;
@@ -257,6 +319,7 @@ __device__ const uint8_t* parse_number(const uint8_t* p, const uint8_t* e, Num* 
         // the full digit string (up to 100 significant digits) decides against the midpoint
         double up;
         if (!dec_to_f64(n->mant + 1, n->exp10, n->neg, &up)) n->exact = false;
+        else if (up != n->f64 && ((__double_as_longlong(n->f64) >> 52) & 0x7FF) == 0) n->exact = false;   // (subnormal)
         else if (up != n->f64) {
             Big A;
             big_set(A, 0);
@@ -341,7 +404,367 @@ __device__ const uint8_t* skip_value(const uint8_t* p, const uint8_t* e) {
 
 __device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint8_t c) { return (h ^ c) * 0x100000001B3ull; }
 
-// One thread per message: parse the object, scatter its schema fields into the columns.
+// One decoded row: the values the row's columns take (ival: int64 / f64 bits / string hash / LIST first element)
+struct RowAcc {
+    int64_t ival[EK_MAX_COLUMNS];
+    int64_t soff[EK_MAX_COLUMNS];
+    int32_t slen[EK_MAX_COLUMNS];
+    uint32_t seen, isnull;
+};
+
+// a JSON string at p (the opening quote): FNV-1a 64 of its raw content, its content range, escape flag; nullptr on a
+// syntax error
+__device__ __forceinline__ const uint8_t* scan_string(const uint8_t* p, const uint8_t* e, uint64_t* h, const uint8_t** cs,
+                                                      int* n_raw, bool* esc) {
+    *cs = ++p;
+    uint64_t x = 0xCBF29CE484222325ull;
+    bool sesc = false;
+    while (p < e && *p != '"') {
+        if (*p == '\\') {
+            sesc = true;
+            if (p + 1 >= e) return nullptr;
+            x = fnv_step(x, *p);
+            ++p;
+        }
+        x = fnv_step(x, *p);
+        ++p;
+    }
+    if (p >= e) return nullptr;
+    *h = x;
+    *n_raw = (int)(p - *cs);
+    *esc = sesc;
+    return p + 1;
+}
+
+// One array element of a LIST column (decodeArray, converter.go:173-244, with an Items field of type t): number ->
+// extractNumberValue, string -> extractStringValue (a BOOLEAN item through strconv.ParseBool), true / false ->
+// extractBooleanFromValue, null -> nil; an object / array item, or a kind the item type does not take, is "array has
+// wrong type:%v, expect:%v". Writes *v / *ok; returns the position after it (nullptr: *err set).
+__device__ __noinline__ const uint8_t* list_item(int t, const uint8_t* p, const uint8_t* e, int64_t* v, uint8_t* ok, uint8_t* err) {
+    const uint8_t c0 = *p;
+    *v = 0;
+    *ok = 0;
+    if (c0 == 'n') {
+        p = skip_value(p, e);
+        if (!p) *err = EK_JSON_ERR_SYNTAX;
+        return p;
+    }
+    if (c0 == '"') {
+        uint64_t h;
+        const uint8_t* cs;
+        int nr;
+        bool esc;
+        p = scan_string(p, e, &h, &cs, &nr, &esc);
+        if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+        const int b = (t == EK_COL_BOOL && !esc) ? parse_bool_str(cs, nr) : -1;
+        if (b < 0) { *err = EK_JSON_ERR_TYPE; return nullptr; }
+        *v = b;
+        *ok = 1;
+        return p;
+    }
+    if (c0 == 't' || c0 == 'f') {
+        p = skip_value(p, e);
+        if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+        if (t != EK_COL_BOOL) { *err = EK_JSON_ERR_TYPE; return nullptr; }
+        *v = c0 == 't' ? 1 : 0;
+        *ok = 1;
+        return p;
+    }
+    if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+        Num num;
+        p = parse_number(p, e, &num);
+        if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+        if (t == EK_COL_I64) {
+            if (!num.fits_i64) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            *v = num.i64;
+        } else {
+            if (!num.exact) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            *v = t == EK_COL_F64 ? __double_as_longlong(num.f64) : (num.f64 != 0.0 ? 1 : 0);
+        }
+        *ok = 1;
+        return p;
+    }
+    if (c0 == '{' || c0 == '[') { *err = EK_JSON_ERR_TYPE; return nullptr; }
+    *err = EK_JSON_ERR_SYNTAX;
+    return nullptr;
+}
+
+// The value at p (not null) of leaf column col: the schema type decides the conversion (converter.go:328-400 ->
+// extractNumberValue / extractStringValue / extractBooleanFromValue :429-505, getBooleanFromValue :600-625; a LIST
+// column decodeArray :173-244). Returns the position after the value (nullptr: *err set).
+__device__ const uint8_t* leaf_value(const JSchema& S, int col, const uint8_t* p, const uint8_t* e, const uint8_t* bytes,
+                                     RowAcc& R, const JOut& out, uint8_t* err) {
+    const uint8_t c0 = *p;
+    const int t = S.type[col];
+    if (t == EK_COL_LIST) {
+        if (c0 != '[') {   // "a has wrong type:number, expect:array"
+            *err = (c0 == '-' || (c0 >= '0' && c0 <= '9') || c0 == '"' || c0 == 't' || c0 == 'f' || c0 == '{')
+                       ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX;
+            return nullptr;
+        }
+        // count the items (one scan), reserve them, then decode them in order
+        int64_t cnt = 0;
+        const uint8_t* q = p + 1;
+        while (q < e && is_ws(*q)) ++q;
+        if (q < e && *q == ']') {
+            ++q;
+        } else {
+            for (;;) {
+                while (q < e && is_ws(*q)) ++q;
+                q = skip_value(q, e);
+                if (!q) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+                cnt++;
+                while (q < e && is_ws(*q)) ++q;
+                if (q < e && *q == ',') { ++q; continue; }
+                if (q < e && *q == ']') { ++q; break; }
+                *err = EK_JSON_ERR_SYNTAX;
+                return nullptr;
+            }
+        }
+        const int64_t base = cnt ? (int64_t)atomicAdd(&out.aux->lcnt[col], (unsigned long long)cnt) : 0;
+        const uint8_t* r = p + 1;
+        for (int64_t k = 0; k < cnt; ++k) {
+            while (r < e && is_ws(*r)) ++r;
+            int64_t v;
+            uint8_t ok;
+            r = list_item(S.elem[col], r, e, &v, &ok, err);
+            if (!r) return nullptr;
+            out.lval[col][base + k] = v;
+            out.lvalid[col][base + k] = ok;
+            while (r < e && is_ws(*r)) ++r;
+            ++r;   // ',' or ']' (checked by the count scan)
+        }
+        R.ival[col] = base;
+        R.slen[col] = (int32_t)cnt;
+        return q;
+    }
+    if (t == EK_COL_STR || t == EK_COL_BOOL) {
+        if (c0 == '"') {
+            uint64_t h;
+            const uint8_t* cs;
+            int n_raw;
+            bool sesc;
+            p = scan_string(p, e, &h, &cs, &n_raw, &sesc);
+            if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+            if (t == EK_COL_STR) {
+                R.ival[col] = (int64_t)h;   // FNV-1a 64 of the raw content (= of the string when nothing is escaped)
+                R.soff[col] = (int64_t)(cs - bytes);
+                R.slen[col] = n_raw | (sesc ? (int32_t)EK_JSON_STR_ESCAPED : 0);
+            } else {
+                const int b = sesc ? -1 : parse_bool_str(cs, n_raw);
+                if (b < 0) { *err = EK_JSON_ERR_TYPE; return nullptr; }   // strconv.ParseBool: invalid syntax
+                R.ival[col] = b;
+            }
+            return p;
+        }
+        if (c0 == 't' || c0 == 'f') {
+            p = skip_value(p, e);
+            if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+            if (t == EK_COL_STR) { *err = EK_JSON_ERR_TYPE; return nullptr; }   // "has wrong type:true, expect:string"
+            R.ival[col] = c0 == 't' ? 1 : 0;
+            return p;
+        }
+        if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+            Num num;
+            p = parse_number(p, e, &num);
+            if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+            if (!num.exact) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            if (t == EK_COL_STR) {
+                // cast.ToStringAlways(float64) (converter.go:446-451): Go's %v of the number, printed by the host
+                // dictionary (a miss: the float's bits travel in soff)
+                R.ival[col] = 0;
+                R.soff[col] = __double_as_longlong(num.f64);
+                R.slen[col] = kStrNumber;
+            } else {
+                R.ival[col] = num.f64 != 0.0 ? 1 : 0;   // cast.ToBool(float64): != 0
+            }
+            return p;
+        }
+        *err = (c0 == '{' || c0 == '[') ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX;   // object / array: wrong type
+        return nullptr;
+    }
+    if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+        Num num;
+        p = parse_number(p, e, &num);
+        if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+        if (t == EK_COL_F64) {
+            if (!num.exact) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            R.ival[col] = __double_as_longlong(num.f64);
+        } else {
+            if (!num.fits_i64) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            if (t == EK_COL_U32 && (num.i64 < 0 || num.i64 > 0xFFFFFFFFll)) { *err = EK_JSON_ERR_NUMBER; return nullptr; }
+            R.ival[col] = num.i64;
+        }
+        return p;
+    }
+    // string / bool / object / array for a numeric schema field (converter.go checkSchema / extract*)
+    *err = (c0 == '"' || c0 == 't' || c0 == 'f' || c0 == '{' || c0 == '[') ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX;
+    return nullptr;
+}
+
+// One object (p at its '{') into R: decodeObject (converter.go:246-409) restated over the schema's column paths. Frame
+// d is the container at path depth d with the columns whose path runs through it (act); a member whose key (an array
+// element whose index) is the next segment of some active column is a leaf of the columns that end there, or the
+// container the others descend into; any other member is skipped. Returns the position after the object (nullptr:
+// *err set). PATHS = false: every column is a top-level field (depth 0 only).
+template <bool PATHS>
+__device__ const uint8_t* decode_object(const JSchema& S, const uint8_t* p, const uint8_t* e, const uint8_t* bytes, RowAcc& R,
+                                        const JOut& out, uint8_t* err) {
+    struct Frame {
+        uint32_t act;
+        int32_t idx;
+        int32_t arr;
+    };
+    Frame fr[PATHS ? kMaxSeg : 1];
+    int d = 0;
+    fr[0].act = S.all;
+    fr[0].idx = 0;
+    fr[0].arr = 0;
+    ++p;
+    bool open = true;   // the current container has no member yet
+    for (;;) {
+        while (p < e && is_ws(*p)) ++p;
+        if (p >= e) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+        const Frame f = fr[PATHS ? d : 0];
+        bool closed = false;
+        if (open && *p == (f.arr ? ']' : '}')) {
+            ++p;
+            closed = true;
+        } else {
+            uint32_t M = 0;
+            if (!f.arr) {
+                if (*p != '"') { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+                const uint8_t* ks = ++p;
+                uint64_t h = 0xCBF29CE484222325ull;
+                bool esc = false;
+                while (p < e && *p != '"') {
+                    if (*p == '\\') {
+                        esc = true;
+                        if (++p >= e) break;
+                    }
+                    h = fnv_step(h, *p);
+                    ++p;
+                }
+                if (p >= e) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+                const int klen = (int)(p - ks);
+                ++p;
+                if (!esc) {
+                    for (uint32_t a = f.act; a; a &= a - 1) {
+                        const int c = __ffs(a) - 1;
+                        if (S.seg_idx[c][PATHS ? d : 0] >= 0 || S.seg_hash[c][PATHS ? d : 0] != h ||
+                            S.seg_len[c][PATHS ? d : 0] != klen)
+                            continue;
+                        const char* nm = S.name[c] + S.seg_off[c][PATHS ? d : 0];
+                        bool eq = true;
+                        for (int k = 0; k < klen; ++k) eq &= (uint8_t)nm[k] == ks[k];
+                        if (eq) M |= 1u << c;
+                    }
+                }
+                while (p < e && is_ws(*p)) ++p;
+                if (p >= e || *p != ':') { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+                ++p;
+                while (p < e && is_ws(*p)) ++p;
+                if (p >= e) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+            } else {
+                const int j = f.idx;
+                fr[PATHS ? d : 0].idx = j + 1;
+                for (uint32_t a = f.act; a; a &= a - 1) {
+                    const int c = __ffs(a) - 1;
+                    if (S.seg_idx[c][PATHS ? d : 0] == j) M |= 1u << c;
+                }
+            }
+            const uint8_t c0 = *p;
+            if (!M) {
+                p = skip_value(p, e);
+                if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+            } else {
+                uint32_t L = 0, I = 0;
+                for (uint32_t a = M; a; a &= a - 1) {
+                    const int c = __ffs(a) - 1;
+                    if (S.nseg[c] == d + 1) L |= 1u << c;
+                    else I |= 1u << c;
+                }
+                if (c0 == 'n') {
+                    // nil: the leaves are nil, and so is every leaf below a nil container (m[key] = nil)
+                    p = skip_value(p, e);
+                    if (!p) { *err = EK_JSON_ERR_SYNTAX; return nullptr; }
+                    R.seen |= M;
+                    R.isnull |= M;
+                } else if (PATHS && I) {
+                    // the path continues: the value must be the container kind the next segments name
+                    // ("a has wrong type:number, expect:struct"; a scalar leaf column on the same key gets a container)
+                    uint32_t want_arr = 0;
+                    for (uint32_t a = I; a; a &= a - 1) {
+                        const int c = __ffs(a) - 1;
+                        if (S.seg_idx[c][d + 1] >= 0) want_arr |= 1u << c;
+                    }
+                    const bool ok = (c0 == '{' && !want_arr) || (c0 == '[' && want_arr == I);
+                    if (!ok) {
+                        *err = (c0 == '{' || c0 == '[' || c0 == '"' || c0 == 't' || c0 == 'f' || c0 == '-' ||
+                                (c0 >= '0' && c0 <= '9')) ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX;
+                        return nullptr;
+                    }
+                    if (L) { *err = EK_JSON_ERR_UNSUPPORTED; return nullptr; }   // a column ends where another descends
+                    // a repeated key replaces the whole subtree (Go map assignment): its leaves start unseen again
+                    R.seen &= ~I;
+                    R.isnull &= ~I;
+                    ++d;
+                    fr[d].act = I;
+                    fr[d].idx = 0;
+                    fr[d].arr = c0 == '[';
+                    ++p;
+                    open = true;
+                    continue;
+                } else {
+                    const uint8_t* q = p;
+                    for (uint32_t a = L; a; a &= a - 1) {   // (two columns may name one field)
+                        const int c = __ffs(a) - 1;
+                        q = leaf_value(S, c, p, e, bytes, R, out, err);
+                        if (!q) return nullptr;
+                    }
+                    p = q;
+                    R.seen |= L;
+                    R.isnull &= ~L;
+                }
+            }
+        }
+        // separators and closing brackets back up the frames
+        for (;;) {
+            if (closed) {
+                if (d == 0) return p;
+                --d;
+            }
+            while (p < e && is_ws(*p)) ++p;
+            const uint8_t cl = fr[PATHS ? d : 0].arr ? ']' : '}';
+            if (p < e && *p == ',') { ++p; open = false; break; }
+            if (p < e && *p == cl) { ++p; closed = true; continue; }
+            *err = EK_JSON_ERR_SYNTAX;
+            return nullptr;
+        }
+    }
+}
+
+__device__ __forceinline__ void emit_row(const JSchema& S, const JOut& out, int64_t r, const RowAcc& R, bool good) {
+    for (int c = 0; c < S.n; ++c) {
+        const bool ok = good && ((R.seen >> c) & 1u) && !((R.isnull >> c) & 1u);
+        if (good && !ok) atomicAdd(&out.aux->nulls[c], 1u);
+        if (out.valid[c]) out.valid[c][r] = ok ? 1 : 0;
+        const int64_t v = ok ? R.ival[c] : 0;
+        if (S.type[c] == EK_COL_U32) ((uint32_t*)out.col[c])[r] = (uint32_t)v;
+        else ((int64_t*)out.col[c])[r] = v;
+        if (S.type[c] == EK_COL_STR) {
+            out.soff[c][r] = ok ? R.soff[c] : 0;
+            out.slen[c][r] = ok ? R.slen[c] : 0;
+        } else if (S.type[c] == EK_COL_LIST) {
+            out.slen[c][r] = ok ? R.slen[c] : 0;
+        }
+    }
+}
+
+// One thread per message: an object is one row; a top-level array of objects (decodeWithSchema's []map case,
+// converter.go:141-158) is one row per element, at rows [rowbase[i], rowbase[i + 1]) (first pass, rowbase = nullptr:
+// the message is marked pending and decoded by the row-based pass). Errors fail the whole message.
+template <bool PATHS>
 __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
                                                          int64_t n, const JSchema* __restrict__ sch, JOut out) {
     const int64_t i = (int64_t)blockIdx.x * kJBlock + threadIdx.x;
@@ -349,149 +772,92 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
     const JSchema& S = *sch;
     const uint8_t* p = bytes + off[i];
     const uint8_t* e = bytes + off[i + 1];
-    int64_t ival[EK_MAX_COLUMNS];
-    int64_t soff[EK_MAX_COLUMNS];
-    int32_t slen[EK_MAX_COLUMNS];
-    uint32_t seen = 0, isnull = 0;
+    RowAcc R;
+    R.seen = 0;
+    R.isnull = 0;
     uint8_t err = EK_JSON_OK;
+    const int64_t r0 = out.rowbase ? out.rowbase[i] : i;
+    const int64_t nr = out.rowbase ? out.rowbase[i + 1] - r0 : 1;
+    int64_t done = 0;
     while (p < e && is_ws(*p)) ++p;
-    if (p >= e || *p != '{') err = (p < e && *p == '[') ? EK_JSON_ERR_UNSUPPORTED : EK_JSON_ERR_SYNTAX;
-    else {
-        ++p;
-        bool after_comma = false;
-        for (;;) {
+    if (p < e && *p == '{') {
+        p = decode_object<PATHS>(S, p, e, bytes, R, out, &err);
+        if (p) {
+            emit_row(S, out, r0, R, true);
+            done = 1;
+        }
+    } else if (p < e && *p == '[') {
+        if (!out.rowbase) {
+            err = kErrPending;
+            atomicOr(&out.aux->pending, 1u);
+        } else {
+            ++p;
             while (p < e && is_ws(*p)) ++p;
-            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
-            if (*p == '}') {
-                if (after_comma) err = EK_JSON_ERR_SYNTAX;   // trailing comma
+            if (p < e && *p == ']') {
                 ++p;
-                break;
-            }
-            if (*p != '"') { err = EK_JSON_ERR_SYNTAX; break; }
-            // key
-            const uint8_t* ks = ++p;
-            uint64_t h = 0xCBF29CE484222325ull;
-            bool esc = false;
-            while (p < e && *p != '"') { if (*p == '\\') { esc = true; ++p; } h = fnv_step(h, *p); ++p; }
-            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
-            const int klen = (int)(p - ks);
-            ++p;
-            int col = -1;
-            if (!esc)
-                for (int c = 0; c < S.n; ++c) {
-                    if (S.hash[c] != h || S.len[c] != klen) continue;
-                    bool eq = true;
-                    for (int k = 0; k < klen; ++k) eq &= (uint8_t)S.name[c][k] == ks[k];
-                    if (eq) { col = c; break; }
-                }
-            while (p < e && is_ws(*p)) ++p;
-            if (p >= e || *p != ':') { err = EK_JSON_ERR_SYNTAX; break; }
-            ++p;
-            while (p < e && is_ws(*p)) ++p;
-            if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
-            const uint8_t c0 = *p;
-            if (col < 0) {
-                p = skip_value(p, e);
-                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
-            } else if (c0 == 'n') {
-                p = skip_value(p, e);
-                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
-                seen |= 1u << col;
-                isnull |= 1u << col;
-            } else if (S.type[col] == EK_COL_STR || S.type[col] == EK_COL_BOOL) {
-                // string / boolean schema fields (converter.go:328-400 -> extractStringValue / extractBooleanFromValue /
-                // extractNumberValue, getBooleanFromValue :600-625)
-                const int t = S.type[col];
-                if (c0 == '"') {
-                    const uint8_t* cs = p + 1;
-                    uint64_t h = 0xCBF29CE484222325ull;
-                    bool sesc = false;
-                    ++p;
-                    while (p < e && *p != '"') {
-                        if (*p == '\\') {
-                            sesc = true;
-                            if (p + 1 >= e) { p = e; break; }
-                            h = fnv_step(h, *p);
-                            ++p;
-                        }
-                        h = fnv_step(h, *p);
-                        ++p;
-                    }
-                    if (p >= e) { err = EK_JSON_ERR_SYNTAX; break; }
-                    const int n_raw = (int)(p - cs);
-                    ++p;
-                    if (t == EK_COL_STR) {
-                        ival[col] = (int64_t)h;   // FNV-1a 64 of the raw content (= of the string when nothing is escaped)
-                        soff[col] = (int64_t)(cs - bytes);
-                        slen[col] = n_raw | (sesc ? (int32_t)EK_JSON_STR_ESCAPED : 0);
-                    } else {
-                        const int b = sesc ? -1 : parse_bool_str(cs, n_raw);
-                        if (b < 0) { err = EK_JSON_ERR_TYPE; break; }   // strconv.ParseBool: invalid syntax
-                        ival[col] = b;
-                    }
-                } else if (c0 == 't' || c0 == 'f') {
-                    p = skip_value(p, e);
-                    if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
-                    if (t == EK_COL_STR) { err = EK_JSON_ERR_TYPE; break; }   // "has wrong type:true, expect:string"
-                    ival[col] = c0 == 't' ? 1 : 0;
-                } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
-                    Num num;
-                    p = parse_number(p, e, &num);
-                    if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
-                    // a number for a string field is cast.ToStringAlways(f64) (%v of the float): left to the host converter
-                    if (t == EK_COL_STR) { err = EK_JSON_ERR_UNSUPPORTED; break; }
-                    if (!num.exact) { err = EK_JSON_ERR_NUMBER; break; }
-                    ival[col] = num.f64 != 0.0 ? 1 : 0;   // cast.ToBool(float64): != 0
-                } else {
-                    err = EK_JSON_ERR_TYPE;   // object / array
+            } else {
+                for (;;) {
+                    while (p < e && is_ws(*p)) ++p;
+                    // every element must be an object ("value doesn't contain object", converter.go:147-150)
+                    if (p >= e || *p != '{' || done >= nr) { err = (p < e && *p != '{') ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX; break; }
+                    R.seen = 0;
+                    R.isnull = 0;
+                    p = decode_object<PATHS>(S, p, e, bytes, R, out, &err);
+                    if (!p) break;
+                    emit_row(S, out, r0 + done, R, true);
+                    done++;
+                    while (p < e && is_ws(*p)) ++p;
+                    if (p < e && *p == ',') { ++p; continue; }
+                    if (p < e && *p == ']') { ++p; break; }
+                    err = EK_JSON_ERR_SYNTAX;
                     break;
                 }
-                seen |= 1u << col;
-                isnull &= ~(1u << col);
-            } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
-                Num num;
-                p = parse_number(p, e, &num);
-                if (!p) { err = EK_JSON_ERR_SYNTAX; break; }
-                const int t = S.type[col];
-                if (t == EK_COL_F64) {
-                    if (!num.exact) { err = EK_JSON_ERR_NUMBER; break; }
-                    ival[col] = __double_as_longlong(num.f64);
-                } else {
-                    if (!num.fits_i64) { err = EK_JSON_ERR_NUMBER; break; }
-                    if (t == EK_COL_U32 && (num.i64 < 0 || num.i64 > 0xFFFFFFFFll)) { err = EK_JSON_ERR_NUMBER; break; }
-                    ival[col] = num.i64;
-                }
-                seen |= 1u << col;
-                isnull &= ~(1u << col);
-            } else {
-                // string / bool / object / array for a numeric schema field (converter.go checkSchema)
-                err = EK_JSON_ERR_TYPE;
-                break;
             }
-            while (p < e && is_ws(*p)) ++p;
-            if (p < e && *p == ',') { ++p; after_comma = true; continue; }
-            if (p < e && *p == '}') { ++p; break; }
-            err = EK_JSON_ERR_SYNTAX;
-            break;
         }
-        if (err == EK_JSON_OK) {
-            while (p < e && is_ws(*p)) ++p;
-            if (p != e) err = EK_JSON_ERR_SYNTAX;   // trailing bytes after the object
-        }
+    } else {
+        err = EK_JSON_ERR_SYNTAX;   // not an object / array payload (decodeWithSchema's "only map ... is supported")
+    }
+    if (err == EK_JSON_OK) {
+        while (p < e && is_ws(*p)) ++p;
+        if (p != e) err = EK_JSON_ERR_SYNTAX;   // trailing bytes after the value
+        else if (done != nr) err = EK_JSON_ERR_SYNTAX;   // (the row count scan disagreed)
     }
     out.err[i] = err;
-    for (int c = 0; c < S.n; ++c) {
-        const bool ok = err == EK_JSON_OK && ((seen >> c) & 1u) && !((isnull >> c) & 1u);
-        if (err == EK_JSON_OK && !ok) atomicAdd(&out.nulls[c], 1u);
-        if (out.valid[c]) out.valid[c][i] = ok ? 1 : 0;
-        const int64_t v = ok ? ival[c] : 0;
-        if (S.type[c] == EK_COL_U32) ((uint32_t*)out.col[c])[i] = (uint32_t)v;
-        else ((int64_t*)out.col[c])[i] = v;
-        if (S.type[c] == EK_COL_STR) {
-            out.soff[c][i] = ok ? soff[c] : 0;
-            out.slen[c][i] = ok ? slen[c] : 0;
+    if (out.rerr != out.err)
+        for (int64_t k = 0; k < nr; ++k) out.rerr[r0 + k] = err;
+    if (err != EK_JSON_OK) {
+        // a failed message leaves no row: its rows are dropped by the compaction (valid bytes zeroed for determinism)
+        R.seen = 0;
+        for (int64_t k = (out.rowbase ? 0 : done); k < nr; ++k) emit_row(S, out, r0 + k, R, false);
+    }
+}
+
+// rows of every message (row-based pass): 1 for an object, the element count of a top-level array
+__global__ __launch_bounds__(kJBlock) void k_json_rows(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
+                                                       int64_t n, int64_t* __restrict__ rows) {
+    const int64_t i = (int64_t)blockIdx.x * kJBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = bytes + off[i];
+    const uint8_t* e = bytes + off[i + 1];
+    while (p < e && is_ws(*p)) ++p;
+    int64_t c = 1;
+    if (p < e && *p == '[') {
+        c = 0;
+        ++p;
+        while (p < e && is_ws(*p)) ++p;
+        if (p < e && *p != ']') {
+            for (;;) {
+                while (p < e && is_ws(*p)) ++p;
+                p = skip_value(p, e);
+                if (!p) break;
+                c++;
+                while (p < e && is_ws(*p)) ++p;
+                if (p < e && *p == ',') { ++p; continue; }
+                break;
+            }
         }
     }
+    rows[i] = c;
 }
 
 // stable compaction of the messages that decoded (same scheme as the range-mode trigger lists)
@@ -543,6 +909,39 @@ __global__ __launch_bounds__(kJBlock) void k_ok_pos(const uint8_t* __restrict__ 
         __syncthreads();
     }
 }
+// exclusive scan of the rows per message -> rowbase[0..n] (per 4096-message tile: sum, tile offsets, block scan)
+__global__ __launch_bounds__(kJBlock) void k_rows_tile_sum(const int64_t* __restrict__ rows, int64_t n, int64_t* tsum) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    int64_t c = 0;
+    for (int k = threadIdx.x; k < kTile; k += kJBlock) { const int64_t i = base + k; if (i < n) c += rows[i]; }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ int64_t s[kJBlock / 64];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tsum[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+__global__ __launch_bounds__(kJBlock) void k_rows_tile_scan(const int64_t* __restrict__ rows, int64_t n,
+                                                            const int64_t* __restrict__ tsum, int nb,
+                                                            int64_t* __restrict__ rowbase) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    __shared__ int64_t wsum[kJBlock / 64];
+    int64_t run = tsum[blockIdx.x];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k0 = 0; k0 < kTile; k0 += kJBlock) {
+        const int64_t i = base + k0 + threadIdx.x;
+        const int64_t v = i < n ? rows[i] : 0;
+        int64_t x = v;
+        for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        int64_t wb = 0, tot = 0;
+        for (int w = 0; w < kJBlock / 64; ++w) { if (w < wv) wb += wsum[w]; tot += wsum[w]; }
+        if (i < n) rowbase[i] = run + wb + x - v;
+        run += tot;
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) rowbase[n] = tsum[nb];
+}
 __global__ void k_compact_col(const int64_t* __restrict__ pos, int64_t n, const void* __restrict__ src, void* __restrict__ dst,
                               int es) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -581,7 +980,7 @@ __global__ __launch_bounds__(256) void k_str_lookup(const int64_t* __restrict__ 
         if (valid[i]) {
             const int32_t L = slen[i];
             bool found = false;
-            if (!(L & EK_JSON_STR_ESCAPED) && bits) {
+            if (!(L & kStrFlags) && bits) {
                 const uint64_t h = str_key((uint64_t)hash[i]);
                 for (uint64_t k = str_slot(h, bits);; k = (k + 1) & mask) {
                     const uint64_t t = tkey[k];
@@ -609,7 +1008,8 @@ __global__ void k_str_gather(const uint8_t* __restrict__ bytes, const MissRec* _
                              int64_t nm, uint8_t* __restrict__ dst) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nm; k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t o = miss[k].off, d = dpos[k];
-        const int32_t L = miss[k].len & ~(int32_t)EK_JSON_STR_ESCAPED;
+        if (miss[k].len & kStrNumber) continue;   // (a number: no payload bytes)
+        const int32_t L = miss[k].len & ~kStrFlags;
         for (int32_t j = 0; j < L; ++j) dst[d + j] = bytes[o + j];
     }
 }
@@ -718,7 +1118,11 @@ struct JsonDecoder {
     hipStream_t stream = nullptr;
     std::string err;
     Buf in_bytes, in_off, raw_col[EK_MAX_COLUMNS], raw_valid[EK_MAX_COLUMNS], out_col[EK_MAX_COLUMNS],
-        out_valid[EK_MAX_COLUMNS], msg_err, pos, cnt, nulls;
+        out_valid[EK_MAX_COLUMNS], msg_err, row_err, pos, cnt, aux, rowbase;
+    Buf lval[EK_MAX_COLUMNS], lvalid[EK_MAX_COLUMNS];   // LIST columns: the elements (ek_json_list)
+    const int64_t* list_start[EK_MAX_COLUMNS] = {};
+    const int32_t* list_len[EK_MAX_COLUMNS] = {};
+    std::vector<int64_t> h_rows_of;                    // rows per message of the last decode (ek_json_rows)
     Buf raw_soff[EK_MAX_COLUMNS], raw_slen[EK_MAX_COLUMNS], out_soff[EK_MAX_COLUMNS], out_slen[EK_MAX_COLUMNS];
     const int64_t* str_off[EK_MAX_COLUMNS] = {};   // the last decode's string references (ek_json_strings)
     const int32_t* str_len[EK_MAX_COLUMNS] = {};
@@ -747,31 +1151,88 @@ struct JsonDecoder {
     }
     ~JsonDecoder() {
         if (stream) hipStreamSynchronize(stream);
-        for (Buf* b : {&in_bytes, &in_off, &msg_err, &pos, &cnt, &nulls, &miss, &n_miss, &gat_pos, &gat_bytes, &fix_rows, &fix_ids})
+        for (Buf* b : {&in_bytes, &in_off, &msg_err, &row_err, &pos, &cnt, &aux, &rowbase, &miss, &n_miss, &gat_pos, &gat_bytes,
+                       &fix_rows, &fix_ids})
             if (b->p) hipFree(b->p);
         for (int c = 0; c < EK_MAX_COLUMNS; ++c)
             for (Buf* b : {&raw_col[c], &raw_valid[c], &out_col[c], &out_valid[c], &raw_soff[c], &raw_slen[c], &out_soff[c],
-                           &out_slen[c], &id_col[c], &tkey[c], &tval[c], &tlen[c]})
+                           &out_slen[c], &id_col[c], &tkey[c], &tval[c], &tlen[c], &lval[c], &lvalid[c]})
                 if (b->p) hipFree(b->p);
         if (d_sch) hipFree(d_sch);
         if (stream) hipStreamDestroy(stream);
     }
 
+    // a column name -> path segments (ABI v14 paths: "a.b", "a[0]", "a[0][0].c"); without paths the name is one key
+    int compile_path(int c, const char* nm, size_t L, bool paths) {
+        int ns = 0;
+        auto key = [&](size_t off, size_t len) {
+            if (len == 0 || ns >= kMaxSeg) return false;
+            uint64_t h = 0xCBF29CE484222325ull;
+            for (size_t k = 0; k < len; ++k) h = (h ^ (uint8_t)nm[off + k]) * 0x100000001B3ull;
+            sch.seg_idx[c][ns] = -1;
+            sch.seg_off[c][ns] = (int32_t)off;
+            sch.seg_len[c][ns] = (int32_t)len;
+            sch.seg_hash[c][ns] = h;
+            ns++;
+            return true;
+        };
+        if (!paths) {
+            key(0, L);
+        } else {
+            size_t k = 0;
+            while (k < L) {
+                size_t ke = k;
+                while (ke < L && nm[ke] != '.' && nm[ke] != '[') ++ke;
+                if (ke > k) {
+                    if (!key(k, ke - k)) return fail(EK_ERR_INVALID, "bad path \"%s\"", nm);
+                } else if (ns == 0 || nm[k] != '[') {
+                    return fail(EK_ERR_INVALID, "bad path \"%s\" (a path starts with a field name)", nm);
+                }
+                k = ke;
+                while (k < L && nm[k] == '[') {
+                    size_t q = k + 1;
+                    int64_t idx = 0;
+                    while (q < L && nm[q] >= '0' && nm[q] <= '9' && idx < (1ll << 30)) idx = idx * 10 + (nm[q++] - '0');
+                    if (q == k + 1 || q >= L || nm[q] != ']' || ns >= kMaxSeg)
+                        return fail(EK_ERR_INVALID, "bad path \"%s\" (array index)", nm);
+                    sch.seg_idx[c][ns] = (int32_t)idx;
+                    sch.seg_off[c][ns] = 0;
+                    sch.seg_len[c][ns] = 0;
+                    sch.seg_hash[c][ns] = 0;
+                    ns++;
+                    k = q + 1;
+                }
+                if (k < L) {
+                    if (nm[k] != '.' || k + 1 >= L) return fail(EK_ERR_INVALID, "bad path \"%s\"", nm);
+                    ++k;
+                }
+            }
+        }
+        if (ns == 0) return fail(EK_ERR_INVALID, "bad field name %d", c);
+        sch.nseg[c] = ns;
+        if (ns > 1) sch.paths = 1;
+        return 0;
+    }
+
     int init(const ek_json_schema* s, int device) {
         if (!s || s->n_fields <= 0 || s->n_fields > EK_MAX_COLUMNS) return fail(EK_ERR_INVALID, "bad schema field count");
         sch.n = s->n_fields;
+        sch.all = sch.n >= 32 ? 0xFFFFFFFFu : (1u << sch.n) - 1u;
         for (int c = 0; c < sch.n; ++c) {
             const int t = s->column_type[c];
-            if (t != EK_COL_I64 && t != EK_COL_F64 && t != EK_COL_U32 && t != EK_COL_STR && t != EK_COL_BOOL)
+            if (t != EK_COL_I64 && t != EK_COL_F64 && t != EK_COL_U32 && t != EK_COL_STR && t != EK_COL_BOOL && t != EK_COL_LIST)
                 return fail(EK_ERR_INVALID, "bad column type");
             sch.type[c] = t;
+            if (t == EK_COL_LIST) {
+                const int et = s->elem_type[c];
+                if (et != EK_COL_I64 && et != EK_COL_F64 && et != EK_COL_BOOL)
+                    return fail(EK_ERR_INVALID, "LIST column %d: element type must be BIGINT, FLOAT or BOOLEAN", c);
+                sch.elem[c] = et;
+            }
             const size_t L = strnlen(s->names[c], EK_JSON_MAX_NAME);
             if (L == 0 || L >= EK_JSON_MAX_NAME) return fail(EK_ERR_INVALID, "bad field name %d", c);
             memcpy(sch.name[c], s->names[c], L);
-            sch.len[c] = (int32_t)L;
-            uint64_t h = 0xCBF29CE484222325ull;
-            for (size_t k = 0; k < L; ++k) h = (h ^ (uint8_t)s->names[c][k]) * 0x100000001B3ull;
-            sch.hash[c] = h;
+            if (int rc = compile_path(c, sch.name[c], L, s->paths != 0)) return rc;
         }
         if (hipSetDevice(device) != hipSuccess) return fail(EK_ERR_DEVICE, "hipSetDevice(%d) failed", device);
         dev = device;
@@ -781,12 +1242,51 @@ struct JsonDecoder {
         return 0;
     }
 
+    int launch_decode(const uint8_t* d_bytes, const int64_t* d_off, int64_t n, const JOut& jo) {
+        const dim3 g((unsigned)((n + kJBlock - 1) / kJBlock));
+        if (sch.paths) hipLaunchKernelGGL(k_json_decode<true>, g, dim3(kJBlock), 0, stream, d_bytes, d_off, n, d_sch, jo);
+        else hipLaunchKernelGGL(k_json_decode<false>, g, dim3(kJBlock), 0, stream, d_bytes, d_off, n, d_sch, jo);
+        return 0;
+    }
+    // the per-row output arrays for `rows` rows (LIST elements: at most one per two payload bytes, plus one per row)
+    int row_buffers(int64_t rows, int64_t n_bytes, JOut& jo) {
+        const int64_t rr = std::max<int64_t>(rows, 1);
+        for (int c = 0; c < sch.n; ++c) {
+            const size_t es = sch.type[c] == EK_COL_U32 ? 4 : 8;
+            if (int rc = ensure(raw_col[c], (size_t)rr * es)) return rc;
+            if (int rc = ensure(raw_valid[c], (size_t)rr)) return rc;
+            jo.col[c] = raw_col[c].p;
+            jo.valid[c] = (uint8_t*)raw_valid[c].p;
+            str_off[c] = nullptr;
+            str_len[c] = nullptr;
+            list_start[c] = nullptr;
+            list_len[c] = nullptr;
+            if (sch.type[c] == EK_COL_STR) {
+                if (int rc = ensure(raw_soff[c], (size_t)rr * 8)) return rc;
+                jo.soff[c] = (int64_t*)raw_soff[c].p;
+            }
+            if (sch.type[c] == EK_COL_STR || sch.type[c] == EK_COL_LIST) {
+                if (int rc = ensure(raw_slen[c], (size_t)rr * 4)) return rc;
+                jo.slen[c] = (int32_t*)raw_slen[c].p;
+            }
+            if (sch.type[c] == EK_COL_LIST) {
+                const size_t cap = (size_t)(n_bytes / 2 + rr + 1);
+                if (int rc = ensure(lval[c], cap * 8)) return rc;
+                if (int rc = ensure(lvalid[c], cap)) return rc;
+                jo.lval[c] = (int64_t*)lval[c].p;
+                jo.lvalid[c] = (uint8_t*)lvalid[c].p;
+            }
+        }
+        return 0;
+    }
+
     int decode(const char* bytes, int64_t n_bytes, const int64_t* offsets, int64_t n, int32_t memory, ek_batch* out) {
         if (!out || n < 0 || n_bytes < 0 || (n > 0 && (!bytes || !offsets))) return fail(EK_ERR_INVALID, "bad arguments");
         memset(out, 0, sizeof *out);
         out->memory = EK_MEM_DEVICE;
         last_n = n;
         last_ok = 0;
+        h_rows_of.clear();
         if (n == 0) return 0;
         const uint8_t* d_bytes = (const uint8_t*)bytes;
         const int64_t* d_off = offsets;
@@ -800,72 +1300,104 @@ struct JsonDecoder {
             d_off = (const int64_t*)in_off.p;
         }
         JOut jo{};
-        for (int c = 0; c < sch.n; ++c) {
-            const size_t es = sch.type[c] == EK_COL_U32 ? 4 : 8;
-            if (int rc = ensure(raw_col[c], (size_t)n * es)) return rc;
-            if (int rc = ensure(raw_valid[c], (size_t)n)) return rc;
-            jo.col[c] = raw_col[c].p;
-            jo.valid[c] = (uint8_t*)raw_valid[c].p;
-            str_off[c] = nullptr;
-            str_len[c] = nullptr;
-            if (sch.type[c] == EK_COL_STR) {
-                if (int rc = ensure(raw_soff[c], (size_t)n * 8)) return rc;
-                if (int rc = ensure(raw_slen[c], (size_t)n * 4)) return rc;
-                jo.soff[c] = (int64_t*)raw_soff[c].p;
-                jo.slen[c] = (int32_t*)raw_slen[c].p;
-            }
-        }
+        if (int rc = row_buffers(n, n_bytes, jo)) return rc;
         if (int rc = ensure(msg_err, (size_t)n)) return rc;
-        if (int rc = ensure(nulls, EK_MAX_COLUMNS * 4)) return rc;
-        hipMemsetAsync(nulls.p, 0, EK_MAX_COLUMNS * 4, stream);
+        if (int rc = ensure(aux, sizeof(JAux))) return rc;
+        hipMemsetAsync(aux.p, 0, sizeof(JAux), stream);
         jo.err = (uint8_t*)msg_err.p;
-        jo.nulls = (unsigned int*)nulls.p;
-        hipLaunchKernelGGL(k_json_decode, dim3((unsigned)((n + kJBlock - 1) / kJBlock)), dim3(kJBlock), 0, stream, d_bytes,
-                           d_off, n, d_sch, jo);
-        const int nb = (int)((n + kTile - 1) / kTile);
+        jo.rerr = jo.err;
+        jo.rowbase = nullptr;
+        jo.aux = (JAux*)aux.p;
+        launch_decode(d_bytes, d_off, n, jo);
+        int nb = (int)((n + kTile - 1) / kTile);
         if (int rc = ensure(cnt, (size_t)(nb + 1) * 8)) return rc;
         hipLaunchKernelGGL(k_ok_count, dim3(nb), dim3(kJBlock), 0, stream, (const uint8_t*)msg_err.p, n, (int64_t*)cnt.p);
         hipLaunchKernelGGL(k_scan_cnt, dim3(1), dim3(1024), 0, stream, (int64_t*)cnt.p, nb);
         int64_t ok = 0;
-        unsigned int h_nulls[EK_MAX_COLUMNS];
+        JAux h_aux;
         hipMemcpyAsync(&ok, (int64_t*)cnt.p + nb, 8, hipMemcpyDeviceToHost, stream);
-        hipMemcpyAsync(h_nulls, nulls.p, sizeof h_nulls, hipMemcpyDeviceToHost, stream);
+        hipMemcpyAsync(&h_aux, aux.p, sizeof h_aux, hipMemcpyDeviceToHost, stream);
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json decode kernel failed");
+        int64_t R = n;              // decoded rows before the compaction
+        int64_t failed = n - ok;    // messages that failed
+        const uint8_t* rerr = (const uint8_t*)msg_err.p;
+        if (h_aux.pending) {
+            // some payload is a top-level array: rows per message, their offsets, and the row-based pass
+            if (int rc = ensure(rowbase, (size_t)(n + 1) * 8 * 2)) return rc;
+            int64_t* d_rows = (int64_t*)rowbase.p + (n + 1);
+            hipLaunchKernelGGL(k_json_rows, dim3((unsigned)((n + kJBlock - 1) / kJBlock)), dim3(kJBlock), 0, stream, d_bytes,
+                               d_off, n, d_rows);
+            hipLaunchKernelGGL(k_rows_tile_sum, dim3(nb), dim3(kJBlock), 0, stream, (const int64_t*)d_rows, n, (int64_t*)cnt.p);
+            hipLaunchKernelGGL(k_scan_cnt, dim3(1), dim3(1024), 0, stream, (int64_t*)cnt.p, nb);
+            hipLaunchKernelGGL(k_rows_tile_scan, dim3(nb), dim3(kJBlock), 0, stream, (const int64_t*)d_rows, n,
+                               (const int64_t*)cnt.p, nb, (int64_t*)rowbase.p);
+            hipMemcpyAsync(&R, (int64_t*)rowbase.p + n, 8, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json row count failed");
+            if (int rc = row_buffers(R, n_bytes, jo)) return rc;
+            if (int rc = ensure(row_err, (size_t)std::max<int64_t>(R, 1))) return rc;
+            hipMemsetAsync(aux.p, 0, sizeof(JAux), stream);
+            jo.rowbase = (const int64_t*)rowbase.p;
+            jo.rerr = (uint8_t*)row_err.p;
+            launch_decode(d_bytes, d_off, n, jo);
+            rerr = (const uint8_t*)row_err.p;
+            nb = (int)((std::max<int64_t>(R, 1) + kTile - 1) / kTile);
+            if (int rc = ensure(cnt, (size_t)(nb + 1) * 8)) return rc;
+            hipLaunchKernelGGL(k_ok_count, dim3(nb), dim3(kJBlock), 0, stream, rerr, R, (int64_t*)cnt.p);
+            hipLaunchKernelGGL(k_scan_cnt, dim3(1), dim3(1024), 0, stream, (int64_t*)cnt.p, nb);
+            std::vector<int64_t> rb((size_t)n + 1);
+            h_err.resize((size_t)n);
+            hipMemcpyAsync(&ok, (int64_t*)cnt.p + nb, 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(&h_aux, aux.p, sizeof h_aux, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(rb.data(), rowbase.p, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, stream);
+            hipMemcpyAsync(h_err.data(), msg_err.p, (size_t)n, hipMemcpyDeviceToHost, stream);
+            if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json decode kernel failed");
+            h_rows_of.resize((size_t)n);
+            failed = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                h_rows_of[i] = h_err[i] ? 0 : rb[i + 1] - rb[i];
+                failed += h_err[i] ? 1 : 0;
+            }
+        }
         last_ok = ok;
         st.messages += n;
-        st.errors += n - ok;
+        st.errors += failed;
         st.bytes += offsets && memory == EK_MEM_HOST ? (offsets[n] - offsets[0]) : 0;
         out->n_rows = ok;
-        if (ok == n) {
+        if (ok == R) {
             for (int c = 0; c < sch.n; ++c) {
-                out->columns[c] = raw_col[c].p;
-                out->validity[c] = h_nulls[c] ? (const uint8_t*)raw_valid[c].p : nullptr;   // no nil: no validity array
+                const bool list = sch.type[c] == EK_COL_LIST;
+                out->columns[c] = list ? nullptr : raw_col[c].p;
+                out->validity[c] = h_aux.nulls[c] ? (const uint8_t*)raw_valid[c].p : nullptr;   // no nil: no validity array
                 str_off[c] = (const int64_t*)raw_soff[c].p;
                 str_len[c] = (const int32_t*)raw_slen[c].p;
+                if (list) { list_start[c] = (const int64_t*)raw_col[c].p; list_len[c] = (const int32_t*)raw_slen[c].p; }
             }
-            return resolve_all(n, false, d_bytes, memory == EK_MEM_HOST ? (const uint8_t*)bytes : nullptr, out);
+            return resolve_all(ok, false, d_bytes, memory == EK_MEM_HOST ? (const uint8_t*)bytes : nullptr, out);
         }
-        // drop the messages that failed to decode (their errors are kept for ek_json_errors)
-        if (int rc = ensure(pos, (size_t)n * 8)) return rc;
-        hipLaunchKernelGGL(k_ok_pos, dim3(nb), dim3(kJBlock), 0, stream, (const uint8_t*)msg_err.p, n, (const int64_t*)cnt.p,
-                           (int64_t*)pos.p);
-        const unsigned g = (unsigned)std::min<int64_t>(8192, (n + 255) / 256);
+        // drop the rows of the messages that failed to decode (their errors are kept for ek_json_errors)
+        if (int rc = ensure(pos, (size_t)R * 8)) return rc;
+        hipLaunchKernelGGL(k_ok_pos, dim3(nb), dim3(kJBlock), 0, stream, rerr, R, (const int64_t*)cnt.p, (int64_t*)pos.p);
+        const unsigned g = (unsigned)std::min<int64_t>(8192, (R + 255) / 256);
         for (int c = 0; c < sch.n; ++c) {
             const int es = sch.type[c] == EK_COL_U32 ? 4 : 8;
+            const bool list = sch.type[c] == EK_COL_LIST;
             if (int rc = ensure(out_col[c], (size_t)std::max<int64_t>(ok, 1) * es)) return rc;
             if (int rc = ensure(out_valid[c], (size_t)std::max<int64_t>(ok, 1))) return rc;
-            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_col[c].p, out_col[c].p, es);
-            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_valid[c].p, out_valid[c].p, 1);
-            out->columns[c] = out_col[c].p;
-            out->validity[c] = h_nulls[c] ? (const uint8_t*)out_valid[c].p : nullptr;
+            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, R, raw_col[c].p, out_col[c].p, es);
+            hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, R, raw_valid[c].p, out_valid[c].p, 1);
+            out->columns[c] = list ? nullptr : out_col[c].p;
+            out->validity[c] = h_aux.nulls[c] ? (const uint8_t*)out_valid[c].p : nullptr;
             if (sch.type[c] == EK_COL_STR) {
                 if (int rc = ensure(out_soff[c], (size_t)std::max<int64_t>(ok, 1) * 8)) return rc;
-                if (int rc = ensure(out_slen[c], (size_t)std::max<int64_t>(ok, 1) * 4)) return rc;
-                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_soff[c].p, out_soff[c].p, 8);
-                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, n, raw_slen[c].p, out_slen[c].p, 4);
+                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, R, raw_soff[c].p, out_soff[c].p, 8);
                 str_off[c] = (const int64_t*)out_soff[c].p;
+            }
+            if (sch.type[c] == EK_COL_STR || list) {
+                if (int rc = ensure(out_slen[c], (size_t)std::max<int64_t>(ok, 1) * 4)) return rc;
+                hipLaunchKernelGGL(k_compact_col, dim3(g), dim3(256), 0, stream, (const int64_t*)pos.p, R, raw_slen[c].p, out_slen[c].p, 4);
                 str_len[c] = (const int32_t*)out_slen[c].p;
             }
+            if (list) { list_start[c] = (const int64_t*)out_col[c].p; list_len[c] = (const int32_t*)out_slen[c].p; }
         }
         if (hipStreamSynchronize(stream) != hipSuccess) return fail(EK_ERR_DEVICE, "json compaction failed");
         return resolve_all(ok, true, d_bytes, memory == EK_MEM_HOST ? (const uint8_t*)bytes : nullptr, out);
@@ -909,7 +1441,7 @@ struct JsonDecoder {
         const uint8_t* src = host_bytes;
         if (!src) {   // device payloads: gather the misses' bytes into one buffer, one copy back
             int64_t tot = 0;
-            for (size_t k = 0; k < mr.size(); ++k) { gpos[k] = tot; tot += mr[k].len & ~(int32_t)EK_JSON_STR_ESCAPED; }
+            for (size_t k = 0; k < mr.size(); ++k) { gpos[k] = tot; tot += (mr[k].len & kStrNumber) ? 0 : (mr[k].len & ~kStrFlags); }
             if (int rc = ensure(gat_pos, mr.size() * 8)) return rc;
             if (int rc = ensure(gat_bytes, (size_t)std::max<int64_t>(tot, 1))) return rc;
             if (int rc = ensure(fix_rows, mr.size() * sizeof(MissRec))) return rc;
@@ -926,10 +1458,17 @@ struct JsonDecoder {
         std::vector<uint32_t> ids(mr.size());
         std::string str;
         for (size_t k = 0; k < mr.size(); ++k) {
-            const int32_t L = mr[k].len & ~(int32_t)EK_JSON_STR_ESCAPED;
+            const int32_t L = mr[k].len & ~kStrFlags;
             const uint8_t* b = src ? src + mr[k].off : gathered.data() + gpos[k];
-            if (mr[k].len & EK_JSON_STR_ESCAPED) str = json_unescape(b, L);
-            else str.assign((const char*)b, (size_t)L);
+            if (mr[k].len & kStrNumber) {
+                double f;   // cast.ToStringAlways(float64): fmt's %v (converter.go:446-451)
+                memcpy(&f, &mr[k].off, 8);
+                str = ek::go_float(f);
+            } else if (mr[k].len & EK_JSON_STR_ESCAPED) {
+                str = json_unescape(b, L);
+            } else {
+                str.assign((const char*)b, (size_t)L);
+            }
             auto it = D.ids.find(str);
             uint32_t id;
             if (it != D.ids.end()) {
@@ -1061,6 +1600,33 @@ int ek_json_dict_string(void* h, int column, uint32_t id, const char** s, int64_
     if (id >= d->dict[column].values.size()) { d->err = "string id out of range"; return EK_ERR_INVALID; }
     *s = d->dict[column].values[id].data();
     *len = (int64_t)d->dict[column].values[id].size();
+    return 0;
+}
+
+int ek_json_list(void* h, int column, const int64_t** start, const int32_t** len, const int64_t** values,
+                 const uint8_t** valid) {
+    if (!h || !start || !len || !values || !valid) return EK_ERR_INVALID;
+    JsonDecoder* d = (JsonDecoder*)h;
+    if (column < 0 || column >= d->sch.n || d->sch.type[column] != EK_COL_LIST) { d->err = "not a LIST column"; return EK_ERR_INVALID; }
+    *start = d->list_start[column];
+    *len = d->list_len[column];
+    *values = (const int64_t*)d->lval[column].p;
+    *valid = (const uint8_t*)d->lvalid[column].p;
+    return 0;
+}
+
+int ek_json_rows(void* h, const int64_t** rows_of, int64_t* n_msgs) {
+    if (!h || !rows_of || !n_msgs) return EK_ERR_INVALID;
+    JsonDecoder* d = (JsonDecoder*)h;
+    JsonDeviceGuard dg(d->dev);
+    if (d->h_rows_of.empty() && d->last_n > 0) {   // one row per decoded message
+        d->h_err.resize((size_t)d->last_n);
+        hipMemcpy(d->h_err.data(), d->msg_err.p, (size_t)d->last_n, hipMemcpyDeviceToHost);
+        d->h_rows_of.resize((size_t)d->last_n);
+        for (int64_t i = 0; i < d->last_n; ++i) d->h_rows_of[i] = d->h_err[i] ? 0 : 1;
+    }
+    *rows_of = d->h_rows_of.data();
+    *n_msgs = d->last_n;
     return 0;
 }
 

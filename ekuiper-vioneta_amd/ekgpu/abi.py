@@ -5,7 +5,7 @@ the compiled library's view (ek_abi_version) and the header constants.
 """
 import ctypes as C
 
-EKGPU_ABI_VERSION = 13
+EKGPU_ABI_VERSION = 14
 EK_MAX_COLUMNS = 16
 EK_MAX_AGGS = 16
 EK_MAX_PROG = 48
@@ -23,6 +23,7 @@ UNIT_MS = {EK_UNIT_DD: 86400000, EK_UNIT_HH: 3600000, EK_UNIT_MI: 60000, EK_UNIT
 
 EK_COL_I64, EK_COL_F64, EK_COL_U32 = 1, 2, 3
 EK_COL_STR, EK_COL_BOOL = 4, 5   # STR: ingest only (ek_json_decode); BOOL: int64 0 / 1 evaluated as a Go bool
+EK_COL_LIST = 6                  # ingest only (ek_json_decode, ABI v14): a JSON array field, read through ek_json_list
 
 (EK_AGG_COUNT_STAR, EK_AGG_COUNT, EK_AGG_SUM, EK_AGG_AVG, EK_AGG_MIN, EK_AGG_MAX, EK_AGG_STDDEV,
  EK_AGG_STDDEVS, EK_AGG_VAR, EK_AGG_VARS, EK_AGG_MEDIAN, EK_AGG_PERCENTILE_CONT,
@@ -204,7 +205,8 @@ EK_JSON_STR_ESCAPED = 0x40000000
 
 class ek_json_schema(C.Structure):
     _fields_ = [("n_fields", C.c_int32), ("column_type", C.c_int32 * EK_MAX_COLUMNS),
-                ("names", (C.c_char * EK_JSON_MAX_NAME) * EK_MAX_COLUMNS)]
+                ("names", (C.c_char * EK_JSON_MAX_NAME) * EK_MAX_COLUMNS),
+                ("elem_type", C.c_int32 * EK_MAX_COLUMNS), ("paths", C.c_int32)]
 
 
 class ek_json_stats(C.Structure):

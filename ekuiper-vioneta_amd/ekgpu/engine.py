@@ -84,6 +84,10 @@ def lib():
         L.ek_json_dict_size.restype = C.c_int
         L.ek_json_dict_string.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
         L.ek_json_dict_string.restype = C.c_int
+        L.ek_json_list.argtypes = [C.c_void_p, C.c_int] + [C.POINTER(C.c_void_p)] * 4
+        L.ek_json_list.restype = C.c_int
+        L.ek_json_rows.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.ek_json_rows.restype = C.c_int
         L.ek_json_destroy.argtypes = [C.c_void_p]
         L.ek_json_destroy.restype = C.c_int
         L.ek_export_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -101,7 +105,8 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
                     "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
-                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async", "ek_route_partition"]
+                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async", "ek_route_partition",
+                    "ek_json_list", "ek_json_rows"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32, A.EK_COL_BOOL: np.int64}
 
@@ -330,6 +335,18 @@ class Engine:
             pass
 
 
+def device_to_host(ptr: int, n: int, dtype, device: int = 0) -> np.ndarray:
+    """n elements of a device array the library handed out (its own HIP runtime allocated them): a view through the
+    CUDA array interface, copied to the host by torch."""
+    import torch
+
+    class _View:
+        __cuda_array_interface__ = {"shape": (int(n),), "typestr": np.dtype(dtype).str, "data": (int(ptr), False),
+                                    "version": 2, "strides": None}
+
+    return torch.as_tensor(_View(), device=torch.device("cuda", device)).cpu().numpy().copy()
+
+
 class JsonDecoder:
     """Columnar JSON ingest on the GPU (include/ekgpu.h ek_json_*): a micro-batch of JSON messages ->
     device columns of an ek_batch, ready for Engine.push_batch."""
@@ -344,18 +361,25 @@ class JsonDecoder:
 
     TYPES = {"bigint": A.EK_COL_I64, "float": A.EK_COL_F64, "key": A.EK_COL_U32, "string": A.EK_COL_STR,
              "boolean": A.EK_COL_BOOL}
+    LIST_TYPES = {"array<bigint>": A.EK_COL_I64, "array<float>": A.EK_COL_F64, "array<boolean>": A.EK_COL_BOOL}
 
-    def __init__(self, schema: dict, device: int = 0):
-        """schema: ordered {field: "bigint" | "float" | "key" | "string" | "boolean"} (same column order as the rule's
-        schema). A "string" field reaches the engine as dense u32 ids of the decoder's dictionary (strings()); a
-        "boolean" field as int64 0 / 1 (the rule's "boolean" column)."""
+    def __init__(self, schema: dict, device: int = 0, paths: bool = False):
+        """schema: ordered {field: "bigint" | "float" | "key" | "string" | "boolean" | "array<bigint|float|boolean>"}
+        (same column order as the rule's schema). A "string" field reaches the engine as dense u32 ids of the
+        decoder's dictionary (strings()); a "boolean" field as int64 0 / 1 (the rule's "boolean" column); an array
+        field is read with lists(). paths=True: field names are paths into nested objects / arrays ("a.b", "a[0]",
+        "a[0][0].c"; ABI v14)."""
         L = lib()
         s = A.ek_json_schema()
         s.n_fields = len(schema)
+        s.paths = 1 if paths else 0
         self.names = list(schema)
-        self.types = [self.TYPES[t] for t in schema.values()]
+        self.types = [A.EK_COL_LIST if t in self.LIST_TYPES else self.TYPES[t] for t in schema.values()]
+        self.elems = [self.LIST_TYPES.get(t, 0) for t in schema.values()]
+        self.device = device
         for k, (name, t) in enumerate(schema.items()):
-            s.column_type[k] = self.TYPES[t]
+            s.column_type[k] = self.types[k]
+            s.elem_type[k] = self.elems[k]
             s.names[k].value = name.encode()
         self.h = C.c_void_p()
         rc = L.ek_json_create(C.byref(s), device, C.byref(self.h))
@@ -402,6 +426,53 @@ class JsonDecoder:
         i.e. a "key" column (GROUP BY it directly; strings() maps the ids back)."""
         return {n: ("key" if t == A.EK_COL_STR else {v: k for k, v in self.TYPES.items()}[t])
                 for n, t in zip(self.names, self.types)}
+
+    def rows_of(self) -> np.ndarray:
+        """Rows of the last decode per message (a top-level array payload yields one row per object element; 0 for a
+        message that failed)."""
+        p, n = C.c_void_p(), C.c_int64()
+        rc = lib().ek_json_rows(self.h, C.byref(p), C.byref(n))
+        if rc != 0:
+            raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(n.value,)).copy() if n.value else np.zeros(0, np.int64)
+
+    def lists(self, column, batch) -> list:
+        """The decoded arrays of LIST column `column` (index or field name) of the last decoded batch: one python
+        list per row (None for a nil / absent array; None elements for nil items), elements typed by the column's
+        element type (int, float, bool)."""
+        c = self.names.index(column) if isinstance(column, str) else int(column)
+        n_rows = int(batch.n_rows)
+        ps = [C.c_void_p() for _ in range(4)]
+        rc = lib().ek_json_list(self.h, c, *[C.byref(x) for x in ps])
+        if rc != 0:
+            raise EngineError(rc, lib().ek_json_last_error(self.h).decode())
+        if n_rows == 0:
+            return []
+        start = device_to_host(ps[0].value, n_rows, np.int64, self.device)
+        ln = device_to_host(ps[1].value, n_rows, np.int32, self.device)
+        total = int((start + ln).max()) if n_rows else 0
+        vals = device_to_host(ps[2].value, max(total, 1), np.int64, self.device)
+        ok = device_to_host(ps[3].value, max(total, 1), np.uint8, self.device)
+        et = self.elems[c]
+        nil = (device_to_host(batch.validity[c], n_rows, np.uint8, self.device) == 0) if batch.validity[c] else \
+            np.zeros(n_rows, bool)
+        out = []
+        for a, m, z in zip(start.tolist(), ln.tolist(), nil.tolist()):
+            if z:
+                out.append(None)
+                continue
+            row = []
+            for k in range(a, a + m):
+                if not ok[k]:
+                    row.append(None)
+                elif et == A.EK_COL_F64:
+                    row.append(float(vals[k:k + 1].view(np.float64)[0]))
+                elif et == A.EK_COL_BOOL:
+                    row.append(bool(vals[k]))
+                else:
+                    row.append(int(vals[k]))
+            out.append(row)
+        return out
 
     def strings(self, column) -> list:
         """The dictionary of a string column (index or field name): id -> str, in id order."""

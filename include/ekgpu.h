@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define EKGPU_ABI_VERSION 13
+#define EKGPU_ABI_VERSION 14
 #define EK_MAX_COLUMNS 16
 #define EK_MAX_AGGS 16
 #define EK_MAX_PROG 48
@@ -59,6 +59,10 @@ enum { EK_COL_I64 = 1, EK_COL_F64 = 2, EK_COL_U32 = 3 };
  * EK_COL_STR is an ingest type only (ek_json_decode): the string's FNV-1a 64 hash in an int64 column plus its byte range
  * (ek_json_strings), resolved to a dense EK_COL_U32 id by the host dictionary before the engine sees it. */
 enum { EK_COL_STR = 4, EK_COL_BOOL = 5 };
+/* ABI v14. EK_COL_LIST is an ingest type only (ek_json_decode): a JSON array field (schema ARRAY(elem), converter.go
+ * decodeArray :173-244) whose elements of type ek_json_schema.elem_type (EK_COL_I64 / EK_COL_F64 / EK_COL_BOOL) are
+ * read through ek_json_list; the batch carries no column for it (columns[c] = NULL, validity = the array's own nil). */
+enum { EK_COL_LIST = 6 };
 
 /* Aggregate functions (internal/binder/function/funcs_agg.go:28-370). */
 enum {
@@ -444,30 +448,41 @@ int ek_shard_triggers(void* h, const ek_batch* batch, const ek_global_ctx* g, in
 
 /* ---------------------------------------------------------------- columnar JSON ingest
  * Replaces the per-message FastJsonConverter.Decode of a schema-typed stream
- * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) for flat JSON objects
- * with numeric, string and boolean fields: a micro-batch of messages (payload bytes concatenated, message i =
- * bytes[offsets[i], offsets[i+1])) is decoded on the GPU straight into the columns of an ek_batch
- * (device memory owned by the decoder, valid until its next decode), ready for ek_push_batch.
+ * (internal/converter/json/converter.go:92-171,246-520; node/decode_op.go:146-193) with numeric, string and boolean
+ * fields: a micro-batch of messages (payload bytes concatenated, message i = bytes[offsets[i], offsets[i+1])) is
+ * decoded on the GPU straight into the columns of an ek_batch (device memory owned by the decoder, valid until its
+ * next decode), ready for ek_push_batch.
  * Schema type BIGINT -> EK_COL_I64 (integer literal, fastfloat.ParseInt64), FLOAT -> EK_COL_F64
- * (correctly rounded), a dense key id column -> EK_COL_U32 (integer literal in [0, 2^32)),
- * STRING -> EK_COL_STR (a JSON string, delivered as its dense dictionary id, ek_json_dict_*; a number is EK_JSON_ERR_UNSUPPORTED — the Go converter's %v formatting —, a bool,
- * object or array EK_JSON_ERR_TYPE), BOOLEAN -> EK_COL_BOOL (true / false; a number n as n != 0; a string
- * by strconv.ParseBool, converter.go:600-625; anything else EK_JSON_ERR_TYPE). null or an
- * absent field -> validity 0; fields outside the schema are skipped. Messages that fail to decode are
- * dropped from the batch and reported by ek_json_errors. */
+ * (correctly rounded, subnormal results included), a dense key id column -> EK_COL_U32 (integer literal in [0, 2^32)),
+ * STRING -> EK_COL_STR (a JSON string, delivered as its dense dictionary id, ek_json_dict_*; a number is
+ * cast.ToStringAlways(float64) = Go's %v of the float, converter.go:446-451; a bool, object or array
+ * EK_JSON_ERR_TYPE), BOOLEAN -> EK_COL_BOOL (true / false; a number n as n != 0; a string by strconv.ParseBool,
+ * converter.go:600-625; anything else EK_JSON_ERR_TYPE), ARRAY -> EK_COL_LIST (ek_json_list). null or an absent
+ * field -> validity 0; fields outside the schema are skipped. Messages that fail to decode are dropped from the
+ * batch and reported by ek_json_errors.
+ * ABI v14, paths (ek_json_schema.paths = 1): a column name is a path into nested objects and arrays, segments
+ * separated by '.', array elements as [k]: "a.b" is field b of the STRUCT a (decodeObject over schema[a].Properties,
+ * converter.go:256-291), "a[0]" element 0 of the ARRAY a, "a[0][0].c" as in TestArrayWithArray. A null or absent
+ * container makes the leaf nil; a container of the wrong kind (a number where the path needs an object) is
+ * EK_JSON_ERR_TYPE ("a has wrong type:number, expect:struct"); a duplicated key replaces the whole subtree (Go map
+ * assignment). A top-level array payload [{...}, {...}] decodes to one row per element, in order
+ * (decodeWithSchema's []map case, converter.go:141-158); any element that is not an object fails the message. */
 #define EK_JSON_MAX_NAME 32
 enum {
     EK_JSON_OK = 0,
     EK_JSON_ERR_SYNTAX = 1,      /* fastjson parse error                                        */
     EK_JSON_ERR_TYPE = 2,        /* "%v has wrong type" (string/bool/object/array for a number)  */
     EK_JSON_ERR_NUMBER = 3,      /* not an int64 literal for BIGINT / number out of range         */
-    EK_JSON_ERR_UNSUPPORTED = 4  /* top-level array payloads (decoded by the Go converter instead) */
+    EK_JSON_ERR_UNSUPPORTED = 4  /* forms the device decoder leaves to the Go converter (escaped keys on a path,
+                                    paths deeper than 8, > 100-digit mantissas on a rounding boundary)            */
 };
 
 typedef struct {
     int32_t n_fields;
     int32_t column_type[EK_MAX_COLUMNS];           /* EK_COL_* of column i                  */
-    char names[EK_MAX_COLUMNS][EK_JSON_MAX_NAME];  /* JSON key of column i (NUL-terminated)   */
+    char names[EK_MAX_COLUMNS][EK_JSON_MAX_NAME];  /* JSON key (or path) of column i (NUL-terminated) */
+    int32_t elem_type[EK_MAX_COLUMNS];             /* ABI v14: EK_COL_LIST columns: the element type */
+    int32_t paths;                                 /* ABI v14: 1 = names are paths ('.' and [k] segments) */
 } ek_json_schema;
 
 typedef struct {
@@ -493,6 +508,14 @@ int ek_json_strings(void* h, int column, const int64_t** offsets, const int32_t*
  * ek_json_dict_string yields id's bytes (not NUL-terminated; valid until the next decode). */
 int ek_json_dict_size(void* h, int column, int64_t* n);
 int ek_json_dict_string(void* h, int column, uint32_t id, const char** s, int64_t* len);
+/* ABI v14. LIST column `column` of the last decode: per decoded row, start[i] / len[i] = its elements in values /
+ * valid (element nil -> valid 0; a nil or absent array: len 0 and the batch validity 0); an element is int64, float64
+ * bits or 0 / 1 by elem_type. Device pointers, valid until the next decode. */
+int ek_json_list(void* h, int column, const int64_t** start, const int32_t** len, const int64_t** values,
+                 const uint8_t** valid);
+/* rows of the last decode per message (a top-level array payload yields one row per element): rows_of[i] for message
+ * i, 0 for a failed one (host memory owned by the decoder, valid until the next decode) */
+int ek_json_rows(void* h, const int64_t** rows_of, int64_t* n_msgs);
 int ek_json_get_stats(void* h, ek_json_stats* out);
 const char* ek_json_last_error(void* h);
 int ek_json_destroy(void* h);

@@ -100,7 +100,7 @@ def _num_cases(rng, k):
 def test_json_float_conversion_exact(engine_mod):
     rng = np.random.default_rng(12)
     nums = _num_cases(rng, 20000)
-    nums = [s for s in nums if 2.3e-308 < abs(float(s)) < 1.7e308 or float(s) == 0.0]
+    nums = [s for s in nums if abs(float(s)) < 1.7e308]   # (subnormal results decode too: ABI v14)
     msgs = [f'{{"x": {s}}}'.encode() for s in nums]
     dec, batch = _decode_cols(engine_mod, {"x": "float"}, msgs)
     assert batch.n_rows == len(msgs), dec.errors()
@@ -141,7 +141,7 @@ def test_json_fields_nulls_and_errors(engine_mod):
         (b'{"id": 1, "ts": 5, "v": 1.}', A.EK_JSON_ERR_SYNTAX, None),
         (b'{"id": 1, "ts": 5 "v": 1}', A.EK_JSON_ERR_SYNTAX, None),
         (b'{"id": 1, "ts": 5, "v": 1} x', A.EK_JSON_ERR_SYNTAX, None),
-        (b'[{"id": 1}]', A.EK_JSON_ERR_UNSUPPORTED, None),
+        (b'[{"id": 1}]', A.EK_JSON_OK, (1, None, None)),                             # top-level array: one row per object
         (b'{"id": 1, "ts": 5,}', A.EK_JSON_ERR_SYNTAX, None),                      # trailing comma
         (b'{"id": 2, "e": {"a": [1, "x}"], "b": "q\\"}"}, "ts": 4}', A.EK_JSON_OK, (2, 4, None)),
         (b'{"id": 7, "ts": -3, "v": 1e2}', A.EK_JSON_OK, (7, -3, 100.0)),
