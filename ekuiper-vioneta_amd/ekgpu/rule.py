@@ -508,8 +508,10 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
             break
     if group_dims is not None:
         key_col = p.columns.index(GROUP_KEY)
-    elif len(dims) == 1 and schema[dims[0]] == "key":
+    elif len(dims) == 1 and schema[dims[0]] == "key" and dims[0] not in nullable:
         key_col = p.columns.index(dims[0])
+    # (a nullable key column goes through the group-key dictionary too: a nil dimension is the reference's own group
+    # "<nil>," — aggregate_operator.go:49-55 — an id of its own, so the engine's key column never holds a nil)
     elif dims:
         raise _Composite(dims)
     having = []

@@ -156,3 +156,78 @@ def test_composite_key_engine_parity(oracle, engine_mod, sql):
     for w in got:
         ks = [group_key_string(t) for t in rule.decode_keys(w.keys)]
         assert len(set(ks)) == len(ks)
+
+
+# ---------------------------------------------------------------- nullable GROUP BY key: nil is its own group "<nil>,"
+NK_SCHEMA = {"k": "key", "ts": "bigint", "v": "float"}
+NK_SQLS = [
+    "SELECT k, count(*), avg(v), max(v) FROM s GROUP BY k, TUMBLINGWINDOW(ms, 500)",
+    "SELECT k, stddev(v), min(v) FROM s GROUP BY k, SLIDINGWINDOW(ms, 300) OVER (WHEN v > 99.0) HAVING count(*) > 1",
+    "SELECT k, median(v), count(*) FROM s GROUP BY k, HOPPINGWINDOW(ms, 600, 200)",
+]
+
+
+def _nk_stream(n=30_000, seed=9):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(0, 40, n).astype(np.uint32)
+    valid = (rng.random(n) > 0.1).astype(np.uint8)   # 10 % nil keys
+    k[valid == 0] = rng.integers(0, 40, int((valid == 0).sum()))   # (a nil row's stored value is arbitrary)
+    ts = (1541152480000 + np.arange(n) // 7).astype(np.int64)
+    return [k, ts, rng.random(n) * 100], [valid, None, None]
+
+
+def _by_key(rule, w, direct):
+    """A window's rows keyed by the reference's group key string (the nil group is "<nil>,")."""
+    out = {}
+    for key, vals in w.rows().items():
+        if direct:
+            dim = (None,) if int(key) in (-1, 0xFFFFFFFF) else (int(key),)
+        else:
+            dim = rule.decode_keys([key])[0]
+        out[group_key_string(dim)] = vals
+    return out
+
+
+@pytest.mark.parametrize("sql", NK_SQLS)
+def test_nullable_key_lowering_matches_direct_oracle(oracle, sql):
+    """Lowering (nullable key -> group-key dictionary, nil an id of its own) == the oracle grouping the nullable key
+    column directly (ekoracle.c run_window: a nil key is the group of key -1, i.e. "<nil>,")."""
+    cols, valid = _nk_stream()
+    rule = compile_rule(sql, NK_SCHEMA, num_keys=64, nullable=("k",))
+    assert rule.key_dict is not None and rule.plan.key_column == len(NK_SCHEMA)
+    dcols, dval = rule.device_columns(cols, valid)
+    lowered = oracle.run(rule.plan, dcols, dval).windows
+    direct_rule = compile_rule(sql, NK_SCHEMA, num_keys=64)
+    assert direct_rule.key_dict is None
+    direct_rule.plan.nullable_mask |= 1 << 0
+    direct = oracle.run(direct_rule.plan, cols, valid).windows
+    assert len(lowered) == len(direct) >= 3
+    n_nil = 0
+    for a, b in zip(lowered, direct):
+        assert (a.start, a.end, a.status) == (b.start, b.end, b.status)
+        ga, gb = _by_key(rule, a, False), _by_key(direct_rule, b, True)
+        assert ga.keys() == gb.keys()
+        for k in ga:
+            for x, y in zip(ga[k], gb[k]):
+                assert x == y or (isinstance(x, float) and abs(x - y) <= 1e-9 * max(1.0, abs(y)))
+        n_nil += "<nil>," in ga
+    assert n_nil >= len(lowered) // 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql", NK_SQLS)
+def test_nullable_key_engine_parity(oracle, engine_mod, sql):
+    """The engine over the lowered rule == the oracle grouping the nullable key directly, window by window."""
+    from parity import assert_windows_equal
+    cols, valid = _nk_stream(60_000, seed=10)
+    rule = compile_rule(sql, NK_SCHEMA, num_keys=64, nullable=("k",), debug_membership=True)
+    dcols, dval = rule.device_columns(cols, valid)
+    got, exp, _ = run_both(oracle, engine_mod, rule, dcols, batches=3, validity=dval)
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+    direct_rule = compile_rule(sql, NK_SCHEMA, num_keys=64)
+    direct_rule.plan.nullable_mask |= 1 << 0
+    direct = oracle.run(direct_rule.plan, cols, valid).windows
+    assert len(got) == len(direct)
+    for a, b in zip(got, direct):
+        ks = {group_key_string(t) for t in rule.decode_keys(a.keys)}
+        assert ks == set(_by_key(direct_rule, b, True))
