@@ -428,9 +428,9 @@ struct Engine {
         if (wtype == EK_WINDOW_STATE) {
             // WindowV2Operator / StateWindowOp (window_v2_op.go:39-58,94-148): rows in arrival order (processing
             // time) or in WatermarkOp release order (event time); no time grid. WHERE is pushed below a
-            // processing-time window (windowPlan.go:82-99) and then decides which rows reach the conditions
-            if (!plan.is_event_time && plan.n_where > 0)
-                return fail(EK_ERR_UNSUPPORTED, "WHERE below a processing-time STATEWINDOW (pushed-down filter) is not built");
+            // processing-time window (windowPlan.go:82-99): with the FILTER it is the FilterOp in front of the window
+            // (planner.go:388-392), so only the rows it keeps reach the begin / emit conditions (proc_prefilter)
+            proc_pushdown = !plan.is_event_time && plan.n_where > 0;
         } else if (plan.is_event_time) {
             // NewEventTimeTrigger (event_window_trigger.go:35-53): COUNTWINDOW is rejected in event time, except on the
             // incremental path (CountWindowIncAggEventOp, window_inc_agg_event_op.go:340-439), decided below
@@ -826,7 +826,8 @@ struct Engine {
         // the rows WatermarkOp accepted (filter_accept)
         pre_filter = proc_pushdown || plan.n_filter > 0;
         if (pre_filter) {
-            const bool push_where = proc && !proc_inc && wtype != EK_WINDOW_SLIDING && plan.n_where > 0;
+            const bool push_where = ((proc && !proc_inc && wtype != EK_WINDOW_SLIDING) || (wtype == EK_WINDOW_STATE && !plan.is_event_time)) &&
+                                    plan.n_where > 0;
             std::vector<ek_instr> prog;
             if (push_where) prog.insert(prog.end(), plan.where_prog, plan.where_prog + plan.n_where);
             if (plan.n_filter > 0) {

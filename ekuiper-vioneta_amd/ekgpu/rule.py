@@ -461,6 +461,11 @@ def _compile(sql: str, schema: Dict[str, str], *, is_event_time: bool, late_tole
                     p.expect(",")
                     emit = p.expr(False)
                     p.expect(")")
+                    if p.kw("filter"):   # the window's FILTER (WHERE <cond>) clause, as for the time windows below
+                        p.expect("(")
+                        p.expect("where")
+                        wfilter = p.expr(False)
+                        p.expect(")")
                     if p.peek() == ",":
                         p.i += 1
                         continue

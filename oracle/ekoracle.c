@@ -1319,6 +1319,23 @@ static int filter_pass(const dataset* d, int64_t row, int64_t* n_err) {
     return 0;
 }
 
+/* The FilterOp in front of a processing-time window (windowPlan.PushDownPredicate, windowPlan.go:82-99, planner.go:
+ * 388-392): combine(WHERE, FILTER) evaluated as the binary AND of valuer.go:574-660 (a false / error lhs decides;
+ * nil AND x -> false unless x errors); an error or a non-bool drops the row and is counted */
+static int pushdown_pass(const dataset* d, int64_t i, int64_t* n_err) {
+    const ek_plan* p = d->p;
+    if (p->n_where <= 0 && p->n_filter <= 0) return 1;
+    val_t r = mk_bool(1);
+    if (p->n_where > 0) r = eval_prog(p->where_prog, p->n_where, d, i, NULL);
+    if (p->n_filter > 0 && r.tag != V_ERR && !(r.tag == V_BOOL && !r.i)) {
+        const val_t rf = eval_prog(p->filter_prog, p->n_filter, d, i, NULL);
+        r = p->n_where > 0 ? (rf.tag == V_ERR ? rf : simple_eval(r, rf, EK_OP_AND)) : rf;
+    }
+    if (r.tag == V_BOOL && r.i) return 1;
+    if (r.tag != V_BOOL && r.tag != V_NULL && n_err) (*n_err)++;
+    return 0;
+}
+
 int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8_t* const* validity, eko_output* out) {
     memset(out, 0, sizeof *out);
     if (!p || p->abi_version != EKGPU_ABI_VERSION) { set_status(out, EK_ERR_INVALID, "abi version mismatch"); return out->status; }
@@ -1334,10 +1351,6 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
     if (p->window_type == EK_WINDOW_SESSION || p->window_type == EK_WINDOW_NONE || p->window_type == EK_WINDOW_STATE) inc_ok = 0;
     if (inc_ok && p->window_type == EK_WINDOW_SLIDING && (!p->is_event_time || p->delay != 0)) {
         set_status(out, EK_ERR_UNSUPPORTED, "incremental sliding windows are restated in event time without delay only"); return out->status;
-    }
-    if (p->window_type == EK_WINDOW_STATE && !p->is_event_time && p->n_where > 0) {
-        /* windowPlan.PushDownPredicate (windowPlan.go:82-99) moves WHERE below a processing-time window */
-        set_status(out, EK_ERR_UNSUPPORTED, "pushed-down WHERE below a processing-time state window is not restated"); return out->status;
     }
     const int v2slide = p->window_version == 2 && p->window_type == EK_WINDOW_SLIDING;
     if (v2slide && !p->is_event_time) {
@@ -1430,8 +1443,10 @@ int eko_run(const ek_plan* p, int64_t n, const void* const* columns, const uint8
         free(buf.a); free(o.inputs.a); free(o.trigger_ts.a); free(o.delay_ts.a); free(o.content.a);
         free(ts);
     } else if (p->window_type == EK_WINDOW_STATE) {
+        /* processing time: WHERE is pushed below the window with the FILTER (windowPlan.go:82-99): the rows it keeps
+         * reach StateWindowOp; WHERE above the window then holds for every row (emit_window re-tests it: a no-op) */
         for (int64_t i = 0; i < n; ++i)
-            if (filter_pass(&d, i, &out->records_filter_error)) state_on_row(&so, i);
+            if (pushdown_pass(&d, i, &out->records_filter_error)) state_on_row(&so, i);
     } else {
         if (p->window_type == EK_WINDOW_NONE) {
             /* window-less rule: FilterOp.Apply per event (filter_operator.go:36-90) + SELECT * projection.
@@ -1783,20 +1798,8 @@ int eko_run_proc_restart(const ek_plan* p, int64_t n, const void* const* columns
         if (i == n) break;
         EKO_ADVANCE(ts[i])
         if (pushdown) {
-            /* WHERE AND FILTER below the window: combine(where, filter) (windowPlan.go:82-99) evaluated as the binary
-             * AND of valuer.go:574-660 (a false / error lhs decides; nil AND x -> false unless x errors) */
-            if (p->n_where > 0 || p->n_filter > 0) {
-                val_t r = mk_bool(1);
-                if (p->n_where > 0) r = eval_prog(p->where_prog, p->n_where, &d, i, NULL);
-                if (p->n_filter > 0 && r.tag != V_ERR && !(r.tag == V_BOOL && !r.i)) {
-                    const val_t rf = eval_prog(p->filter_prog, p->n_filter, &d, i, NULL);
-                    r = p->n_where > 0 ? (rf.tag == V_ERR ? rf : simple_eval(r, rf, EK_OP_AND)) : rf;
-                }
-                if (!(r.tag == V_BOOL && r.i)) {
-                    if (r.tag != V_BOOL && r.tag != V_NULL) out->records_filter_error++;
-                    continue;
-                }
-            }
+            /* WHERE AND FILTER below the window */
+            if (!pushdown_pass(&d, i, &out->records_filter_error)) continue;
         } else if (!filter_pass(&d, i, &out->records_filter_error)) {
             continue;   /* the window's FILTER op before a sliding window */
         }

@@ -79,12 +79,26 @@ def test_state_window_event_time_out_of_order(oracle, engine_mod, batches):
     assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
 
 
+@pytest.mark.parametrize("batches", [1, 11])
+@pytest.mark.parametrize("where", ["temperature > 20", "temperature / (humidity - 50) > 0.1"])
+def test_state_window_processing_time_where_pushdown(oracle, engine_mod, batches, where):
+    """Processing time: WHERE is pushed below the window (windowPlan.PushDownPredicate, windowPlan.go:82-99) and
+    combined with the window FILTER into the FilterOp in front of it (planner.go:388-392): only the rows it keeps reach
+    the begin / emit conditions (a row with humidity 50 makes the second WHERE fail: dropped and counted)."""
+    sql = (f"SELECT deviceId, count(*), avg(temperature), max(humidity) FROM demo WHERE {where} "
+           "GROUP BY deviceId, STATEWINDOW(trig = 1, humidity > 98) FILTER (WHERE humidity > 3) HAVING count(*) > 1")
+    rule = compile_rule(sql, TRIG_SCHEMA, num_keys=300, is_event_time=False, debug_membership=True)
+    cols = _with_trig(_iot(120_000, 300, seed=94, epm=10), 300)
+    cols[3][::97] = 50.0   # humidity 50: the division WHERE fails on these rows
+    got, exp, st = run_both(oracle, engine_mod, rule, cols, batches=batches)
+    assert len(got) > 20
+    assert st.records_filter_error == exp.records_filter_error
+    if "/" in where:
+        assert exp.records_filter_error > 0
+    assert_windows_equal(rule.plan, got, exp.windows, check_members=True)
+
+
 def test_state_window_rejections(engine_mod):
-    r1 = compile_rule("SELECT count(*) FROM demo WHERE trig > 0 GROUP BY STATEWINDOW(trig = 1, trig = 2)", TRIG_SCHEMA,
-                      is_event_time=False)
-    with pytest.raises(engine_mod.EngineError) as e:
-        engine_mod.Engine(r1.plan)
-    assert e.value.code == A.EK_ERR_UNSUPPORTED
     r2 = compile_rule("SELECT deviceId, count(*) FROM demo GROUP BY deviceId, TUMBLINGWINDOW(ss, 1)", TRIG_SCHEMA,
                       num_keys=10, window_version="v2")
     with pytest.raises(engine_mod.EngineError) as e:
