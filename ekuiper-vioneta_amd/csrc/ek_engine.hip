@@ -791,6 +791,7 @@ struct Engine {
         sw_grid = std::max(1, env_int("EKGPU_SW_GRID", 4096));
         fin_ring = env_int("EKGPU_FIN_RING", 1) != 0;
         fin_ring_chunks = env_int("EKGPU_FIN_RING_CHUNKS", 0);
+        fin_ring_split = env_int("EKGPU_FIN_RING_SPLIT", 0);
         km_mode = env_int("EKGPU_KEYMAJOR", 2);
         ung_mode = env_int("EKGPU_UNG", 1);
         km_one = env_int("EKGPU_KM_ONE", 1);
@@ -1329,8 +1330,20 @@ struct Engine {
                 chunks = std::max<int64_t>(1, std::min<int64_t>(chunks, nf));
                 const int64_t cw = (nf + chunks - 1) / chunks;
                 dim3 grid_r((unsigned)kb, (unsigned)((nf + cw - 1) / cw));
-                ek::launch_fin_ring((int)span, (dp.vc_flags[0] & NEED_CNT) != 0, dp.n_having > 0, grid_r, stream, d_plan, wd, (int32_t)nf,
-                                    (int32_t)cw, dstate, ring, (const int32_t*)pane_err.p, rv);
+                const bool vcr = (dp.vc_flags[0] & NEED_CNT) != 0;
+                // split walk (no HAVING, both halves needed): count / sum, then min / max, each at twice the occupancy
+                const int fl = dp.vc_flags[0];
+                const bool split = fin_ring_split && dp.n_having == 0 && (fl & NEED_SUM) && (fl & (NEED_MIN | NEED_MAX));
+                if (split) {
+                    if (int rc = ensure(ring_gbase, (size_t)grid_r.x * grid_r.y * cw * 4 + 64)) return rc;
+                    ek::launch_fin_ring((int)span, vcr, false, 1, grid_r, stream, d_plan, wd, (int32_t)nf, (int32_t)cw, dstate, ring,
+                                        (const int32_t*)pane_err.p, rv, (uint32_t*)ring_gbase.p);
+                    ek::launch_fin_ring((int)span, vcr, false, 2, grid_r, stream, d_plan, wd, (int32_t)nf, (int32_t)cw, dstate, ring,
+                                        (const int32_t*)pane_err.p, rv, (uint32_t*)ring_gbase.p);
+                } else {
+                    ek::launch_fin_ring((int)span, vcr, dp.n_having > 0, 0, grid_r, stream, d_plan, wd, (int32_t)nf, (int32_t)cw, dstate,
+                                        ring, (const int32_t*)pane_err.p, rv, nullptr);
+                }
             } else {
                 dim3 grid_f((unsigned)((K + kBlock - 1) / kBlock), (unsigned)nf);
                 ek::launch_fin(nvc, dp.pseudo_keys != 0, grid_f, stream, d_plan, wd, dstate, ring, (const int32_t*)pane_err.p, rv);
@@ -1939,19 +1952,32 @@ struct Engine {
         for (int c = 0; c < plan.n_columns; ++c)
             if (db.valid[c]) if (int rc = eb_enable_valid(c)) return rc;
         if (int rc = eb_reserve(cnt)) return rc;
+        // every copied column (and validity, and shard-mode arrivals) in one k_eb_copy launch
+        CopySegs cs{};
+        int ns = 0;
+        auto seg = [&](const void* src, void* dst, int64_t bytes, int es) {
+            if (bytes > 0) cs.s[ns++] = CopySeg{(const unsigned char*)src, (unsigned char*)dst, bytes, es, 0};
+        };
         for (int c = 0; c < plan.n_columns; ++c) {
             const size_t es = col_es(c);
-            if (eb_need[c])
-                hipMemcpyAsync((char*)eb.col[c].p + eb.n * es, (const char*)db.col[c] + start * es, (size_t)cnt * es,
-                               hipMemcpyDeviceToDevice, stream);
+            if (eb_need[c]) seg((const char*)db.col[c] + start * es, (char*)eb.col[c].p + eb.n * es, cnt * (int64_t)es, (int)es);
             if (eb_valid_on[c]) {
-                if (db.valid[c]) hipMemcpyAsync((uint8_t*)eb.valid[c].p + eb.n, db.valid[c] + start, (size_t)cnt, hipMemcpyDeviceToDevice, stream);
+                if (db.valid[c]) seg(db.valid[c] + start, (uint8_t*)eb.valid[c].p + eb.n, cnt, 1);
                 else fill_valid_ones(c, eb.n, cnt);
             }
         }
         if (g_row_arr) {   // shard mode: the rows' global arrival indices
             if (int rc = arr_materialize()) return rc;
-            if (cnt > 0) hipMemcpyAsync((int64_t*)eb.arr.p + eb.n, g_row_arr + start, (size_t)cnt * 8, hipMemcpyDeviceToDevice, stream);
+            seg(g_row_arr + start, (int64_t*)eb.arr.p + eb.n, cnt * 8, 8);
+        }
+        if (ns > 0) {
+            int64_t mx = 0;
+            for (int k = 0; k < ns; ++k) mx = std::max(mx, cs.s[k].bytes);
+            const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (mx + 16 * 256 * 4 - 1) / (16 * 256 * 4)));
+            hipLaunchKernelGGL(k_eb_copy, dim3(gx, (unsigned)ns), dim3(256), 0, stream, cs);
+        }
+        if (g_row_arr) {
+            // (shard mode: the global arrivals were copied above)
         } else if (eb_arr_impl && (eb.n == 0 || arr_base + start == eb_arr0 + eb.n)) {
             if (eb.n == 0) eb_arr0 = arr_base + start;   // consecutive arrivals: the column stays implicit
         } else {
@@ -2095,6 +2121,8 @@ struct Engine {
     int sw_grid = 4096;   // EKGPU_SW_GRID: waves of a k_small_win launch
     bool fin_ring = true;       // EKGPU_FIN_RING=0: hopping windows always through k_finalize
     int fin_ring_chunks = 0;    // EKGPU_FIN_RING_CHUNKS: window chunks of a k_finalize_ring launch (0: by the key blocks)
+    int fin_ring_split = 0;     // EKGPU_FIN_RING_SPLIT=1: the split walk (count / sum, then min / max; measured slower on C3)
+    DevBuf ring_gbase;          // split walk: each (window, key block)'s row base, written by part 1 and read by part 2
     // HS: HAVING absent or over count(*) alone (decided from dp.hstar_tab): the kernel carries no interpreter. When the
     // full candidate tables would cost more LDS than the bitmaps, the launch caps them (kSwCandCap rows) and a second
     // launch redoes the few windows with more candidates (their list and count stay on the device)

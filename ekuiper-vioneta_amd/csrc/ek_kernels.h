@@ -1923,10 +1923,17 @@ __global__ __launch_bounds__(kBlock) void k_finalize(DPlan* __restrict__ pp, con
 #define EK_RING_AHEAD 3
 #endif
 constexpr int kRingAhead = EK_RING_AHEAD;   // k_finalize_ring: panes loaded ahead of the one being merged
-template <int R, bool VC, bool HV>
+// PART 0: every aggregate in one walk. The split walk (no HAVING) halves the ring's registers: PART 1 carries count /
+// non-nil count / sum and stores the row's key and its count / sum / avg slots, reserving the block's rows with the
+// atomic and recording each (window, block) base in gbase; PART 2 carries count / non-nil count / min / max and stores
+// the min / max slots of the same rows — same presence (count > 0), same ballots, the base read back from gbase.
+template <int R, bool VC, bool HV, int PART>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_WPE))) void k_finalize_ring(DPlan* __restrict__ pp, const WinDesc* __restrict__ wins,
                                                           int32_t nwin, int32_t cw, DState ds, int32_t ring,
-                                                          const int32_t* __restrict__ pane_err, Results res) {
+                                                          const int32_t* __restrict__ pane_err, Results res,
+                                                          uint32_t* __restrict__ gbase) {
+    static_assert(PART == 0 || !HV, "the split walk decides presence by the row count alone");
+    constexpr bool kSum = PART != 2, kMinMax = PART != 1;
     const DPlan& p = *pp;
     const int c0 = (int)blockIdx.y * cw, c1 = min(nwin, c0 + cw);
     if (c0 >= c1) return;   // uniform over the block
@@ -1959,11 +1966,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
         if (!pd_has || !pd_present) return;
         const int pp_ = par ^ 1;
         const int64_t pos = pd_out + (int64_t)esh[16 + pp_] + esh[8 * pp_ + wv] + __popcll(pd_mask & ((1ull << lane) - 1ull));
-        res.key[pos] = (uint32_t)key;
+        if (PART != 2) res.key[pos] = (uint32_t)key;
         for (int k = 0; k < p.n_aggs; ++k) {
             const int fn = p.agg_fn[k];
             int64_t v = 0;
             uint8_t tg = EK_TAG_I64;
+            if (PART == 1 && (fn == EK_AGG_MIN || fn == EK_AGG_MAX)) continue;
+            if (PART == 2 && fn != EK_AGG_MIN && fn != EK_AGG_MAX) continue;
             if (fn == EK_AGG_COUNT_STAR) v = pd_cnt;
             else if (fn == EK_AGG_COUNT) v = pd_vcn;
             else if (pd_vcn == 0) tg = EK_TAG_NULL;
@@ -1996,9 +2005,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
         pe[d] = ok ? pane_err[slot] : 0;
         pc[d] = l ? (int32_t)ds.cnt[e] : 0;
         pv[d] = (VC && l) ? (int32_t)ds.vcnt[0][e] : 0;
-        ps[d] = (l && (f & NEED_SUM)) ? ds.sum[0][e] : 0;
-        pmn[d] = (l && (f & NEED_MIN)) ? (uint64_t)ds.mn[0][e] : 0ull;
-        pmx[d] = (l && (f & NEED_MAX)) ? (uint64_t)ds.mx[0][e] : 0ull;
+        ps[d] = (kSum && l && (f & NEED_SUM)) ? ds.sum[0][e] : 0;
+        pmn[d] = (kMinMax && l && (f & NEED_MIN)) ? (uint64_t)ds.mn[0][e] : 0ull;
+        pmx[d] = (kMinMax && l && (f & NEED_MAX)) ? (uint64_t)ds.mx[0][e] : 0ull;
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -2022,7 +2031,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
 #pragma unroll
             for (int t = 0; t < R; ++t) werr |= t >= R - span ? re[t] : 0;
             if (werr) {
-                if (blockIdx.x == 0 && threadIdx.x == 0) {
+                if (PART != 2 && blockIdx.x == 0 && threadIdx.x == 0) {
                     atomicOr(&res.win_err[wd.idx], werr);
                     if (res.wwit)   // the first pane with an error holds the window's first failed row
                         for (int64_t qq = wd.q_first; qq <= q; ++qq)
@@ -2041,11 +2050,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
                     if (nb == 0) continue;
                     const bool first = vcn == 0;
                     vcn += nb;
-                    isum = (int64_t)((uint64_t)isum + (uint64_t)(isf ? 0 : rs[t]));
-                    const double fs = isf ? __longlong_as_double(rs[t]) : 0.0;
-                    fsum = first ? fs : __dadd_rn(fsum, fs);
-                    omn = (first || rmn[t] < omn) ? rmn[t] : omn;
-                    omx = (first || rmx[t] > omx) ? rmx[t] : omx;
+                    if (kSum) {
+                        isum = (int64_t)((uint64_t)isum + (uint64_t)(isf ? 0 : rs[t]));
+                        const double fs = isf ? __longlong_as_double(rs[t]) : 0.0;
+                        fsum = first ? fs : __dadd_rn(fsum, fs);
+                    }
+                    if (kMinMax) {
+                        omn = (first || rmn[t] < omn) ? rmn[t] : omn;
+                        omx = (first || rmx[t] > omx) ? rmx[t] : omx;
+                    }
                 }
                 bool present = live && cnt > 0;
                 if (HV && present) {
@@ -2061,7 +2074,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EK_RING_
                 if (threadIdx.x == 0) {
                     uint32_t run = 0;
                     for (int x = 0; x < kBlock / 64; ++x) { const uint32_t c = esh[8 * par + x]; esh[8 * par + x] = run; run += c; }
-                    esh[16 + par] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[wd.idx], (unsigned long long)run) : 0u;
+                    if (PART == 2) {
+                        esh[16 + par] = run ? gbase[(int64_t)w * gridDim.x + blockIdx.x] : 0u;
+                    } else {
+                        esh[16 + par] = run ? (uint32_t)atomicAdd((unsigned long long*)&res.win_cnt[wd.idx], (unsigned long long)run) : 0u;
+                        if (PART == 1) gbase[(int64_t)w * gridDim.x + blockIdx.x] = esh[16 + par];
+                    }
                 }
                 pd_has = true;
                 pd_present = present;

@@ -841,23 +841,46 @@ __global__ __launch_bounds__(1024) void k_msd_plan1(const unsigned int* __restri
 // over[1] gets the largest sub-bucket (atomicMax)
 __global__ __launch_bounds__(1024) void k_msd_plan2(const unsigned int* __restrict__ tot2, int nsub, int64_t* __restrict__ base2,
                                                     unsigned int cap, unsigned int* __restrict__ over) {
+    // rounds of 8192 counts staged through LDS with coalesced loads / stores (one thread's 8 consecutive counts summed
+    // from LDS, a block scan, the exclusive starts written back coalesced): no strided global access
+    constexpr int kR = 8192, kPer = kR / 1024;
+    __shared__ unsigned int s[kR];
     __shared__ int64_t wsum[16];
-    const int per = (nsub + 1023) / 1024;
-    const int a = threadIdx.x * per, e = min(nsub, a + per);
-    int64_t sm = 0;
+    __shared__ int64_t s_run;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_run = 0;
     unsigned int mx = 0;
-    for (int i = a; i < e; ++i) { sm += tot2[i]; mx = max(mx, tot2[i]); }
-    if (mx > cap) atomicOr(over, 1u);
-    if (mx) atomicMax(over + 1, mx);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int64_t v = sm;
-    for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(v, o, 64); if (lane >= o) v += y; }
-    if (lane == 63) wsum[w] = v;
-    __syncthreads();
-    int64_t r = v - sm;
-    for (int k = 0; k < w; ++k) r += wsum[k];
-    if (threadIdx.x == 1023) base2[nsub] = r + sm;
-    for (int i = a; i < e; ++i) { base2[i] = r; r += tot2[i]; }
+    for (int c0 = 0; c0 < nsub; c0 += kR) {
+        const int n = min(kR, nsub - c0);
+        for (int i = t; i < kR; i += 1024) s[i] = i < n ? tot2[c0 + i] : 0u;
+        __syncthreads();
+        int64_t sm = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) { const unsigned int x = s[t * kPer + k]; sm += x; mx = max(mx, x); }
+        int64_t v = sm;
+        for (int o = 1; o < 64; o <<= 1) { const int64_t y = __shfl_up(v, o, 64); if (lane >= o) v += y; }
+        if (lane == 63) wsum[w] = v;
+        __syncthreads();
+        int64_t r = v - sm;
+        for (int k = 0; k < w; ++k) r += wsum[k];
+        const int64_t run0 = s_run;
+        // exclusive starts inside the round (< 2^32: a round holds at most 8192 sub-buckets of < 2^32 rows in all,
+        // host-checked batch bound 2^31) back into LDS, then out with the round's base
+        uint32_t rr = (uint32_t)r;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) { const unsigned int x = s[t * kPer + k]; s[t * kPer + k] = rr; rr += x; }
+        __syncthreads();
+        for (int i = t; i < n; i += 1024) base2[c0 + i] = run0 + (int64_t)s[i];
+        if (t == 1023) s_run = run0 + r + sm;
+        __syncthreads();
+    }
+    if (t == 0) base2[nsub] = s_run;
+    unsigned int m = mx;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o, 64));
+    if (lane == 0 && m) {
+        if (m > cap) atomicOr(over, 1u);
+        atomicMax(over + 1, m);
+    }
 }
 
 __global__ __launch_bounds__(kKmFixBlock) void k_kmsd_fix(const int64_t* __restrict__ base2, int nsub, int s2, uint32_t K,

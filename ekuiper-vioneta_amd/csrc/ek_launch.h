@@ -22,8 +22,8 @@ void launch_fin(int nvc, bool merge, dim3 grid, hipStream_t s, DPlan* p, const W
                 int32_t ring, const int32_t* pane_err, const Results& res);
 // k_finalize_ring<R, VC, HV>: R = ring slots (4 / 8 / 12 / 16, >= the panes of a window), VC: the value column's
 // non-nil count, HV: a HAVING; grid (key blocks, window chunks)
-void launch_fin_ring(int r, bool vc, bool hv, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, int32_t nwin,
-                     int32_t cw, const DState& ds, int32_t ring, const int32_t* pane_err, const Results& res);
+void launch_fin_ring(int r, bool vc, bool hv, int part, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, int32_t nwin,
+                     int32_t cw, const DState& ds, int32_t ring, const int32_t* pane_err, const Results& res, uint32_t* gbase);
 void launch_ung(int nvc, bool where, dim3 grid, hipStream_t s, DPlan* p, const DBatch& db, const GroupDesc& gd,
                 const uint8_t* acc, const DState& ds, int64_t tile, int32_t* pane_err);
 

@@ -25,12 +25,14 @@ void launch_fin(int nvc, bool merge, dim3 grid, hipStream_t s, DPlan* p, const W
 #undef EK_FIN
 }
 
-void launch_fin_ring(int r, bool vc, bool hv, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, int32_t nwin,
-                     int32_t cw, const DState& ds, int32_t ring, const int32_t* pane_err, const Results& res) {
-#define EK_FR(R, V, H) hipLaunchKernelGGL((k_finalize_ring<R, V, H>), grid, dim3(kBlock), 0, s, p, w, nwin, cw, ds, ring, pane_err, res)
-#define EK_FR_R(V, H) if (r <= 4) EK_FR(4, V, H); else if (r <= 8) EK_FR(8, V, H); else if (r <= 12) EK_FR(12, V, H); else EK_FR(16, V, H)
-    if (vc) { if (hv) { EK_FR_R(true, true); } else { EK_FR_R(true, false); } }
-    else { if (hv) { EK_FR_R(false, true); } else { EK_FR_R(false, false); } }
+void launch_fin_ring(int r, bool vc, bool hv, int part, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, int32_t nwin,
+                     int32_t cw, const DState& ds, int32_t ring, const int32_t* pane_err, const Results& res, uint32_t* gbase) {
+#define EK_FR(R, V, H, P) hipLaunchKernelGGL((k_finalize_ring<R, V, H, P>), grid, dim3(kBlock), 0, s, p, w, nwin, cw, ds, ring, pane_err, res, gbase)
+#define EK_FR_R(V, H, P) if (r <= 4) EK_FR(4, V, H, P); else if (r <= 8) EK_FR(8, V, H, P); else if (r <= 12) EK_FR(12, V, H, P); else EK_FR(16, V, H, P)
+    if (part == 1) { if (vc) { EK_FR_R(true, false, 1); } else { EK_FR_R(false, false, 1); } return; }
+    if (part == 2) { if (vc) { EK_FR_R(true, false, 2); } else { EK_FR_R(false, false, 2); } return; }
+    if (vc) { if (hv) { EK_FR_R(true, true, 0); } else { EK_FR_R(true, false, 0); } }
+    else { if (hv) { EK_FR_R(false, true, 0); } else { EK_FR_R(false, false, 0); } }
 #undef EK_FR_R
 #undef EK_FR
 }
