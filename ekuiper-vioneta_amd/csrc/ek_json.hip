@@ -764,14 +764,40 @@ __device__ __forceinline__ void emit_row(const JSchema& S, const JOut& out, int6
 // One thread per message: an object is one row; a top-level array of objects (decodeWithSchema's []map case,
 // converter.go:141-158) is one row per element, at rows [rowbase[i], rowbase[i + 1]) (first pass, rowbase = nullptr:
 // the message is marked pending and decoded by the row-based pass). Errors fail the whole message.
+// The block's messages are contiguous in the payload: when they fit kJStage bytes they are first copied into LDS with
+// 16-byte loads (consecutive lanes on consecutive chunks) and every thread parses its message from there — a thread's
+// byte loads straight from HBM touch a different line per lane (one line per lane per byte step), the LDS copy reads
+// each line once. String offsets stay payload offsets (src maps payload offset g to the LDS copy of byte g).
+constexpr int kJStage = 16384;
 template <bool PATHS>
 __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
                                                          int64_t n, const JSchema* __restrict__ sch, JOut out) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_msg[kJStage];
     const int64_t i = (int64_t)blockIdx.x * kJBlock + threadIdx.x;
+    const uint8_t* src = bytes;
+    {
+        const int64_t b0 = (int64_t)blockIdx.x * kJBlock, b1 = b0 + kJBlock < n ? b0 + kJBlock : n;
+        const uintptr_t a_lo = (uintptr_t)(bytes + off[b0]), a_hi = (uintptr_t)(bytes + off[b1]);
+        const uintptr_t base = a_lo & ~(uintptr_t)15;
+        if (a_hi > a_lo && a_hi - base <= (uintptr_t)kJStage) {   // uniform over the block
+            const uintptr_t f_lo = (a_lo + 15) & ~(uintptr_t)15, f_hi = a_hi & ~(uintptr_t)15;   // whole chunks inside
+            uintptr_t h1 = a_hi, t0 = a_hi;
+            if (f_lo < f_hi) {
+                for (uintptr_t a = f_lo + 16 * (uintptr_t)threadIdx.x; a < f_hi; a += 16 * (uintptr_t)kJBlock)
+                    *(uint4*)(s_msg + (a - base)) = *(const uint4*)a;
+                h1 = f_lo;
+                t0 = f_hi;
+            }
+            for (uintptr_t a = a_lo + threadIdx.x; a < h1; a += kJBlock) s_msg[a - base] = *(const uint8_t*)a;
+            for (uintptr_t a = t0 + threadIdx.x; a < a_hi; a += kJBlock) s_msg[a - base] = *(const uint8_t*)a;
+            __syncthreads();
+            src = (const uint8_t*)((uintptr_t)(const uint8_t*)s_msg - (base - (uintptr_t)bytes));
+        }
+    }
     if (i >= n) return;
     const JSchema& S = *sch;
-    const uint8_t* p = bytes + off[i];
-    const uint8_t* e = bytes + off[i + 1];
+    const uint8_t* p = src + off[i];
+    const uint8_t* e = src + off[i + 1];
     RowAcc R;
     R.seen = 0;
     R.isnull = 0;
@@ -781,7 +807,7 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
     int64_t done = 0;
     while (p < e && is_ws(*p)) ++p;
     if (p < e && *p == '{') {
-        p = decode_object<PATHS>(S, p, e, bytes, R, out, &err);
+        p = decode_object<PATHS>(S, p, e, src, R, out, &err);
         if (p) {
             emit_row(S, out, r0, R, true);
             done = 1;
@@ -802,7 +828,7 @@ __global__ __launch_bounds__(kJBlock) void k_json_decode(const uint8_t* __restri
                     if (p >= e || *p != '{' || done >= nr) { err = (p < e && *p != '{') ? EK_JSON_ERR_TYPE : EK_JSON_ERR_SYNTAX; break; }
                     R.seen = 0;
                     R.isnull = 0;
-                    p = decode_object<PATHS>(S, p, e, bytes, R, out, &err);
+                    p = decode_object<PATHS>(S, p, e, src, R, out, &err);
                     if (!p) break;
                     emit_row(S, out, r0 + done, R, true);
                     done++;

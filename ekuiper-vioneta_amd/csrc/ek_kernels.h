@@ -1780,7 +1780,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
         for (int kl = threadIdx.x; kl < kk; kl += kAggBlock) {
             const int c = kl >> 6;
             const unsigned long long m = (unsigned long long)pmask[2 * c] | ((unsigned long long)pmask[2 * c + 1] << 32);
-            if (!((m >> (kl & 63)) & 1ull)) continue;
+            if (!((m >> (kl & 63)) & 1ull) || (gd.pad & 64)) continue;   // (diagnostic knob 64: no row stores)
             const int64_t pos = rbase + ppre[c] + __popcll(m & ((1ull << (kl & 63)) - 1ull));
             int64_t cc, vc[NVC], is[NVC];
             double fs[NVC], m2[NVC];
