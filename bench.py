@@ -196,7 +196,7 @@ def cpu_model():
 def committed_traffic(config, sim, events):
     """HBM bytes per step from the newest committed rocprofv3 PMC summary of this workload (tools/profile_configs.py);
     (None, None) when none matches its size."""
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         pmc = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{config}{sim}.json")
         if not os.path.exists(pmc):
             continue
