@@ -156,11 +156,22 @@ def test_state_window_reopen_chain(oracle):
     assert [w.value(1, 0) for w in run.windows] == [7, 12, 8]
 
 
-def test_state_window_processing_time_where_rejected(oracle):
-    rule = compile_rule("SELECT count(*) FROM demo WHERE a > 0 GROUP BY STATEWINDOW(a > 1, a > 5)", {"a": "bigint"},
+def test_state_window_processing_time_where_pushdown(oracle):
+    """Processing time: WHERE is pushed below the STATEWINDOW (windowPlan.go:82-99, round 6): a row it drops never reaches
+    the begin / emit conditions. The rule over the whole stream equals the WHERE-less rule over the rows WHERE keeps
+    (members mapped back to input rows); a = 20 satisfies the emit condition but fails WHERE, so the window it would
+    have closed stays open (the post-window filter would give two windows, 1 and 2 rows)."""
+    a = np.array([3, 20, 4, 7, 0, 9, 20, 2, 6, 1], np.int64)
+    rule = compile_rule("SELECT count(*) FROM demo WHERE a != 20 GROUP BY STATEWINDOW(a > 1, a > 5)", {"a": "bigint"},
                         is_event_time=False)
-    with pytest.raises(RuntimeError):
-        oracle.run(rule.plan, [np.arange(5, dtype=np.int64)])
+    bare = compile_rule("SELECT count(*) FROM demo GROUP BY STATEWINDOW(a > 1, a > 5)", {"a": "bigint"},
+                        is_event_time=False)
+    keep = np.nonzero(a != 20)[0]
+    got = oracle.run(rule.plan, [a])
+    exp = oracle.run(bare.plan, [a[keep]])
+    assert [sorted(int(i) for i in m) for m in got.members] == [sorted(int(keep[i]) for i in m) for m in exp.members]
+    assert [w.value(0, 0) for w in got.windows] == [w.value(0, 0) for w in exp.windows]
+    assert [list(map(int, m)) for m in got.members][0] == [0, 2, 3]   # 3, 4, 7: the 20 between them is gone
 
 
 # ------------------------------------------------------------------ v2 event-time sliding windows
