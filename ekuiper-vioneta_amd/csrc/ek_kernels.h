@@ -1412,7 +1412,8 @@ __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Sta
 }
 
 // HV: the plan has a HAVING clause (without one, the emission carries no expression evaluator: fewer registers)
-template <int NVC, bool SORT, bool HV>
+// NUL: some staged value column carries validity (without, the fold keeps no per-row validity bytes in registers)
+template <int NVC, bool SORT, bool HV, bool NUL = true>
 __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AGG_WAVES_PER_EU))) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
                                                    Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err,
@@ -1528,7 +1529,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
 #pragma unroll
             for (int v = 0; v < NVC; ++v) {
                 sp.rv[v][u] = (pos[u] >= 0 && fl[v]) ? st.val[v][pos[u]] : 0;
-                sp.vd[v][u] = (pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
+                sp.vd[v][u] = (NUL && pos[u] >= 0 && (nullm & (1u << v))) ? st.valid[v][pos[u]] : (uint8_t)1;
             }
         }
     };

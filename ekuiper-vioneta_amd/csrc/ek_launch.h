@@ -10,7 +10,7 @@
 
 namespace ek {
 
-// pane mode (ek_kernels.h): k_part<MODE, WHERE, NVC>, k_agg<NVC, SORT, HAVING>, k_finalize / k_finalize_merge<NVC>,
+// pane mode (ek_kernels.h): k_part<MODE, WHERE, NVC>, k_agg<NVC, SORT, HAVING, NULLABLE>, k_finalize / k_finalize_merge<NVC>,
 // k_ung_tile<NVC, WHERE>
 void launch_part(int mode, bool where, int nvc, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const DBatch& db,
                  const PaneGrid& g, const GroupDesc& gd, const uint8_t* acc, const Staging& st, uint32_t* ctab, int ls,

@@ -8,11 +8,14 @@ namespace ek {
 void launch_agg(int nvc, bool sort, bool having, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const GroupDesc& gd,
                 const LdsLayout& lay, const uint32_t* ctab, int ls, int64_t rs, const Staging& st, const DState& ds,
                 const Results& res, const int32_t* pane_err, const int64_t* pbase, uint64_t* scratch, int64_t scr_stride) {
-#define EK_AGG(N, S, H) hipLaunchKernelGGL((k_agg<N, S, H>), grid, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err, pbase, scratch, scr_stride)
-#define EK_AGG_N(S, H) switch (nvc) { case 1: EK_AGG(1, S, H); break; case 2: EK_AGG(2, S, H); break; \
-                                      case 3: EK_AGG(3, S, H); break; default: EK_AGG(4, S, H); break; }
-    if (sort) { if (having) { EK_AGG_N(true, true) } else { EK_AGG_N(true, false) } }
-    else { if (having) { EK_AGG_N(false, true) } else { EK_AGG_N(false, false) } }
+#define EK_AGG(N, S, H, U) hipLaunchKernelGGL((k_agg<N, S, H, U>), grid, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err, pbase, scratch, scr_stride)
+#define EK_AGG_N(S, H, U) switch (nvc) { case 1: EK_AGG(1, S, H, U); break; case 2: EK_AGG(2, S, H, U); break; \
+                                         case 3: EK_AGG(3, S, H, U); break; default: EK_AGG(4, S, H, U); break; }
+    // (no staged validity: the fold's instantiation without per-row validity registers; the sort path keeps one)
+    const bool nul = st.nullable_mask != 0 || (gd.pad2 & 8);   // EKGPU_VARIANT bit 3: the nullable instantiation always
+    if (sort) { if (having) { EK_AGG_N(true, true, true) } else { EK_AGG_N(true, false, true) } }
+    else if (nul) { if (having) { EK_AGG_N(false, true, true) } else { EK_AGG_N(false, false, true) } }
+    else { if (having) { EK_AGG_N(false, true, false) } else { EK_AGG_N(false, false, false) } }
 #undef EK_AGG_N
 #undef EK_AGG
 }
