@@ -804,6 +804,7 @@ struct Engine {
         sw_cap_on = env_int("EKGPU_SW_CAP", 1);
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
+        agg_small = env_int("EKGPU_AGG_SMALL", 1) != 0;
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         variant = env_int("EKGPU_VARIANT", 0);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
@@ -1631,7 +1632,9 @@ struct Engine {
                 scr = (uint64_t*)sort_scr.p;
             }
             const size_t lds_a = (size_t)lay.bytes + agg_run_lds_bytes(gd.mruns);
-            ek::launch_agg(nvc, pbase != nullptr, dp.n_having > 0, ga, lds_a, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
+            // partitions averaging under 8 192 rows: the fold with 4 rows in flight per lane (k_agg<.., UR = 4>)
+            const bool small = agg_small && (gd.hi - gd.lo) < (int64_t)gd.np * 8192;
+            ek::launch_agg(nvc, pbase != nullptr, dp.n_having > 0, small, ga, lds_a, stream, d_plan, gd, lay, ct, ls, rs, st, dstate, rv, perr, pbase, scr,
                        scr_stride);
             phase_end(ph);
         }
@@ -1887,6 +1890,7 @@ struct Engine {
     bool small_win_on = true;           // EKGPU_SMALL_WIN=0: every range window through k_part + k_agg
     int stats_blocks = 1024;            // k_stats grid (EKGPU_STATS_BLOCKS)
     int variant = 0;                    // layout variants under measurement (EKGPU_VARIANT bits)
+    bool agg_small = true;              // EKGPU_AGG_SMALL=0: k_agg keeps 8 rows per lane for small partitions too
 
     size_t col_es(int c) const { return plan.column_type[c] == EK_COL_U32 ? 4 : 8; }
 

@@ -1413,7 +1413,9 @@ __device__ inline void agg_sparse(const DPlan& p, const GroupDesc& gd, const Sta
 
 // HV: the plan has a HAVING clause (without one, the emission carries no expression evaluator: fewer registers)
 // NUL: some staged value column carries validity (without, the fold keeps no per-row validity bytes in registers)
-template <int NVC, bool SORT, bool HV, bool NUL = true>
+// UR: rows in flight per lane in the fold (EK_AGG_U; 4 for launches whose partitions average under 8 192 rows, where a
+// 512-thread span of 8 rows per lane leaves most lanes idle: C3 0.262 -> 0.222 ms)
+template <int NVC, bool SORT, bool HV, bool NUL = true, int UR = EK_AGG_U>
 __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AGG_WAVES_PER_EU))) void k_agg(DPlan* __restrict__ pp, GroupDesc gd, LdsLayout lay,
                                                    const uint32_t* __restrict__ ctab, int ls, int64_t rs,
                                                    Staging st, DState ds, Results res, const int32_t* __restrict__ pane_err,
@@ -1497,7 +1499,7 @@ __global__ __launch_bounds__(kAggBlock) __attribute__((amdgpu_waves_per_eu(EK_AG
     // rows of the partition as one virtual array: row v lives in run j = max{j : r_pre[j] <= v}.
     // Each wave takes a span of 64*U consecutive rows (coalesced loads); its first run is found by
     // one binary search, and every lane then advances its run pointer monotonically.
-    constexpr int U = EK_AGG_U;   // rows in flight per lane (per pipeline stage with EK_AGG_PIPE)
+    constexpr int U = UR;   // rows in flight per lane (per pipeline stage with EK_AGG_PIPE)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto run_of = [&](uint32_t v) {
         int lo = 0, hi = nruns - 1;

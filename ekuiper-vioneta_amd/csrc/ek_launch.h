@@ -15,7 +15,7 @@ namespace ek {
 void launch_part(int mode, bool where, int nvc, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const DBatch& db,
                  const PaneGrid& g, const GroupDesc& gd, const uint8_t* acc, const Staging& st, uint32_t* ctab, int ls,
                  int64_t rs, int32_t* pane_err);
-void launch_agg(int nvc, bool sort, bool having, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const GroupDesc& gd,
+void launch_agg(int nvc, bool sort, bool having, bool small, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const GroupDesc& gd,
                 const LdsLayout& lay, const uint32_t* ctab, int ls, int64_t rs, const Staging& st, const DState& ds,
                 const Results& res, const int32_t* pane_err, const int64_t* pbase, uint64_t* scratch, int64_t scr_stride);
 void launch_fin(int nvc, bool merge, dim3 grid, hipStream_t s, DPlan* p, const WinDesc* w, const DState& ds,

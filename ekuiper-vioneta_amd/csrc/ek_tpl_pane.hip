@@ -5,10 +5,11 @@
 
 namespace ek {
 
-void launch_agg(int nvc, bool sort, bool having, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const GroupDesc& gd,
+void launch_agg(int nvc, bool sort, bool having, bool small, dim3 grid, size_t lds, hipStream_t s, DPlan* p, const GroupDesc& gd,
                 const LdsLayout& lay, const uint32_t* ctab, int ls, int64_t rs, const Staging& st, const DState& ds,
                 const Results& res, const int32_t* pane_err, const int64_t* pbase, uint64_t* scratch, int64_t scr_stride) {
-#define EK_AGG(N, S, H, U) hipLaunchKernelGGL((k_agg<N, S, H, U>), grid, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err, pbase, scratch, scr_stride)
+#define EK_AGG(N, S, H, U) do { if constexpr (!(S) && !(U)) { if (small) { hipLaunchKernelGGL((k_agg<N, S, H, U, 4>), grid, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err, pbase, scratch, scr_stride); break; } } \
+                                hipLaunchKernelGGL((k_agg<N, S, H, U>), grid, dim3(kAggBlock), lds, s, p, gd, lay, ctab, ls, rs, st, ds, res, pane_err, pbase, scratch, scr_stride); } while (0)
 #define EK_AGG_N(S, H, U) switch (nvc) { case 1: EK_AGG(1, S, H, U); break; case 2: EK_AGG(2, S, H, U); break; \
                                          case 3: EK_AGG(3, S, H, U); break; default: EK_AGG(4, S, H, U); break; }
     // (no staged validity: the fold's instantiation without per-row validity registers; the sort path keeps one)
