@@ -193,6 +193,9 @@ def cpu_model():
     return None
 
 
+PHASE_EVERY = int(os.environ.get("EKGPU_BENCH_PHASE_EVERY", "4"))   # timed steps per step with phase events
+
+
 def committed_traffic(config, sim, events):
     """HBM bytes per step from the newest committed rocprofv3 PMC summary of this workload (tools/profile_configs.py);
     (None, None) when none matches its size."""
@@ -686,9 +689,17 @@ def main():
     torch.cuda.synchronize()
     st0 = eng.stats()   # running totals (the engine's pushes are asynchronous: read back after the loop)
     route_ms[0] = route_ms[1] = 0.0
+    # per-kernel HIP-event timing is sampled: the engine records its phase events on one timed step in PHASE_EVERY
+    # (ek_set_phase_timing; each event is a queue marker worth ~5-10 us of device idle per push), and the per-launch
+    # averages come from those steps
+    sampled = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        on = i % PHASE_EVERY == 0
+        sampled += on
+        eng.set_phase_timing(on)
         step()
+    eng.set_phase_timing(True)
     # the engine's library links the system HIP runtime, torch its own: wait on the engines' streams themselves
     eng.sync()
     if cnt_eng is not None:
@@ -736,7 +747,7 @@ def main():
         if ph_n[k] == 0:
             continue
         launch_ms = ph_ms[k] / ph_n[k]
-        per_step = ph_n[k] / args.steps
+        per_step = ph_n[k] / sampled
         if ph == "stats":
             kb = n * 8 if iet else 0
         elif ph == "partition":
@@ -786,7 +797,9 @@ def main():
                      "formula_bytes_per_step": formula_bytes,
                      "formula_frac": formula_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "required_bytes": required,
-                     "dominant_kernel": dominant, "kernels": kernels},
+                     "dominant_kernel": dominant, "kernels": kernels,
+                     "kernel_timing": f"HIP events on the engine stream around each phase, recorded on {sampled} of the "
+                                      f"{args.steps} timed steps (one in {PHASE_EVERY}); launch_ms = their average"},
     }
     out["config"]["fused_sorted_batches_last_step"] = int(st1.fused_batches)   # (stream counters restart at ek_reset)
     if routed:

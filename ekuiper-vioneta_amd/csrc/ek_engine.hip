@@ -175,6 +175,7 @@ struct Engine {
     std::vector<PhaseEv> phase_ev;
     size_t phase_used = 0;
     int phase_begin(int ph) {
+        if (!phase_events) return -1;
         if (phase_used == phase_ev.size()) {
             PhaseEv e{nullptr, nullptr, 0};
             hipEventCreate(&e.a);
@@ -185,7 +186,8 @@ struct Engine {
         hipEventRecord(phase_ev[phase_used].a, stream);
         return (int)phase_used++;
     }
-    void phase_end(int idx) { hipEventRecord(phase_ev[idx].b, stream); }
+    void phase_end(int idx) { if (idx >= 0) hipEventRecord(phase_ev[idx].b, stream); }
+    bool phase_events = true;   // ek_set_phase_timing (EKGPU_PHASE_EVENTS=0 at create: off)
 
     // ---- derived configuration
     int wtype = 0;
@@ -805,6 +807,7 @@ struct Engine {
         grp_on = env_int("EKGPU_GRP", 1);
         eb_need_init();
         agg_small = env_int("EKGPU_AGG_SMALL", 1) != 0;
+        phase_events = env_int("EKGPU_PHASE_EVENTS", 1) != 0;
         stats_blocks = std::max(1, env_int("EKGPU_STATS_BLOCKS", 1024));
         variant = env_int("EKGPU_VARIANT", 0);
         // one group per batch by default (full-chip launches); bounded by the per-partition run list of k_agg
@@ -6083,6 +6086,12 @@ int ek_set_async(void* h, int32_t on) {
     if (!on) { hipStreamSynchronize(e->stream); rc = e->fold_time(); }
     e->async_push = on != 0;
     return rc;
+}
+
+int ek_set_phase_timing(void* h, int32_t on) {
+    if (!h) return EK_ERR_INVALID;
+    ((Engine*)h)->phase_events = on != 0;
+    return 0;
 }
 
 int ek_get_stats(void* h, ek_stats* out) {

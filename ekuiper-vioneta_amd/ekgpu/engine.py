@@ -52,6 +52,8 @@ def lib():
         L.ek_set_stream.restype = C.c_int
         L.ek_set_async.argtypes = [C.c_void_p, C.c_int32]
         L.ek_set_async.restype = C.c_int
+        L.ek_set_phase_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.ek_set_phase_timing.restype = C.c_int
         L.ek_get_stats.argtypes = [C.c_void_p, C.POINTER(A.ek_stats)]
         L.ek_get_stats.restype = C.c_int
         L.ek_last_error.argtypes = [C.c_void_p]
@@ -105,7 +107,7 @@ EXPORTED_SYMBOLS = ["ek_abi_version", "ek_device_count", "ek_create", "ek_push_b
                     "ek_destroy", "ek_json_create", "ek_json_decode", "ek_json_errors", "ek_json_get_stats",
                     "ek_json_last_error", "ek_json_destroy", "ek_export_state", "ek_import_state",
                     "ek_push_batch_global", "ek_advance_watermark", "ek_shard_triggers", "ek_advance_time",
-                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async", "ek_route_partition",
+                    "ek_window_error", "ek_batch_ts_stats", "ek_json_strings", "ek_json_dict_size", "ek_json_dict_string", "ek_set_async", "ek_set_phase_timing", "ek_route_partition",
                     "ek_json_list", "ek_json_rows"]
 
 _NP = {A.EK_COL_I64: np.int64, A.EK_COL_F64: np.float64, A.EK_COL_U32: np.uint32, A.EK_COL_BOOL: np.int64}
@@ -305,6 +307,10 @@ class Engine:
         """Pushes return with their work queued (ek_set_async): a device batch stays borrowed until the next push,
         sync, poll or stats call."""
         self._check(lib().ek_set_async(self.h, 1 if on else 0))
+
+    def set_phase_timing(self, on: bool = True):
+        """Per-phase HIP-event timing of the pushes (ek_set_phase_timing; on by default)."""
+        self._check(lib().ek_set_phase_timing(self.h, 1 if on else 0))
 
     def stats(self) -> A.ek_stats:
         s = A.ek_stats()

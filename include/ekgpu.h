@@ -341,6 +341,12 @@ int ek_set_stream(void* h, void* hip_stream);
  * queued work is returned by the next push, ek_advance_time, ek_get_stats or ek_set_async(h, 0) (EK_ERR_DEVICE).
  * Turning it off waits for queued work. */
 int ek_set_async(void* h, int32_t on);
+/* Per-phase device timing (on != 0, the default): every push brackets its statistics / partition / aggregate /
+ * finalize launches with HIP events, read into ek_stats.phase_ms / phase_*_total. Each event is a queue marker that
+ * costs the push ≈ 5-10 µs of device idle, so a caller that samples the phase times (bench.py: one step in four) turns
+ * it off for the other pushes; their phase counters then do not move. Instrumentation only (no reference
+ * counterpart; the reference exposes operator metrics, internal/topo/node/metric). */
+int ek_set_phase_timing(void* h, int32_t on);
 int ek_get_stats(void* h, ek_stats* out);
 const char* ek_last_error(void* h);
 int ek_destroy(void* h);
